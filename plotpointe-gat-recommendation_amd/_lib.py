@@ -1,0 +1,106 @@
+"""ctypes binding of libppgat.so (include/ppgat.h).
+
+The product path has no CPU fallback: if the shared library is missing or fails to
+load, every op raises ``RuntimeError`` (build it with ``python -c "import
+__graft_entry__ as g; g.build()"`` or ``make -C plotpointe-gat-recommendation_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("PPGAT_LIB", _HERE / "libppgat.so"))
+
+c_int, c_i64, c_u64, c_f, c_vp, c_sz = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
+                                         ctypes.c_void_p, ctypes.c_size_t)
+
+# name -> (restype, argtypes); mirrors include/ppgat.h
+SIGNATURES = {
+    "ppgat_version": (c_int, []),
+    "ppgat_last_error": (ctypes.c_char_p, []),
+    "ppgat_supported_channels": (c_int, [c_int]),
+    "ppgat_csr_workspace_bytes": (c_int, [c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "ppgat_csr_build": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
+                                c_vp]),
+    "ppgat_node_scores": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp]),
+    "ppgat_fwd": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
+                          c_u64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_bwd_workspace_bytes": (c_int, [c_i64, c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_bwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_sz,
+                          c_vp]),
+    "ppgat_profile_enable": (c_int, [c_int]),
+    "ppgat_profile_reset": (c_int, []),
+    "ppgat_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
+}
+
+KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6}
+MODE_PYG, MODE_CUSTOM = 0, 1
+
+_lib = None
+_load_error = None
+
+
+def load(path: Path = None):
+    """Load (once) and return the ctypes library; raise RuntimeError if unavailable.
+
+    torch must be imported first so the already-loaded HIP runtime
+    (soname libamdhip64.so.7) is shared with torch's streams and allocator.
+    """
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (HIP runtime first)
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        _load_error = f"libppgat.so not found at {p}; build it first (make -C {_HERE / 'csrc'})"
+        raise RuntimeError(_load_error)
+    try:
+        lib = ctypes.CDLL(str(p))
+    except OSError as e:  # pragma: no cover
+        _load_error = f"failed to load {p}: {e}"
+        raise RuntimeError(_load_error) from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.ppgat_last_error().decode() if _lib is not None else "library not loaded"
+        if rc == 2:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def profile_enable(on: bool = True):
+    lib = load()
+    check(lib.ppgat_profile_enable(1 if on else 0), "profile_enable")
+
+
+def profile_reset():
+    lib = load()
+    check(lib.ppgat_profile_reset(), "profile_reset")
+
+
+def profile_read(kernel: str):
+    lib = load()
+    ms = ctypes.c_double(0.0)
+    n = ctypes.c_int64(0)
+    check(lib.ppgat_profile_read(KERNELS[kernel], ctypes.byref(ms), ctypes.byref(n)), "profile_read")
+    return ms.value, n.value

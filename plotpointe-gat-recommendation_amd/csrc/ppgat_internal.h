@@ -1,0 +1,39 @@
+// Internal declarations shared by the kernel, graph and ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace ppgat {
+
+constexpr int kModePyg = 0;
+constexpr int kModeCustom = 1;
+constexpr int kMaxHeads = 8;
+constexpr int64_t kEpiMaxWaves = 8192;
+
+hipError_t launch_scores(const float* h, const float* as, const float* ad, int64_t n, int heads, int C, float* ss,
+                         float* sd, hipStream_t st);
+hipError_t launch_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* eid, int64_t n, int heads, int C,
+                      const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
+                      float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
+                      hipStream_t st);
+hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, int64_t n,
+                          int heads, int C, float gscale, float* D, hipStream_t st);
+hipError_t launch_bwd_src(const int32_t* colptr, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                          int64_t n, int heads, int C, const float* h, const float* ss, const float* sd,
+                          const float* m, const float* invl, const float* D, const float* go, int mode, float slope,
+                          float gscale, float p, uint64_t seed, float* dh, float* ds_src, float* dz,
+                          hipStream_t st);
+int64_t epi_waves(int64_t n);
+hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
+                          const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,
+                          int64_t waves, hipStream_t st);
+hipError_t launch_bwd_red(const float* partial, int64_t waves, int hc, float* das, float* dad, hipStream_t st);
+
+// graph preprocessing (ppgat_graph.hip)
+size_t csr_workspace_bytes(int64_t n_nodes, int64_t n_edges);
+hipError_t csr_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t* rowptr, int32_t* col, int32_t* csr_eid,
+                     int32_t* colptr, int32_t* row, int32_t* csc_eid, int32_t* csc2csr, int32_t* bad,
+                     void* ws, size_t ws_bytes, hipStream_t st);
+
+}  // namespace ppgat

@@ -1,0 +1,467 @@
+// ppgat_kernels.hip -- fused GAT message-passing kernels for CDNA4 (gfx950, MI355X).
+//
+// Hot path of BASELINE.json north_star: one GAT layer = per-node attention terms,
+// per-edge LeakyReLU logit, per-destination segmented softmax, alpha-weighted
+// neighbour aggregation (forward), and its atomic-free backward.
+//
+// Reference semantics restated (oracle/gat_oracle.py):
+//   PyG GATConv (scripts/train_gat_pyg.py:77, concat=False, add_self_loops=False)
+//   SimpleGATLayer.forward (scripts/train_gat_custom.py:75-93)
+//
+// Layout in HBM (all fp32 row-major, int32 indices):
+//   h      [N, H, C]  projected node rows (one 512 B row per node at H=1, C=128)
+//   s_src, s_dst, m, inv_l, D, ds_src  [N, H]
+//   CSR by dst: rowptr[N+1], col[E] (src), csr_eid[E]
+//   CSC by src: colptr[N+1], row[E] (dst), csc_eid[E], csc2csr[E]
+//   dz     [E, H]  per-edge logit gradient, stored in CSR slot order
+//
+// Work decomposition: one 64-lane wavefront per node row.  A row of C floats is
+// C/4 lanes x float4 (a "subgroup"); 64/(C/4) subgroups take different edges of
+// the same row, each keeping U gathers in flight, so a wave has 8 neighbour rows
+// (4 KB at C=128) outstanding.  Softmax state is wave-uniform (online max/sum over
+// 64-edge chunks); subgroup partial aggregates merge with xor-shuffles at the end.
+// No float atomics anywhere: every sum is owned by one wave in a fixed order, so
+// results are bitwise reproducible run to run.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "ppgat_internal.h"
+
+namespace ppgat {
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 fma4(float s, float4 v, float4 a) {
+  return make_float4(fmaf(s, v.x, a.x), fmaf(s, v.y, a.y), fmaf(s, v.z, a.z), fmaf(s, v.w, a.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 mul4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+__device__ __forceinline__ float4 shfl_xor4(float4 v, int m) {
+  return make_float4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+
+// attention logit e(z) and de/dz, per mode (torch leaky_relu / clamp backward rules:
+// slope where z <= 0; clamp passes gradient where min <= e <= max).
+__device__ __forceinline__ float logit(float z, float slope, int mode) {
+  float e = z > 0.f ? z : z * slope;
+  if (mode == kModeCustom) e = fminf(fmaxf(e, -10.f), 10.f);
+  return e;
+}
+__device__ __forceinline__ float dlogit(float z, float slope, int mode) {
+  const float e = z > 0.f ? z : z * slope;
+  float d = z > 0.f ? 1.f : slope;
+  if (mode == kModeCustom && (e < -10.f || e > 10.f)) d = 0.f;
+  return d;
+}
+
+// Counter-based dropout mask on alpha (restated in oracle/gat_oracle.py:dropout_scale).
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t eid, uint32_t head, float p,
+                                            float inv_keep) {
+  uint64_t x = seed ^ ((uint64_t)eid * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)head * 0xC2B2AE3D27D4EB4Full);
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+  return u >= p ? inv_keep : 0.f;
+}
+
+template <int C>
+struct Geo {
+  static constexpr int LPR = C / 4;              // lanes per row (float4 each)
+  static constexpr int EPW = 64 / LPR;           // edges handled side by side per wave
+  static constexpr int U = EPW >= 8 ? 1 : 8 / EPW;  // unroll: 8 gathers in flight per wave
+  static_assert(C % 4 == 0 && LPR <= 64 && 64 % LPR == 0, "C must be 4*2^k <= 256");
+  static_assert(64 % (EPW * U) == 0, "chunk tiling");
+};
+
+// ---------------------------------------------------------------------------
+// s_src[n,h] = <h[n,h,:], att_src[h,:]>, s_dst likewise.  One subgroup per (n,h).
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) k_scores(const float* __restrict__ h, const float* __restrict__ att_src,
+                                                const float* __restrict__ att_dst, int64_t pairs, int heads,
+                                                float* __restrict__ s_src, float* __restrict__ s_dst) {
+  using G = Geo<C>;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pr = t / G::LPR;
+  const int sl = (int)(t % G::LPR);
+  const bool valid = pr < pairs;
+  const int hd = valid ? (int)(pr % heads) : 0;
+  const float4 v = valid ? ld4(h + pr * C + sl * 4) : f4(0.f);
+  float x = dot4(v, ld4(att_src + hd * C + sl * 4));
+  float y = dot4(v, ld4(att_dst + hd * C + sl * 4));
+#pragma unroll
+  for (int off = G::LPR / 2; off > 0; off >>= 1) {
+    x += __shfl_xor(x, off);
+    y += __shfl_xor(y, off);
+  }
+  if (valid && sl == 0) {
+    s_src[pr] = x;
+    s_dst[pr] = y;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused forward: one wave per destination row i (CSR by dst).
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) k_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                             const int32_t* __restrict__ eid, int64_t n_nodes, int heads,
+                                             const float* __restrict__ h, const float* __restrict__ s_src,
+                                             const float* __restrict__ s_dst, const float* __restrict__ bias,
+                                             int mode, float slope, float eps, float p, float inv_keep,
+                                             uint64_t seed, float* __restrict__ out, float* __restrict__ m_out,
+                                             float* __restrict__ invl_out, float* __restrict__ agg_out) {
+  using G = Geo<C>;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= n_nodes) return;  // wave-uniform
+  const int sg = lane / G::LPR, sl = lane % G::LPR;
+  const int rs = rowptr[i], re = rowptr[i + 1];
+  const bool pyg = mode == kModePyg;
+  float4 osum = f4(0.f);
+  for (int hd = 0; hd < heads; ++hd) {
+    const float sd = s_dst[i * heads + hd];
+    float m = pyg ? -INFINITY : 0.f, l = 0.f;
+    float4 acc = f4(0.f);
+    for (int base = rs; base < re; base += 64) {
+      const int k = base + lane;
+      const bool valid = k < re;
+      const int j = valid ? col[k] : 0;
+      float e = -INFINITY;
+      if (valid) e = logit(s_src[(int64_t)j * heads + hd] + sd, slope, mode);
+      float pe;
+      if (pyg) {
+        const float mn = fmaxf(m, wave_max(e));
+        const float sc = expf(m - mn);
+        pe = valid ? expf(e - mn) : 0.f;
+        l = fmaf(l, sc, wave_sum(pe));
+        acc = mul4(acc, sc);
+        m = mn;
+      } else {
+        pe = valid ? expf(e) : 0.f;
+        l += wave_sum(pe);
+      }
+      float pw = pe;
+      if (p > 0.f && valid) pw *= drop_scale(seed, (uint32_t)eid[k], (uint32_t)hd, p, inv_keep);
+      const int n = min(64, re - base);
+      for (int q0 = 0; q0 < n; q0 += G::EPW * G::U) {
+        float4 v[G::U];
+        float pq[G::U];
+#pragma unroll
+        for (int u = 0; u < G::U; ++u) {
+          const int q = q0 + u * G::EPW + sg;
+          const int jq = __shfl(j, q);
+          pq[u] = __shfl(pw, q);
+          v[u] = q < n ? ld4(h + ((int64_t)jq * heads + hd) * C + sl * 4) : f4(0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < G::U; ++u) acc = fma4(pq[u], v[u], acc);
+      }
+    }
+#pragma unroll
+    for (int off = G::LPR; off < 64; off <<= 1) acc = add4(acc, shfl_xor4(acc, off));
+    const float invl = 1.f / (l + eps);
+    const float4 a = mul4(acc, invl);
+    if (agg_out != nullptr && sg == 0) st4(agg_out + (i * heads + hd) * C + sl * 4, a);
+    osum = add4(osum, a);
+    if (lane == 0) {
+      m_out[i * heads + hd] = (pyg && re > rs) ? m : 0.f;
+      invl_out[i * heads + hd] = invl;
+    }
+  }
+  if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
+  if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
+  if (sg == 0) st4(out + i * C + sl * 4, osum);
+}
+
+// ---------------------------------------------------------------------------
+// Backward prologue: D[n,h] = <g_n, agg[n,h]>,  g = gscale * grad_out
+// (= sum_k alpha_k dalpha_k over the in-edges of n; SURVEY Appendix B D_i).
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_out, const float* __restrict__ out,
+                                                 const float* __restrict__ agg, const float* __restrict__ bias,
+                                                 int64_t pairs, int heads, float gscale, float* __restrict__ D) {
+  using G = Geo<C>;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pr = t / G::LPR;
+  const int sl = (int)(t % G::LPR);
+  const bool valid = pr < pairs;
+  const int64_t n = valid ? pr / heads : 0;
+  float x = 0.f;
+  if (valid) {
+    const float4 g = ld4(grad_out + n * C + sl * 4);
+    float4 a;
+    if (agg != nullptr) {
+      a = ld4(agg + pr * C + sl * 4);
+    } else {
+      a = ld4(out + n * C + sl * 4);
+      if (bias != nullptr) {
+        const float4 b = ld4(bias + sl * 4);
+        a = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+      }
+    }
+    x = dot4(g, a);
+  }
+#pragma unroll
+  for (int off = G::LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  if (valid && sl == 0) D[pr] = x * gscale;
+}
+
+// ---------------------------------------------------------------------------
+// Backward pass B: one wave per SOURCE node j (CSC by src).
+//   dh_j   = sum_k beta_k g_{i_k}                          (message term, complete)
+//   dz_k   = alpha_k (d_k gscale <dOut_i, h_j> - D_i) e'(z_k) (logit gradient)
+//   ds_src_j = sum_k dz_k ;  dz_k stored at its CSR slot for the dst-side sum.
+// alpha is recomputed from the saved (m, inv_l): nothing [E]-sized was saved.
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) k_bwd_src(
+    const int32_t* __restrict__ colptr, const int32_t* __restrict__ row, const int32_t* __restrict__ csc_eid,
+    const int32_t* __restrict__ csc2csr, int64_t n_nodes, int heads, const float* __restrict__ h,
+    const float* __restrict__ s_src, const float* __restrict__ s_dst, const float* __restrict__ m_in,
+    const float* __restrict__ invl_in, const float* __restrict__ D, const float* __restrict__ grad_out, int mode,
+    float slope, float gscale, float p, float inv_keep, uint64_t seed, float* __restrict__ dh,
+    float* __restrict__ ds_src, float* __restrict__ dz) {
+  using G = Geo<C>;
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (j >= n_nodes) return;
+  const int sg = lane / G::LPR, sl = lane % G::LPR;
+  const int cs = colptr[j], ce = colptr[j + 1];
+  for (int hd = 0; hd < heads; ++hd) {
+    const float ss = s_src[j * heads + hd];
+    const float4 hv = ld4(h + (j * heads + hd) * C + sl * 4);
+    float4 acc = f4(0.f);
+    float ds = 0.f;
+    for (int base = cs; base < ce; base += 64) {
+      const int k = base + lane;
+      const bool valid = k < ce;
+      const int i = valid ? row[k] : 0;
+      float alpha = 0.f, f = 0.f, Dv = 0.f, dm = 1.f;
+      if (valid) {
+        const int64_t ih = (int64_t)i * heads + hd;
+        const float z = ss + s_dst[ih];
+        const float e = logit(z, slope, mode);
+        f = dlogit(z, slope, mode);
+        alpha = expf(e - m_in[ih]) * invl_in[ih];
+        Dv = D[ih];
+        if (p > 0.f) dm = drop_scale(seed, (uint32_t)csc_eid[k], (uint32_t)hd, p, inv_keep);
+      }
+      const float bg = alpha * dm * gscale;  // beta * gscale
+      const float dg = dm * gscale;
+      const int n = min(64, ce - base);
+      for (int q0 = 0; q0 < n; q0 += G::EPW * G::U) {
+        float4 g[G::U];
+        float part[G::U];
+#pragma unroll
+        for (int u = 0; u < G::U; ++u) {
+          const int q = q0 + u * G::EPW + sg;
+          const int iq = __shfl(i, q);
+          g[u] = q < n ? ld4(grad_out + (int64_t)iq * C + sl * 4) : f4(0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < G::U; ++u) {
+          const int q = q0 + u * G::EPW + sg;
+          acc = fma4(__shfl(bg, q), g[u], acc);
+          part[u] = dot4(g[u], hv);
+        }
+#pragma unroll
+        for (int off = G::LPR / 2; off > 0; off >>= 1) {
+#pragma unroll
+          for (int u = 0; u < G::U; ++u) part[u] += __shfl_xor(part[u], off);
+        }
+#pragma unroll
+        for (int u = 0; u < G::U; ++u) {
+          const int q = q0 + u * G::EPW + sg;
+          const float aq = __shfl(alpha, q), Dq = __shfl(Dv, q), fq = __shfl(f, q), dq = __shfl(dg, q);
+          const float dzv = aq * fmaf(dq, part[u], -Dq) * fq;
+          if (sl == 0 && q < n) {
+            ds += dzv;
+            dz[(int64_t)csc2csr[base + q] * heads + hd] = dzv;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int off = G::LPR; off < 64; off <<= 1) acc = add4(acc, shfl_xor4(acc, off));
+    ds = wave_sum(ds);
+    if (sg == 0) st4(dh + (j * heads + hd) * C + sl * 4, acc);
+    if (lane == 0) ds_src[j * heads + hd] = ds;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward node epilogue (grid-stride, fixed partition => deterministic):
+//   ds_dst_i = sum_{k in CSR(i)} dz_k            (ordered segment sum)
+//   dh_i    += ds_src_i att_src + ds_dst_i att_dst
+//   partial datt_src += ds_src_i h_i, datt_dst += ds_dst_i h_i   (per wave)
+// partial layout [waves, 2, H, C]; heads <= kMaxHeads.
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ rowptr, int64_t n_nodes, int heads,
+                                                 const float* __restrict__ h, const float* __restrict__ att_src,
+                                                 const float* __restrict__ att_dst,
+                                                 const float* __restrict__ ds_src, const float* __restrict__ dz,
+                                                 float* __restrict__ dh, float* __restrict__ partial) {
+  using G = Geo<C>;
+  const int lane = threadIdx.x & 63;
+  const int sg = lane / G::LPR, sl = lane % G::LPR;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  float4 pa_s[kMaxHeads], pa_d[kMaxHeads];
+#pragma unroll
+  for (int hd = 0; hd < kMaxHeads; ++hd) { pa_s[hd] = f4(0.f); pa_d[hd] = f4(0.f); }
+  for (int64_t base = wave * G::EPW; base < n_nodes; base += n_waves * G::EPW) {
+    const int64_t i = base + sg;
+    const bool valid = i < n_nodes;
+    int rs = 0, re = 0;
+    if (valid) { rs = rowptr[i]; re = rowptr[i + 1]; }
+#pragma unroll
+    for (int hd = 0; hd < kMaxHeads; ++hd) {
+      if (hd >= heads) break;
+      float x = 0.f;
+      for (int k = rs + sl; k < re; k += G::LPR) x += dz[(int64_t)k * heads + hd];
+#pragma unroll
+      for (int off = G::LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+      if (valid) {
+        const int64_t pr = i * heads + hd;
+        const float dsd = x, dss = ds_src[pr];
+        const float4 hv = ld4(h + pr * C + sl * 4);
+        float4 d = ld4(dh + pr * C + sl * 4);
+        d = fma4(dss, ld4(att_src + hd * C + sl * 4), d);
+        d = fma4(dsd, ld4(att_dst + hd * C + sl * 4), d);
+        st4(dh + pr * C + sl * 4, d);
+        pa_s[hd] = fma4(dss, hv, pa_s[hd]);
+        pa_d[hd] = fma4(dsd, hv, pa_d[hd]);
+      }
+    }
+  }
+#pragma unroll
+  for (int hd = 0; hd < kMaxHeads; ++hd) {
+    if (hd >= heads) break;
+    float4 a = pa_s[hd], b = pa_d[hd];
+#pragma unroll
+    for (int off = G::LPR; off < 64; off <<= 1) {
+      a = add4(a, shfl_xor4(a, off));
+      b = add4(b, shfl_xor4(b, off));
+    }
+    if (sg == 0) {
+      st4(partial + ((wave * 2 + 0) * heads + hd) * C + sl * 4, a);
+      st4(partial + ((wave * 2 + 1) * heads + hd) * C + sl * 4, b);
+    }
+  }
+}
+
+// Final ordered reduction of the per-wave partials: out[2, H*C].
+__global__ void __launch_bounds__(256) k_bwd_red(const float* __restrict__ partial, int64_t n_waves, int hc,
+                                                 float* __restrict__ datt_src, float* __restrict__ datt_dst) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * hc) return;
+  const int which = t / hc, c = t % hc;
+  float s = 0.f;
+  for (int64_t w = 0; w < n_waves; ++w) s += partial[(w * 2 + which) * hc + c];
+  (which == 0 ? datt_src : datt_dst)[c] = s;
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (called from ppgat_abi.cpp)
+// ---------------------------------------------------------------------------
+#define PPGAT_DISPATCH_C(C_, ...)                      \
+  switch (C_) {                                        \
+    case 4: { constexpr int CC = 4; __VA_ARGS__; break; }     \
+    case 8: { constexpr int CC = 8; __VA_ARGS__; break; }     \
+    case 16: { constexpr int CC = 16; __VA_ARGS__; break; }   \
+    case 32: { constexpr int CC = 32; __VA_ARGS__; break; }   \
+    case 64: { constexpr int CC = 64; __VA_ARGS__; break; }   \
+    case 128: { constexpr int CC = 128; __VA_ARGS__; break; } \
+    case 256: { constexpr int CC = 256; __VA_ARGS__; break; } \
+    default: return hipErrorInvalidValue;              \
+  }
+
+static inline unsigned blocks_for(int64_t threads) { return (unsigned)((threads + 255) / 256); }
+
+hipError_t launch_scores(const float* h, const float* as, const float* ad, int64_t n, int heads, int C, float* ss,
+                         float* sd, hipStream_t st) {
+  const int64_t pairs = n * heads;
+  if (pairs == 0) return hipSuccess;
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_scores<CC>, dim3(blocks_for(pairs * (CC / 4))), dim3(256), 0, st, h, as,
+                                         ad, pairs, heads, ss, sd));
+  return hipGetLastError();
+}
+
+hipError_t launch_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* eid, int64_t n, int heads, int C,
+                      const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
+                      float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
+                      hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd<CC>, dim3(blocks_for(n * 64)), dim3(256), 0, st, rowptr, col, eid, n,
+                                         heads, h, ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m, invl,
+                                         agg));
+  return hipGetLastError();
+}
+
+hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, int64_t n,
+                          int heads, int C, float gscale, float* D, hipStream_t st) {
+  const int64_t pairs = n * heads;
+  if (pairs == 0) return hipSuccess;
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_pro<CC>, dim3(blocks_for(pairs * (CC / 4))), dim3(256), 0, st, go,
+                                         out, agg, bias, pairs, heads, gscale, D));
+  return hipGetLastError();
+}
+
+hipError_t launch_bwd_src(const int32_t* colptr, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                          int64_t n, int heads, int C, const float* h, const float* ss, const float* sd,
+                          const float* m, const float* invl, const float* D, const float* go, int mode, float slope,
+                          float gscale, float p, uint64_t seed, float* dh, float* ds_src, float* dz,
+                          hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(n * 64)), dim3(256), 0, st, colptr, row,
+                                         csc_eid, csc2csr, n, heads, h, ss, sd, m, invl, D, go, mode, slope, gscale,
+                                         p, inv_keep, seed, dh, ds_src, dz));
+  return hipGetLastError();
+}
+
+int64_t epi_waves(int64_t n) {
+  // fixed partition: enough waves to fill the chip several times over, capped so the
+  // partial buffer stays small (kEpiMaxWaves x 2 x H x C floats)
+  int64_t w = (n + 7) / 8;
+  if (w < 1) w = 1;
+  if (w > kEpiMaxWaves) w = kEpiMaxWaves;
+  return (w + 3) / 4 * 4;  // whole 256-thread blocks
+}
+
+hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
+                          const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,
+                          int64_t waves, hipStream_t st) {
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_epi<CC>, dim3((unsigned)(waves / 4)), dim3(256), 0, st, rowptr, n,
+                                         heads, h, as, ad, ds_src, dz, dh, partial));
+  return hipGetLastError();
+}
+
+hipError_t launch_bwd_red(const float* partial, int64_t waves, int hc, float* das, float* dad, hipStream_t st) {
+  hipLaunchKernelGGL(k_bwd_red, dim3(blocks_for(2 * hc)), dim3(256), 0, st, partial, waves, hc, das, dad);
+  return hipGetLastError();
+}
+
+}  // namespace ppgat

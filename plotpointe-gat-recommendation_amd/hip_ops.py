@@ -1,0 +1,220 @@
+"""Torch-facing wrappers over the C ABI (include/ppgat.h).
+
+PyTorch is plumbing here: it owns device memory (caching allocator), the current
+HIP stream and autograd.  All message-passing arithmetic runs in libppgat.so.
+Every function raises if the library is absent or a tensor is not a contiguous
+fp32/int64 ROCm tensor of the expected shape -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+
+def _require(cond: bool, msg: str):
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _check_dev(name: str, t: torch.Tensor, dtype, device=None):
+    _require(isinstance(t, torch.Tensor), f"{name}: expected a tensor")
+    _require(t.is_cuda, f"{name}: ppgat runs on ROCm devices only (got {t.device}); there is no CPU path")
+    _require(t.dtype == dtype, f"{name}: expected {dtype}, got {t.dtype}")
+    _require(t.is_contiguous(), f"{name}: must be contiguous")
+    if device is not None:
+        _require(t.device == device, f"{name}: on {t.device}, expected {device}")
+
+
+# ---------------------------------------------------------------------------
+# graph preprocessing
+# ---------------------------------------------------------------------------
+@dataclass
+class CSRGraph:
+    """Static CSR-by-dst / CSC-by-src view of a COO edge_index (int32 indices)."""
+    n_nodes: int
+    n_edges: int
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    csr_eid: torch.Tensor
+    colptr: torch.Tensor
+    row: torch.Tensor
+    csc_eid: torch.Tensor
+    csc2csr: torch.Tensor
+
+    @property
+    def device(self):
+        return self.rowptr.device
+
+    def in_degree(self) -> torch.Tensor:
+        return (self.rowptr[1:] - self.rowptr[:-1])
+
+    def out_degree(self) -> torch.Tensor:
+        return (self.colptr[1:] - self.colptr[:-1])
+
+
+def csr_build(edge_index: torch.Tensor, n_nodes: int) -> CSRGraph:
+    """edge_index LongTensor[2,E] (row 0 src, row 1 dst) -> CSRGraph on the same device.
+
+    One host sync (the out-of-range index count), once per static graph.
+    """
+    lib = _lib.load()
+    _require(edge_index.dim() == 2 and edge_index.size(0) == 2, "edge_index must be [2, E]")
+    ei = edge_index.contiguous()
+    _check_dev("edge_index", ei, torch.int64)
+    dev = ei.device
+    E = int(ei.size(1))
+    N = int(n_nodes)
+    i32 = dict(dtype=torch.int32, device=dev)
+    rowptr = torch.empty(N + 1, **i32)
+    colptr = torch.empty(N + 1, **i32)
+    col = torch.empty(max(E, 1), **i32)
+    csr_eid = torch.empty(max(E, 1), **i32)
+    row = torch.empty(max(E, 1), **i32)
+    csc_eid = torch.empty(max(E, 1), **i32)
+    csc2csr = torch.empty(max(E, 1), **i32)
+    bad = torch.empty(1, **i32)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_csr_workspace_bytes(N, E, ctypes.byref(nbytes)), "csr_workspace_bytes")
+    ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(lib.ppgat_csr_build(ei.data_ptr(), E, N, rowptr.data_ptr(), col.data_ptr(), csr_eid.data_ptr(),
+                                       colptr.data_ptr(), row.data_ptr(), csc_eid.data_ptr(), csc2csr.data_ptr(),
+                                       bad.data_ptr(), ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)),
+                   "csr_build")
+    nbad = int(bad.item())
+    if nbad:
+        raise RuntimeError(f"edge_index has {nbad} entries outside [0, {N})")
+    return CSRGraph(N, E, rowptr, col[:E], csr_eid[:E], colptr, row[:E], csc_eid[:E], csc2csr[:E])
+
+
+class _GraphCache:
+    """Static-graph cache keyed on (data_ptr, _version, N, device); holds the key tensor."""
+
+    def __init__(self, capacity: int = 8):
+        self.capacity = capacity
+        self.entries = []  # list of (key, edge_index ref, graph)
+
+    def get(self, edge_index: torch.Tensor, n_nodes: int) -> CSRGraph:
+        key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape), int(n_nodes),
+               str(edge_index.device))
+        for k, ref, g in self.entries:
+            if k == key and ref is edge_index:
+                return g
+        g = csr_build(edge_index, n_nodes)
+        self.entries.append((key, edge_index, g))
+        if len(self.entries) > self.capacity:
+            self.entries.pop(0)
+        return g
+
+    def clear(self):
+        self.entries.clear()
+
+
+graph_cache = _GraphCache()
+
+
+# ---------------------------------------------------------------------------
+# node scores / fused forward / fused backward
+# ---------------------------------------------------------------------------
+def node_scores(h: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, heads: int, channels: int):
+    lib = _lib.load()
+    N = h.size(0)
+    _check_dev("h", h, torch.float32)
+    _check_dev("att_src", att_src, torch.float32, h.device)
+    _check_dev("att_dst", att_dst, torch.float32, h.device)
+    _require(h.numel() == N * heads * channels, "h must be [N, heads*channels]")
+    _require(att_src.numel() == heads * channels and att_dst.numel() == heads * channels, "att must be [H, C]")
+    s_src = torch.empty(N, heads, dtype=torch.float32, device=h.device)
+    s_dst = torch.empty(N, heads, dtype=torch.float32, device=h.device)
+    _lib.check(lib.ppgat_node_scores(h.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), N, heads, channels,
+                                     s_src.data_ptr(), s_dst.data_ptr(), _lib.stream_handle(h.device)),
+               "node_scores")
+    return s_src, s_dst
+
+
+def gat_fwd(g: CSRGraph, h, s_src, s_dst, bias, heads: int, channels: int, mode: int, slope: float,
+            dropout_p: float, seed: int, want_agg: bool):
+    lib = _lib.load()
+    N = g.n_nodes
+    dev = h.device
+    _require(h.size(0) == N, f"x has {h.size(0)} rows but the graph has {N} nodes")
+    out = torch.empty(N, channels, dtype=torch.float32, device=dev)
+    m = torch.empty(N, heads, dtype=torch.float32, device=dev)
+    inv_l = torch.empty(N, heads, dtype=torch.float32, device=dev)
+    agg = torch.empty(N, heads, channels, dtype=torch.float32, device=dev) if want_agg else None
+    _lib.check(lib.ppgat_fwd(g.rowptr.data_ptr(), _lib.ptr(g.col) if g.n_edges else None,
+                             _lib.ptr(g.csr_eid) if g.n_edges else None, N, g.n_edges, heads, channels,
+                             h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), _lib.ptr(bias), mode, float(slope),
+                             float(dropout_p), int(seed) & (2**64 - 1), out.data_ptr(), m.data_ptr(),
+                             inv_l.data_ptr(), _lib.ptr(agg), _lib.stream_handle(dev)), "gat_fwd")
+    return out, m, inv_l, agg
+
+
+def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, inv_l, grad_out, heads: int,
+            channels: int, mode: int, slope: float, dropout_p: float, seed: int):
+    lib = _lib.load()
+    N = g.n_nodes
+    dev = h.device
+    _check_dev("grad_out", grad_out, torch.float32, dev)
+    grad_h = torch.empty(N, heads * channels, dtype=torch.float32, device=dev)
+    datt_src = torch.empty(heads, channels, dtype=torch.float32, device=dev)
+    datt_dst = torch.empty(heads, channels, dtype=torch.float32, device=dev)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_bwd_workspace_bytes(N, g.n_edges, heads, channels, ctypes.byref(nbytes)),
+               "bwd_workspace_bytes")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    E = g.n_edges
+    _lib.check(lib.ppgat_bwd(g.rowptr.data_ptr(), g.colptr.data_ptr(), _lib.ptr(g.row) if E else None,
+                             _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, N, E, heads,
+                             channels, h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), att_src.data_ptr(),
+                             att_dst.data_ptr(), _lib.ptr(bias), out.data_ptr(), _lib.ptr(agg), m.data_ptr(),
+                             inv_l.data_ptr(), grad_out.data_ptr(), mode, float(slope), float(dropout_p),
+                             int(seed) & (2**64 - 1), grad_h.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(),
+                             ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "gat_bwd")
+    return grad_h, datt_src, datt_dst
+
+
+class GATAggregate(torch.autograd.Function):
+    """h [N, H*C] -> out [N, C]: node scores + fused softmax-aggregate (fwd) and the
+    atomic-free backward.  The projection ``h = lin(x)`` stays outside, in autograd."""
+
+    @staticmethod
+    def forward(ctx, h, att_src, att_dst, bias, graph: CSRGraph, heads: int, channels: int, mode: int,
+                slope: float, dropout_p: float, seed: int):
+        h = h.contiguous()
+        att_src_c = att_src.detach().contiguous().view(heads, channels)
+        att_dst_c = att_dst.detach().contiguous().view(heads, channels)
+        bias_c = bias.detach().contiguous() if bias is not None else None
+        s_src, s_dst = node_scores(h, att_src_c, att_dst_c, heads, channels)
+        need_grad = any(ctx.needs_input_grad[:4])
+        out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, bias_c, heads, channels, mode, slope, dropout_p, seed,
+                                     want_agg=need_grad and heads > 1)
+        if need_grad:
+            ctx.save_for_backward(h, att_src_c, att_dst_c, s_src, s_dst, out, m, inv_l,
+                                  agg if agg is not None else torch.empty(0, device=h.device),
+                                  bias_c if bias_c is not None else torch.empty(0, device=h.device))
+        ctx.graph = graph
+        ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None)
+        ctx.att_shapes = (att_src.shape, att_dst.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        h, att_src, att_dst, s_src, s_dst, out, m, inv_l, agg, bias = ctx.saved_tensors
+        heads, channels, mode, slope, p, seed, has_bias, has_agg = ctx.meta
+        grad_out = grad_out.contiguous()
+        grad_h, datt_src, datt_dst = gat_bwd(ctx.graph, h, s_src, s_dst, att_src, att_dst,
+                                             bias if has_bias else None, out, agg if has_agg else None, m, inv_l,
+                                             grad_out, heads, channels, mode, slope, p, seed)
+        dbias = grad_out.sum(0) if (has_bias and ctx.needs_input_grad[3]) else None
+        return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None, None)
+
+
+def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p=0.0, seed=0):
+    return GATAggregate.apply(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)

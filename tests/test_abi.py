@@ -1,0 +1,71 @@
+"""The C-ABI library loads and exports every symbol include/ppgat.h declares; argument
+validation works without a GPU (no compute calls here) -- CPU."""
+import ctypes
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    text = (ROOT / "include" / "ppgat.h").read_text()
+    return sorted(set(re.findall(r"\b(ppgat_[a-z_]+)\s*\(", text)))
+
+
+def test_all_header_symbols_exported(pkg):
+    lib = pkg._lib.load()
+    names = _declared()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(pkg._lib.SIGNATURES)
+
+
+def test_version_and_channels(pkg):
+    lib = pkg._lib.load()
+    assert lib.ppgat_version() == 1
+    assert [c for c in range(1, 300) if lib.ppgat_supported_channels(c)] == [4, 8, 16, 32, 64, 128, 256]
+
+
+def test_invalid_arguments_return_codes(pkg):
+    lib = pkg._lib.load()
+    # unsupported channel count -> PPGAT_ERR_UNSUPPORTED before any device work
+    rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 96, None, None, None, None, 0, 0.2, 0.0, 0,
+                       None, None, None, None, None)
+    assert rc == 2 and b"channels" in lib.ppgat_last_error()
+    # custom mode with a bias -> invalid
+    rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, ctypes.c_void_p(16), 1, 0.2, 0.0, 0,
+                       None, None, None, None, None)
+    assert rc == 1 and b"custom" in lib.ppgat_last_error()
+    # dropout out of range
+    rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 1.0, 0,
+                       None, None, None, None, None)
+    assert rc == 1
+    with pytest.raises(NotImplementedError):
+        pkg._lib.check(2, "x")
+
+
+def test_bwd_workspace_size_is_host_only(pkg):
+    lib = pkg._lib.load()
+    n = ctypes.c_size_t(0)
+    assert lib.ppgat_bwd_workspace_bytes(1000, 5000, 1, 128, ctypes.byref(n)) == 0
+    assert n.value >= (2 * 1000 + 5000) * 4
+
+
+def test_product_path_refuses_cpu_tensors(pkg):
+    import torch
+    conv = pkg.GATConv(8, 8, heads=1, concat=False, add_self_loops=False)
+    x = torch.randn(5, 8)
+    ei = torch.tensor([[0, 1], [1, 2]])
+    with pytest.raises(RuntimeError, match="ROCm"):
+        conv(x, ei)
+
+
+def test_unsupported_configs_raise(pkg):
+    with pytest.raises(NotImplementedError):
+        pkg.GATConv(8, 8, heads=1, concat=True, add_self_loops=False)
+    with pytest.raises(NotImplementedError):
+        pkg.GATConv(8, 8, heads=1, concat=False, add_self_loops=True)
+    with pytest.raises(NotImplementedError):
+        pkg.GATConv(8, 96, heads=1, concat=False, add_self_loops=False)

@@ -1,0 +1,95 @@
+"""The CPU oracle, pinned against the real reference (tests/golden, made by importing
+scripts/train_gat_custom.py) -- CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+CASES = ["small_c8", "uniform_c128", "skewed_c128", "clamp_c128"]
+
+
+def _load(name):
+    return dict(np.load(GOLDEN / f"layer_{name}.npz"))
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_custom_oracle_matches_reference_golden(oracle, name):
+    g = _load(name)
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    W = torch.from_numpy(g["lin_weight"]).requires_grad_(True)
+    a_s = torch.from_numpy(g["a_src"]).requires_grad_(True)
+    a_d = torch.from_numpy(g["a_dst"]).requires_grad_(True)
+    out = oracle.custom_gat_layer(x, torch.from_numpy(g["edge_index"]), W, a_s, a_d)
+    (out * torch.from_numpy(g["G"])).sum().backward()
+    # same op order as the reference on the same CPU -> (near) bitwise
+    assert _rel(out.detach(), g["out"]) <= 1e-6
+    assert _rel(x.grad, g["dx"]) <= 1e-5
+    assert _rel(W.grad, g["dW"]) <= 1e-5
+    assert _rel(a_s.grad, g["da_src"]) <= 1e-5
+    assert _rel(a_d.grad, g["da_dst"]) <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["small_c8", "uniform_c128", "skewed_c128"])
+def test_pyg_restatement_equals_reference_custom_layer(oracle, name):
+    """PyG GATConv restatement == imported custom reference when H=1, bias=0, |e|<10
+    (SURVEY.md 8(c) partial pin), forward and all gradients, fp64."""
+    g = _load(name)
+    assert float(g["emax"]) < 10.0
+    d = torch.float64
+    x = torch.from_numpy(g["x"]).to(d).requires_grad_(True)
+    W = torch.from_numpy(g["lin_weight"]).to(d).requires_grad_(True)
+    a_s = torch.from_numpy(g["a_src"]).to(d).requires_grad_(True)
+    a_d = torch.from_numpy(g["a_dst"]).to(d).requires_grad_(True)
+    ei = torch.from_numpy(g["edge_index"])
+    Gt = torch.from_numpy(g["G"]).to(d)
+    out = oracle.pyg_gat_conv(x, ei, W, a_s.view(1, 1, -1), a_d.view(1, 1, -1), None, heads=1)
+    (out * Gt).sum().backward()
+    grads = [t.grad.clone() for t in (x, W, a_s, a_d)]
+    for t in (x, W, a_s, a_d):
+        t.grad = None
+    ref = oracle.custom_gat_layer(x, ei, W, a_s, a_d)
+    (ref * Gt).sum().backward()
+    # the only difference is the softmax eps (custom 1e-9 vs PyG 1e-16): ~1e-9 relative
+    assert _rel(out.detach(), ref.detach()) <= 1e-8
+    for a, t in zip(grads, (x, W, a_s, a_d)):
+        assert _rel(a, t.grad) <= 1e-7
+    # and against the fp32 reference output itself
+    assert _rel(out.detach(), g["out"]) <= 1e-5
+
+
+def test_dropout_mask_properties(oracle):
+    eid = np.arange(200_000)
+    m = oracle.dropout_scale(1234, eid, 0, 0.1)
+    keep = (m > 0).mean()
+    assert abs(keep - 0.9) < 0.005
+    assert np.allclose(m[m > 0], 1 / 0.9)
+    assert np.array_equal(m, oracle.dropout_scale(1234, eid, 0, 0.1))
+    assert not np.array_equal(m, oracle.dropout_scale(1234, eid, 1, 0.1))
+    assert not np.array_equal(m, oracle.dropout_scale(1235, eid, 0, 0.1))
+    assert np.all(oracle.dropout_scale(1, eid, 0, 0.0) == 1)
+
+
+def test_csr_oracle_simple(oracle):
+    ei = np.array([[0, 2, 1, 2, 0], [1, 1, 0, 2, 1]])
+    rowptr, col, eid, colptr, row, ceid, c2r = oracle.csr_from_edge_index(ei, 4)
+    assert rowptr.tolist() == [0, 1, 4, 5, 5]
+    assert eid.tolist() == [2, 0, 1, 4, 3]
+    assert col.tolist() == [1, 0, 2, 0, 2]
+    assert colptr.tolist() == [0, 2, 3, 5, 5]
+    assert ceid.tolist() == [0, 4, 2, 1, 3]
+    assert row.tolist() == [1, 1, 0, 1, 2]
+    assert all(eid[c2r[k]] == ceid[k] for k in range(5))
+
+
+def test_serving_topk_and_rank(oracle):
+    v = np.eye(10, dtype=np.float32)
+    idx, sc = oracle.serving_topk(v, [0, 1], 3)
+    assert 0 not in idx and 1 not in idx and len(idx) == 3
+    assert all(sc[i] >= sc[i + 1] for i in range(2))
+    assert oracle.sampled_rank(np.array([1.0, 2.0, 1.0, 0.5])) == 2

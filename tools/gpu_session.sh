@@ -1,0 +1,30 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, bench, rocprofv3 kernel stats.
+# Stops at the first step that does not end with 0 or 1 (a fault, abort, timeout...).
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$(pwd)
+export TMPDIR=/tmp
+OUT=$R/gpurun_out
+mkdir -p "$OUT"
+STEPS="${STEPS:-tests smoke bench prof}"
+BENCH_ARGS="${BENCH_ARGS:---steps 20 --warmup 5}"
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py $BENCH_ARGS ;;
+    prof)  (cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --steps 10 --warmup 3 --cpu-baseline-seconds 0) ;;
+  esac
+done
+echo "session done"
