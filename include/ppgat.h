@@ -68,6 +68,33 @@ int ppgat_csr_build(const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
                     int32_t* colptr, int32_t* row, int32_t* csc_eid, int32_t* csc2csr,
                     int32_t* bad_count, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- work schedule -------------------------------------------------------
+ * Cuts the rows of a CSR/CSC (ptr[N+1]) into work items of at most max_edges edges for
+ * the fused kernels: rows with deg > max_edges ("hubs") become ceil(deg/max_edges)
+ * pieces listed first (hubs in row order, pieces merged deterministically afterwards),
+ * then every other row as one item in descending-degree order (longest work first).
+ * Capacities: items <= ppgat_schedule_capacity(), hub_row <= N, hub_ptr <= N+1.
+ * counts (device int32[3]) receives {n_hubs, n_hub_items, n_items}; the caller reads it
+ * once (a one-time host sync per static graph) to fill a ppgat_schedule.
+ */
+typedef struct ppgat_schedule {
+  const int32_t* item_row;  /* [n_items] row (dst for CSR, src for CSC) */
+  const int32_t* item_beg;  /* [n_items] first edge slot */
+  const int32_t* item_end;  /* [n_items] one past the last edge slot */
+  int64_t n_items;
+  int64_t n_hub_items;      /* items [0, n_hub_items) are hub pieces */
+  const int32_t* hub_row;   /* [n_hubs] */
+  const int32_t* hub_ptr;   /* [n_hubs+1] piece (= item) ranges per hub */
+  int64_t n_hubs;
+} ppgat_schedule;
+
+int64_t ppgat_schedule_capacity(int64_t n_nodes, int64_t n_edges, int32_t max_edges);
+int ppgat_schedule_workspace_bytes(int64_t n_nodes, size_t* bytes);
+int ppgat_schedule_build(const int32_t* ptr, int64_t n_nodes, int64_t n_edges, int32_t max_edges,
+                         int32_t* item_row, int32_t* item_beg, int32_t* item_end,
+                         int32_t* hub_row, int32_t* hub_ptr, int32_t* counts,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- per-node attention terms -------------------------------------------
  * Replaces: PyG alpha_src = (x * att_src).sum(-1), alpha_dst likewise (GATConv.forward);
  *           custom (h[src]*a_src).sum(-1) / (h[dst]*a_dst).sum(-1) (train_gat_custom.py:79),
@@ -78,29 +105,34 @@ int ppgat_node_scores(const float* h, const float* att_src, const float* att_dst
                       int64_t n_nodes, int heads, int channels,
                       float* s_src, float* s_dst, void* stream);
 
-/* ---- fused forward (one kernel) ----------------------------------------
+/* ---- fused forward -------------------------------------------------------
  * Replaces: GATConv edge_update + softmax + dropout + propagate/SumAggregation + head mean + bias
  *           (train_gat_pyg.py:77,87 -> PyG), and train_gat_custom.py:78-93.
- * Writes out [N,C], per-(node,head) softmax state m [N,H] and inv_l = 1/(l+eps) [N,H]
- * (saved for the backward), and agg [N,H,C] (per-head aggregate) when agg != NULL
- * (required for heads > 1 training).
+ * dst_sched: schedule over the CSR by destination (rowptr).  Writes out [N,C], the
+ * per-(node,head) softmax state m [N,H] and inv_l = 1/(l+eps) [N,H] (saved for the
+ * backward), and agg [N,H,C] (per-head aggregate) when agg != NULL (required for heads > 1
+ * training).  workspace: hub-piece partials, ppgat_fwd_workspace_bytes().
  */
-int ppgat_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* csr_eid,
+int ppgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int channels, size_t* bytes);
+int ppgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid,
               int64_t n_nodes, int64_t n_edges, int heads, int channels,
               const float* h, const float* s_src, const float* s_dst, const float* bias,
               int mode, float negative_slope, float dropout_p, uint64_t seed,
-              float* out, float* m, float* inv_l, float* agg, void* stream);
+              float* out, float* m, float* inv_l, float* agg,
+              void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- fused backward ------------------------------------------------------
  * Replaces: autograd of the ops above (index_put_ accumulate, mul backward, scatter
  *           backward; 34%+25%+11.5% of the reference CPU step).
- * Given grad_out [N,C] returns grad_h [N,H,C] (message term plus the attention-logit
- * terms ds_src (x) att_src + ds_dst (x) att_dst), grad_att_src/grad_att_dst [H,C].
- * Atomic-free and deterministic (segment-owned sums in a fixed order).
- * agg may be NULL when heads == 1 (out - bias is used).
+ * src_sched: schedule over the CSC by source (colptr).  Given grad_out [N,C] returns
+ * grad_h [N,H,C] (message term plus the attention-logit terms ds_src (x) att_src +
+ * ds_dst (x) att_dst) and grad_att_src/grad_att_dst [H,C].  Atomic-free and
+ * deterministic (segment-owned sums in a fixed order).  agg may be NULL when heads == 1
+ * (out - bias is used).
  */
-int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int heads, int channels, size_t* bytes);
-int ppgat_bwd(const int32_t* rowptr, const int32_t* colptr, const int32_t* row,
+int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int64_t n_hub_items, int heads, int channels,
+                              size_t* bytes);
+int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int32_t* row,
               const int32_t* csc_eid, const int32_t* csc2csr,
               int64_t n_nodes, int64_t n_edges, int heads, int channels,
               const float* h, const float* s_src, const float* s_dst,
@@ -119,7 +151,8 @@ int ppgat_bwd(const int32_t* rowptr, const int32_t* colptr, const int32_t* row,
 #define PPGAT_K_BWD_SRC 4
 #define PPGAT_K_BWD_EPI 5
 #define PPGAT_K_BWD_RED 6
-#define PPGAT_K_COUNT 7
+#define PPGAT_K_SCHED 7
+#define PPGAT_K_COUNT 8
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

@@ -16,6 +16,16 @@ LIB_PATH = Path(os.environ.get("PPGAT_LIB", _HERE / "libppgat.so"))
 c_int, c_i64, c_u64, c_f, c_vp, c_sz = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_size_t)
 
+
+
+class Schedule(ctypes.Structure):
+    """include/ppgat.h ppgat_schedule"""
+    _fields_ = [("item_row", c_vp), ("item_beg", c_vp), ("item_end", c_vp), ("n_items", c_i64),
+                ("n_hub_items", c_i64), ("hub_row", c_vp), ("hub_ptr", c_vp), ("n_hubs", c_i64)]
+
+
+SP = ctypes.POINTER(Schedule)
+
 # name -> (restype, argtypes); mirrors include/ppgat.h
 SIGNATURES = {
     "ppgat_version": (c_int, []),
@@ -24,11 +34,16 @@ SIGNATURES = {
     "ppgat_csr_workspace_bytes": (c_int, [c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "ppgat_csr_build": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
                                 c_vp]),
+    "ppgat_schedule_capacity": (c_i64, [c_i64, c_i64, ctypes.c_int32]),
+    "ppgat_schedule_workspace_bytes": (c_int, [c_i64, ctypes.POINTER(c_sz)]),
+    "ppgat_schedule_build": (c_int, [c_vp, c_i64, c_i64, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_sz, c_vp]),
     "ppgat_node_scores": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp]),
-    "ppgat_fwd": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
-                          c_u64, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "ppgat_bwd_workspace_bytes": (c_int, [c_i64, c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
-    "ppgat_bwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+    "ppgat_fwd_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_fwd": (c_int, [SP, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
+                          c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_bwd_workspace_bytes": (c_int, [c_i64, c_i64, c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_bwd": (c_int, [SP, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_sz,
                           c_vp]),
     "ppgat_profile_enable": (c_int, [c_int]),
@@ -36,7 +51,7 @@ SIGNATURES = {
     "ppgat_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
 }
 
-KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6}
+KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6, "sched": 7}
 MODE_PYG, MODE_CUSTOM = 0, 1
 
 _lib = None

@@ -120,6 +120,46 @@ int ppgat_csr_build(const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
   return PPGAT_OK;
 }
 
+int64_t ppgat_schedule_capacity(int64_t n_nodes, int64_t n_edges, int32_t max_edges) {
+  if (n_nodes < 0 || n_edges < 0 || max_edges < 1) return -1;
+  return ppgat::schedule_capacity(n_nodes, n_edges, max_edges);
+}
+
+int ppgat_schedule_workspace_bytes(int64_t n_nodes, size_t* bytes) {
+  if (!bytes || n_nodes < 0) return fail(PPGAT_ERR_INVALID, "schedule_workspace_bytes: bad arguments");
+  *bytes = ppgat::schedule_workspace_bytes(n_nodes);
+  return PPGAT_OK;
+}
+
+int ppgat_schedule_build(const int32_t* ptr, int64_t n_nodes, int64_t n_edges, int32_t max_edges, int32_t* item_row,
+                         int32_t* item_beg, int32_t* item_end, int32_t* hub_row, int32_t* hub_ptr, int32_t* counts,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  if (n_nodes < 0 || n_edges < 0 || max_edges < 1 || max_edges >= (1 << 20) - 2)
+    return fail(PPGAT_ERR_INVALID, "schedule_build: bad sizes (1 <= max_edges < 2^20-2)");
+  if (!ptr || !hub_ptr || !counts || (n_nodes > 0 && (!item_row || !item_beg || !item_end || !hub_row)))
+    return fail(PPGAT_ERR_INVALID, "schedule_build: null pointer");
+  if (!workspace || workspace_bytes < ppgat::schedule_workspace_bytes(n_nodes))
+    return fail(PPGAT_ERR_INVALID, "schedule_build: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_SCHED, st);
+  hipError_t e = ppgat::schedule_build(ptr, n_nodes, max_edges, item_row, item_beg, item_end, hub_row, hub_ptr,
+                                       counts, workspace, workspace_bytes, st);
+  if (e != hipSuccess) return hip_fail(e, "schedule_build");
+  return PPGAT_OK;
+}
+
+static int check_sched(const ppgat_schedule* s, int64_t n_nodes, const char* who) {
+  if (!s) return fail(PPGAT_ERR_INVALID, std::string(who) + ": null schedule");
+  if (s->n_items < 0 || s->n_hub_items < 0 || s->n_hubs < 0 || s->n_hub_items > s->n_items ||
+      s->n_items < n_nodes - s->n_hubs)
+    return fail(PPGAT_ERR_INVALID, std::string(who) + ": inconsistent schedule counts");
+  if (s->n_items > 0 && (!s->item_row || !s->item_beg || !s->item_end))
+    return fail(PPGAT_ERR_INVALID, std::string(who) + ": null schedule arrays");
+  if (s->n_hubs > 0 && (!s->hub_row || !s->hub_ptr))
+    return fail(PPGAT_ERR_INVALID, std::string(who) + ": null hub arrays");
+  return PPGAT_OK;
+}
+
 int ppgat_node_scores(const float* h, const float* att_src, const float* att_dst, int64_t n_nodes, int heads,
                       int channels, float* s_src, float* s_dst, void* stream) {
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "node_scores: unsupported channels");
@@ -142,38 +182,56 @@ static int check_mode(int mode, int heads, const float* bias, float p) {
   return PPGAT_OK;
 }
 
-int ppgat_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* csr_eid, int64_t n_nodes, int64_t n_edges,
-              int heads, int channels, const float* h, const float* s_src, const float* s_dst, const float* bias,
-              int mode, float negative_slope, float dropout_p, uint64_t seed, float* out, float* m, float* inv_l,
-              float* agg, void* stream) {
+static size_t partial_bytes(int64_t n_hub_items, int heads, int channels) {
+  return align_up((size_t)(n_hub_items > 0 ? n_hub_items : 1) * heads * (channels + 4) * 4);
+}
+
+int ppgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int channels, size_t* bytes) {
+  if (!bytes || n_hub_items < 0 || heads < 1 || channels < 1)
+    return fail(PPGAT_ERR_INVALID, "fwd_workspace_bytes: bad arguments");
+  *bytes = partial_bytes(n_hub_items, heads, channels);
+  return PPGAT_OK;
+}
+
+int ppgat_fwd(const ppgat_schedule* sched, const int32_t* col, const int32_t* csr_eid, int64_t n_nodes,
+              int64_t n_edges, int heads, int channels, const float* h, const float* s_src, const float* s_dst,
+              const float* bias, int mode, float negative_slope, float dropout_p, uint64_t seed, float* out, float* m,
+              float* inv_l, float* agg, void* workspace, size_t workspace_bytes, void* stream) {
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "fwd: unsupported channels");
   if (heads < 1 || n_nodes < 0 || n_edges < 0) return fail(PPGAT_ERR_INVALID, "fwd: bad sizes");
   if (int rc = check_mode(mode, heads, bias, dropout_p)) return rc;
-  if (n_nodes > 0 && (!rowptr || !h || !s_src || !s_dst || !out || !m || !inv_l))
+  if (int rc = check_sched(sched, n_nodes, "fwd")) return rc;
+  if (n_nodes > 0 && (!h || !s_src || !s_dst || !out || !m || !inv_l))
     return fail(PPGAT_ERR_INVALID, "fwd: null pointer");
   if (n_edges > 0 && !col) return fail(PPGAT_ERR_INVALID, "fwd: null col");
   if (dropout_p > 0.f && n_edges > 0 && !csr_eid) return fail(PPGAT_ERR_INVALID, "fwd: dropout needs csr_eid");
+  if (sched->n_hub_items > 0 && (!workspace || workspace_bytes < partial_bytes(sched->n_hub_items, heads, channels)))
+    return fail(PPGAT_ERR_INVALID, "fwd: workspace too small");
   const float eps = mode == PPGAT_MODE_PYG ? 1e-16f : 1e-9f;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{sched->item_row, sched->item_beg, sched->item_end, sched->n_items, sched->n_hub_items};
   Timed t(PPGAT_K_FWD, st);
-  hipError_t e = ppgat::launch_fwd(rowptr, col, csr_eid, n_nodes, heads, channels, h, s_src, s_dst, bias, mode,
-                                   negative_slope, eps, dropout_p, seed, out, m, inv_l, agg, st);
+  hipError_t e = ppgat::launch_fwd(it, col, csr_eid, heads, channels, h, s_src, s_dst, bias, mode, negative_slope,
+                                   eps, dropout_p, seed, out, m, inv_l, agg, static_cast<float*>(workspace),
+                                   sched->hub_row, sched->hub_ptr, sched->n_hubs, st);
   if (e != hipSuccess) return hip_fail(e, "fwd");
   return PPGAT_OK;
 }
 
-// workspace: D [N*H] | ds_src [N*H] | dz [E*H] | partial [waves*2*H*C]
-int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int heads, int channels, size_t* bytes) {
-  if (!bytes || n_nodes < 0 || n_edges < 0 || heads < 1 || channels < 1)
+// workspace: nstate [N*H float4] | ds_src [N*H] | dz [E*H] | block partial [blocks*2*H*C] | hub partial
+int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int64_t n_hub_items, int heads, int channels,
+                              size_t* bytes) {
+  if (!bytes || n_nodes < 0 || n_edges < 0 || n_hub_items < 0 || heads < 1 || channels < 1)
     return fail(PPGAT_ERR_INVALID, "bwd_workspace_bytes: bad arguments");
+  const size_t ns = align_up((size_t)n_nodes * heads * 16 + 16);
   const size_t nh = align_up((size_t)n_nodes * heads * 4 + 4);
   const size_t eh = align_up((size_t)n_edges * heads * 4 + 4);
-  const size_t part = align_up((size_t)ppgat::epi_waves(n_nodes) * 2 * heads * channels * 4);
-  *bytes = 2 * nh + eh + part;
+  const size_t part = align_up((size_t)ppgat::epi_blocks(n_nodes) * 2 * heads * channels * 4);
+  *bytes = ns + nh + eh + part + partial_bytes(n_hub_items, heads, channels);
   return PPGAT_OK;
 }
 
-int ppgat_bwd(const int32_t* rowptr, const int32_t* colptr, const int32_t* row, const int32_t* csc_eid,
+int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t* row, const int32_t* csc_eid,
               const int32_t* csc2csr, int64_t n_nodes, int64_t n_edges, int heads, int channels, const float* h,
               const float* s_src, const float* s_dst, const float* att_src, const float* att_dst, const float* bias,
               const float* out, const float* agg, const float* m, const float* inv_l, const float* grad_out, int mode,
@@ -182,48 +240,54 @@ int ppgat_bwd(const int32_t* rowptr, const int32_t* colptr, const int32_t* row, 
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd: unsupported channels");
   if (heads < 1 || n_nodes < 0 || n_edges < 0) return fail(PPGAT_ERR_INVALID, "bwd: bad sizes");
   if (int rc = check_mode(mode, heads, bias, dropout_p)) return rc;
+  if (int rc = check_sched(sched, n_nodes, "bwd")) return rc;
   if (heads > 1 && agg == nullptr) return fail(PPGAT_ERR_INVALID, "bwd: heads > 1 needs the saved agg");
   if (!grad_att_src || !grad_att_dst || !att_src || !att_dst)
     return fail(PPGAT_ERR_INVALID, "bwd: null attention pointer");
-  if (n_nodes > 0 && (!rowptr || !colptr || !h || !s_src || !s_dst || !out || !m || !inv_l || !grad_out || !grad_h))
+  if (n_nodes > 0 && (!rowptr || !h || !s_src || !s_dst || !out || !m || !inv_l || !grad_out || !grad_h))
     return fail(PPGAT_ERR_INVALID, "bwd: null pointer");
   if (n_edges > 0 && (!row || !csc2csr)) return fail(PPGAT_ERR_INVALID, "bwd: null CSC pointer");
   if (dropout_p > 0.f && n_edges > 0 && !csc_eid) return fail(PPGAT_ERR_INVALID, "bwd: dropout needs csc_eid");
   size_t need = 0;
-  ppgat_bwd_workspace_bytes(n_nodes, n_edges, heads, channels, &need);
+  ppgat_bwd_workspace_bytes(n_nodes, n_edges, sched->n_hub_items, heads, channels, &need);
   if (!workspace || workspace_bytes < need) return fail(PPGAT_ERR_INVALID, "bwd: workspace too small");
+  const size_t ns = align_up((size_t)n_nodes * heads * 16 + 16);
   const size_t nh = align_up((size_t)n_nodes * heads * 4 + 4);
   const size_t eh = align_up((size_t)n_edges * heads * 4 + 4);
+  const int64_t blocks = ppgat::epi_blocks(n_nodes);
+  const size_t part = align_up((size_t)blocks * 2 * heads * channels * 4);
   char* p = static_cast<char*>(workspace);
-  float* D = reinterpret_cast<float*>(p);
-  float* ds_src = reinterpret_cast<float*>(p + nh);
-  float* dz = reinterpret_cast<float*>(p + 2 * nh);
-  float* partial = reinterpret_cast<float*>(p + 2 * nh + eh);
+  float* nstate = reinterpret_cast<float*>(p);
+  float* ds_src = reinterpret_cast<float*>(p + ns);
+  float* dz = reinterpret_cast<float*>(p + ns + nh);
+  float* bpart = reinterpret_cast<float*>(p + ns + nh + eh);
+  float* hpart = reinterpret_cast<float*>(p + ns + nh + eh + part);
   const float gscale = mode == PPGAT_MODE_PYG ? 1.f / (float)heads : 1.f;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{sched->item_row, sched->item_beg, sched->item_end, sched->n_items, sched->n_hub_items};
   hipError_t e;
   {
     Timed t(PPGAT_K_BWD_PRO, st);
-    e = ppgat::launch_bwd_pro(grad_out, out, agg, heads == 1 ? bias : nullptr, n_nodes, heads, channels, gscale, D,
-                              st);
+    e = ppgat::launch_bwd_pro(grad_out, out, agg, heads == 1 ? bias : nullptr, s_dst, m, inv_l, n_nodes, heads,
+                              channels, gscale, nstate, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_prologue");
   {
     Timed t(PPGAT_K_BWD_SRC, st);
-    e = ppgat::launch_bwd_src(colptr, row, csc_eid, csc2csr, n_nodes, heads, channels, h, s_src, s_dst, m, inv_l, D,
-                              grad_out, mode, negative_slope, gscale, dropout_p, seed, grad_h, ds_src, dz, st);
+    e = ppgat::launch_bwd_src(it, row, csc_eid, csc2csr, heads, channels, h, s_src, nstate, grad_out, mode,
+                              negative_slope, gscale, dropout_p, seed, grad_h, ds_src, dz, hpart, sched->hub_row,
+                              sched->hub_ptr, sched->n_hubs, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_src");
-  const int64_t waves = ppgat::epi_waves(n_nodes);
   {
     Timed t(PPGAT_K_BWD_EPI, st);
-    e = ppgat::launch_bwd_epi(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, partial,
-                              waves, st);
+    e = ppgat::launch_bwd_epi(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, bpart,
+                              blocks, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_epilogue");
   {
     Timed t(PPGAT_K_BWD_RED, st);
-    e = ppgat::launch_bwd_red(partial, waves, heads * channels, grad_att_src, grad_att_dst, st);
+    e = ppgat::launch_bwd_red(bpart, blocks, heads * channels, grad_att_src, grad_att_dst, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_reduce");
   return PPGAT_OK;

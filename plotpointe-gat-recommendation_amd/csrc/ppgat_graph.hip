@@ -8,6 +8,7 @@
 // of `bad` (out-of-range index count).
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 
 #include "ppgat_internal.h"
@@ -118,6 +119,117 @@ hipError_t csr_build(const int64_t* ei, int64_t E, int64_t N, int32_t* rowptr, i
   }
   hipLaunchKernelGGL(k_ptr, dim3(gE1), dim3(256), 0, st, key_out, E, N, colptr);
   if (E > 0) hipLaunchKernelGGL(k_csc_rows, dim3(gE), dim3(256), 0, st, ei, E, N, csc_eid, pos, row, csc2csr);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Work schedule for the fused edge kernels (see ppgat_kernels.hip "Work items"):
+// rows with deg > T become ceil(deg/T) hub pieces, listed first (hubs in row order);
+// the other rows follow in descending degree (stable).  counts = {n_hubs, n_hub_items, n_items}.
+// ---------------------------------------------------------------------------
+int64_t schedule_capacity(int64_t N, int64_t E, int32_t T) { return N + (E + T - 1) / T + 1; }
+
+__global__ void k_sched_keys(const int32_t* __restrict__ ptr, int64_t N, int32_t T, int32_t* __restrict__ key,
+                             int32_t* __restrict__ iota, int32_t* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int32_t deg = ptr[i + 1] - ptr[i];
+  const bool hub = deg > T;
+  key[i] = hub ? 0 : (T + 1 - deg);
+  iota[i] = (int32_t)i;
+  if (hub) atomicAdd(&counts[0], 1);
+}
+
+__global__ void k_sched_np(const int32_t* __restrict__ order, const int32_t* __restrict__ ptr, int64_t N, int32_t T,
+                           int32_t* __restrict__ np) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= N) return;
+  const int32_t r = order[s];
+  const int32_t deg = ptr[r + 1] - ptr[r];
+  np[s] = deg > T ? (deg + T - 1) / T : 1;
+}
+
+__global__ void k_sched_fill(const int32_t* __restrict__ order, const int32_t* __restrict__ ptr, int64_t N,
+                             int32_t T, const int32_t* __restrict__ offs, const int32_t* __restrict__ np,
+                             int32_t* __restrict__ item_row, int32_t* __restrict__ item_beg,
+                             int32_t* __restrict__ item_end, int32_t* __restrict__ hub_row,
+                             int32_t* __restrict__ hub_ptr, int32_t* __restrict__ counts) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= N) return;
+  const int32_t r = order[s];
+  const int32_t d0 = ptr[r], d1 = ptr[r + 1];
+  const int32_t base = offs[s], n = np[s];
+  for (int32_t q = 0; q < n; ++q) {
+    item_row[base + q] = r;
+    item_beg[base + q] = d0 + q * T;
+    item_end[base + q] = min(d0 + (q + 1) * T, d1);
+  }
+  const bool hub = d1 - d0 > T;
+  bool next_hub = false;
+  if (s + 1 < N) {
+    const int32_t r2 = order[s + 1];
+    next_hub = ptr[r2 + 1] - ptr[r2] > T;
+  }
+  if (hub) {
+    hub_row[s] = r;
+    hub_ptr[s] = base;
+    if (!next_hub) {
+      hub_ptr[s + 1] = base + n;
+      counts[1] = base + n;
+    }
+  } else if (s == 0) {
+    hub_ptr[0] = 0;
+    counts[1] = 0;
+  }
+  if (s == N - 1) counts[2] = base + n;
+}
+
+static size_t sched_temp_bytes(int64_t N, int32_t T) {
+  size_t a = 0, b = 0;
+  const size_t n = (size_t)(N > 0 ? N : 1);
+  (void)rocprim::radix_sort_pairs(nullptr, a, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                                  (int32_t*)nullptr, n, 0u, key_bits((int64_t)T + 2));
+  (void)rocprim::exclusive_scan(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t)0, n,
+                                rocprim::plus<int32_t>());
+  return a > b ? a : b;
+}
+
+size_t schedule_workspace_bytes(int64_t N) {
+  const size_t n4 = align_up((size_t)(N > 0 ? N : 1) * 4);
+  // temp size depends on T only through key_bits; use the widest key we allow (T < 2^20)
+  return 5 * n4 + align_up(sched_temp_bytes(N, (1 << 20) - 2));
+}
+
+hipError_t schedule_build(const int32_t* ptr, int64_t N, int32_t T, int32_t* item_row, int32_t* item_beg,
+                          int32_t* item_end, int32_t* hub_row, int32_t* hub_ptr, int32_t* counts, void* ws,
+                          size_t ws_bytes, hipStream_t st) {
+  if (T < 1 || T >= (1 << 20) - 2 || ws_bytes < schedule_workspace_bytes(N)) return hipErrorInvalidValue;
+  hipError_t err = hipMemsetAsync(counts, 0, 3 * sizeof(int32_t), st);
+  if (err != hipSuccess) return err;
+  err = hipMemsetAsync(hub_ptr, 0, sizeof(int32_t), st);
+  if (err != hipSuccess) return err;
+  if (N == 0) return hipSuccess;
+  const size_t n4 = align_up((size_t)N * 4);
+  char* p = static_cast<char*>(ws);
+  int32_t* key = reinterpret_cast<int32_t*>(p);
+  int32_t* key_out = reinterpret_cast<int32_t*>(p + n4);
+  int32_t* iota = reinterpret_cast<int32_t*>(p + 2 * n4);
+  int32_t* order = reinterpret_cast<int32_t*>(p + 3 * n4);
+  int32_t* np = reinterpret_cast<int32_t*>(p + 4 * n4);
+  int32_t* offs = key;  // key is dead after the sort
+  void* tmp = p + 5 * n4;
+  size_t tmp_bytes = ws_bytes - 5 * n4;
+  const unsigned g = (unsigned)((N + 255) / 256);
+  hipLaunchKernelGGL(k_sched_keys, dim3(g), dim3(256), 0, st, ptr, N, T, key, iota, counts);
+  err = rocprim::radix_sort_pairs(tmp, tmp_bytes, key, key_out, iota, order, (size_t)N, 0u, key_bits((int64_t)T + 2),
+                                  st);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(k_sched_np, dim3(g), dim3(256), 0, st, order, ptr, N, T, np);
+  tmp_bytes = ws_bytes - 5 * n4;
+  err = rocprim::exclusive_scan(tmp, tmp_bytes, np, offs, (int32_t)0, (size_t)N, rocprim::plus<int32_t>(), st);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(k_sched_fill, dim3(g), dim3(256), 0, st, order, ptr, N, T, offs, np, item_row, item_beg,
+                     item_end, hub_row, hub_ptr, counts);
   return hipGetLastError();
 }
 

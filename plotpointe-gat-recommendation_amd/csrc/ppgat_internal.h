@@ -9,31 +9,47 @@ namespace ppgat {
 constexpr int kModePyg = 0;
 constexpr int kModeCustom = 1;
 constexpr int kMaxHeads = 8;
-constexpr int64_t kEpiMaxWaves = 8192;
+constexpr int64_t kEpiMaxBlocks = 1024;
+
+// host-side view of a work schedule (see include/ppgat.h ppgat_schedule)
+struct ItemsArg {
+  const int32_t* row;
+  const int32_t* beg;
+  const int32_t* end;
+  int64_t n_items;
+  int64_t n_hub_items;
+};
 
 hipError_t launch_scores(const float* h, const float* as, const float* ad, int64_t n, int heads, int C, float* ss,
                          float* sd, hipStream_t st);
-hipError_t launch_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* eid, int64_t n, int heads, int C,
+hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, int heads, int C,
                       const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
                       float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
+                      float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                       hipStream_t st);
-hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, int64_t n,
-                          int heads, int C, float gscale, float* D, hipStream_t st);
-hipError_t launch_bwd_src(const int32_t* colptr, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
-                          int64_t n, int heads, int C, const float* h, const float* ss, const float* sd,
-                          const float* m, const float* invl, const float* D, const float* go, int mode, float slope,
-                          float gscale, float p, uint64_t seed, float* dh, float* ds_src, float* dz,
+hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
+                          const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
+                          float* nstate, hipStream_t st);
+hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                          int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
+                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, float* ds_src,
+                          float* dz, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                           hipStream_t st);
-int64_t epi_waves(int64_t n);
+int64_t epi_blocks(int64_t n);
 hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
                           const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,
-                          int64_t waves, hipStream_t st);
-hipError_t launch_bwd_red(const float* partial, int64_t waves, int hc, float* das, float* dad, hipStream_t st);
+                          int64_t blocks, hipStream_t st);
+hipError_t launch_bwd_red(const float* partial, int64_t rows, int hc, float* das, float* dad, hipStream_t st);
 
 // graph preprocessing (ppgat_graph.hip)
 size_t csr_workspace_bytes(int64_t n_nodes, int64_t n_edges);
 hipError_t csr_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t* rowptr, int32_t* col, int32_t* csr_eid,
                      int32_t* colptr, int32_t* row, int32_t* csc_eid, int32_t* csc2csr, int32_t* bad,
                      void* ws, size_t ws_bytes, hipStream_t st);
+int64_t schedule_capacity(int64_t n_nodes, int64_t n_edges, int32_t max_edges);
+size_t schedule_workspace_bytes(int64_t n_nodes);
+hipError_t schedule_build(const int32_t* ptr, int64_t N, int32_t T, int32_t* item_row, int32_t* item_beg,
+                          int32_t* item_end, int32_t* hub_row, int32_t* hub_ptr, int32_t* counts, void* ws,
+                          size_t ws_bytes, hipStream_t st);
 
 }  // namespace ppgat

@@ -119,22 +119,44 @@ __global__ void __launch_bounds__(256) k_scores(const float* __restrict__ h, con
 }
 
 // ---------------------------------------------------------------------------
-// Fused forward: one wave per destination row i (CSR by dst).
+// Work items.  Rows (dst rows for the forward, src rows for backward pass B) are
+// cut into items of at most T edges by ppgat_schedule_build: hub rows (deg > T) become
+// ceil(deg/T) pieces that write partial state to a scratch slab and are merged in
+// piece order by a second small kernel (deterministic); all other rows are one item.
+// Items are ordered hub pieces first, then rows by descending degree, so the longest
+// work starts first and the tail is short (largest in-degree on config 2: 5,180).
+// ---------------------------------------------------------------------------
+struct Items {
+  const int32_t* row;
+  const int32_t* beg;
+  const int32_t* end;
+  int64_t n_items;
+  int64_t n_hub_items;  // items [0, n_hub_items) are hub pieces, slot = item index
+};
+
+// ---------------------------------------------------------------------------
+// Fused forward: one wave per item (destination row or hub piece), CSR by dst.
+//   e_k = logit(s_src[j] + s_dst[i]);  online softmax over 64-edge chunks;
+//   acc = sum_k exp(e_k - m) * d_k * h[j]  (d_k = dropout multiplier)
+// partial slab (hub pieces) per (item, head): [acc C | m | l | pad pad]
 // ---------------------------------------------------------------------------
 template <int C>
-__global__ void __launch_bounds__(256) k_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                             const int32_t* __restrict__ eid, int64_t n_nodes, int heads,
+__global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict__ col,
+                                             const int32_t* __restrict__ eid, int heads,
                                              const float* __restrict__ h, const float* __restrict__ s_src,
                                              const float* __restrict__ s_dst, const float* __restrict__ bias,
                                              int mode, float slope, float eps, float p, float inv_keep,
                                              uint64_t seed, float* __restrict__ out, float* __restrict__ m_out,
-                                             float* __restrict__ invl_out, float* __restrict__ agg_out) {
+                                             float* __restrict__ invl_out, float* __restrict__ agg_out,
+                                             float* __restrict__ partial) {
   using G = Geo<C>;
   const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (i >= n_nodes) return;  // wave-uniform
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (w >= it.n_items) return;  // wave-uniform
   const int sg = lane / G::LPR, sl = lane % G::LPR;
-  const int rs = rowptr[i], re = rowptr[i + 1];
+  const int64_t i = it.row[w];
+  const int rs = it.beg[w], re = it.end[w];
+  const bool hub = w < it.n_hub_items;
   const bool pyg = mode == kModePyg;
   float4 osum = f4(0.f);
   for (int hd = 0; hd < heads; ++hd) {
@@ -178,6 +200,12 @@ __global__ void __launch_bounds__(256) k_fwd(const int32_t* __restrict__ rowptr,
     }
 #pragma unroll
     for (int off = G::LPR; off < 64; off <<= 1) acc = add4(acc, shfl_xor4(acc, off));
+    if (hub) {
+      float* slot = partial + (w * heads + hd) * (C + 4);
+      if (sg == 0) st4(slot + sl * 4, acc);
+      if (lane == 0) st4(slot + C, make_float4(m, l, 0.f, 0.f));
+      continue;
+    }
     const float invl = 1.f / (l + eps);
     const float4 a = mul4(acc, invl);
     if (agg_out != nullptr && sg == 0) st4(agg_out + (i * heads + hd) * C + sl * 4, a);
@@ -187,19 +215,70 @@ __global__ void __launch_bounds__(256) k_fwd(const int32_t* __restrict__ rowptr,
       invl_out[i * heads + hd] = invl;
     }
   }
+  if (hub) return;
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
   if (sg == 0) st4(out + i * C + sl * 4, osum);
 }
 
+// Merge the pieces of each hub row, in piece order.  One wave per hub row.
+template <int C>
+__global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ hub_row,
+                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
+                                                   const float* __restrict__ partial,
+                                                   const float* __restrict__ bias, int mode, float eps,
+                                                   float* __restrict__ out, float* __restrict__ m_out,
+                                                   float* __restrict__ invl_out, float* __restrict__ agg_out) {
+  using G = Geo<C>;
+  const int lane = threadIdx.x & 63;
+  const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;
+  const int sg = lane / G::LPR, sl = lane % G::LPR;
+  if (sg != 0) return;  // one subgroup does the (small) merge
+  const int64_t i = hub_row[hb];
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  float4 osum = f4(0.f);
+  for (int hd = 0; hd < heads; ++hd) {
+    float M = -INFINITY;
+    if (mode == kModePyg) {
+      for (int q = p0; q < p1; ++q) M = fmaxf(M, partial[((int64_t)q * heads + hd) * (C + 4) + C]);
+    } else {
+      M = 0.f;
+    }
+    float l = 0.f;
+    float4 acc = f4(0.f);
+    for (int q = p0; q < p1; ++q) {
+      const float* slot = partial + ((int64_t)q * heads + hd) * (C + 4);
+      const float sc = expf(slot[C] - M);
+      l = fmaf(slot[C + 1], sc, l);
+      acc = fma4(sc, ld4(slot + sl * 4), acc);
+    }
+    const float invl = 1.f / (l + eps);
+    const float4 a = mul4(acc, invl);
+    if (agg_out != nullptr) st4(agg_out + (i * heads + hd) * C + sl * 4, a);
+    osum = add4(osum, a);
+    if (sl == 0) {
+      m_out[i * heads + hd] = M;
+      invl_out[i * heads + hd] = invl;
+    }
+  }
+  if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
+  if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
+  st4(out + i * C + sl * 4, osum);
+}
+
 // ---------------------------------------------------------------------------
-// Backward prologue: D[n,h] = <g_n, agg[n,h]>,  g = gscale * grad_out
-// (= sum_k alpha_k dalpha_k over the in-edges of n; SURVEY Appendix B D_i).
+// Backward prologue, one subgroup per (n, h):
+//   D[n,h] = <g_n, agg[n,h]>, g = gscale * grad_out   (= sum_k alpha_k dalpha_k, Appendix B)
+// and the per-node state pass B gathers once per edge, packed as one float4:
+//   nstate[n,h] = {s_dst, m, inv_l, D}
 // ---------------------------------------------------------------------------
 template <int C>
 __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_out, const float* __restrict__ out,
                                                  const float* __restrict__ agg, const float* __restrict__ bias,
-                                                 int64_t pairs, int heads, float gscale, float* __restrict__ D) {
+                                                 const float* __restrict__ s_dst, const float* __restrict__ m_in,
+                                                 const float* __restrict__ invl_in, int64_t pairs, int heads,
+                                                 float gscale, float4* __restrict__ nstate) {
   using G = Geo<C>;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pr = t / G::LPR;
@@ -223,30 +302,35 @@ __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_
   }
 #pragma unroll
   for (int off = G::LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
-  if (valid && sl == 0) D[pr] = x * gscale;
+  if (valid && sl == 0) nstate[pr] = make_float4(s_dst[pr], m_in[pr], invl_in[pr], x * gscale);
 }
 
 // ---------------------------------------------------------------------------
-// Backward pass B: one wave per SOURCE node j (CSC by src).
-//   dh_j   = sum_k beta_k g_{i_k}                          (message term, complete)
-//   dz_k   = alpha_k (d_k gscale <dOut_i, h_j> - D_i) e'(z_k) (logit gradient)
+// Backward pass B: one wave per item (SOURCE row j or hub piece), CSC by src.
+//   dh_j     = sum_k beta_k g_{i_k}                              (message term)
+//   dz_k     = alpha_k (d_k gscale <dOut_i, h_j> - D_i) e'(z_k)  (logit gradient)
 //   ds_src_j = sum_k dz_k ;  dz_k stored at its CSR slot for the dst-side sum.
 // alpha is recomputed from the saved (m, inv_l): nothing [E]-sized was saved.
+// hub-piece partial slab per (item, head): [dh C | ds | pad pad pad]
 // ---------------------------------------------------------------------------
 template <int C>
-__global__ void __launch_bounds__(256) k_bwd_src(
-    const int32_t* __restrict__ colptr, const int32_t* __restrict__ row, const int32_t* __restrict__ csc_eid,
-    const int32_t* __restrict__ csc2csr, int64_t n_nodes, int heads, const float* __restrict__ h,
-    const float* __restrict__ s_src, const float* __restrict__ s_dst, const float* __restrict__ m_in,
-    const float* __restrict__ invl_in, const float* __restrict__ D, const float* __restrict__ grad_out, int mode,
-    float slope, float gscale, float p, float inv_keep, uint64_t seed, float* __restrict__ dh,
-    float* __restrict__ ds_src, float* __restrict__ dz) {
+__global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __restrict__ row,
+                                                 const int32_t* __restrict__ csc_eid,
+                                                 const int32_t* __restrict__ csc2csr, int heads,
+                                                 const float* __restrict__ h, const float* __restrict__ s_src,
+                                                 const float4* __restrict__ nstate,
+                                                 const float* __restrict__ grad_out, int mode, float slope,
+                                                 float gscale, float p, float inv_keep, uint64_t seed,
+                                                 float* __restrict__ dh, float* __restrict__ ds_src,
+                                                 float* __restrict__ dz, float* __restrict__ partial) {
   using G = Geo<C>;
   const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (j >= n_nodes) return;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (w >= it.n_items) return;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
-  const int cs = colptr[j], ce = colptr[j + 1];
+  const int64_t j = it.row[w];
+  const int cs = it.beg[w], ce = it.end[w];
+  const bool hub = w < it.n_hub_items;
   for (int hd = 0; hd < heads; ++hd) {
     const float ss = s_src[j * heads + hd];
     const float4 hv = ld4(h + (j * heads + hd) * C + sl * 4);
@@ -257,13 +341,15 @@ __global__ void __launch_bounds__(256) k_bwd_src(
       const bool valid = k < ce;
       const int i = valid ? row[k] : 0;
       float alpha = 0.f, f = 0.f, Dv = 0.f, dm = 1.f;
+      int slot = 0;
       if (valid) {
-        const int64_t ih = (int64_t)i * heads + hd;
-        const float z = ss + s_dst[ih];
+        const float4 st = nstate[(int64_t)i * heads + hd];  // {s_dst, m, inv_l, D}
+        const float z = ss + st.x;
         const float e = logit(z, slope, mode);
         f = dlogit(z, slope, mode);
-        alpha = expf(e - m_in[ih]) * invl_in[ih];
-        Dv = D[ih];
+        alpha = expf(e - st.y) * st.z;
+        Dv = st.w;
+        slot = csc2csr[k];
         if (p > 0.f) dm = drop_scale(seed, (uint32_t)csc_eid[k], (uint32_t)hd, p, inv_keep);
       }
       const float bg = alpha * dm * gscale;  // beta * gscale
@@ -293,10 +379,11 @@ __global__ void __launch_bounds__(256) k_bwd_src(
         for (int u = 0; u < G::U; ++u) {
           const int q = q0 + u * G::EPW + sg;
           const float aq = __shfl(alpha, q), Dq = __shfl(Dv, q), fq = __shfl(f, q), dq = __shfl(dg, q);
+          const int sq = __shfl(slot, q);
           const float dzv = aq * fmaf(dq, part[u], -Dq) * fq;
           if (sl == 0 && q < n) {
             ds += dzv;
-            dz[(int64_t)csc2csr[base + q] * heads + hd] = dzv;
+            dz[(int64_t)sq * heads + hd] = dzv;
           }
         }
       }
@@ -304,17 +391,49 @@ __global__ void __launch_bounds__(256) k_bwd_src(
 #pragma unroll
     for (int off = G::LPR; off < 64; off <<= 1) acc = add4(acc, shfl_xor4(acc, off));
     ds = wave_sum(ds);
+    if (hub) {
+      float* s = partial + (w * heads + hd) * (C + 4);
+      if (sg == 0) st4(s + sl * 4, acc);
+      if (lane == 0) s[C] = ds;
+      continue;
+    }
     if (sg == 0) st4(dh + (j * heads + hd) * C + sl * 4, acc);
     if (lane == 0) ds_src[j * heads + hd] = ds;
   }
 }
 
+template <int C>
+__global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ hub_row,
+                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
+                                                   const float* __restrict__ partial, float* __restrict__ dh,
+                                                   float* __restrict__ ds_src) {
+  using G = Geo<C>;
+  const int lane = threadIdx.x & 63;
+  const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;
+  const int sg = lane / G::LPR, sl = lane % G::LPR;
+  if (sg != 0) return;
+  const int64_t j = hub_row[hb];
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  for (int hd = 0; hd < heads; ++hd) {
+    float4 acc = f4(0.f);
+    float ds = 0.f;
+    for (int q = p0; q < p1; ++q) {
+      const float* s = partial + ((int64_t)q * heads + hd) * (C + 4);
+      acc = add4(acc, ld4(s + sl * 4));
+      ds += s[C];
+    }
+    st4(dh + (j * heads + hd) * C + sl * 4, acc);
+    if (sl == 0) ds_src[j * heads + hd] = ds;
+  }
+}
+
 // ---------------------------------------------------------------------------
-// Backward node epilogue (grid-stride, fixed partition => deterministic):
+// Backward node epilogue (grid-stride over nodes, fixed partition => deterministic):
 //   ds_dst_i = sum_{k in CSR(i)} dz_k            (ordered segment sum)
 //   dh_i    += ds_src_i att_src + ds_dst_i att_dst
-//   partial datt_src += ds_src_i h_i, datt_dst += ds_dst_i h_i   (per wave)
-// partial layout [waves, 2, H, C]; heads <= kMaxHeads.
+//   block partial datt_src += ds_src_i h_i, datt_dst += ds_dst_i h_i
+// block partial layout [blocks, 2, H, C]; heads <= kMaxHeads.
 // ---------------------------------------------------------------------------
 template <int C>
 __global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ rowptr, int64_t n_nodes, int heads,
@@ -323,9 +442,11 @@ __global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ row
                                                  const float* __restrict__ ds_src, const float* __restrict__ dz,
                                                  float* __restrict__ dh, float* __restrict__ partial) {
   using G = Geo<C>;
+  __shared__ float4 red[4][2 * kMaxHeads * (C / 4)];
   const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
-  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   float4 pa_s[kMaxHeads], pa_d[kMaxHeads];
 #pragma unroll
@@ -355,6 +476,7 @@ __global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ row
       }
     }
   }
+  // wave combine (subgroups), then block combine in wave order via LDS
 #pragma unroll
   for (int hd = 0; hd < kMaxHeads; ++hd) {
     if (hd >= heads) break;
@@ -365,21 +487,47 @@ __global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ row
       b = add4(b, shfl_xor4(b, off));
     }
     if (sg == 0) {
-      st4(partial + ((wave * 2 + 0) * heads + hd) * C + sl * 4, a);
-      st4(partial + ((wave * 2 + 1) * heads + hd) * C + sl * 4, b);
+      red[wv][(0 * heads + hd) * (C / 4) + sl] = a;
+      red[wv][(1 * heads + hd) * (C / 4) + sl] = b;
     }
+  }
+  __syncthreads();
+  const int nv = 2 * heads * (C / 4);
+  for (int t = threadIdx.x; t < nv; t += blockDim.x) {
+    float4 s = red[0][t];
+    s = add4(s, red[1][t]);
+    s = add4(s, red[2][t]);
+    s = add4(s, red[3][t]);
+    st4(partial + ((int64_t)blockIdx.x * nv + t) * 4, s);
   }
 }
 
-// Final ordered reduction of the per-wave partials: out[2, H*C].
-__global__ void __launch_bounds__(256) k_bwd_red(const float* __restrict__ partial, int64_t n_waves, int hc,
-                                                 float* __restrict__ datt_src, float* __restrict__ datt_dst) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * hc) return;
-  const int which = t / hc, c = t % hc;
+// Ordered reduction of the block partials: rows = blocks, cols = 2*H*C.
+// One 1024-thread block per 64 columns: wave w sums rows w, w+16, ...; then the 16
+// wave sums are added in wave order.
+__global__ void __launch_bounds__(1024) k_bwd_red(const float* __restrict__ partial, int64_t rows, int cols,
+                                                  float* __restrict__ datt_src, float* __restrict__ datt_dst) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int64_t w = 0; w < n_waves; ++w) s += partial[(w * 2 + which) * hc + c];
-  (which == 0 ? datt_src : datt_dst)[c] = s;
+  if (c < cols) {
+    int64_t r = wv;
+    for (; r + 48 < rows; r += 64) {
+      const float a = partial[r * cols + c], b = partial[(r + 16) * cols + c];
+      const float d = partial[(r + 32) * cols + c], e = partial[(r + 48) * cols + c];
+      s += a; s += b; s += d; s += e;
+    }
+    for (; r < rows; r += 16) s += partial[r * cols + c];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && c < cols) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    const int hc = cols / 2;
+    (c < hc ? datt_src : datt_dst)[c % hc] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -408,59 +556,77 @@ hipError_t launch_scores(const float* h, const float* as, const float* ad, int64
   return hipGetLastError();
 }
 
-hipError_t launch_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* eid, int64_t n, int heads, int C,
+hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, int heads, int C,
                       const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
                       float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
+                      float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                       hipStream_t st) {
-  if (n == 0) return hipSuccess;
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd<CC>, dim3(blocks_for(n * 64)), dim3(256), 0, st, rowptr, col, eid, n,
-                                         heads, h, ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m, invl,
-                                         agg));
+  const Items its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  if (it.n_items > 0) {
+    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its, col,
+                                           eid, heads, h, ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m,
+                                           invl, agg, partial));
+  }
+  if (n_hubs > 0) {
+    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,
+                                           hub_row, hub_ptr, n_hubs, heads, partial, bias, mode, eps, out, m, invl,
+                                           agg));
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, int64_t n,
-                          int heads, int C, float gscale, float* D, hipStream_t st) {
+hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
+                          const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
+                          float* nstate, hipStream_t st) {
   const int64_t pairs = n * heads;
   if (pairs == 0) return hipSuccess;
   PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_pro<CC>, dim3(blocks_for(pairs * (CC / 4))), dim3(256), 0, st, go,
-                                         out, agg, bias, pairs, heads, gscale, D));
+                                         out, agg, bias, sd, m, invl, pairs, heads, gscale,
+                                         reinterpret_cast<float4*>(nstate)));
   return hipGetLastError();
 }
 
-hipError_t launch_bwd_src(const int32_t* colptr, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
-                          int64_t n, int heads, int C, const float* h, const float* ss, const float* sd,
-                          const float* m, const float* invl, const float* D, const float* go, int mode, float slope,
-                          float gscale, float p, uint64_t seed, float* dh, float* ds_src, float* dz,
+hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                          int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
+                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, float* ds_src,
+                          float* dz, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                           hipStream_t st) {
-  if (n == 0) return hipSuccess;
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(n * 64)), dim3(256), 0, st, colptr, row,
-                                         csc_eid, csc2csr, n, heads, h, ss, sd, m, invl, D, go, mode, slope, gscale,
-                                         p, inv_keep, seed, dh, ds_src, dz));
+  const Items its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  if (it.n_items > 0) {
+    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its,
+                                           row, csc_eid, csc2csr, heads, h, ss,
+                                           reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, p,
+                                           inv_keep, seed, dh, ds_src, dz, partial));
+  }
+  if (n_hubs > 0) {
+    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,
+                                           hub_row, hub_ptr, n_hubs, heads, partial, dh, ds_src));
+  }
   return hipGetLastError();
 }
 
-int64_t epi_waves(int64_t n) {
-  // fixed partition: enough waves to fill the chip several times over, capped so the
-  // partial buffer stays small (kEpiMaxWaves x 2 x H x C floats)
-  int64_t w = (n + 7) / 8;
-  if (w < 1) w = 1;
-  if (w > kEpiMaxWaves) w = kEpiMaxWaves;
-  return (w + 3) / 4 * 4;  // whole 256-thread blocks
+int64_t epi_blocks(int64_t n) {
+  // fixed partition: >= 4 blocks per CU when N allows, capped so the block-partial
+  // slab (blocks x 2 x H x C floats) stays small
+  int64_t b = (n + 31) / 32;
+  if (b < 1) b = 1;
+  if (b > kEpiMaxBlocks) b = kEpiMaxBlocks;
+  return b;
 }
 
 hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
                           const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,
-                          int64_t waves, hipStream_t st) {
-  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_epi<CC>, dim3((unsigned)(waves / 4)), dim3(256), 0, st, rowptr, n,
-                                         heads, h, as, ad, ds_src, dz, dh, partial));
+                          int64_t blocks, hipStream_t st) {
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_epi<CC>, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, n, heads,
+                                         h, as, ad, ds_src, dz, dh, partial));
   return hipGetLastError();
 }
 
-hipError_t launch_bwd_red(const float* partial, int64_t waves, int hc, float* das, float* dad, hipStream_t st) {
-  hipLaunchKernelGGL(k_bwd_red, dim3(blocks_for(2 * hc)), dim3(256), 0, st, partial, waves, hc, das, dad);
+hipError_t launch_bwd_red(const float* partial, int64_t rows, int hc, float* das, float* dad, hipStream_t st) {
+  const int cols = 2 * hc;
+  hipLaunchKernelGGL(k_bwd_red, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, partial, rows, cols, das, dad);
   return hipGetLastError();
 }
 

@@ -33,9 +33,59 @@ def _check_dev(name: str, t: torch.Tensor, dtype, device=None):
 # ---------------------------------------------------------------------------
 # graph preprocessing
 # ---------------------------------------------------------------------------
+# rows longer than this many edges are split into pieces (include/ppgat.h ppgat_schedule)
+MAX_EDGES_PER_ITEM = 256
+
+
+@dataclass
+class Schedule:
+    """Device work schedule over a CSR/CSC (owns the arrays ppgat_schedule points at)."""
+    item_row: torch.Tensor
+    item_beg: torch.Tensor
+    item_end: torch.Tensor
+    hub_row: torch.Tensor
+    hub_ptr: torch.Tensor
+    n_items: int
+    n_hub_items: int
+    n_hubs: int
+    max_edges: int
+
+    def cstruct(self) -> "_lib.Schedule":
+        return _lib.Schedule(self.item_row.data_ptr(), self.item_beg.data_ptr(), self.item_end.data_ptr(),
+                             self.n_items, self.n_hub_items, self.hub_row.data_ptr(), self.hub_ptr.data_ptr(),
+                             self.n_hubs)
+
+
+def schedule_build(ptr: torch.Tensor, n_edges: int, max_edges: int = MAX_EDGES_PER_ITEM) -> Schedule:
+    """Work items over ptr[N+1] (one host sync to read the three counts)."""
+    lib = _lib.load()
+    _check_dev("ptr", ptr, torch.int32)
+    N = ptr.numel() - 1
+    dev = ptr.device
+    cap = int(lib.ppgat_schedule_capacity(N, n_edges, max_edges))
+    _require(cap >= 0, "schedule_capacity: bad arguments")
+    i32 = dict(dtype=torch.int32, device=dev)
+    item_row = torch.empty(max(cap, 1), **i32)
+    item_beg = torch.empty(max(cap, 1), **i32)
+    item_end = torch.empty(max(cap, 1), **i32)
+    hub_row = torch.empty(max(N, 1), **i32)
+    hub_ptr = torch.empty(N + 1, **i32)
+    counts = torch.empty(3, **i32)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_schedule_workspace_bytes(N, ctypes.byref(nbytes)), "schedule_workspace_bytes")
+    ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
+    _lib.check(lib.ppgat_schedule_build(ptr.data_ptr(), N, n_edges, max_edges, item_row.data_ptr(),
+                                        item_beg.data_ptr(), item_end.data_ptr(), hub_row.data_ptr(),
+                                        hub_ptr.data_ptr(), counts.data_ptr(), ws.data_ptr(), nbytes.value,
+                                        _lib.stream_handle(dev)), "schedule_build")
+    n_hubs, n_hub_items, n_items = (int(v) for v in counts.cpu().tolist())
+    return Schedule(item_row, item_beg, item_end, hub_row, hub_ptr, n_items, n_hub_items, n_hubs, max_edges)
+
+
 @dataclass
 class CSRGraph:
-    """Static CSR-by-dst / CSC-by-src view of a COO edge_index (int32 indices)."""
+    """Static CSR-by-dst / CSC-by-src view of a COO edge_index (int32 indices) plus the
+    work schedules of the forward (over rowptr) and backward pass B (over colptr)."""
     n_nodes: int
     n_edges: int
     rowptr: torch.Tensor
@@ -45,6 +95,8 @@ class CSRGraph:
     row: torch.Tensor
     csc_eid: torch.Tensor
     csc2csr: torch.Tensor
+    fwd_sched: Schedule = None
+    bwd_sched: Schedule = None
 
     @property
     def device(self):
@@ -57,7 +109,7 @@ class CSRGraph:
         return (self.colptr[1:] - self.colptr[:-1])
 
 
-def csr_build(edge_index: torch.Tensor, n_nodes: int) -> CSRGraph:
+def csr_build(edge_index: torch.Tensor, n_nodes: int, max_edges: int = MAX_EDGES_PER_ITEM) -> CSRGraph:
     """edge_index LongTensor[2,E] (row 0 src, row 1 dst) -> CSRGraph on the same device.
 
     One host sync (the out-of-range index count), once per static graph.
@@ -89,7 +141,10 @@ def csr_build(edge_index: torch.Tensor, n_nodes: int) -> CSRGraph:
     nbad = int(bad.item())
     if nbad:
         raise RuntimeError(f"edge_index has {nbad} entries outside [0, {N})")
-    return CSRGraph(N, E, rowptr, col[:E], csr_eid[:E], colptr, row[:E], csc_eid[:E], csc2csr[:E])
+    with torch.cuda.device(dev):
+        fs = schedule_build(rowptr, E, max_edges)
+        bs = schedule_build(colptr, E, max_edges)
+    return CSRGraph(N, E, rowptr, col[:E], csr_eid[:E], colptr, row[:E], csc_eid[:E], csc2csr[:E], fs, bs)
 
 
 class _GraphCache:
@@ -147,11 +202,18 @@ def gat_fwd(g: CSRGraph, h, s_src, s_dst, bias, heads: int, channels: int, mode:
     m = torch.empty(N, heads, dtype=torch.float32, device=dev)
     inv_l = torch.empty(N, heads, dtype=torch.float32, device=dev)
     agg = torch.empty(N, heads, channels, dtype=torch.float32, device=dev) if want_agg else None
-    _lib.check(lib.ppgat_fwd(g.rowptr.data_ptr(), _lib.ptr(g.col) if g.n_edges else None,
+    sched = g.fwd_sched
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_fwd_workspace_bytes(sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
+               "fwd_workspace_bytes")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    cs = sched.cstruct()
+    _lib.check(lib.ppgat_fwd(ctypes.byref(cs), _lib.ptr(g.col) if g.n_edges else None,
                              _lib.ptr(g.csr_eid) if g.n_edges else None, N, g.n_edges, heads, channels,
                              h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), _lib.ptr(bias), mode, float(slope),
                              float(dropout_p), int(seed) & (2**64 - 1), out.data_ptr(), m.data_ptr(),
-                             inv_l.data_ptr(), _lib.ptr(agg), _lib.stream_handle(dev)), "gat_fwd")
+                             inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
+                             _lib.stream_handle(dev)), "gat_fwd")
     return out, m, inv_l, agg
 
 
@@ -165,11 +227,13 @@ def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, i
     datt_src = torch.empty(heads, channels, dtype=torch.float32, device=dev)
     datt_dst = torch.empty(heads, channels, dtype=torch.float32, device=dev)
     nbytes = ctypes.c_size_t(0)
-    _lib.check(lib.ppgat_bwd_workspace_bytes(N, g.n_edges, heads, channels, ctypes.byref(nbytes)),
-               "bwd_workspace_bytes")
+    sched = g.bwd_sched
+    _lib.check(lib.ppgat_bwd_workspace_bytes(N, g.n_edges, sched.n_hub_items, heads, channels,
+                                             ctypes.byref(nbytes)), "bwd_workspace_bytes")
     ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
     E = g.n_edges
-    _lib.check(lib.ppgat_bwd(g.rowptr.data_ptr(), g.colptr.data_ptr(), _lib.ptr(g.row) if E else None,
+    cs = sched.cstruct()
+    _lib.check(lib.ppgat_bwd(ctypes.byref(cs), g.rowptr.data_ptr(), _lib.ptr(g.row) if E else None,
                              _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, N, E, heads,
                              channels, h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), att_src.data_ptr(),
                              att_dst.data_ptr(), _lib.ptr(bias), out.data_ptr(), _lib.ptr(agg), m.data_ptr(),

@@ -32,16 +32,26 @@ def test_invalid_arguments_return_codes(pkg):
     lib = pkg._lib.load()
     # unsupported channel count -> PPGAT_ERR_UNSUPPORTED before any device work
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 96, None, None, None, None, 0, 0.2, 0.0, 0,
-                       None, None, None, None, None)
+                       None, None, None, None, None, 0, None)
     assert rc == 2 and b"channels" in lib.ppgat_last_error()
     # custom mode with a bias -> invalid
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, ctypes.c_void_p(16), 1, 0.2, 0.0, 0,
-                       None, None, None, None, None)
+                       None, None, None, None, None, 0, None)
     assert rc == 1 and b"custom" in lib.ppgat_last_error()
     # dropout out of range
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 1.0, 0,
-                       None, None, None, None, None)
+                       None, None, None, None, None, 0, None)
     assert rc == 1
+    # missing schedule
+    rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 0.0, 0,
+                       None, None, None, None, None, 0, None)
+    assert rc == 1 and b"schedule" in lib.ppgat_last_error()
+    # inconsistent schedule counts
+    bad = pkg._lib.Schedule(None, None, None, 3, 5, None, None, 0)
+    rc = lib.ppgat_fwd(ctypes.byref(bad), None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 0.0, 0,
+                       None, None, None, None, None, 0, None)
+    assert rc == 1 and b"inconsistent" in lib.ppgat_last_error()
+    assert lib.ppgat_schedule_capacity(100, 1000, 256) == 100 + 4 + 1
     with pytest.raises(NotImplementedError):
         pkg._lib.check(2, "x")
 
@@ -49,7 +59,7 @@ def test_invalid_arguments_return_codes(pkg):
 def test_bwd_workspace_size_is_host_only(pkg):
     lib = pkg._lib.load()
     n = ctypes.c_size_t(0)
-    assert lib.ppgat_bwd_workspace_bytes(1000, 5000, 1, 128, ctypes.byref(n)) == 0
+    assert lib.ppgat_bwd_workspace_bytes(1000, 5000, 10, 1, 128, ctypes.byref(n)) == 0
     assert n.value >= (2 * 1000 + 5000) * 4
 
 
