@@ -143,6 +143,37 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
               float* grad_h, float* grad_att_src, float* grad_att_dst,
               void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- loss of the training step ---------------------------------------------
+ * Replaces: pos = (U[u]*I[i]).sum(-1); neg = (U[u]*I[j]).sum(-1); BPR
+ *           -log(sigmoid(pos-neg)+1e-8).mean() (loss_kind 0) or BCE-with-logits over
+ *           [pos; neg] with labels [1; 0] (loss_kind 1)  -- scripts/train_gat_pyg.py:313-322,
+ *           and its autograd (gather backward = index_put_ accumulate).
+ * Z [N, C] with users in rows [0, n_users) and items in [n_users, N); u, i, j int64 [S].
+ * Forward writes the scalar mean loss and coef [S, 2] (dloss/dpos, dloss/dneg); the
+ * backward writes the full grad_Z [N, C] (zero rows included) = grad_loss * sum of the
+ * per-triple contributions, deterministically (sorted contributions, ordered sums).
+ * Indices outside their range are clamped (the caller validates them).
+ */
+int ppgat_bpr_workspace_bytes(int64_t n_nodes, int64_t n_samples, int channels, size_t* bytes);
+int ppgat_bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int channels,
+                  const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, int loss_kind,
+                  float* loss, float* coef, void* workspace, size_t workspace_bytes, void* stream);
+int ppgat_bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int channels,
+                  const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+                  const float* coef, const float* grad_loss, float* grad_Z,
+                  void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- projection weight gradient ----------------------------------------------
+ * Replaces: the weight (and bias) gradient of torch.nn.Linear in GATConv.lin /
+ *           SimpleGATLayer.lin (train_gat_custom.py:66,77) and PyGGAT.item_proj
+ *           (train_gat_pyg.py:74,81): out[M,K] = A[N,M]^T B[N,K]; colsum[M] = sum_n A[n,:]
+ *           when colsum != NULL.  fp32 in, fp32 MFMA (exact fp32 FMA), N split over
+ *           workgroups with an ordered reduction of the partials (deterministic).
+ */
+int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, size_t* bytes);
+int ppgat_gemm_tn(const float* A, const float* B, int64_t n, int m, int k, float* out, float* colsum,
+                  void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- in-process kernel timing (HIP events on the launch stream) --------- */
 #define PPGAT_K_CSR 0
 #define PPGAT_K_SCORES 1
@@ -152,7 +183,8 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
 #define PPGAT_K_BWD_EPI 5
 #define PPGAT_K_BWD_RED 6
 #define PPGAT_K_SCHED 7
-#define PPGAT_K_COUNT 8
+#define PPGAT_K_GEMM_TN 8
+#define PPGAT_K_COUNT 9
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

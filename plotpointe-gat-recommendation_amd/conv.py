@@ -22,7 +22,7 @@ import math
 import torch
 
 from . import _lib
-from .hip_ops import gat_aggregate, graph_cache
+from .hip_ops import gat_aggregate, graph_cache, linear
 
 
 def _dropout_seed() -> int:
@@ -88,7 +88,7 @@ class GATConv(torch.nn.Module):
         if return_attention_weights:
             raise NotImplementedError("return_attention_weights not implemented")
         graph = graph_cache.get(edge_index, x.size(0))
-        h = self.lin(x)
+        h = linear(x, self.lin.weight)
         p = float(self.dropout) if self.training else 0.0
         seed = _dropout_seed() if p > 0 else 0
         return gat_aggregate(h, self.att_src, self.att_dst, self.bias, graph, self.heads, self.out_channels,
@@ -119,7 +119,7 @@ class SimpleGATLayer(torch.nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
         graph = graph_cache.get(edge_index, x.size(0))
-        h = self.lin(x)
+        h = linear(x, self.lin.weight)
         p = float(self.drop.p) if self.training else 0.0
         seed = _dropout_seed() if p > 0 else 0
         return gat_aggregate(h, self.a_src, self.a_dst, None, graph, 1, self.out_dim, _lib.MODE_CUSTOM,

@@ -293,6 +293,70 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
   return PPGAT_OK;
 }
 
+// ---- training-step kernels ----
+int ppgat_bpr_workspace_bytes(int64_t n_nodes, int64_t n_samples, int channels, size_t* bytes) {
+  if (!bytes || n_nodes < 0 || n_samples < 0) return fail(PPGAT_ERR_INVALID, "bpr_workspace_bytes: bad arguments");
+  if (!ppgat::bpr_channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bpr: channels must be 32/64/128/256");
+  *bytes = ppgat::bpr_workspace_bytes(n_nodes, n_samples, channels);
+  return PPGAT_OK;
+}
+
+static int check_bpr(int64_t n_users, int64_t n_items, int channels, int64_t S, const void* Z, const void* u,
+                     const void* i, const void* j, const char* who) {
+  if (!ppgat::bpr_channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, std::string(who) + ": channels");
+  if (n_users < 1 || n_items < 1 || S < 0) return fail(PPGAT_ERR_INVALID, std::string(who) + ": bad sizes");
+  if (n_users + n_items >= ((int64_t)1 << 31) || 4 * S >= ((int64_t)1 << 31))
+    return fail(PPGAT_ERR_UNSUPPORTED, std::string(who) + ": sizes exceed int32 indexing");
+  if (!Z || (S > 0 && (!u || !i || !j))) return fail(PPGAT_ERR_INVALID, std::string(who) + ": null pointer");
+  return PPGAT_OK;
+}
+
+int ppgat_bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int channels, const int64_t* u, const int64_t* i,
+                  const int64_t* j, int64_t n_samples, int loss_kind, float* loss, float* coef, void* workspace,
+                  size_t workspace_bytes, void* stream) {
+  if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_fwd")) return rc;
+  if (loss_kind != 0 && loss_kind != 1) return fail(PPGAT_ERR_INVALID, "bpr_fwd: loss_kind must be 0 (bpr) or 1 (bce)");
+  if (!loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_fwd: null output");
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_users + n_items, n_samples, channels))
+    return fail(PPGAT_ERR_INVALID, "bpr_fwd: workspace too small");
+  hipError_t e = ppgat::bpr_fwd(Z, n_users, n_items, channels, u, i, j, n_samples, loss_kind, loss, coef, workspace,
+                                static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "bpr_fwd");
+  return PPGAT_OK;
+}
+
+int ppgat_bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int channels, const int64_t* u, const int64_t* i,
+                  const int64_t* j, int64_t n_samples, const float* coef, const float* grad_loss, float* grad_Z,
+                  void* workspace, size_t workspace_bytes, void* stream) {
+  if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_bwd")) return rc;
+  if (!grad_Z || !grad_loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_bwd: null pointer");
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_users + n_items, n_samples, channels))
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd: workspace too small");
+  hipError_t e = ppgat::bpr_bwd(Z, n_users, n_items, channels, u, i, j, n_samples, coef, grad_loss, grad_Z, workspace,
+                                workspace_bytes, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "bpr_bwd");
+  return PPGAT_OK;
+}
+
+int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, size_t* bytes) {
+  if (!bytes || n < 0 || m < 1 || k < 1) return fail(PPGAT_ERR_INVALID, "gemm_tn_workspace_bytes: bad arguments");
+  *bytes = ppgat::gemm_tn_workspace_bytes(n, m, k);
+  return PPGAT_OK;
+}
+
+int ppgat_gemm_tn(const float* A, const float* B, int64_t n, int m, int k, float* out, float* colsum,
+                  void* workspace, size_t workspace_bytes, void* stream) {
+  if (n < 0 || m < 1 || k < 1) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad sizes");
+  if (!out || (n > 0 && (!A || !B))) return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
+  if (!workspace || workspace_bytes < ppgat::gemm_tn_workspace_bytes(n, m, k))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = ppgat::gemm_tn(A, B, n, m, k, out, colsum, workspace, st);
+  if (e != hipSuccess) return hip_fail(e, "gemm_tn");
+  return PPGAT_OK;
+}
+
 int ppgat_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
   g_prof.on = on != 0;

@@ -1,0 +1,460 @@
+// ppgat_train.hip -- the rest of the training step around the GAT layers, for CDNA4.
+//
+//  * BPR / BCE loss over sampled triples (scripts/train_gat_pyg.py:313-322): fused gather
+//    of U[u], I[i], I[j] + dot products + loss terms (forward), and the gradient
+//    dZ = A Z where A has 4 nonzeros per triple, computed deterministically by sorting
+//    the 4S contributions by destination row and summing fixed 32-entry chunks with an
+//    ordered fix-up for rows that span chunks (no float atomics).
+//  * dW = A^T B for tall-skinny fp32 operands (A [N,M], B [N,K], N ~ 10^5..10^7, M,K <= 1024):
+//    the weight gradient of every projection (GATConv.lin, item_proj).  hipBLASLt picks a
+//    16-workgroup tile for this shape; here N is split over ~512 workgroups, each
+//    accumulating a 128x128 tile with v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains),
+//    followed by an ordered reduction of the split partials.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <stdint.h>
+#include <math.h>
+
+#include "ppgat_internal.h"
+
+namespace ppgat {
+
+namespace {
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+__device__ __forceinline__ float4 fma4(float s, float4 v, float4 a) {
+  return make_float4(fmaf(s, v.x, a.x), fmaf(s, v.y, a.y), fmaf(s, v.z, a.z), fmaf(s, v.w, a.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+unsigned key_bits(int64_t n) {
+  unsigned b = 1;
+  while (b < 31 && ((int64_t)1 << b) < n) ++b;
+  return b;
+}
+
+__device__ __forceinline__ int64_t clamp_idx(int64_t v, int64_t n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+
+// ---------------------------------------------------------------------------
+// BPR forward: one subgroup (C/4 lanes) per triple.
+//   pos = <U[u], I[i]>, neg = <U[u], I[j]>
+//   bpr: l = -log(sigmoid(pos - neg) + 1e-8); dl/dpos = -dl/dneg = -s(1-s)/(s+1e-8)/S
+//   bce: l = bce_logits(pos, 1) + bce_logits(neg, 0); dl/dpos = (s(pos)-1)/2S, dl/dneg = s(neg)/2S
+// coef[t] = {dl/dpos, dl/dneg} (before the upstream scalar grad); per-block loss sums.
+// ---------------------------------------------------------------------------
+template <int C>
+__global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, int64_t n_users, int64_t n_items,
+                                                 const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
+                                                 const int64_t* __restrict__ jj, int64_t S, int kind,
+                                                 float2* __restrict__ coef, float* __restrict__ block_loss) {
+  constexpr int LPR = C / 4;
+  constexpr int SPB = 256 / LPR;  // subgroups (triples) per block
+  __shared__ float sl_loss[SPB];
+  const int tid = threadIdx.x;
+  const int sg = tid / LPR, sl = tid % LPR;
+  const int64_t t = (int64_t)blockIdx.x * SPB + sg;
+  const bool valid = t < S;
+  float pos = 0.f, neg = 0.f;
+  if (valid) {
+    const int64_t ur = clamp_idx(u[t], n_users);
+    const int64_t ir = n_users + clamp_idx(ii[t], n_items);
+    const int64_t jr = n_users + clamp_idx(jj[t], n_items);
+    const float4 a = ld4(Z + ur * C + sl * 4);
+    pos = dot4(a, ld4(Z + ir * C + sl * 4));
+    neg = dot4(a, ld4(Z + jr * C + sl * 4));
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) {
+    pos += __shfl_xor(pos, off);
+    neg += __shfl_xor(neg, off);
+  }
+  if (sl == 0) {
+    float l = 0.f;
+    float2 cf = make_float2(0.f, 0.f);
+    if (valid) {
+      if (kind == 0) {
+        const float x = pos - neg;
+        const float s = 1.f / (1.f + expf(-x));
+        l = -logf(s + 1e-8f);
+        const float d = -(s * (1.f - s)) / (s + 1e-8f) / (float)S;
+        cf = make_float2(d, -d);
+      } else {
+        const float sp = 1.f / (1.f + expf(-pos)), sn = 1.f / (1.f + expf(-neg));
+        l = (fmaxf(pos, 0.f) - pos + log1pf(expf(-fabsf(pos)))) + (fmaxf(neg, 0.f) + log1pf(expf(-fabsf(neg))));
+        cf = make_float2((sp - 1.f) / (2.f * S), sn / (2.f * S));
+      }
+      coef[t] = cf;
+    }
+    sl_loss[sg] = l;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int k = 0; k < SPB; ++k) s += sl_loss[k];
+    block_loss[blockIdx.x] = s;
+  }
+}
+
+// ordered sum of the block losses -> loss (mean)
+__global__ void __launch_bounds__(256) k_bpr_loss(const float* __restrict__ block_loss, int64_t nb, float denom,
+                                                  float* __restrict__ loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t b = threadIdx.x; b < nb; b += 256) s += block_loss[b];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / denom;
+}
+
+// contribution c = 4t + kind -> destination row (sort key)
+__global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
+                           const int64_t* __restrict__ jj, int64_t S, int64_t n_users, int64_t n_items,
+                           int32_t* __restrict__ key, int32_t* __restrict__ val) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 4 * S) return;
+  const int64_t t = c >> 2;
+  const int kd = (int)(c & 3);
+  int64_t d;
+  if (kd < 2) d = clamp_idx(u[t], n_users);
+  else if (kd == 2) d = n_users + clamp_idx(ii[t], n_items);
+  else d = n_users + clamp_idx(jj[t], n_items);
+  key[c] = (int32_t)d;
+  val[c] = (int32_t)c;
+}
+
+// ---------------------------------------------------------------------------
+// BPR backward, chunk pass: a subgroup owns 32 consecutive sorted contributions.
+// Segments (runs of one destination row) complete inside the chunk are written to dZ;
+// a segment touching the chunk start while continuing from the previous chunk goes to
+// slot "head"; one touching the chunk end and continuing goes to slot "tail".
+// ---------------------------------------------------------------------------
+constexpr int kChunk = 32;
+
+template <int C>
+__global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ skey, const int32_t* __restrict__ scid,
+                                                    int64_t total, const int64_t* __restrict__ u,
+                                                    const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
+                                                    int64_t n_users, int64_t n_items,
+                                                    const float2* __restrict__ coef,
+                                                    const float* __restrict__ grad_loss, const float* __restrict__ Z,
+                                                    float* __restrict__ dZ, float* __restrict__ slots) {
+  constexpr int LPR = C / 4;
+  constexpr int SPB = 256 / LPR;
+  __shared__ int32_t s_src[SPB][kChunk];
+  __shared__ int32_t s_dst[SPB][kChunk];
+  __shared__ float s_cf[SPB][kChunk];
+  const int tid = threadIdx.x;
+  const int sg = tid / LPR, sl = tid % LPR;
+  const int64_t ch = (int64_t)blockIdx.x * SPB + sg;
+  const int64_t b0 = ch * kChunk;
+  const float g = grad_loss[0];
+  if (b0 < total) {
+    for (int q = sl; q < kChunk; q += LPR) {
+      const int64_t p = b0 + q;
+      int32_t src = 0, dst = -1;
+      float cf = 0.f;
+      if (p < total) {
+        const int32_t c = scid[p];
+        const int64_t t = c >> 2;
+        const int kd = c & 3;
+        const float2 tc = coef[t];
+        dst = skey[p];
+        if (kd == 0) { src = (int32_t)(n_users + clamp_idx(ii[t], n_items)); cf = tc.x; }
+        else if (kd == 1) { src = (int32_t)(n_users + clamp_idx(jj[t], n_items)); cf = tc.y; }
+        else { src = (int32_t)clamp_idx(u[t], n_users); cf = kd == 2 ? tc.x : tc.y; }
+      }
+      s_src[sg][q] = src;
+      s_dst[sg][q] = dst;
+      s_cf[sg][q] = cf * g;
+    }
+  }
+  __syncthreads();
+  if (b0 >= total) return;
+  const int len = (int)min((int64_t)kChunk, total - b0);
+  const bool starts_before = b0 > 0 && skey[b0 - 1] == s_dst[sg][0];
+  const bool ends_after = b0 + len < total && skey[b0 + len] == s_dst[sg][len - 1];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int seg_start = 0;
+  constexpr int U = 4;
+  for (int q0 = 0; q0 < len; q0 += U) {
+    float4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int q = q0 + k;
+      v[k] = q < len ? ld4(Z + (int64_t)s_src[sg][q] * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int q = q0 + k;
+      if (q >= len) break;
+      acc = fma4(s_cf[sg][q], v[k], acc);
+      const bool last_of_seg = q == len - 1 || s_dst[sg][q + 1] != s_dst[sg][q];
+      if (last_of_seg) {
+        const int32_t r = s_dst[sg][q];
+        const bool first = seg_start == 0, last = q == len - 1;
+        if (first && starts_before) st4(slots + (ch * 2 + 0) * C + sl * 4, acc);
+        else if (last && ends_after) st4(slots + (ch * 2 + 1) * C + sl * 4, acc);
+        else st4(dZ + (int64_t)r * C + sl * 4, acc);
+        acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        seg_start = q + 1;
+      }
+    }
+  }
+}
+
+// Fix-up: the chunk in which a chunk-spanning segment starts sums its tail slot and the
+// head slots of the following chunks, in chunk order, and writes the row.
+template <int C>
+__global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ skey, int64_t total,
+                                                   const float* __restrict__ slots, float* __restrict__ dZ) {
+  constexpr int LPR = C / 4;
+  constexpr int SPB = 256 / LPR;
+  const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
+  const int64_t ch = (int64_t)blockIdx.x * SPB + sg;
+  const int64_t b0 = ch * kChunk;
+  if (b0 >= total) return;
+  const int64_t b1 = min(b0 + kChunk, total);
+  if (b1 >= total) return;
+  const int32_t r = skey[b1 - 1];
+  if (skey[b1] != r) return;                           // last segment does not continue
+  if (skey[b0] == r && b0 > 0 && skey[b0 - 1] == r) return;  // segment started in an earlier chunk
+  float4 acc = ld4(slots + (ch * 2 + 1) * C + sl * 4);
+  for (int64_t c2 = ch + 1;; ++c2) {
+    const int64_t e0 = c2 * kChunk;
+    const int64_t e1 = min(e0 + kChunk, total);
+    acc = add4(acc, ld4(slots + (c2 * 2 + 0) * C + sl * 4));
+    if (!(skey[e1 - 1] == r && e1 < total && skey[e1] == r)) break;
+  }
+  st4(dZ + (int64_t)r * C + sl * 4, acc);
+}
+
+// ---------------------------------------------------------------------------
+// dW = A^T B.  Block = 256 threads (4 waves) -> 128x128 output tile over rows
+// [n0, n1) of A and B; wave (wm, wk) owns a 64x64 sub-tile = 2x2 MFMA 32x32 tiles.
+// LDS stages of 32 rows x 128 columns of A and B (16 KB each), double-buffered.
+// v_mfma_f32_32x32x2_f32 lane maps: A operand A'[i=l&31][k=l>>5] = A[n+(l>>5)][m0+(l&31)],
+// B operand B'[k=l>>5][j=l&31] = B[n+(l>>5)][k0+(l&31)]; C/D: col = l&31,
+// row = (r&3) + 8*(r>>2) + 4*(l>>5) for r in [0,16).
+// ---------------------------------------------------------------------------
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+constexpr int kTN = 128;  // output tile edge
+constexpr int kNB = 32;   // rows per LDS stage
+
+__global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, const float* __restrict__ B, int64_t N,
+                                                 int M, int K, int64_t rows_per_split, float* __restrict__ part,
+                                                 float* __restrict__ colsum_part) {
+  __shared__ float sA[2][kNB][kTN];
+  __shared__ float sB[2][kNB][kTN];
+  const int tiles_k = (K + kTN - 1) / kTN;
+  const int tile = blockIdx.x;
+  const int split = blockIdx.y;
+  const int m0 = (tile / tiles_k) * kTN, k0 = (tile % tiles_k) * kTN;
+  const int64_t n_beg = (int64_t)split * rows_per_split;
+  const int64_t n_end = min(N, n_beg + rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wk = w & 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float csum = 0.f;  // colsum of A for column m0 + tid (tid < 128), waves 0-1 only
+  // stage loader: 32 rows x 128 cols = 1024 float4 per operand; 256 threads x 4
+  auto load_stage = [&](int buf, int64_t n0) {
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int idx = pass * 256 + tid;  // float4 index within the stage
+      const int r = idx >> 5, c4 = (idx & 31) * 4;
+      const int64_t n = n0 + r;
+      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      if (n < n_end) {
+        if (m0 + c4 + 3 < M) va = ld4(A + n * M + m0 + c4);
+        else {
+          float t[4] = {0.f, 0.f, 0.f, 0.f};
+          for (int e = 0; e < 4; ++e) if (m0 + c4 + e < M) t[e] = A[n * M + m0 + c4 + e];
+          va = make_float4(t[0], t[1], t[2], t[3]);
+        }
+        if (k0 + c4 + 3 < K) vb = ld4(B + n * K + k0 + c4);
+        else {
+          float t[4] = {0.f, 0.f, 0.f, 0.f};
+          for (int e = 0; e < 4; ++e) if (k0 + c4 + e < K) t[e] = B[n * K + k0 + c4 + e];
+          vb = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+      *reinterpret_cast<float4*>(&sA[buf][r][c4]) = va;
+      *reinterpret_cast<float4*>(&sB[buf][r][c4]) = vb;
+    }
+  };
+  int buf = 0;
+  if (n_beg < n_end) load_stage(0, n_beg);
+  __syncthreads();
+  for (int64_t n0 = n_beg; n0 < n_end; n0 += kNB) {
+    if (n0 + kNB < n_end) load_stage(buf ^ 1, n0 + kNB);
+#pragma unroll 4
+    for (int kk = 0; kk < kNB; kk += 2) {
+      const int r = kk + (lane >> 5);
+      const float a0 = sA[buf][r][wm * 64 + (lane & 31)];
+      const float a1 = sA[buf][r][wm * 64 + 32 + (lane & 31)];
+      const float b0 = sB[buf][r][wk * 64 + (lane & 31)];
+      const float b1 = sB[buf][r][wk * 64 + 32 + (lane & 31)];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (colsum_part != nullptr && k0 == 0 && tid < kTN) {
+      for (int r = 0; r < kNB; ++r) csum += sA[buf][r][tid];
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  // write the split partial tile: part[split][M][K]
+  float* P = part + (int64_t)split * M * K;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = k0 + wk * 64 + b * 32 + (lane & 31);
+        if (row < M && col < K) P[(int64_t)row * K + col] = acc[a][b][r];
+      }
+  if (colsum_part != nullptr && k0 == 0 && tid < kTN && m0 + tid < M)
+    colsum_part[(int64_t)split * M + m0 + tid] = csum;
+}
+
+// out[e] = sum_s part[s][e] in split order
+__global__ void __launch_bounds__(256) k_split_reduce(const float* __restrict__ part, int64_t splits, int64_t elems,
+                                                      float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= elems) return;
+  float s = 0.f;
+  for (int64_t k = 0; k < splits; ++k) s += part[k * elems + e];
+  out[e] = s;
+}
+
+}  // namespace
+
+#define PPGAT_DISPATCH_LOSS_C(C_, ...)                         \
+  switch (C_) {                                                \
+    case 32: { constexpr int CC = 32; __VA_ARGS__; break; }    \
+    case 64: { constexpr int CC = 64; __VA_ARGS__; break; }    \
+    case 128: { constexpr int CC = 128; __VA_ARGS__; break; }  \
+    case 256: { constexpr int CC = 256; __VA_ARGS__; break; }  \
+    default: return hipErrorInvalidValue;                      \
+  }
+
+bool bpr_channels_ok(int C) { return C == 32 || C == 64 || C == 128 || C == 256; }
+
+static int64_t bpr_fwd_blocks(int64_t S, int C) { return (S + 256 / (C / 4) - 1) / (256 / (C / 4)); }
+
+static size_t bpr_sort_temp(int64_t S, int64_t N) {
+  size_t b = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                                  (int32_t*)nullptr, (size_t)(4 * S > 0 ? 4 * S : 1), 0u, key_bits(N));
+  return b;
+}
+
+// workspace: block_loss | keys | vals | skeys | scid | slots | sort temp
+size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
+  const int64_t c4 = 4 * S > 0 ? 4 * S : 1;
+  const int64_t chunks = (c4 + kChunk - 1) / kChunk;
+  return align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4) + 4 * align_up((size_t)c4 * 4) +
+         align_up((size_t)chunks * 2 * C * 4) + align_up(bpr_sort_temp(S, N));
+}
+
+hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
+                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, void* ws, hipStream_t st) {
+  float* block_loss = static_cast<float*>(ws);
+  const int64_t nb = bpr_fwd_blocks(S, C);
+  if (S > 0) {
+    PPGAT_DISPATCH_LOSS_C(C, hipLaunchKernelGGL(k_bpr_fwd<CC>, dim3((unsigned)nb), dim3(256), 0, st, Z, n_users,
+                                                n_items, u, i, j, S, kind, reinterpret_cast<float2*>(coef),
+                                                block_loss));
+  }
+  const float denom = kind == 0 ? (float)S : 2.f * (float)S;
+  hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(256), 0, st, block_loss, S > 0 ? nb : 0, denom > 0 ? denom : 1.f,
+                     loss);
+  return hipGetLastError();
+}
+
+hipError_t bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
+                   const int64_t* j, int64_t S, const float* coef, const float* grad_loss, float* dZ, void* ws,
+                   size_t ws_bytes, hipStream_t st) {
+  const int64_t N = n_users + n_items;
+  hipError_t err = hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);
+  if (err != hipSuccess || S == 0) return err;
+  const int64_t total = 4 * S;
+  const int64_t chunks = (total + kChunk - 1) / kChunk;
+  char* p = static_cast<char*>(ws) + align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4);
+  const size_t e4 = align_up((size_t)total * 4);
+  int32_t* keys = reinterpret_cast<int32_t*>(p);
+  int32_t* vals = reinterpret_cast<int32_t*>(p + e4);
+  int32_t* skeys = reinterpret_cast<int32_t*>(p + 2 * e4);
+  int32_t* scid = reinterpret_cast<int32_t*>(p + 3 * e4);
+  float* slots = reinterpret_cast<float*>(p + 4 * e4);
+  void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
+  size_t tmp_bytes = ws_bytes - (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws));
+  hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
+                     n_items, keys, vals);
+  err = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, vals, scid, (size_t)total, 0u, key_bits(N), st);
+  if (err != hipSuccess) return err;
+  PPGAT_DISPATCH_LOSS_C(C, {
+    constexpr int SPB = 256 / (CC / 4);
+    const unsigned g = (unsigned)((chunks + SPB - 1) / SPB);
+    hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, skeys, scid, total, u, i, j, n_users, n_items,
+                       reinterpret_cast<const float2*>(coef), grad_loss, Z, dZ, slots);
+    hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, dZ);
+  });
+  return hipGetLastError();
+}
+
+// ---- dW = A^T B ----
+static int64_t gemm_splits(int64_t N, int M, int K) {
+  const int64_t tiles = (int64_t)((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
+  int64_t s = 512 / tiles;
+  if (s < 1) s = 1;
+  const int64_t max_s = (N + 255) / 256;  // >= 256 rows per split
+  if (s > max_s) s = max_s;
+  if (s < 1) s = 1;
+  return s;
+}
+
+size_t gemm_tn_workspace_bytes(int64_t N, int M, int K) {
+  const int64_t s = gemm_splits(N, M, K);
+  return align_up((size_t)s * M * K * 4) + align_up((size_t)s * M * 4);
+}
+
+hipError_t gemm_tn(const float* A, const float* B, int64_t N, int M, int K, float* out, float* colsum, void* ws,
+                   hipStream_t st) {
+  const int64_t s = gemm_splits(N, M, K);
+  const int64_t rows = ((N + s - 1) / s + kNB - 1) / kNB * kNB;
+  float* part = static_cast<float*>(ws);
+  float* cpart = colsum ? reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)s * M * K * 4)) : nullptr;
+  const int tiles = ((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
+  hipLaunchKernelGGL(k_gemm_tn, dim3((unsigned)tiles, (unsigned)s), dim3(256), 0, st, A, B, N, M, K, rows, part,
+                     cpart);
+  const int64_t elems = (int64_t)M * K;
+  hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, st, part, s, elems, out);
+  if (colsum)
+    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, cpart, s, (int64_t)M,
+                       colsum);
+  return hipGetLastError();
+}
+
+}  // namespace ppgat

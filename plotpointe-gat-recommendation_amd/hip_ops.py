@@ -282,3 +282,105 @@ class GATAggregate(torch.autograd.Function):
 
 def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p=0.0, seed=0):
     return GATAggregate.apply(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
+
+
+# ---------------------------------------------------------------------------
+# projection with the MFMA weight-gradient kernel, and the fused BPR/BCE loss
+# ---------------------------------------------------------------------------
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False):
+    """A [N,M], B [N,K] -> (A^T B [M,K], colsum(A) [M] or None), deterministic."""
+    lib = _lib.load()
+    _check_dev("A", A, torch.float32)
+    _check_dev("B", B, torch.float32, A.device)
+    _require(A.dim() == 2 and B.dim() == 2 and A.size(0) == B.size(0), "gemm_tn: A [N,M], B [N,K]")
+    N, M, K = A.size(0), A.size(1), B.size(1)
+    out = torch.empty(M, K, dtype=torch.float32, device=A.device)
+    cs = torch.empty(M, dtype=torch.float32, device=A.device) if want_colsum else None
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_gemm_tn_workspace_bytes(N, M, K, ctypes.byref(nbytes)), "gemm_tn_workspace_bytes")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=A.device)
+    _lib.check(lib.ppgat_gemm_tn(A.data_ptr(), B.data_ptr(), N, M, K, out.data_ptr(), _lib.ptr(cs), ws.data_ptr(),
+                                 nbytes.value, _lib.stream_handle(A.device)), "gemm_tn")
+    return out, cs
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T + b.  Forward and dx through the BLAS library GEMM (square, well-shaped);
+    dW (and db) through ppgat_gemm_tn (N = 10^5..10^7 rows split over the chip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = x.contiguous()
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        g = g.contiguous()
+        dx = g @ weight if ctx.needs_input_grad[0] else None
+        dW = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dW, db = gemm_tn(g, x, want_colsum=ctx.has_bias)
+        return dx, dW, db if ctx.has_bias else None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _require(x.is_cuda, "linear: ppgat runs on ROCm devices only; there is no CPU path")
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise NotImplementedError("ppgat linear: fp32 2-D input only")
+    return _Linear.apply(x, weight, bias)
+
+
+LOSS_KINDS = {"bpr": 0, "bce": 1}
+
+
+class _BPRLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Z, u, i, j, n_users: int, kind: int):
+        lib = _lib.load()
+        Z = Z.contiguous()
+        _check_dev("Z", Z, torch.float32)
+        N, C = Z.shape
+        n_items = N - n_users
+        S = u.numel()
+        u, i, j = (t.contiguous().to(torch.int64) for t in (u, i, j))
+        for name, t, hi in (("u", u, n_users), ("i", i, n_items), ("j", j, n_items)):
+            _check_dev(name, t, torch.int64, Z.device)
+            if S:
+                torch._assert_async(((t >= 0) & (t < hi)).all(), f"bpr: {name} index out of range")
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_bpr_workspace_bytes(N, S, C, ctypes.byref(nbytes)), "bpr_workspace_bytes")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=Z.device)
+        loss = torch.empty(1, dtype=torch.float32, device=Z.device)
+        coef = torch.empty(max(S, 1), 2, dtype=torch.float32, device=Z.device)
+        _lib.check(lib.ppgat_bpr_fwd(Z.data_ptr(), n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S,
+                                     kind, loss.data_ptr(), coef.data_ptr(), ws.data_ptr(), nbytes.value,
+                                     _lib.stream_handle(Z.device)), "bpr_fwd")
+        ctx.save_for_backward(Z, u, i, j, coef)
+        ctx.ws = ws
+        ctx.meta = (n_users, n_items, C, S)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, gl):
+        lib = _lib.load()
+        Z, u, i, j, coef = ctx.saved_tensors
+        n_users, n_items, C, S = ctx.meta
+        gl = gl.reshape(1).to(torch.float32).contiguous()
+        dZ = torch.empty_like(Z)
+        ws = ctx.ws
+        _lib.check(lib.ppgat_bpr_bwd(Z.data_ptr(), n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S,
+                                     coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(), ws.numel(),
+                                     _lib.stream_handle(Z.device)), "bpr_bwd")
+        ctx.ws = None
+        return dZ, None, None, None, None, None
+
+
+def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch.Tensor:
+    """Fused loss of train_gat_pyg.py:313-322 (``loss`` in {"bpr", "bce"})."""
+    _require(Z.is_cuda, "bpr_loss: ppgat runs on ROCm devices only; there is no CPU path")
+    if Z.size(1) not in (32, 64, 128, 256):
+        raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), LOSS_KINDS[loss])

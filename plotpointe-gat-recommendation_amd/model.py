@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import torch
 
+from . import hip_ops
 from .conv import GATConv, SimpleGATLayer
 
 
@@ -29,7 +30,7 @@ class PyGGAT(torch.nn.Module):
 
     def node_features(self, item_feats: torch.Tensor) -> torch.Tensor:
         u = self.user_emb.weight
-        v = self.item_proj(item_feats)
+        v = hip_ops.linear(item_feats, self.item_proj.weight, self.item_proj.bias)
         return torch.cat([u, v], dim=0)
 
     def forward(self, item_feats: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
@@ -50,7 +51,7 @@ class CustomGAT(torch.nn.Module):
 
     def node_features(self, item_feats: torch.Tensor) -> torch.Tensor:
         u = self.user_emb.weight
-        v = self.item_proj(item_feats)
+        v = hip_ops.linear(item_feats, self.item_proj.weight, self.item_proj.bias)
         return torch.cat([u, v], dim=0)
 
     def forward(self, item_feats: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
@@ -61,13 +62,6 @@ class CustomGAT(torch.nn.Module):
 
 
 def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch.Tensor:
-    """Loss of the train step, scripts/train_gat_pyg.py:313-322."""
-    U = Z[:n_users]
-    I = Z[n_users:]
-    pos = (U[u] * I[i]).sum(dim=-1)
-    neg = (U[u] * I[j]).sum(dim=-1)
-    if loss == "bpr":
-        return -torch.log(torch.sigmoid(pos - neg) + 1e-8).mean()
-    logits = torch.cat([pos, neg], dim=0)
-    labels = torch.cat([torch.ones_like(pos), torch.zeros_like(neg)], dim=0)
-    return torch.nn.functional.binary_cross_entropy_with_logits(logits, labels)
+    """Loss of the train step, scripts/train_gat_pyg.py:313-322 (BPR or BCE), fused on the
+    device (ppgat_bpr_fwd / ppgat_bpr_bwd)."""
+    return hip_ops.bpr_loss(Z, n_users, u, i, j, loss)
