@@ -126,7 +126,8 @@ int ppgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t
  *           backward; 34%+25%+11.5% of the reference CPU step).
  * src_sched: schedule over the CSC by source (colptr).  Given grad_out [N,C] returns
  * grad_h [N,H,C] (message term plus the attention-logit terms ds_src (x) att_src +
- * ds_dst (x) att_dst) and grad_att_src/grad_att_dst [H,C].  Atomic-free and
+ * ds_dst (x) att_dst), grad_att_src/grad_att_dst [H,C] and, when grad_bias != NULL,
+ * grad_bias [C] = column sums of grad_out.  Atomic-free and
  * deterministic (segment-owned sums in a fixed order).  agg may be NULL when heads == 1
  * (out - bias is used).
  */
@@ -140,7 +141,7 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
               const float* out, const float* agg, const float* m, const float* inv_l,
               const float* grad_out,
               int mode, float negative_slope, float dropout_p, uint64_t seed,
-              float* grad_h, float* grad_att_src, float* grad_att_dst,
+              float* grad_h, float* grad_att_src, float* grad_att_dst, float* grad_bias,
               void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- loss of the training step ---------------------------------------------
@@ -152,12 +153,14 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
  * Forward writes the scalar mean loss and coef [S, 2] (dloss/dpos, dloss/dneg); the
  * backward writes the full grad_Z [N, C] (zero rows included) = grad_loss * sum of the
  * per-triple contributions, deterministically (sorted contributions, ordered sums).
- * Indices outside their range are clamped (the caller validates them).
+ * Indices outside their range are clamped and counted into bad_count (device int32[1],
+ * nullable; zeroed by the call) so the caller can raise without a host sync here.
  */
 int ppgat_bpr_workspace_bytes(int64_t n_nodes, int64_t n_samples, int channels, size_t* bytes);
 int ppgat_bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int channels,
                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, int loss_kind,
-                  float* loss, float* coef, void* workspace, size_t workspace_bytes, void* stream);
+                  float* loss, float* coef, int32_t* bad_count, void* workspace, size_t workspace_bytes,
+                  void* stream);
 int ppgat_bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int channels,
                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
                   const float* coef, const float* grad_loss, float* grad_Z,

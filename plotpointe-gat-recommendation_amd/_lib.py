@@ -44,11 +44,11 @@ SIGNATURES = {
                           c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_bwd_workspace_bytes": (c_int, [c_i64, c_i64, c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_bwd": (c_int, [SP, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
-                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_sz,
-                          c_vp]),
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                          c_sz, c_vp]),
     "ppgat_bpr_workspace_bytes": (c_int, [c_i64, c_i64, c_int, ctypes.POINTER(c_sz)]),
-    "ppgat_bpr_fwd": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_sz,
-                              c_vp]),
+    "ppgat_bpr_fwd": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp,
+                              c_sz, c_vp]),
     "ppgat_bpr_bwd": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz,
                               c_vp]),
     "ppgat_gemm_tn_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),

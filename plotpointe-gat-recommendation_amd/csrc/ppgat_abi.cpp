@@ -218,7 +218,7 @@ int ppgat_fwd(const ppgat_schedule* sched, const int32_t* col, const int32_t* cs
   return PPGAT_OK;
 }
 
-// workspace: nstate [N*H float4] | ds_src [N*H] | dz [E*H] | block partial [blocks*2*H*C] | hub partial
+// workspace: nstate [N*H float4] | ds_src [N*H] | dz [E*H] | block partial [blocks*(2*H*C + C)] | hub partial
 int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int64_t n_hub_items, int heads, int channels,
                               size_t* bytes) {
   if (!bytes || n_nodes < 0 || n_edges < 0 || n_hub_items < 0 || heads < 1 || channels < 1)
@@ -226,7 +226,7 @@ int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int64_t n_hub_it
   const size_t ns = align_up((size_t)n_nodes * heads * 16 + 16);
   const size_t nh = align_up((size_t)n_nodes * heads * 4 + 4);
   const size_t eh = align_up((size_t)n_edges * heads * 4 + 4);
-  const size_t part = align_up((size_t)ppgat::epi_blocks(n_nodes) * 2 * heads * channels * 4);
+  const size_t part = align_up((size_t)ppgat::epi_blocks(n_nodes) * (2 * heads + 1) * channels * 4);
   *bytes = ns + nh + eh + part + partial_bytes(n_hub_items, heads, channels);
   return PPGAT_OK;
 }
@@ -236,7 +236,7 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
               const float* s_src, const float* s_dst, const float* att_src, const float* att_dst, const float* bias,
               const float* out, const float* agg, const float* m, const float* inv_l, const float* grad_out, int mode,
               float negative_slope, float dropout_p, uint64_t seed, float* grad_h, float* grad_att_src,
-              float* grad_att_dst, void* workspace, size_t workspace_bytes, void* stream) {
+              float* grad_att_dst, float* grad_bias, void* workspace, size_t workspace_bytes, void* stream) {
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd: unsupported channels");
   if (heads < 1 || n_nodes < 0 || n_edges < 0) return fail(PPGAT_ERR_INVALID, "bwd: bad sizes");
   if (int rc = check_mode(mode, heads, bias, dropout_p)) return rc;
@@ -255,13 +255,14 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
   const size_t nh = align_up((size_t)n_nodes * heads * 4 + 4);
   const size_t eh = align_up((size_t)n_edges * heads * 4 + 4);
   const int64_t blocks = ppgat::epi_blocks(n_nodes);
-  const size_t part = align_up((size_t)blocks * 2 * heads * channels * 4);
+  const size_t part = align_up((size_t)blocks * (2 * heads + 1) * channels * 4);
   char* p = static_cast<char*>(workspace);
   float* nstate = reinterpret_cast<float*>(p);
   float* ds_src = reinterpret_cast<float*>(p + ns);
   float* dz = reinterpret_cast<float*>(p + ns + nh);
   float* bpart = reinterpret_cast<float*>(p + ns + nh + eh);
   float* hpart = reinterpret_cast<float*>(p + ns + nh + eh + part);
+  float* bias_part = grad_bias ? bpart + (size_t)blocks * 2 * heads * channels : nullptr;
   const float gscale = mode == PPGAT_MODE_PYG ? 1.f / (float)heads : 1.f;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const ppgat::ItemsArg it{sched->item_row, sched->item_beg, sched->item_end, sched->n_items, sched->n_hub_items};
@@ -269,7 +270,7 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
   {
     Timed t(PPGAT_K_BWD_PRO, st);
     e = ppgat::launch_bwd_pro(grad_out, out, agg, heads == 1 ? bias : nullptr, s_dst, m, inv_l, n_nodes, heads,
-                              channels, gscale, nstate, st);
+                              channels, gscale, nstate, bias_part, blocks, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_prologue");
   {
@@ -287,7 +288,10 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
   if (e != hipSuccess) return hip_fail(e, "bwd_epilogue");
   {
     Timed t(PPGAT_K_BWD_RED, st);
-    e = ppgat::launch_bwd_red(bpart, blocks, heads * channels, grad_att_src, grad_att_dst, st);
+    e = ppgat::launch_col_reduce(bpart, blocks, 2 * heads * channels, heads * channels, grad_att_src, grad_att_dst,
+                                 st);
+    if (e == hipSuccess && grad_bias)
+      e = ppgat::launch_col_reduce(bias_part, blocks, channels, channels, grad_bias, nullptr, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_reduce");
   return PPGAT_OK;
@@ -312,15 +316,15 @@ static int check_bpr(int64_t n_users, int64_t n_items, int channels, int64_t S, 
 }
 
 int ppgat_bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int channels, const int64_t* u, const int64_t* i,
-                  const int64_t* j, int64_t n_samples, int loss_kind, float* loss, float* coef, void* workspace,
-                  size_t workspace_bytes, void* stream) {
+                  const int64_t* j, int64_t n_samples, int loss_kind, float* loss, float* coef, int32_t* bad_count,
+                  void* workspace, size_t workspace_bytes, void* stream) {
   if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_fwd")) return rc;
   if (loss_kind != 0 && loss_kind != 1) return fail(PPGAT_ERR_INVALID, "bpr_fwd: loss_kind must be 0 (bpr) or 1 (bce)");
   if (!loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_fwd: null output");
   if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_users + n_items, n_samples, channels))
     return fail(PPGAT_ERR_INVALID, "bpr_fwd: workspace too small");
-  hipError_t e = ppgat::bpr_fwd(Z, n_users, n_items, channels, u, i, j, n_samples, loss_kind, loss, coef, workspace,
-                                static_cast<hipStream_t>(stream));
+  hipError_t e = ppgat::bpr_fwd(Z, n_users, n_items, channels, u, i, j, n_samples, loss_kind, loss, coef, bad_count,
+                                workspace, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "bpr_fwd");
   return PPGAT_OK;
 }

@@ -29,7 +29,7 @@ hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid
                       hipStream_t st);
 hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
                           const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
-                          float* nstate, hipStream_t st);
+                          float* nstate, float* bias_part, int64_t blocks, hipStream_t st);
 hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
                           int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
                           int mode, float slope, float gscale, float p, uint64_t seed, float* dh, float* ds_src,
@@ -39,7 +39,8 @@ int64_t epi_blocks(int64_t n);
 hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
                           const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,
                           int64_t blocks, hipStream_t st);
-hipError_t launch_bwd_red(const float* partial, int64_t rows, int hc, float* das, float* dad, hipStream_t st);
+hipError_t launch_col_reduce(const float* partial, int64_t rows, int cols, int split, float* out_a, float* out_b,
+                             hipStream_t st);
 
 // graph preprocessing (ppgat_graph.hip)
 size_t csr_workspace_bytes(int64_t n_nodes, int64_t n_edges);
@@ -56,7 +57,8 @@ hipError_t schedule_build(const int32_t* ptr, int64_t N, int32_t T, int32_t* ite
 bool bpr_channels_ok(int C);
 size_t bpr_workspace_bytes(int64_t N, int64_t S, int C);
 hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
-                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, void* ws, hipStream_t st);
+                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, int32_t* bad, void* ws,
+                   hipStream_t st);
 hipError_t bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
                    const int64_t* j, int64_t S, const float* coef, const float* grad_loss, float* dZ, void* ws,
                    size_t ws_bytes, hipStream_t st);

@@ -268,41 +268,57 @@ __global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ h
 }
 
 // ---------------------------------------------------------------------------
-// Backward prologue, one subgroup per (n, h):
+// Backward prologue, one subgroup per (n, h), grid-stride over a fixed grid:
 //   D[n,h] = <g_n, agg[n,h]>, g = gscale * grad_out   (= sum_k alpha_k dalpha_k, Appendix B)
 // and the per-node state pass B gathers once per edge, packed as one float4:
 //   nstate[n,h] = {s_dst, m, inv_l, D}
+// When bias_part != NULL also the block partial column sums of grad_out (dbias), in a
+// fixed order (subgroups in order within a block, blocks reduced by k_col_reduce).
 // ---------------------------------------------------------------------------
 template <int C>
 __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_out, const float* __restrict__ out,
                                                  const float* __restrict__ agg, const float* __restrict__ bias,
                                                  const float* __restrict__ s_dst, const float* __restrict__ m_in,
                                                  const float* __restrict__ invl_in, int64_t pairs, int heads,
-                                                 float gscale, float4* __restrict__ nstate) {
+                                                 float gscale, float4* __restrict__ nstate,
+                                                 float* __restrict__ bias_part) {
   using G = Geo<C>;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t pr = t / G::LPR;
-  const int sl = (int)(t % G::LPR);
-  const bool valid = pr < pairs;
-  const int64_t n = valid ? pr / heads : 0;
-  float x = 0.f;
-  if (valid) {
-    const float4 g = ld4(grad_out + n * C + sl * 4);
-    float4 a;
-    if (agg != nullptr) {
-      a = ld4(agg + pr * C + sl * 4);
-    } else {
-      a = ld4(out + n * C + sl * 4);
-      if (bias != nullptr) {
-        const float4 b = ld4(bias + sl * 4);
-        a = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+  constexpr int SPB = 256 / G::LPR;
+  __shared__ float4 red[SPB][G::LPR];
+  const int sg = threadIdx.x / G::LPR, sl = threadIdx.x % G::LPR;
+  float4 bsum = f4(0.f);
+  for (int64_t pr0 = (int64_t)blockIdx.x * SPB; pr0 < pairs; pr0 += (int64_t)gridDim.x * SPB) {
+    const int64_t pr = pr0 + sg;
+    const bool valid = pr < pairs;
+    const int64_t n = valid ? pr / heads : 0;
+    float x = 0.f;
+    if (valid) {
+      const float4 g = ld4(grad_out + n * C + sl * 4);
+      if (pr % heads == 0) bsum = add4(bsum, g);
+      float4 a;
+      if (agg != nullptr) {
+        a = ld4(agg + pr * C + sl * 4);
+      } else {
+        a = ld4(out + n * C + sl * 4);
+        if (bias != nullptr) {
+          const float4 b = ld4(bias + sl * 4);
+          a = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+        }
       }
+      x = dot4(g, a);
     }
-    x = dot4(g, a);
-  }
 #pragma unroll
-  for (int off = G::LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
-  if (valid && sl == 0) nstate[pr] = make_float4(s_dst[pr], m_in[pr], invl_in[pr], x * gscale);
+    for (int off = G::LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (valid && sl == 0) nstate[pr] = make_float4(s_dst[pr], m_in[pr], invl_in[pr], x * gscale);
+  }
+  if (bias_part == nullptr) return;
+  red[sg][sl] = bsum;
+  __syncthreads();
+  for (int t = threadIdx.x; t < G::LPR; t += blockDim.x) {
+    float4 s = red[0][t];
+    for (int q = 1; q < SPB; ++q) s = add4(s, red[q][t]);
+    st4(bias_part + ((int64_t)blockIdx.x * G::LPR + t) * 4, s);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -502,11 +518,12 @@ __global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ row
   }
 }
 
-// Ordered reduction of the block partials: rows = blocks, cols = 2*H*C.
-// One 1024-thread block per 64 columns: wave w sums rows w, w+16, ...; then the 16
-// wave sums are added in wave order.
-__global__ void __launch_bounds__(1024) k_bwd_red(const float* __restrict__ partial, int64_t rows, int cols,
-                                                  float* __restrict__ datt_src, float* __restrict__ datt_dst) {
+// Ordered column reduction of block partials [rows, cols] -> out_a[0:split], out_b[0:cols-split].
+// One 1024-thread block per 64 columns: wave w sums rows w, w+16, ... (4 loads in flight);
+// then the 16 wave sums are added in wave order.
+__global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ partial, int64_t rows, int cols,
+                                                     int split, float* __restrict__ out_a,
+                                                     float* __restrict__ out_b) {
   __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -525,8 +542,8 @@ __global__ void __launch_bounds__(1024) k_bwd_red(const float* __restrict__ part
   if (wv == 0 && c < cols) {
     float t = 0.f;
     for (int k = 0; k < 16; ++k) t += red[k][lane];
-    const int hc = cols / 2;
-    (c < hc ? datt_src : datt_dst)[c % hc] = t;
+    if (c < split) out_a[c] = t;
+    else out_b[c - split] = t;
   }
 }
 
@@ -578,12 +595,11 @@ hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid
 
 hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
                           const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
-                          float* nstate, hipStream_t st) {
+                          float* nstate, float* bias_part, int64_t blocks, hipStream_t st) {
   const int64_t pairs = n * heads;
-  if (pairs == 0) return hipSuccess;
-  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_pro<CC>, dim3(blocks_for(pairs * (CC / 4))), dim3(256), 0, st, go,
-                                         out, agg, bias, sd, m, invl, pairs, heads, gscale,
-                                         reinterpret_cast<float4*>(nstate)));
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_pro<CC>, dim3((unsigned)blocks), dim3(256), 0, st, go, out, agg, bias,
+                                         sd, m, invl, pairs, heads, gscale, reinterpret_cast<float4*>(nstate),
+                                         bias_part));
   return hipGetLastError();
 }
 
@@ -624,9 +640,10 @@ hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, co
   return hipGetLastError();
 }
 
-hipError_t launch_bwd_red(const float* partial, int64_t rows, int hc, float* das, float* dad, hipStream_t st) {
-  const int cols = 2 * hc;
-  hipLaunchKernelGGL(k_bwd_red, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, partial, rows, cols, das, dad);
+hipError_t launch_col_reduce(const float* partial, int64_t rows, int cols, int split, float* out_a, float* out_b,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_col_reduce, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, partial, rows, cols, split,
+                     out_a, out_b);
   return hipGetLastError();
 }
 

@@ -54,7 +54,8 @@ template <int C>
 __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, int64_t n_users, int64_t n_items,
                                                  const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
                                                  const int64_t* __restrict__ jj, int64_t S, int kind,
-                                                 float2* __restrict__ coef, float* __restrict__ block_loss) {
+                                                 float2* __restrict__ coef, float* __restrict__ block_loss,
+                                                 int32_t* __restrict__ bad) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;  // subgroups (triples) per block
   __shared__ float sl_loss[SPB];
@@ -64,9 +65,13 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
   const bool valid = t < S;
   float pos = 0.f, neg = 0.f;
   if (valid) {
-    const int64_t ur = clamp_idx(u[t], n_users);
-    const int64_t ir = n_users + clamp_idx(ii[t], n_items);
-    const int64_t jr = n_users + clamp_idx(jj[t], n_items);
+    const int64_t u0 = u[t], i0 = ii[t], j0 = jj[t];
+    if (bad != nullptr && sl == 0 &&
+        (u0 < 0 || u0 >= n_users || i0 < 0 || i0 >= n_items || j0 < 0 || j0 >= n_items))
+      atomicAdd(bad, 1);  // integer count; indices are clamped below, the caller raises
+    const int64_t ur = clamp_idx(u0, n_users);
+    const int64_t ir = n_users + clamp_idx(i0, n_items);
+    const int64_t jr = n_users + clamp_idx(j0, n_items);
     const float4 a = ld4(Z + ur * C + sl * 4);
     pos = dot4(a, ld4(Z + ir * C + sl * 4));
     neg = dot4(a, ld4(Z + jr * C + sl * 4));
@@ -338,14 +343,20 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, co
     colsum_part[(int64_t)split * M + m0 + tid] = csum;
 }
 
-// out[e] = sum_s part[s][e] in split order
+// out[e] = sum_s part[s][e]: 8 interleaved partial sums (split s goes to sum s % 8, in
+// split order), then combined in a fixed order -- deterministic, 8 loads in flight.
 __global__ void __launch_bounds__(256) k_split_reduce(const float* __restrict__ part, int64_t splits, int64_t elems,
                                                       float* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= elems) return;
-  float s = 0.f;
-  for (int64_t k = 0; k < splits; ++k) s += part[k * elems + e];
-  out[e] = s;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t k = 0;
+  for (; k + 8 <= splits; k += 8) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] += part[(k + q) * elems + e];
+  }
+  for (int q = 0; k + q < splits; ++q) a[q] += part[(k + q) * elems + e];
+  out[e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 }  // namespace
@@ -379,13 +390,18 @@ size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
 }
 
 hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
-                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, void* ws, hipStream_t st) {
+                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, int32_t* bad, void* ws,
+                   hipStream_t st) {
   float* block_loss = static_cast<float*>(ws);
   const int64_t nb = bpr_fwd_blocks(S, C);
+  if (bad != nullptr) {
+    hipError_t e = hipMemsetAsync(bad, 0, sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+  }
   if (S > 0) {
     PPGAT_DISPATCH_LOSS_C(C, hipLaunchKernelGGL(k_bpr_fwd<CC>, dim3((unsigned)nb), dim3(256), 0, st, Z, n_users,
                                                 n_items, u, i, j, S, kind, reinterpret_cast<float2*>(coef),
-                                                block_loss));
+                                                block_loss, bad));
   }
   const float denom = kind == 0 ? (float)S : 2.f * (float)S;
   hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(256), 0, st, block_loss, S > 0 ? nb : 0, denom > 0 ? denom : 1.f,
@@ -427,7 +443,7 @@ hipError_t bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int C, cons
 // ---- dW = A^T B ----
 static int64_t gemm_splits(int64_t N, int M, int K) {
   const int64_t tiles = (int64_t)((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
-  int64_t s = 512 / tiles;
+  int64_t s = 256 / tiles;
   if (s < 1) s = 1;
   const int64_t max_s = (N + 255) / 256;  // >= 256 rows per split
   if (s > max_s) s = max_s;

@@ -218,7 +218,7 @@ def gat_fwd(g: CSRGraph, h, s_src, s_dst, bias, heads: int, channels: int, mode:
 
 
 def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, inv_l, grad_out, heads: int,
-            channels: int, mode: int, slope: float, dropout_p: float, seed: int):
+            channels: int, mode: int, slope: float, dropout_p: float, seed: int, want_bias_grad: bool = False):
     lib = _lib.load()
     N = g.n_nodes
     dev = h.device
@@ -226,6 +226,7 @@ def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, i
     grad_h = torch.empty(N, heads * channels, dtype=torch.float32, device=dev)
     datt_src = torch.empty(heads, channels, dtype=torch.float32, device=dev)
     datt_dst = torch.empty(heads, channels, dtype=torch.float32, device=dev)
+    dbias = torch.empty(channels, dtype=torch.float32, device=dev) if want_bias_grad else None
     nbytes = ctypes.c_size_t(0)
     sched = g.bwd_sched
     _lib.check(lib.ppgat_bwd_workspace_bytes(N, g.n_edges, sched.n_hub_items, heads, channels,
@@ -239,8 +240,8 @@ def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, i
                              att_dst.data_ptr(), _lib.ptr(bias), out.data_ptr(), _lib.ptr(agg), m.data_ptr(),
                              inv_l.data_ptr(), grad_out.data_ptr(), mode, float(slope), float(dropout_p),
                              int(seed) & (2**64 - 1), grad_h.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(),
-                             ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "gat_bwd")
-    return grad_h, datt_src, datt_dst
+                             _lib.ptr(dbias), ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "gat_bwd")
+    return grad_h, datt_src, datt_dst, dbias
 
 
 class GATAggregate(torch.autograd.Function):
@@ -272,10 +273,11 @@ class GATAggregate(torch.autograd.Function):
         h, att_src, att_dst, s_src, s_dst, out, m, inv_l, agg, bias = ctx.saved_tensors
         heads, channels, mode, slope, p, seed, has_bias, has_agg = ctx.meta
         grad_out = grad_out.contiguous()
-        grad_h, datt_src, datt_dst = gat_bwd(ctx.graph, h, s_src, s_dst, att_src, att_dst,
-                                             bias if has_bias else None, out, agg if has_agg else None, m, inv_l,
-                                             grad_out, heads, channels, mode, slope, p, seed)
-        dbias = grad_out.sum(0) if (has_bias and ctx.needs_input_grad[3]) else None
+        want_db = has_bias and ctx.needs_input_grad[3]
+        grad_h, datt_src, datt_dst, dbias = gat_bwd(ctx.graph, h, s_src, s_dst, att_src, att_dst,
+                                                    bias if has_bias else None, out, agg if has_agg else None, m,
+                                                    inv_l, grad_out, heads, channels, mode, slope, p, seed,
+                                                    want_bias_grad=want_db)
         return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
                 None, None, None, None, None, None, None)
 
@@ -336,6 +338,40 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 LOSS_KINDS = {"bpr": 0, "bce": 1}
 
 
+class _BadIndex:
+    """Out-of-range u/i/j are clamped on the device and counted; the count is copied to
+    pinned host memory asynchronously and checked at the next loss call (or by
+    ``check_bpr_indices()``), so the hot path never waits on the host."""
+    pending = []
+
+    @classmethod
+    def track(cls, bad: torch.Tensor):
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(bad, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        cls.pending.append((ev, host))
+
+    @classmethod
+    def raise_pending(cls, wait: bool = False):
+        keep = []
+        for ev, host in cls.pending:
+            if wait:
+                ev.synchronize()
+            if wait or ev.query():
+                if int(host.item()) != 0:
+                    cls.pending = []
+                    raise IndexError(f"bpr_loss: {int(host.item())} triples with u/i/j out of range")
+            else:
+                keep.append((ev, host))
+        cls.pending = keep
+
+
+def check_bpr_indices():
+    """Raise IndexError if any earlier bpr_loss call saw out-of-range indices (syncs)."""
+    _BadIndex.raise_pending(wait=True)
+
+
 class _BPRLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, Z, u, i, j, n_users: int, kind: int):
@@ -346,18 +382,19 @@ class _BPRLoss(torch.autograd.Function):
         n_items = N - n_users
         S = u.numel()
         u, i, j = (t.contiguous().to(torch.int64) for t in (u, i, j))
-        for name, t, hi in (("u", u, n_users), ("i", i, n_items), ("j", j, n_items)):
+        for name, t in (("u", u), ("i", i), ("j", j)):
             _check_dev(name, t, torch.int64, Z.device)
-            if S:
-                torch._assert_async(((t >= 0) & (t < hi)).all(), f"bpr: {name} index out of range")
+        _BadIndex.raise_pending()
         nbytes = ctypes.c_size_t(0)
         _lib.check(lib.ppgat_bpr_workspace_bytes(N, S, C, ctypes.byref(nbytes)), "bpr_workspace_bytes")
         ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=Z.device)
         loss = torch.empty(1, dtype=torch.float32, device=Z.device)
         coef = torch.empty(max(S, 1), 2, dtype=torch.float32, device=Z.device)
+        bad = torch.empty(1, dtype=torch.int32, device=Z.device)
         _lib.check(lib.ppgat_bpr_fwd(Z.data_ptr(), n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S,
-                                     kind, loss.data_ptr(), coef.data_ptr(), ws.data_ptr(), nbytes.value,
-                                     _lib.stream_handle(Z.device)), "bpr_fwd")
+                                     kind, loss.data_ptr(), coef.data_ptr(), bad.data_ptr(), ws.data_ptr(),
+                                     nbytes.value, _lib.stream_handle(Z.device)), "bpr_fwd")
+        _BadIndex.track(bad)
         ctx.save_for_backward(Z, u, i, j, coef)
         ctx.ws = ws
         ctx.meta = (n_users, n_items, C, S)
