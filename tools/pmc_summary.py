@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON
+
+gfx950 corrections (MI355X_MICROARCH.md "HBM"): counters are in KiB (x1024); FETCH_SIZE
+reports 1/2 of the bytes of a wide (16 B/lane) coalesced read -- all of our kernels read
+with 16-byte float4 accesses, so FETCH is doubled; WRITE_SIZE is exact for 16-B stores.
+The correction is cross-checked on k_scores, whose algorithmic bytes are exact
+(reads h once: N*H*C*4, writes 2*N*H*4).
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+KERNELS = {"k_fwd<": "fwd", "k_bwd_src<": "bwd_src", "k_bwd_epi<": "bwd_epi", "k_bwd_pro<": "bwd_pro",
+           "k_scores<": "scores", "k_gemm_tn": "gemm_tn", "k_bpr_chunks<": "bpr_chunks", "k_bpr_fwd<": "bpr_fwd"}
+
+
+def load(d, counter):
+    files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+    vals = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r.get("Kernel_Name", "")
+            for pat, key in KERNELS.items():
+                if pat in name:
+                    vals[key].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    fd, wd, out = sys.argv[1:4]
+    fetch = load(fd, "FETCH_SIZE")
+    write = load(wd, "WRITE_SIZE")
+    res = {"note": "per-launch HBM-side bytes (L2 fabric requests, Infinity-Cache hits included); "
+                   "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes",
+           "per_launch_bytes": {}, "raw_kib": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1)
+        w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
+        res["raw_kib"][k] = {"fetch": f, "write": w, "launches": len(fetch.get(k, []))}
+        res["per_launch_bytes"][k] = (2 * f + w) * 1024
+    json.dump(res, open(out, "w"), indent=2)
+    print(json.dumps(res, indent=2))
+
+
+if __name__ == "__main__":
+    main()
