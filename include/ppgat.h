@@ -144,25 +144,49 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
               float* grad_h, float* grad_att_src, float* grad_att_dst, float* grad_bias,
               void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- backward, staged (multi-GPU: collectives go between the stages) ----------
+ * ppgat_bwd == prologue -> edges -> epilogue on one device.  Row-sharded:
+ *  prologue over the rank's own destination rows -> nstate (all-gathered with grad_out),
+ *  edges over the rank's own SOURCE rows (CSC slice; `row` indexes the gathered dst space,
+ *  dz_slot gives each edge's position in a [world x max-local-edges] dz buffer that is then
+ *  reduce-scattered), epilogue over the own destination rows with the local dz.
+ *  nstate: [N_dst, H] float4 {s_dst, m, inv_l, D}.  grad_bias (nullable) needs bias_part
+ *  [ppgat_bwd_partial_rows(n) * C]; epilogue part: [ppgat_bwd_partial_rows(n) * 2*H*C].
+ */
+int64_t ppgat_bwd_partial_rows(int64_t n_nodes);
+int ppgat_bwd_prologue(const float* grad_out, const float* out, const float* agg, const float* bias,
+                       const float* s_dst, const float* m, const float* inv_l, int64_t n_nodes, int heads,
+                       int channels, int mode, float* nstate, float* grad_bias, float* bias_part, void* stream);
+int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                    const int32_t* dz_slot, int64_t n_edges, int heads, int channels, const float* h,
+                    const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
+                    float dropout_p, uint64_t seed, float* grad_h, float* ds_src, float* dz,
+                    void* workspace, size_t workspace_bytes, void* stream);
+int ppgat_bwd_epilogue(const int32_t* rowptr, int64_t n_nodes, int heads, int channels, const float* h,
+                       const float* att_src, const float* att_dst, const float* ds_src, const float* dz,
+                       float* grad_h, float* grad_att_src, float* grad_att_dst, float* part, void* stream);
+
 /* ---- loss of the training step ---------------------------------------------
  * Replaces: pos = (U[u]*I[i]).sum(-1); neg = (U[u]*I[j]).sum(-1); BPR
  *           -log(sigmoid(pos-neg)+1e-8).mean() (loss_kind 0) or BCE-with-logits over
  *           [pos; neg] with labels [1; 0] (loss_kind 1)  -- scripts/train_gat_pyg.py:313-322,
  *           and its autograd (gather backward = index_put_ accumulate).
- * Z [N, C] with users in rows [0, n_users) and items in [n_users, N); u, i, j int64 [S].
+ * Z [n_rows, C]; node id v (users [0, n_users), items n_users + i) lives in row v, or in
+ * row row_map[v] when row_map != NULL (int32 [n_users + n_items]; the row-sharded path keeps
+ * the gathered Z in a padded per-rank layout).  u, i, j int64 [S].
  * Forward writes the scalar mean loss and coef [S, 2] (dloss/dpos, dloss/dneg); the
  * backward writes the full grad_Z [N, C] (zero rows included) = grad_loss * sum of the
  * per-triple contributions, deterministically (sorted contributions, ordered sums).
  * Indices outside their range are clamped and counted into bad_count (device int32[1],
  * nullable; zeroed by the call) so the caller can raise without a host sync here.
  */
-int ppgat_bpr_workspace_bytes(int64_t n_nodes, int64_t n_samples, int channels, size_t* bytes);
-int ppgat_bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int channels,
-                  const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, int loss_kind,
-                  float* loss, float* coef, int32_t* bad_count, void* workspace, size_t workspace_bytes,
-                  void* stream);
-int ppgat_bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int channels,
-                  const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+int ppgat_bpr_workspace_bytes(int64_t n_rows, int64_t n_samples, int channels, size_t* bytes);
+int ppgat_bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                  int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+                  int loss_kind, float* loss, float* coef, int32_t* bad_count, void* workspace,
+                  size_t workspace_bytes, void* stream);
+int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                  int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
                   const float* coef, const float* grad_loss, float* grad_Z,
                   void* workspace, size_t workspace_bytes, void* stream);
 

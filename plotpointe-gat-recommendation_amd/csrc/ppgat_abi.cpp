@@ -218,7 +218,95 @@ int ppgat_fwd(const ppgat_schedule* sched, const int32_t* col, const int32_t* cs
   return PPGAT_OK;
 }
 
-// workspace: nstate [N*H float4] | ds_src [N*H] | dz [E*H] | block partial [blocks*(2*H*C + C)] | hub partial
+// ---- backward, staged ---------------------------------------------------------------
+int64_t ppgat_bwd_partial_rows(int64_t n_nodes) { return n_nodes < 0 ? -1 : ppgat::epi_blocks(n_nodes); }
+
+int ppgat_bwd_prologue(const float* grad_out, const float* out, const float* agg, const float* bias,
+                       const float* s_dst, const float* m, const float* inv_l, int64_t n_nodes, int heads,
+                       int channels, int mode, float* nstate, float* grad_bias, float* bias_part, void* stream) {
+  if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd_prologue: unsupported channels");
+  if (heads < 1 || heads > ppgat::kMaxHeads || n_nodes < 0) return fail(PPGAT_ERR_INVALID, "bwd_prologue: bad sizes");
+  if (mode != PPGAT_MODE_PYG && mode != PPGAT_MODE_CUSTOM) return fail(PPGAT_ERR_INVALID, "unknown mode");
+  if (heads > 1 && agg == nullptr) return fail(PPGAT_ERR_INVALID, "bwd_prologue: heads > 1 needs the saved agg");
+  if (n_nodes > 0 && (!grad_out || !out || !s_dst || !m || !inv_l || !nstate))
+    return fail(PPGAT_ERR_INVALID, "bwd_prologue: null pointer");
+  if (grad_bias && !bias_part) return fail(PPGAT_ERR_INVALID, "bwd_prologue: grad_bias needs bias_part");
+  const float gscale = mode == PPGAT_MODE_PYG ? 1.f / (float)heads : 1.f;
+  const int64_t blocks = ppgat::epi_blocks(n_nodes);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  {
+    Timed t(PPGAT_K_BWD_PRO, st);
+    e = ppgat::launch_bwd_pro(grad_out, out, agg, heads == 1 ? bias : nullptr, s_dst, m, inv_l, n_nodes, heads,
+                              channels, gscale, nstate, grad_bias ? bias_part : nullptr, blocks, st);
+    if (e == hipSuccess && grad_bias)
+      e = ppgat::launch_col_reduce(bias_part, blocks, channels, channels, grad_bias, nullptr, st);
+  }
+  if (e != hipSuccess) return hip_fail(e, "bwd_prologue");
+  return PPGAT_OK;
+}
+
+int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                    const int32_t* dz_slot, int64_t n_edges, int heads, int channels, const float* h,
+                    const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
+                    float dropout_p, uint64_t seed, float* grad_h, float* ds_src, float* dz, void* workspace,
+                    size_t workspace_bytes, void* stream) {
+  if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd_edges: unsupported channels");
+  if (heads < 1 || heads > ppgat::kMaxHeads || n_edges < 0) return fail(PPGAT_ERR_INVALID, "bwd_edges: bad sizes");
+  if (mode != PPGAT_MODE_PYG && mode != PPGAT_MODE_CUSTOM) return fail(PPGAT_ERR_INVALID, "unknown mode");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
+  if (int rc = check_sched(src_sched, 0, "bwd_edges")) return rc;
+  if (src_sched->n_items > 0 && (!h || !s_src || !grad_h || !ds_src))
+    return fail(PPGAT_ERR_INVALID, "bwd_edges: null pointer");
+  if (n_edges > 0 && (!row || !dz_slot || !nstate || !grad_out || !dz))
+    return fail(PPGAT_ERR_INVALID, "bwd_edges: null edge pointer");
+  if (dropout_p > 0.f && n_edges > 0 && !csc_eid) return fail(PPGAT_ERR_INVALID, "bwd_edges: dropout needs csc_eid");
+  if (src_sched->n_hub_items > 0 &&
+      (!workspace || workspace_bytes < partial_bytes(src_sched->n_hub_items, heads, channels)))
+    return fail(PPGAT_ERR_INVALID, "bwd_edges: workspace too small");
+  const float gscale = mode == PPGAT_MODE_PYG ? 1.f / (float)heads : 1.f;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{src_sched->item_row, src_sched->item_beg, src_sched->item_end, src_sched->n_items,
+                           src_sched->n_hub_items};
+  hipError_t e;
+  {
+    Timed t(PPGAT_K_BWD_SRC, st);
+    e = ppgat::launch_bwd_src(it, row, csc_eid, dz_slot, heads, channels, h, s_src, nstate, grad_out, mode,
+                              negative_slope, gscale, dropout_p, seed, grad_h, ds_src, dz,
+                              static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
+                              src_sched->n_hubs, st);
+  }
+  if (e != hipSuccess) return hip_fail(e, "bwd_edges");
+  return PPGAT_OK;
+}
+
+int ppgat_bwd_epilogue(const int32_t* rowptr, int64_t n_nodes, int heads, int channels, const float* h,
+                       const float* att_src, const float* att_dst, const float* ds_src, const float* dz,
+                       float* grad_h, float* grad_att_src, float* grad_att_dst, float* part, void* stream) {
+  if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd_epilogue: unsupported channels");
+  if (heads < 1 || heads > ppgat::kMaxHeads || n_nodes < 0) return fail(PPGAT_ERR_INVALID, "bwd_epilogue: bad sizes");
+  if (!att_src || !att_dst || !grad_att_src || !grad_att_dst || !part)
+    return fail(PPGAT_ERR_INVALID, "bwd_epilogue: null pointer");
+  if (n_nodes > 0 && (!rowptr || !h || !ds_src || !grad_h)) return fail(PPGAT_ERR_INVALID, "bwd_epilogue: null pointer");
+  const int64_t blocks = ppgat::epi_blocks(n_nodes);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  {
+    Timed t(PPGAT_K_BWD_EPI, st);
+    e = ppgat::launch_bwd_epi(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, part, blocks,
+                              st);
+  }
+  if (e != hipSuccess) return hip_fail(e, "bwd_epilogue");
+  {
+    Timed t(PPGAT_K_BWD_RED, st);
+    e = ppgat::launch_col_reduce(part, blocks, 2 * heads * channels, heads * channels, grad_att_src, grad_att_dst,
+                                 st);
+  }
+  if (e != hipSuccess) return hip_fail(e, "bwd_reduce");
+  return PPGAT_OK;
+}
+
+// ---- backward, composed (single device): nstate | ds_src | dz | partials | hub partial ----
 int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int64_t n_hub_items, int heads, int channels,
                               size_t* bytes) {
   if (!bytes || n_nodes < 0 || n_edges < 0 || n_hub_items < 0 || heads < 1 || channels < 1)
@@ -241,13 +329,6 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
   if (heads < 1 || n_nodes < 0 || n_edges < 0) return fail(PPGAT_ERR_INVALID, "bwd: bad sizes");
   if (int rc = check_mode(mode, heads, bias, dropout_p)) return rc;
   if (int rc = check_sched(sched, n_nodes, "bwd")) return rc;
-  if (heads > 1 && agg == nullptr) return fail(PPGAT_ERR_INVALID, "bwd: heads > 1 needs the saved agg");
-  if (!grad_att_src || !grad_att_dst || !att_src || !att_dst)
-    return fail(PPGAT_ERR_INVALID, "bwd: null attention pointer");
-  if (n_nodes > 0 && (!rowptr || !h || !s_src || !s_dst || !out || !m || !inv_l || !grad_out || !grad_h))
-    return fail(PPGAT_ERR_INVALID, "bwd: null pointer");
-  if (n_edges > 0 && (!row || !csc2csr)) return fail(PPGAT_ERR_INVALID, "bwd: null CSC pointer");
-  if (dropout_p > 0.f && n_edges > 0 && !csc_eid) return fail(PPGAT_ERR_INVALID, "bwd: dropout needs csc_eid");
   size_t need = 0;
   ppgat_bwd_workspace_bytes(n_nodes, n_edges, sched->n_hub_items, heads, channels, &need);
   if (!workspace || workspace_bytes < need) return fail(PPGAT_ERR_INVALID, "bwd: workspace too small");
@@ -262,46 +343,23 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
   float* dz = reinterpret_cast<float*>(p + ns + nh);
   float* bpart = reinterpret_cast<float*>(p + ns + nh + eh);
   float* hpart = reinterpret_cast<float*>(p + ns + nh + eh + part);
-  float* bias_part = grad_bias ? bpart + (size_t)blocks * 2 * heads * channels : nullptr;
-  const float gscale = mode == PPGAT_MODE_PYG ? 1.f / (float)heads : 1.f;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const ppgat::ItemsArg it{sched->item_row, sched->item_beg, sched->item_end, sched->n_items, sched->n_hub_items};
-  hipError_t e;
-  {
-    Timed t(PPGAT_K_BWD_PRO, st);
-    e = ppgat::launch_bwd_pro(grad_out, out, agg, heads == 1 ? bias : nullptr, s_dst, m, inv_l, n_nodes, heads,
-                              channels, gscale, nstate, bias_part, blocks, st);
-  }
-  if (e != hipSuccess) return hip_fail(e, "bwd_prologue");
-  {
-    Timed t(PPGAT_K_BWD_SRC, st);
-    e = ppgat::launch_bwd_src(it, row, csc_eid, csc2csr, heads, channels, h, s_src, nstate, grad_out, mode,
-                              negative_slope, gscale, dropout_p, seed, grad_h, ds_src, dz, hpart, sched->hub_row,
-                              sched->hub_ptr, sched->n_hubs, st);
-  }
-  if (e != hipSuccess) return hip_fail(e, "bwd_src");
-  {
-    Timed t(PPGAT_K_BWD_EPI, st);
-    e = ppgat::launch_bwd_epi(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, bpart,
-                              blocks, st);
-  }
-  if (e != hipSuccess) return hip_fail(e, "bwd_epilogue");
-  {
-    Timed t(PPGAT_K_BWD_RED, st);
-    e = ppgat::launch_col_reduce(bpart, blocks, 2 * heads * channels, heads * channels, grad_att_src, grad_att_dst,
-                                 st);
-    if (e == hipSuccess && grad_bias)
-      e = ppgat::launch_col_reduce(bias_part, blocks, channels, channels, grad_bias, nullptr, st);
-  }
-  if (e != hipSuccess) return hip_fail(e, "bwd_reduce");
-  return PPGAT_OK;
+  float* bias_part = bpart + (size_t)blocks * 2 * heads * channels;
+  if (int rc = ppgat_bwd_prologue(grad_out, out, agg, bias, s_dst, m, inv_l, n_nodes, heads, channels, mode, nstate,
+                                  grad_bias, bias_part, stream))
+    return rc;
+  if (int rc = ppgat_bwd_edges(sched, row, csc_eid, csc2csr, n_edges, heads, channels, h, s_src, nstate, grad_out,
+                               mode, negative_slope, dropout_p, seed, grad_h, ds_src, dz, hpart,
+                               partial_bytes(sched->n_hub_items, heads, channels), stream))
+    return rc;
+  return ppgat_bwd_epilogue(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, grad_att_src,
+                            grad_att_dst, bpart, stream);
 }
 
 // ---- training-step kernels ----
-int ppgat_bpr_workspace_bytes(int64_t n_nodes, int64_t n_samples, int channels, size_t* bytes) {
-  if (!bytes || n_nodes < 0 || n_samples < 0) return fail(PPGAT_ERR_INVALID, "bpr_workspace_bytes: bad arguments");
+int ppgat_bpr_workspace_bytes(int64_t n_rows, int64_t n_samples, int channels, size_t* bytes) {
+  if (!bytes || n_rows < 0 || n_samples < 0) return fail(PPGAT_ERR_INVALID, "bpr_workspace_bytes: bad arguments");
   if (!ppgat::bpr_channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bpr: channels must be 32/64/128/256");
-  *bytes = ppgat::bpr_workspace_bytes(n_nodes, n_samples, channels);
+  *bytes = ppgat::bpr_workspace_bytes(n_rows, n_samples, channels);
   return PPGAT_OK;
 }
 
@@ -315,29 +373,35 @@ static int check_bpr(int64_t n_users, int64_t n_items, int channels, int64_t S, 
   return PPGAT_OK;
 }
 
-int ppgat_bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int channels, const int64_t* u, const int64_t* i,
-                  const int64_t* j, int64_t n_samples, int loss_kind, float* loss, float* coef, int32_t* bad_count,
-                  void* workspace, size_t workspace_bytes, void* stream) {
+int ppgat_bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                  int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, int loss_kind,
+                  float* loss, float* coef, int32_t* bad_count, void* workspace, size_t workspace_bytes,
+                  void* stream) {
   if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_fwd")) return rc;
+  if (row_map == nullptr ? n_rows != n_users + n_items : n_rows < 1)
+    return fail(PPGAT_ERR_INVALID, "bpr_fwd: n_rows must be n_users + n_items without a row_map");
   if (loss_kind != 0 && loss_kind != 1) return fail(PPGAT_ERR_INVALID, "bpr_fwd: loss_kind must be 0 (bpr) or 1 (bce)");
   if (!loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_fwd: null output");
-  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_users + n_items, n_samples, channels))
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_rows, n_samples, channels))
     return fail(PPGAT_ERR_INVALID, "bpr_fwd: workspace too small");
-  hipError_t e = ppgat::bpr_fwd(Z, n_users, n_items, channels, u, i, j, n_samples, loss_kind, loss, coef, bad_count,
-                                workspace, static_cast<hipStream_t>(stream));
+  hipError_t e = ppgat::bpr_fwd(Z, n_users, n_items, row_map, channels, u, i, j, n_samples, loss_kind, loss, coef,
+                                bad_count, workspace, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "bpr_fwd");
   return PPGAT_OK;
 }
 
-int ppgat_bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int channels, const int64_t* u, const int64_t* i,
-                  const int64_t* j, int64_t n_samples, const float* coef, const float* grad_loss, float* grad_Z,
-                  void* workspace, size_t workspace_bytes, void* stream) {
+int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                  int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+                  const float* coef, const float* grad_loss, float* grad_Z, void* workspace, size_t workspace_bytes,
+                  void* stream) {
   if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_bwd")) return rc;
+  if (row_map == nullptr ? n_rows != n_users + n_items : n_rows < 1)
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd: n_rows must be n_users + n_items without a row_map");
   if (!grad_Z || !grad_loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_bwd: null pointer");
-  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_users + n_items, n_samples, channels))
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_rows, n_samples, channels))
     return fail(PPGAT_ERR_INVALID, "bpr_bwd: workspace too small");
-  hipError_t e = ppgat::bpr_bwd(Z, n_users, n_items, channels, u, i, j, n_samples, coef, grad_loss, grad_Z, workspace,
-                                workspace_bytes, static_cast<hipStream_t>(stream));
+  hipError_t e = ppgat::bpr_bwd(Z, n_rows, n_users, n_items, row_map, channels, u, i, j, n_samples, coef, grad_loss,
+                                grad_Z, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "bpr_bwd");
   return PPGAT_OK;
 }

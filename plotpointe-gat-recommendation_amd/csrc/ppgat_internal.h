@@ -56,12 +56,12 @@ hipError_t schedule_build(const int32_t* ptr, int64_t N, int32_t T, int32_t* ite
 // training-step kernels (ppgat_train.hip)
 bool bpr_channels_ok(int C);
 size_t bpr_workspace_bytes(int64_t N, int64_t S, int C);
-hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
-                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, int32_t* bad, void* ws,
-                   hipStream_t st);
-hipError_t bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
-                   const int64_t* j, int64_t S, const float* coef, const float* grad_loss, float* dZ, void* ws,
-                   size_t ws_bytes, hipStream_t st);
+hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, int kind, float* loss,
+                   float* coef, int32_t* bad, void* ws, hipStream_t st);
+hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
+                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st);
 size_t gemm_tn_workspace_bytes(int64_t N, int M, int K);
 hipError_t gemm_tn(const float* A, const float* B, int64_t N, int M, int K, float* out, float* colsum, void* ws,
                    hipStream_t st);

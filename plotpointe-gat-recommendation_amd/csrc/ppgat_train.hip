@@ -42,6 +42,9 @@ unsigned key_bits(int64_t n) {
 }
 
 __device__ __forceinline__ int64_t clamp_idx(int64_t v, int64_t n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+// Z row of node id v (users [0, n_users), items n_users + i); row_map != NULL remaps (sharded
+// runs keep Z in a padded per-rank row space)
+__device__ __forceinline__ int64_t zrow(const int32_t* row_map, int64_t v) { return row_map ? row_map[v] : v; }
 
 // ---------------------------------------------------------------------------
 // BPR forward: one subgroup (C/4 lanes) per triple.
@@ -55,7 +58,7 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
                                                  const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
                                                  const int64_t* __restrict__ jj, int64_t S, int kind,
                                                  float2* __restrict__ coef, float* __restrict__ block_loss,
-                                                 int32_t* __restrict__ bad) {
+                                                 int32_t* __restrict__ bad, const int32_t* __restrict__ row_map) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;  // subgroups (triples) per block
   __shared__ float sl_loss[SPB];
@@ -69,9 +72,9 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
     if (bad != nullptr && sl == 0 &&
         (u0 < 0 || u0 >= n_users || i0 < 0 || i0 >= n_items || j0 < 0 || j0 >= n_items))
       atomicAdd(bad, 1);  // integer count; indices are clamped below, the caller raises
-    const int64_t ur = clamp_idx(u0, n_users);
-    const int64_t ir = n_users + clamp_idx(i0, n_items);
-    const int64_t jr = n_users + clamp_idx(j0, n_items);
+    const int64_t ur = zrow(row_map, clamp_idx(u0, n_users));
+    const int64_t ir = zrow(row_map, n_users + clamp_idx(i0, n_items));
+    const int64_t jr = zrow(row_map, n_users + clamp_idx(j0, n_items));
     const float4 a = ld4(Z + ur * C + sl * 4);
     pos = dot4(a, ld4(Z + ir * C + sl * 4));
     neg = dot4(a, ld4(Z + jr * C + sl * 4));
@@ -126,7 +129,8 @@ __global__ void __launch_bounds__(256) k_bpr_loss(const float* __restrict__ bloc
 // contribution c = 4t + kind -> destination row (sort key)
 __global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
                            const int64_t* __restrict__ jj, int64_t S, int64_t n_users, int64_t n_items,
-                           int32_t* __restrict__ key, int32_t* __restrict__ val) {
+                           const int32_t* __restrict__ row_map, int32_t* __restrict__ key,
+                           int32_t* __restrict__ val) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= 4 * S) return;
   const int64_t t = c >> 2;
@@ -135,7 +139,7 @@ __global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restr
   if (kd < 2) d = clamp_idx(u[t], n_users);
   else if (kd == 2) d = n_users + clamp_idx(ii[t], n_items);
   else d = n_users + clamp_idx(jj[t], n_items);
-  key[c] = (int32_t)d;
+  key[c] = (int32_t)zrow(row_map, d);
   val[c] = (int32_t)c;
 }
 
@@ -152,6 +156,7 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
                                                     int64_t total, const int64_t* __restrict__ u,
                                                     const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
                                                     int64_t n_users, int64_t n_items,
+                                                    const int32_t* __restrict__ row_map,
                                                     const float2* __restrict__ coef,
                                                     const float* __restrict__ grad_loss, const float* __restrict__ Z,
                                                     float* __restrict__ dZ, float* __restrict__ slots) {
@@ -176,9 +181,9 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
         const int kd = c & 3;
         const float2 tc = coef[t];
         dst = skey[p];
-        if (kd == 0) { src = (int32_t)(n_users + clamp_idx(ii[t], n_items)); cf = tc.x; }
-        else if (kd == 1) { src = (int32_t)(n_users + clamp_idx(jj[t], n_items)); cf = tc.y; }
-        else { src = (int32_t)clamp_idx(u[t], n_users); cf = kd == 2 ? tc.x : tc.y; }
+        if (kd == 0) { src = (int32_t)zrow(row_map, n_users + clamp_idx(ii[t], n_items)); cf = tc.x; }
+        else if (kd == 1) { src = (int32_t)zrow(row_map, n_users + clamp_idx(jj[t], n_items)); cf = tc.y; }
+        else { src = (int32_t)zrow(row_map, clamp_idx(u[t], n_users)); cf = kd == 2 ? tc.x : tc.y; }
       }
       s_src[sg][q] = src;
       s_dst[sg][q] = dst;
@@ -389,9 +394,9 @@ size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
          align_up((size_t)chunks * 2 * C * 4) + align_up(bpr_sort_temp(S, N));
 }
 
-hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
-                   const int64_t* j, int64_t S, int kind, float* loss, float* coef, int32_t* bad, void* ws,
-                   hipStream_t st) {
+hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, int kind, float* loss,
+                   float* coef, int32_t* bad, void* ws, hipStream_t st) {
   float* block_loss = static_cast<float*>(ws);
   const int64_t nb = bpr_fwd_blocks(S, C);
   if (bad != nullptr) {
@@ -401,7 +406,7 @@ hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, cons
   if (S > 0) {
     PPGAT_DISPATCH_LOSS_C(C, hipLaunchKernelGGL(k_bpr_fwd<CC>, dim3((unsigned)nb), dim3(256), 0, st, Z, n_users,
                                                 n_items, u, i, j, S, kind, reinterpret_cast<float2*>(coef),
-                                                block_loss, bad));
+                                                block_loss, bad, row_map));
   }
   const float denom = kind == 0 ? (float)S : 2.f * (float)S;
   hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(256), 0, st, block_loss, S > 0 ? nb : 0, denom > 0 ? denom : 1.f,
@@ -409,10 +414,10 @@ hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, int C, cons
   return hipGetLastError();
 }
 
-hipError_t bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int C, const int64_t* u, const int64_t* i,
-                   const int64_t* j, int64_t S, const float* coef, const float* grad_loss, float* dZ, void* ws,
-                   size_t ws_bytes, hipStream_t st) {
-  const int64_t N = n_users + n_items;
+hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
+                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t N = n_rows;
   hipError_t err = hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);
   if (err != hipSuccess || S == 0) return err;
   const int64_t total = 4 * S;
@@ -427,14 +432,14 @@ hipError_t bpr_bwd(const float* Z, int64_t n_users, int64_t n_items, int C, cons
   void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
   size_t tmp_bytes = ws_bytes - (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws));
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
-                     n_items, keys, vals);
+                     n_items, row_map, keys, vals);
   err = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, vals, scid, (size_t)total, 0u, key_bits(N), st);
   if (err != hipSuccess) return err;
   PPGAT_DISPATCH_LOSS_C(C, {
     constexpr int SPB = 256 / (CC / 4);
     const unsigned g = (unsigned)((chunks + SPB - 1) / SPB);
     hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, skeys, scid, total, u, i, j, n_users, n_items,
-                       reinterpret_cast<const float2*>(coef), grad_loss, Z, dZ, slots);
+                       row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, dZ, slots);
     hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, dZ);
   });
   return hipGetLastError();

@@ -1,0 +1,351 @@
+"""Row-sharded multi-GPU GAT: one process per GPU, RCCL over xGMI.
+
+Partition.  Node ids [0, N) are cut into `world` contiguous ranges balanced by
+in-degree + out-degree + a per-node constant.  Every range is padded to R rows so all
+per-node tensors are [R, ...] per rank and [world*R, ...] gathered ("padded space";
+node n lives at row owner(n)*R + n - lo(owner)).  The graph is static: the global
+CSR/CSC in padded space is built once on every rank (device radix sort) and each rank
+keeps slices of it:
+  forward : CSR rows of its own destinations (col indexes the gathered padded space)
+  backward: CSC rows of its own sources with their full out-edge lists (row indexes the
+            gathered padded space); each edge's logit gradient goes to its slot in a
+            [world, E_max] buffer laid out by destination owner and CSR slot.
+
+Per layer.
+  forward : local lin -> node scores -> all_gather(h, s_src) -> fused kernel on own rows
+  backward: prologue on own rows -> all_gather(grad_out, nstate) -> edge pass on own
+            sources (complete dh for them: no reverse exchange) -> reduce_scatter(dz)
+            (every slot is written by exactly one rank, so the sum is exact) -> epilogue
+            on own rows.
+Loss: all_gather of Z, each rank evaluates its contiguous share of the BPR triples, the
+gradient returns by reduce_scatter.  Dense parameters (lin, att, bias, item_proj) are
+replicated and all-reduced once per step; user-embedding rows are owner-held.
+On a locality-free graph the halo is ~all nodes, so all_gather is the natural collective
+here (a per-peer all-to-all index list would carry the same rows).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+
+# ---------------------------------------------------------------------------
+# communication
+# ---------------------------------------------------------------------------
+class Comm:
+    """Row collectives on [R, ...] shards.  NCCL(=RCCL) runs on device tensors directly;
+    gloo (CPU tests, or device tensors staged through the host when several ranks share
+    one GPU in a test) uses list all_gather and all_reduce+slice for reduce_scatter."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.backend = dist.get_backend(group)
+
+    def _host(self, t):
+        return self.backend == "gloo" and t.is_cuda
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.contiguous()
+        if self.world == 1:
+            return t
+        if self.backend == "gloo":
+            src = t.cpu() if t.is_cuda else t
+            parts = [torch.empty_like(src) for _ in range(self.world)]
+            dist.all_gather(parts, src, group=self.group)
+            return torch.cat(parts, 0).to(t.device)
+        out = torch.empty((self.world * t.size(0),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.contiguous()
+        if self.world == 1:
+            return t
+        R = t.size(0) // self.world
+        if self.backend == "gloo":
+            src = t.cpu() if t.is_cuda else t.clone()
+            dist.all_reduce(src, group=self.group)
+            return src[self.rank * R:(self.rank + 1) * R].contiguous().to(t.device)
+        out = torch.empty((R,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t, group=self.group)
+        return out
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if self._host(t):
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+            return t
+        dist.all_reduce(t, group=self.group)
+        return t
+
+
+class _AllGatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t, comm):
+        ctx.comm = comm
+        return comm.all_gather_rows(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.comm.reduce_scatter_rows(g), None
+
+
+def all_gather_rows(t, comm):
+    return _AllGatherRows.apply(t, comm)
+
+
+# ---------------------------------------------------------------------------
+# partition and the per-rank graph views
+# ---------------------------------------------------------------------------
+def partition_bounds(weights: np.ndarray, world: int) -> np.ndarray:
+    """Contiguous ranges [b_r, b_{r+1}) with ~equal sum of weights."""
+    n = len(weights)
+    cum = np.concatenate([[0], np.cumsum(weights, dtype=np.float64)])
+    targets = cum[-1] * np.arange(1, world) / world
+    inner = np.searchsorted(cum, targets, side="left")
+    b = np.concatenate([[0], np.clip(inner, 0, n), [n]]).astype(np.int64)
+    return np.maximum.accumulate(b)
+
+
+@dataclass
+class LocalView:
+    """Slices of the padded-space CSR/CSC a rank runs the stages on."""
+    n_rows: int                 # R
+    rowptr: torch.Tensor        # [R+1] rebased, CSR of own destination rows
+    col: torch.Tensor           # [E_fwd] padded source ids
+    csr_eid: torch.Tensor       # [E_fwd] original column ids (dropout hash key)
+    n_fwd_edges: int
+    colptr: torch.Tensor        # [R+1] rebased, CSC of own source rows
+    row: torch.Tensor           # [E_bwd] padded destination ids
+    csc_eid: torch.Tensor       # [E_bwd]
+    dz_slot: torch.Tensor       # [E_bwd] position in the [world * E_max] dz buffer
+    n_bwd_edges: int
+    fwd_sched: object = None
+    bwd_sched: object = None
+
+
+@dataclass
+class DistGraph:
+    world: int
+    rank: int
+    n_nodes: int
+    n_edges: int
+    bounds: np.ndarray
+    R: int
+    row_map: torch.Tensor       # [N] int32, node id -> padded row
+    e_max: int
+    view: LocalView
+
+    @property
+    def lo(self) -> int:
+        return int(self.bounds[self.rank])
+
+    @property
+    def hi(self) -> int:
+        return int(self.bounds[self.rank + 1])
+
+    @property
+    def P(self) -> int:
+        return self.world * self.R
+
+
+def _hip_csr(ei, P):
+    from .hip_ops import csr_build
+    return csr_build(ei, P)
+
+
+def _hip_sched(ptr, E):
+    from .hip_ops import schedule_build
+    return schedule_build(ptr, E)
+
+
+def build_dist_graph(edge_index: torch.Tensor, n_nodes: int, world: int, rank: int,
+                     csr_builder: Callable = _hip_csr, sched_builder: Optional[Callable] = _hip_sched,
+                     node_weight: float = 4.0) -> DistGraph:
+    """Every rank calls this with the same global edge_index (LongTensor [2, E], original
+    node ids) and gets its own slices.  Deterministic: all ranks agree on every array."""
+    dev = edge_index.device
+    N = int(n_nodes)
+    E = int(edge_index.size(1))
+    deg = (torch.bincount(edge_index[1], minlength=N) + torch.bincount(edge_index[0], minlength=N)).cpu().numpy()
+    bounds = partition_bounds(deg.astype(np.float64) + node_weight, world)
+    R = max(int(np.max(np.diff(bounds))), 1)
+    owner = np.repeat(np.arange(world), np.diff(bounds))
+    row_map_np = (owner * R + (np.arange(N) - bounds[owner])).astype(np.int64)
+    row_map = torch.from_numpy(row_map_np).to(dev)
+    ei_p = row_map[edge_index]                       # [2, E] padded ids
+    P = world * R
+    G = csr_builder(ei_p, P)
+    rowptr = G.rowptr.to(torch.int64)
+    colptr = G.colptr.to(torch.int64)
+    starts = rowptr[torch.arange(world, device=dev) * R].cpu().numpy()
+    ends = rowptr[torch.arange(1, world + 1, device=dev) * R].cpu().numpy()
+    e_max = max(int(np.max(ends - starts)), 1)
+    r0, r1 = rank * R, (rank + 1) * R
+    e0, e1 = int(starts[rank]), int(ends[rank])
+    c0, c1 = int(colptr[r0].item()), int(colptr[r1].item())
+    v_rowptr = (rowptr[r0:r1 + 1] - e0).to(torch.int32).contiguous()
+    v_colptr = (colptr[r0:r1 + 1] - c0).to(torch.int32).contiguous()
+    row = G.row[c0:c1].contiguous()
+    glob_slot = G.csc2csr[c0:c1].to(torch.int64)
+    dst_owner = row.to(torch.int64) // R
+    starts_t = torch.from_numpy(starts).to(dev)
+    dz_slot = (dst_owner * e_max + glob_slot - starts_t[dst_owner]).to(torch.int32).contiguous()
+    view = LocalView(R, v_rowptr, G.col[e0:e1].contiguous(), G.csr_eid[e0:e1].contiguous(), e1 - e0,
+                     v_colptr, row, G.csc_eid[c0:c1].contiguous(), dz_slot, c1 - c0)
+    if sched_builder is not None:
+        view.fwd_sched = sched_builder(v_rowptr, e1 - e0)
+        view.bwd_sched = sched_builder(v_colptr, c1 - c0)
+    return DistGraph(world, rank, N, E, bounds, R, row_map.to(torch.int32), e_max, view)
+
+
+# ---------------------------------------------------------------------------
+# the sharded layer
+# ---------------------------------------------------------------------------
+class _ShardedGAT(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, att_src, att_dst, bias, dg: DistGraph, comm: Comm, stages, heads: int, C: int, mode: int,
+                slope: float, p: float, seed: int):
+        h = h.contiguous()
+        a_s = att_src.detach().reshape(heads, C).contiguous()
+        a_d = att_dst.detach().reshape(heads, C).contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        s_src, s_dst = stages.scores(h, a_s, a_d, heads, C)
+        h_full = comm.all_gather_rows(h)
+        s_src_full = comm.all_gather_rows(s_src)
+        need = any(ctx.needs_input_grad[:4])
+        out, m, inv_l, agg = stages.fwd(dg.view, h_full, s_src_full, s_dst, b, heads, C, mode, slope, p, seed,
+                                        need and heads > 1)
+        if need:
+            empty = torch.empty(0, device=h.device)
+            ctx.save_for_backward(h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg if agg is not None else empty,
+                                  b if b is not None else empty)
+        ctx.dg, ctx.comm, ctx.stages = dg, comm, stages
+        ctx.meta = (heads, C, mode, slope, p, seed, bias is not None, agg is not None)
+        ctx.att_shapes = (att_src.shape, att_dst.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg, b = ctx.saved_tensors
+        heads, C, mode, slope, p, seed, has_bias, has_agg = ctx.meta
+        dg, comm, st = ctx.dg, ctx.comm, ctx.stages
+        g = g.contiguous()
+        want_db = has_bias and ctx.needs_input_grad[3]
+        nstate, dbias = st.bwd_prologue(g, out, agg if has_agg else None, b if has_bias else None, s_dst, m, inv_l,
+                                        heads, C, mode, want_db)
+        g_full = comm.all_gather_rows(g)
+        nstate_full = comm.all_gather_rows(nstate)
+        dz = torch.zeros(dg.world * dg.e_max * heads, dtype=h.dtype, device=h.device)
+        grad_h, ds_src = st.bwd_edges(dg.view, h, s_src, nstate_full, g_full, dz, heads, C, mode, slope, p, seed)
+        dz_local = comm.reduce_scatter_rows(dz.view(dg.world, dg.e_max * heads)).reshape(-1)
+        datt_src, datt_dst = st.bwd_epilogue(dg.view, h, a_s, a_d, ds_src, dz_local, grad_h, heads, C)
+        return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None, None, None, None)
+
+
+def _dropout_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+class ShardedPyGGAT(torch.nn.Module):
+    """PyGGAT (train_gat_pyg.py:68-88) with row-sharded nodes.  Built from a full model
+    constructed identically on every rank (same seed), so the sharded and single-GPU runs
+    start from the same parameters; ``full_state_dict`` reassembles the reference keys."""
+
+    def __init__(self, full, dg: DistGraph, comm: Comm, stages=None):
+        super().__init__()
+        from .hip_ops import HipStages
+        self.dg, self.comm = dg, comm
+        self.stages = stages if stages is not None else HipStages()
+        self.n_users, self.n_items = full.n_users, full.n_items
+        nu = self.n_users
+        lo, hi = dg.lo, dg.hi
+        self.u0, self.u1 = min(max(lo, 0), nu), min(max(hi, 0), nu)
+        self.i0, self.i1 = min(max(lo - nu, 0), self.n_items), min(max(hi - nu, 0), self.n_items)
+        self.pad = dg.R - (hi - lo)
+        self.user_emb_local = torch.nn.Parameter(full.user_emb.weight.detach()[self.u0:self.u1].clone())
+        self.item_proj = full.item_proj
+        self.convs = full.convs
+
+    def dense_parameters(self):
+        return [p for n, p in self.named_parameters() if n != "user_emb_local"]
+
+    def node_features(self, item_feats):
+        v = self.stages.linear(item_feats[self.i0:self.i1].contiguous(), self.item_proj.weight, self.item_proj.bias)
+        parts = [self.user_emb_local, v]
+        if self.pad:
+            parts.append(torch.zeros(self.pad, v.size(1), dtype=v.dtype, device=v.device))
+        return torch.cat(parts, 0)
+
+    def forward(self, item_feats):
+        x = self.node_features(item_feats)
+        for conv in self.convs:
+            h = self.stages.linear(x, conv.lin.weight, None)
+            p = float(conv.dropout) if self.training else 0.0
+            seed = _dropout_seed() if p > 0 else 0
+            x = _ShardedGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, self.dg, self.comm, self.stages,
+                                  conv.heads, conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p, seed)
+        return x  # own rows of Z, [R, C] (pad rows last)
+
+    def allreduce_grads(self):
+        """One flat all-reduce of every dense parameter gradient (replicated params)."""
+        ps = [p for p in self.dense_parameters() if p.grad is not None]
+        if not ps or self.comm.world == 1:
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        self.comm.all_reduce_(flat)
+        off = 0
+        for p in ps:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+
+    def full_state_dict(self):
+        """Reference-keyed state_dict (user_emb gathered from the owners)."""
+        dev = self.user_emb_local.device
+        C = self.user_emb_local.size(1)
+        blk = torch.zeros(self.dg.R, C, dtype=torch.float32, device=dev)
+        blk[:self.u1 - self.u0] = self.user_emb_local.detach()
+        allb = self.comm.all_gather_rows(blk)
+        rows = []
+        for r in range(self.dg.world):
+            lo, hi = int(self.dg.bounds[r]), int(self.dg.bounds[r + 1])
+            u0, u1 = min(lo, self.n_users), min(hi, self.n_users)
+            rows.append(allb[r * self.dg.R: r * self.dg.R + (u1 - u0)])
+        sd = {"user_emb.weight": torch.cat(rows, 0)}
+        for k, v in self.state_dict().items():
+            if k != "user_emb_local":
+                sd[k] = v
+        return sd
+
+
+def sharded_bpr_loss(Z_local, dg: DistGraph, comm: Comm, u, i, j, n_users: int, n_items: int, loss: str = "bpr",
+                     stages=None):
+    """This rank's contiguous share of the S triples over the all-gathered Z; the returned
+    value is weighted so that the sum over ranks is the reference's mean loss."""
+    if stages is None:
+        from .hip_ops import HipStages
+        stages = HipStages()
+    S = int(u.numel())
+    a, b = S * comm.rank // comm.world, S * (comm.rank + 1) // comm.world
+    Z_full = all_gather_rows(Z_local, comm)
+    part = stages.bpr(Z_full, n_users, n_items, dg.row_map, u[a:b], i[a:b], j[a:b], loss)
+    return part * ((b - a) / max(S, 1))
+
+
+def gather_rows_to_global(Z_local, dg: DistGraph, comm: Comm) -> torch.Tensor:
+    """[R, C] own rows -> [N, C] in node-id order (every rank gets the full matrix)."""
+    Z_full = comm.all_gather_rows(Z_local.contiguous())
+    return Z_full.index_select(0, dg.row_map.to(torch.int64))

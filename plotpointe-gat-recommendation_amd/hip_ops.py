@@ -374,45 +374,48 @@ def check_bpr_indices():
 
 class _BPRLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, Z, u, i, j, n_users: int, kind: int):
+    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map):
         lib = _lib.load()
         Z = Z.contiguous()
         _check_dev("Z", Z, torch.float32)
-        N, C = Z.shape
-        n_items = N - n_users
+        n_rows, C = Z.shape
         S = u.numel()
         u, i, j = (t.contiguous().to(torch.int64) for t in (u, i, j))
         for name, t in (("u", u), ("i", i), ("j", j)):
             _check_dev(name, t, torch.int64, Z.device)
+        if row_map is not None:
+            _check_dev("row_map", row_map, torch.int32, Z.device)
         _BadIndex.raise_pending()
         nbytes = ctypes.c_size_t(0)
-        _lib.check(lib.ppgat_bpr_workspace_bytes(N, S, C, ctypes.byref(nbytes)), "bpr_workspace_bytes")
+        _lib.check(lib.ppgat_bpr_workspace_bytes(n_rows, S, C, ctypes.byref(nbytes)), "bpr_workspace_bytes")
         ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=Z.device)
         loss = torch.empty(1, dtype=torch.float32, device=Z.device)
         coef = torch.empty(max(S, 1), 2, dtype=torch.float32, device=Z.device)
         bad = torch.empty(1, dtype=torch.int32, device=Z.device)
-        _lib.check(lib.ppgat_bpr_fwd(Z.data_ptr(), n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S,
-                                     kind, loss.data_ptr(), coef.data_ptr(), bad.data_ptr(), ws.data_ptr(),
-                                     nbytes.value, _lib.stream_handle(Z.device)), "bpr_fwd")
+        _lib.check(lib.ppgat_bpr_fwd(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(row_map), C, u.data_ptr(),
+                                     i.data_ptr(), j.data_ptr(), S, kind, loss.data_ptr(), coef.data_ptr(),
+                                     bad.data_ptr(), ws.data_ptr(), nbytes.value, _lib.stream_handle(Z.device)),
+                   "bpr_fwd")
         _BadIndex.track(bad)
         ctx.save_for_backward(Z, u, i, j, coef)
         ctx.ws = ws
-        ctx.meta = (n_users, n_items, C, S)
+        ctx.row_map = row_map
+        ctx.meta = (n_rows, n_users, n_items, C, S)
         return loss[0]
 
     @staticmethod
     def backward(ctx, gl):
         lib = _lib.load()
         Z, u, i, j, coef = ctx.saved_tensors
-        n_users, n_items, C, S = ctx.meta
+        n_rows, n_users, n_items, C, S = ctx.meta
         gl = gl.reshape(1).to(torch.float32).contiguous()
         dZ = torch.empty_like(Z)
         ws = ctx.ws
-        _lib.check(lib.ppgat_bpr_bwd(Z.data_ptr(), n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S,
-                                     coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(), ws.numel(),
-                                     _lib.stream_handle(Z.device)), "bpr_bwd")
+        _lib.check(lib.ppgat_bpr_bwd(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(ctx.row_map), C, u.data_ptr(),
+                                     i.data_ptr(), j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), _lib.stream_handle(Z.device)), "bpr_bwd")
         ctx.ws = None
-        return dZ, None, None, None, None, None
+        return dZ, None, None, None, None, None, None, None
 
 
 def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch.Tensor:
@@ -420,4 +423,99 @@ def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch
     _require(Z.is_cuda, "bpr_loss: ppgat runs on ROCm devices only; there is no CPU path")
     if Z.size(1) not in (32, 64, 128, 256):
         raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
-    return _BPRLoss.apply(Z, u, i, j, int(n_users), LOSS_KINDS[loss])
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), Z.size(0) - int(n_users), LOSS_KINDS[loss], None)
+
+
+def bpr_loss_mapped(Z: torch.Tensor, n_users: int, n_items: int, row_map: torch.Tensor, u, i, j,
+                    loss: str = "bpr") -> torch.Tensor:
+    """bpr_loss over a Z whose rows are laid out by row_map (node id -> row)."""
+    if Z.size(1) not in (32, 64, 128, 256):
+        raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map)
+
+
+# ---------------------------------------------------------------------------
+# staged kernels for the row-sharded path (dist.py); one object so tests can swap in
+# a CPU restatement of the same stages
+# ---------------------------------------------------------------------------
+class HipStages:
+    """The GAT layer as the stages of include/ppgat.h, over explicit (possibly sliced)
+    CSR/CSC views: see dist.LocalView for the fields used."""
+
+    def linear(self, x, weight, bias):
+        return linear(x, weight, bias)
+
+    def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss):
+        return bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, loss)
+
+    def scores(self, h, att_src, att_dst, heads, channels):
+        return node_scores(h, att_src, att_dst, heads, channels)
+
+    def fwd(self, v, h_full, s_src_full, s_dst, bias, heads, channels, mode, slope, p, seed, want_agg):
+        lib = _lib.load()
+        dev = h_full.device
+        R = v.n_rows
+        out = torch.empty(R, channels, dtype=torch.float32, device=dev)
+        m = torch.empty(R, heads, dtype=torch.float32, device=dev)
+        inv_l = torch.empty(R, heads, dtype=torch.float32, device=dev)
+        agg = torch.empty(R, heads, channels, dtype=torch.float32, device=dev) if want_agg else None
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_fwd_workspace_bytes(v.fwd_sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
+                   "fwd_workspace_bytes")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = v.fwd_sched.cstruct()
+        _lib.check(lib.ppgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if v.n_fwd_edges else None,
+                                 _lib.ptr(v.csr_eid) if v.n_fwd_edges else None, R, v.n_fwd_edges, heads, channels,
+                                 h_full.data_ptr(), s_src_full.data_ptr(), s_dst.data_ptr(), _lib.ptr(bias), mode,
+                                 float(slope), float(p), int(seed) & (2**64 - 1), out.data_ptr(), m.data_ptr(),
+                                 inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
+                                 _lib.stream_handle(dev)), "gat_fwd")
+        return out, m, inv_l, agg
+
+    def bwd_prologue(self, grad_out, out, agg, bias, s_dst, m, inv_l, heads, channels, mode, want_bias_grad):
+        lib = _lib.load()
+        dev = grad_out.device
+        R = grad_out.size(0)
+        nstate = torch.empty(R, heads, 4, dtype=torch.float32, device=dev)
+        dbias = torch.empty(channels, dtype=torch.float32, device=dev) if want_bias_grad else None
+        rows = int(lib.ppgat_bwd_partial_rows(R))
+        part = torch.empty(max(rows, 1) * channels, dtype=torch.float32, device=dev) if want_bias_grad else None
+        _lib.check(lib.ppgat_bwd_prologue(grad_out.data_ptr(), out.data_ptr(), _lib.ptr(agg), _lib.ptr(bias),
+                                          s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), R, heads, channels, mode,
+                                          nstate.data_ptr(), _lib.ptr(dbias), _lib.ptr(part),
+                                          _lib.stream_handle(dev)), "bwd_prologue")
+        return nstate, dbias
+
+    def bwd_edges(self, v, h, s_src, nstate_full, grad_out_full, dz, heads, channels, mode, slope, p, seed):
+        lib = _lib.load()
+        dev = h.device
+        R = v.n_rows
+        grad_h = torch.empty(R, heads * channels, dtype=torch.float32, device=dev)
+        ds_src = torch.empty(R, heads, dtype=torch.float32, device=dev)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_fwd_workspace_bytes(v.bwd_sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
+                   "workspace_bytes")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = v.bwd_sched.cstruct()
+        E = v.n_bwd_edges
+        _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                       _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None, E,
+                                       heads, channels, h.data_ptr(), s_src.data_ptr(), nstate_full.data_ptr(),
+                                       grad_out_full.data_ptr(), mode, float(slope), float(p),
+                                       int(seed) & (2**64 - 1), grad_h.data_ptr(), ds_src.data_ptr(), dz.data_ptr(),
+                                       ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "bwd_edges")
+        return grad_h, ds_src
+
+    def bwd_epilogue(self, v, h, att_src, att_dst, ds_src, dz, grad_h, heads, channels):
+        lib = _lib.load()
+        dev = h.device
+        R = v.n_rows
+        datt_src = torch.empty(heads, channels, dtype=torch.float32, device=dev)
+        datt_dst = torch.empty(heads, channels, dtype=torch.float32, device=dev)
+        rows = int(lib.ppgat_bwd_partial_rows(R))
+        part = torch.empty(max(rows, 1) * 2 * heads * channels, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_bwd_epilogue(v.rowptr.data_ptr(), R, heads, channels, h.data_ptr(), att_src.data_ptr(),
+                                          att_dst.data_ptr(), ds_src.data_ptr(), dz.data_ptr(), grad_h.data_ptr(),
+                                          datt_src.data_ptr(), datt_dst.data_ptr(), part.data_ptr(),
+                                          _lib.stream_handle(dev)), "bwd_epilogue")
+        return datt_src, datt_dst

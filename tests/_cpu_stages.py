@@ -1,0 +1,115 @@
+"""CPU restatement of the GAT layer STAGES (test infrastructure only).
+
+Used by the world_size>1 gloo tests to exercise the row-sharded orchestration of
+plotpointe-gat-recommendation_amd/dist.py on CPU: same stage interface as
+hip_ops.HipStages, arithmetic restated with torch CPU ops (any dtype), dropout from
+oracle.dropout_scale.  Each stage mirrors the kernel of the same name in
+csrc/ppgat_kernels.hip; the end-to-end result is checked against the unsharded oracle.
+"""
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+from oracle import gat_oracle as O
+
+
+def csr_builder(ei: torch.Tensor, n: int):
+    rowptr, col, eid, colptr, row, ceid, c2r = O.csr_from_edge_index(ei.cpu().numpy(), n)
+    t = lambda a: torch.from_numpy(np.asarray(a, np.int64)).to(torch.int32)
+    return SimpleNamespace(rowptr=t(rowptr), col=t(col), csr_eid=t(eid), colptr=t(colptr), row=t(row),
+                           csc_eid=t(ceid), csc2csr=t(c2r))
+
+
+def _logit(z, slope, mode):
+    e = torch.where(z > 0, z, z * slope)
+    return e.clamp(-10, 10) if mode == 1 else e
+
+
+def _dlogit(z, slope, mode):
+    e = torch.where(z > 0, z, z * slope)
+    d = torch.where(z > 0, torch.ones_like(z), torch.full_like(z, slope))
+    if mode == 1:
+        d = torch.where((e < -10) | (e > 10), torch.zeros_like(d), d)
+    return d
+
+
+def _drop(seed, eid, H, p, dtype):
+    if p <= 0:
+        return torch.ones(len(eid), H, dtype=dtype)
+    e = eid.numpy().astype(np.int64)
+    return torch.from_numpy(np.stack([O.dropout_scale(seed, e, h, p) for h in range(H)], 1)).to(dtype)
+
+
+class CpuStages:
+    def linear(self, x, W, b):
+        return torch.nn.functional.linear(x, W, b)
+
+    def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss):
+        rm = row_map.long()
+        Zn = Z.index_select(0, rm)          # node-id order
+        return O.bpr_loss(Zn, n_users, u, i, j, loss)
+
+    def scores(self, h, a_s, a_d, H, C):
+        hv = h.view(-1, H, C)
+        return (hv * a_s).sum(-1), (hv * a_d).sum(-1)
+
+    def fwd(self, v, h_full, s_src_full, s_dst, bias, H, C, mode, slope, p, seed, want_agg):
+        R = v.n_rows
+        rowptr = v.rowptr.long()
+        col = v.col.long()
+        deg = rowptr[1:] - rowptr[:-1]
+        dst = torch.repeat_interleave(torch.arange(R), deg)
+        e = _logit(s_src_full[col] + s_dst[dst], slope, mode)
+        if mode == 0:
+            m = torch.full((R, H), -float("inf"), dtype=e.dtype).scatter_reduce(
+                0, dst[:, None].expand_as(e), e, reduce="amax", include_self=True)
+            m = torch.where(deg[:, None] > 0, m, torch.zeros_like(m))
+            eps = 1e-16
+        else:
+            m = torch.zeros(R, H, dtype=e.dtype)
+            eps = 1e-9
+        ex = torch.exp(e - m[dst])
+        l = torch.zeros(R, H, dtype=e.dtype).index_add_(0, dst, ex)
+        inv_l = 1.0 / (l + eps)
+        beta = ex * inv_l[dst] * _drop(seed, v.csr_eid.long(), H, p, e.dtype)
+        agg = torch.zeros(R, H, C, dtype=e.dtype).index_add_(0, dst, h_full.view(-1, H, C)[col] * beta[..., None])
+        out = agg.mean(1) if mode == 0 else agg[:, 0]
+        if bias is not None:
+            out = out + bias
+        return out, m, inv_l, (agg if want_agg else None)
+
+    def bwd_prologue(self, g, out, agg, bias, s_dst, m, inv_l, H, C, mode, want_db):
+        gscale = 1.0 / H if mode == 0 else 1.0
+        a = agg if agg is not None else (out - bias if bias is not None else out).view(-1, 1, C)
+        D = gscale * (g.view(-1, 1, C) * a).sum(-1)
+        nstate = torch.stack([s_dst, m, inv_l, D], -1)
+        return nstate, (g.sum(0) if want_db else None)
+
+    def bwd_edges(self, v, h, s_src, nstate_full, g_full, dz, H, C, mode, slope, p, seed):
+        R = v.n_rows
+        colptr = v.colptr.long()
+        src = torch.repeat_interleave(torch.arange(R), colptr[1:] - colptr[:-1])
+        dst = v.row.long()
+        st = nstate_full.view(-1, H, 4)[dst]
+        z = s_src[src] + st[..., 0]
+        e, f = _logit(z, slope, mode), _dlogit(z, slope, mode)
+        alpha = torch.exp(e - st[..., 1]) * st[..., 2]
+        dm = _drop(seed, v.csc_eid.long(), H, p, alpha.dtype)
+        gscale = 1.0 / H if mode == 0 else 1.0
+        gi = g_full[dst]
+        grad_h = torch.zeros(R, H, C, dtype=h.dtype).index_add_(0, src, (alpha * dm * gscale)[..., None] * gi[:, None, :])
+        dot = (gi[:, None, :] * h.view(-1, H, C)[src]).sum(-1)
+        dzv = alpha * (dm * gscale * dot - st[..., 3]) * f
+        ds_src = torch.zeros(R, H, dtype=h.dtype).index_add_(0, src, dzv)
+        dz.view(-1, H)[v.dz_slot.long()] = dzv
+        return grad_h.view(R, H * C), ds_src
+
+    def bwd_epilogue(self, v, h, a_s, a_d, ds_src, dz, grad_h, H, C):
+        R = v.n_rows
+        rowptr = v.rowptr.long()
+        dst = torch.repeat_interleave(torch.arange(R), rowptr[1:] - rowptr[:-1])
+        ds_dst = torch.zeros(R, H, dtype=h.dtype).index_add_(0, dst, dz.view(-1, H)[:v.n_fwd_edges])
+        grad_h += (ds_src[..., None] * a_s + ds_dst[..., None] * a_d).reshape(R, H * C)
+        hv = h.view(R, H, C)
+        return (ds_src[..., None] * hv).sum(0), (ds_dst[..., None] * hv).sum(0)

@@ -1,0 +1,116 @@
+"""Row-sharded path with the real HIP stages (GPU): world_size 1 over RCCL, and world_size
+2 as two processes sharing the box's single GPU with gloo (device tensors staged through
+the host) -- both must equal the unsharded single-GPU model (fp32 tolerance 1e-5)."""
+import importlib
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(dev, heads=1):
+    pkg = importlib.import_module("plotpointe-gat-recommendation_amd")
+    g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
+    ei = torch.from_numpy(g.edge_index_numpy()).to(dev)
+    feats = torch.from_numpy(pkg.data.synthetic_item_features(g.n_items, 64, seed=5)).to(dev)
+    torch.manual_seed(0)
+    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=64, hidden=128, layers=2, heads=heads, attn_dropout=0.2)
+    with torch.no_grad():
+        for conv in full.convs:
+            conv.bias.uniform_(-0.1, 0.1)
+    full = full.to(dev).train()
+    u, i, j = pkg.data.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items, 20_000, seed=1)
+    return pkg, g, ei, feats, full, [torch.from_numpy(a).to(dev) for a in (u, i, j)]
+
+
+def _sharded(rank, world, out_dir, heads):
+    dev = torch.device("cuda", 0)
+    pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads)
+    D = pkg.dist
+    comm = D.Comm()
+    dg = D.build_dist_graph(ei, g.n_nodes, world, rank)
+    model = D.ShardedPyGGAT(full, dg, comm).train()
+    torch.manual_seed(123)
+    Z = model(feats)
+    loss = D.sharded_bpr_loss(Z, dg, comm, u, i, j, g.n_users, g.n_items)
+    loss.backward()
+    model.allreduce_grads()
+    tot = loss.detach().clone()
+    comm.all_reduce_(tot)
+    Zg = D.gather_rows_to_global(Z.detach(), dg, comm)
+    grads = {n: p.grad.detach().cpu() for n, p in model.named_parameters() if n != "user_emb_local"}
+    C = model.user_emb_local.size(1)
+    blk = torch.zeros(dg.R, C, device=dev)
+    blk[:model.u1 - model.u0] = model.user_emb_local.grad
+    ug = comm.all_gather_rows(blk).cpu()
+    rows = [ug[r * dg.R: r * dg.R + (min(int(dg.bounds[r + 1]), g.n_users) - min(int(dg.bounds[r]), g.n_users))]
+            for r in range(world)]
+    if rank == 0:
+        torch.save({"Z": Zg.cpu(), "loss": tot.cpu(), "grads": grads, "user_grad": torch.cat(rows)},
+                   os.path.join(out_dir, f"sharded_{world}.pt"))
+
+
+def _worker(rank, world, port, out_dir, heads):
+    sys.path.insert(0, str(ROOT))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _sharded(rank, world, out_dir, heads)
+    finally:
+        dist.destroy_process_group()
+
+
+def _unsharded(dev, heads):
+    pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads)
+    torch.manual_seed(123)
+    Z = full(feats, ei)
+    loss = pkg.bpr_loss(Z, g.n_users, u, i, j)
+    loss.backward()
+    return Z.detach().cpu(), loss.detach().cpu(), {n: p.grad.detach().cpu() for n, p in full.named_parameters()}
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _check(res, ref):
+    Z, loss, grads = ref
+    assert _rel(res["Z"], Z) <= 1e-5
+    assert abs(float(res["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
+    assert _rel(res["user_grad"], grads["user_emb.weight"]) <= 1e-5
+    for k, v in res["grads"].items():
+        assert _rel(v, grads[k]) <= 1e-5, k
+
+
+@pytest.mark.parametrize("heads", [1, 2])
+def test_sharded_world1_rccl(cuda, tmp_path, heads):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    try:
+        _sharded(0, 1, str(tmp_path), heads)
+    finally:
+        dist.destroy_process_group()
+    _check(torch.load(tmp_path / "sharded_1.pt", weights_only=False), _unsharded(cuda, heads))
+
+
+def test_sharded_world2_shared_gpu(cuda, tmp_path):
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), 1), nprocs=2, join=True, start_method="spawn")
+    _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), _unsharded(cuda, 1))
