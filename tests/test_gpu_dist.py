@@ -95,8 +95,11 @@ def _check(res, ref):
     assert _rel(res["Z"], Z) <= 1e-5
     assert abs(float(res["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
     assert _rel(res["user_grad"], grads["user_emb.weight"]) <= 1e-5
+    # vector-valued grads (att_*, bias, item_proj.bias) are sums over every node with
+    # cancellation, and the two sides sum in different orders: same 1e-4 bound as the
+    # attention-vector grads of test_gpu_parity.py
     for k, v in res["grads"].items():
-        assert _rel(v, grads[k]) <= 1e-5, k
+        assert _rel(v, grads[k]) <= (1e-5 if v.dim() == 2 and "att" not in k else 1e-4), k
 
 
 @pytest.mark.parametrize("heads", [1, 2])
