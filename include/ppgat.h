@@ -201,6 +201,16 @@ int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, size_t* bytes);
 int ppgat_gemm_tn(const float* A, const float* B, int64_t n, int m, int k, float* out, float* colsum,
                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- sampled ranking (evaluation) ------------------------------------------------
+ * Replaces: the per-user loop of eval_sampled, scripts/train_gat_pyg.py:160-175:
+ *   scores = I[cands[b]] @ U[users[b]];  rank[b] = #(scores[1:] > scores[0]) + 1
+ * cands [n_eval, n_cand] int64 item ids (column 0 = the held-out positive); Z rows as in
+ * ppgat_bpr_fwd (row_map nullable).
+ */
+int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                       int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
+                       int32_t* rank, void* stream);
+
 /* ---- in-process kernel timing (HIP events on the launch stream) --------- */
 #define PPGAT_K_CSR 0
 #define PPGAT_K_SCORES 1

@@ -425,6 +425,20 @@ int ppgat_gemm_tn(const float* A, const float* B, int64_t n, int m, int k, float
   return PPGAT_OK;
 }
 
+int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                       int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
+                       int32_t* rank, void* stream) {
+  if (!ppgat::bpr_channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "sampled_rank: channels");
+  if (n_users < 1 || n_items < 1 || n_eval < 0 || n_cand < 1) return fail(PPGAT_ERR_INVALID, "sampled_rank: sizes");
+  if (row_map == nullptr && n_rows != n_users + n_items)
+    return fail(PPGAT_ERR_INVALID, "sampled_rank: n_rows must be n_users + n_items without a row_map");
+  if (!Z || (n_eval > 0 && (!users || !cands || !rank))) return fail(PPGAT_ERR_INVALID, "sampled_rank: null pointer");
+  hipError_t e = ppgat::sampled_rank(Z, n_users, n_items, row_map, channels, users, cands, n_eval, n_cand, rank,
+                                     static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "sampled_rank");
+  return PPGAT_OK;
+}
+
 int ppgat_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
   g_prof.on = on != 0;

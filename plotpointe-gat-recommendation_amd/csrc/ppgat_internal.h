@@ -66,4 +66,9 @@ size_t gemm_tn_workspace_bytes(int64_t N, int M, int K);
 hipError_t gemm_tn(const float* A, const float* B, int64_t N, int M, int K, float* out, float* colsum, void* ws,
                    hipStream_t st);
 
+// evaluation (ppgat_eval.hip)
+hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                        const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,
+                        hipStream_t st);
+
 }  // namespace ppgat
