@@ -60,6 +60,7 @@ SIGNATURES = {
                               c_vp, c_sz, c_vp]),
     "ppgat_gemm_tn_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_gemm_tn": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ppgat_profile_enable": (c_int, [c_int]),
     "ppgat_profile_reset": (c_int, []),
     "ppgat_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
