@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--heads", type=int, default=1)
     ap.add_argument("--samples", type=int, default=200_000)
     ap.add_argument("--attn-dropout", type=float, default=0.1)
+    ap.add_argument("--config", type=int, choices=[2, 3], default=2,
+                    help="2: U-I graph (headline); 3: U-I + I-I kNN k=20 edges (SURVEY.md 8(d) cfg 3)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
@@ -134,6 +136,9 @@ def main():
     g = data.synthetic_ui_graph(seed=42)
     feats_np = data.synthetic_item_features(g.n_items, 128, seed=42)
     ei_np = g.edge_index_numpy()
+    if args.config == 3:  # I-I kNN relation appended to the homogeneous edge_index (A10, "extension")
+        rows, cols, _ = data.synthetic_ii_edges(g, k=20, seed=42)
+        ei_np = np.concatenate([ei_np, data.ii_edge_columns(g.n_users, rows, cols)], 1)
     E, N = ei_np.shape[1], g.n_nodes
     u, i, j = data.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items, args.samples, seed=42)
     ei = torch.from_numpy(ei_np).to(dev)
@@ -221,8 +226,9 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (config-2 statistics-matched U-I graph, random-init weights)",
-        "config": {"workload": "cfg2: PyGGAT train step (fwd+BPR+bwd+Adam), 1,689,116 interactions, "
-                               "192,403 users + 63,001 items",
+        "config": {"workload": ("cfg2: PyGGAT train step (fwd+BPR+bwd+Adam), 1,689,116 interactions, "
+                                "192,403 users + 63,001 items") if args.config == 2 else
+                               "cfg3: cfg2 + I-I kNN (k=20, sim>=0.3) edges, PyGGAT train step",
                    "edges": E, "nodes": N, "layers": args.layers, "heads": H, "hidden": C,
                    "bpr_samples": args.samples, "attn_dropout": args.attn_dropout,
                    "parallelism": f"row-sharded x{world} (RCCL all_gather/reduce_scatter)" if world > 1

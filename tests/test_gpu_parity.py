@@ -291,3 +291,31 @@ def test_custom_model_one_train_step(pkg, cuda, cfg1):
     # Adam's first step is ~lr*sign(g): a gradient element that is ~0 on both sides
     # can flip sign, so the bound here is looser than the forward bound
     assert rel(Z1, cfg1["Z1_items"]) <= 1e-4
+
+
+def test_config3_ui_plus_ii_edges_model(pkg, oracle, cuda):
+    """A10 (extension, no reference trainer consumes I-I edges): the U-I edge_index with the
+    I-I kNN relation appended (src = neighbour item, dst = item) through PyGGAT, forward and
+    all parameter gradients vs the oracle model on the same concatenated edge_index."""
+    d = pkg.data
+    g = d.synthetic_ui_graph(n_users=2000, n_items=600, n_interactions=20_000, seed=4)
+    rows, cols, _ = d.synthetic_ii_edges(g, k=20, seed=4)
+    ei = np.concatenate([g.edge_index_numpy(), d.ii_edge_columns(g.n_users, rows, cols)], 1)
+    assert ei.shape[1] > 2 * len(g.user_items)
+    feats = torch.from_numpy(d.synthetic_item_features(g.n_items, 128, seed=4))
+    torch.manual_seed(1)
+    m = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=128, hidden=128, layers=2, heads=1, attn_dropout=0.0)
+    with torch.no_grad():
+        for c in m.convs:
+            c.bias.uniform_(-0.1, 0.1)
+    m = m.to(cuda)
+    G = torch.randn(g.n_nodes, 128, dtype=torch.float64)
+    Z = m(feats.to(cuda), torch.from_numpy(ei).to(cuda))
+    (Z * G.float().to(cuda)).sum().backward()
+    P = {k: v.detach().double().cpu().requires_grad_(True) for k, v in m.named_parameters()}
+    Zr = oracle.pyg_gat_model(P, feats.double(), torch.from_numpy(ei), 2, 1)
+    (Zr * G).sum().backward()
+    assert rel(Z, Zr) <= 1e-5
+    for k, v in m.named_parameters():
+        tol = 1e-4 if v.dim() != 2 else 1e-5
+        assert rel(v.grad, P[k].grad) <= tol, k
