@@ -211,6 +211,21 @@ int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t 
                        int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
                        int32_t* rank, void* stream);
 
+/* ---- fusion MLP inference on the matrix cores (north star's MFMA target) ----------
+ * Replaces: FusionMLP.forward + the normalisation and the per-row image copy loop of the
+ *           inference pass, embeddings/fuse_modal.py:18-36,227-241:
+ *   out = normalize?(relu([txt | img_row] W1^T + b1) W2^T + b2)   (norm: y / (||y|| + 1e-8))
+ * img_row = img[img_index[b]] when img_index != NULL and img_index[b] >= 0, img_fallback
+ * (the mean image embedding) when img_index[b] < 0, img[b] when img_index == NULL.
+ * z1 (nullable) receives the pre-activation [n, hidden] for a training backward.
+ * fp32 MFMA (exact fp32 FMA chains).  hidden_dim must be 256, output_dim 128, text_dim and
+ * img_dim multiples of 32 (the reference's 384 + 512 -> 256 -> 128).
+ */
+int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                     int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
+                     const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
+                     void* stream);
+
 /* ---- in-process kernel timing (HIP events on the launch stream) --------- */
 #define PPGAT_K_CSR 0
 #define PPGAT_K_SCORES 1
@@ -221,7 +236,8 @@ int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t 
 #define PPGAT_K_BWD_RED 6
 #define PPGAT_K_SCHED 7
 #define PPGAT_K_GEMM_TN 8
-#define PPGAT_K_COUNT 9
+#define PPGAT_K_FUSION 9
+#define PPGAT_K_COUNT 10
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

@@ -439,6 +439,26 @@ int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t 
   return PPGAT_OK;
 }
 
+int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                     int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
+                     const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
+                     void* stream) {
+  if (!ppgat::fusion_shape_ok(text_dim, img_dim, hidden_dim, output_dim))
+    return fail(PPGAT_ERR_UNSUPPORTED, "fusion_fwd: needs hidden 256, output 128, text/img dims % 32 == 0");
+  if (n < 0) return fail(PPGAT_ERR_INVALID, "fusion_fwd: n < 0");
+  if (n > 0 && (!w1 || !b1 || !w2 || !b2 || !out || (text_dim > 0 && !txt) ||
+                (img_dim > 0 && !img && !img_fallback)))
+    return fail(PPGAT_ERR_INVALID, "fusion_fwd: null pointer");
+  if (img_dim > 0 && img_index != nullptr && !img_fallback)
+    return fail(PPGAT_ERR_INVALID, "fusion_fwd: img_index needs img_fallback for rows without an image");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_FUSION, st);
+  hipError_t e = ppgat::fusion_fwd(txt, img, img_index, img_fallback, n, text_dim, img_dim, w1, b1, w2, b2, normalize,
+                                   out, z1, st);
+  if (e != hipSuccess) return hip_fail(e, "fusion_fwd");
+  return PPGAT_OK;
+}
+
 int ppgat_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
   g_prof.on = on != 0;

@@ -71,4 +71,10 @@ hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const 
                         const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,
                         hipStream_t st);
 
+// fusion MLP (ppgat_fusion.hip)
+bool fusion_shape_ok(int Dt, int Di, int h1, int d_out);
+hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                      int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
+                      int normalize, float* out, float* z1_out, hipStream_t st);
+
 }  // namespace ppgat

@@ -1,0 +1,136 @@
+"""Multimodal fusion (the north star's MFMA target):
+embeddings/fuse_modal.py.
+
+``FusionMLP``             -- :18-36, same modules/keys (mlp.0, mlp.3, txt_proj, img_proj) and
+                             construction order (seeded construction = reference weights).
+                             Eval-mode forward runs the fused fp32-MFMA kernel
+                             (``ppgat_fusion_fwd``); train-mode forward uses torch ops
+                             (dropout needs torch's RNG stream to match the reference).
+``contrastive_fusion_loss`` -- :39-72 (InfoNCE, tau = 0.07, both modalities).
+``infer_fused_embeddings``  -- :220-244: all items, mean-image fallback for items without an
+                             image, L2-normalised; the per-row host->device image copy loop
+                             becomes an index gather inside the kernel.
+``train_fusion``            -- :167-214 training loop (Adam, contiguous batches).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+def fusion_forward(txt: torch.Tensor, img: Optional[torch.Tensor], W1, b1, W2, b2, normalize: bool,
+                   img_index: Optional[torch.Tensor] = None, img_fallback: Optional[torch.Tensor] = None,
+                   want_z1: bool = False):
+    lib = _lib.load()
+    if not txt.is_cuda or txt.dtype != torch.float32:
+        raise RuntimeError("fusion_forward: fp32 ROCm tensors required (no CPU path)")
+    dev = txt.device
+    txt = txt.contiguous()
+    n, Dt = txt.shape
+    Di = W1.size(1) - Dt
+    H1, Do = W1.size(0), W2.size(0)
+    out = torch.empty(n, Do, dtype=torch.float32, device=dev)
+    z1 = torch.empty(n, H1, dtype=torch.float32, device=dev) if want_z1 else None
+    ptr = _lib.ptr
+    # keep every converted tensor alive until the launch is enqueued
+    imgc = img.contiguous() if img is not None else None
+    idx32 = img_index.to(torch.int32).contiguous() if img_index is not None else None
+    fb = img_fallback.contiguous() if img_fallback is not None else None
+    W1c, b1c, W2c, b2c = (t.detach().contiguous() for t in (W1, b1, W2, b2))
+    _lib.check(lib.ppgat_fusion_fwd(ptr(txt), ptr(imgc), ptr(idx32), ptr(fb), n, Dt, Di, W1c.data_ptr(), b1c.data_ptr(),
+                                    H1, W2c.data_ptr(), b2c.data_ptr(), Do, 1 if normalize else 0, out.data_ptr(),
+                                    ptr(z1), _lib.stream_handle(dev)), "fusion_fwd")
+    return (out, z1) if want_z1 else out
+
+
+class FusionMLP(nn.Module):
+    """embeddings/fuse_modal.py:18-36."""
+
+    def __init__(self, text_dim, img_dim, output_dim=128, hidden_dim=256):
+        super().__init__()
+        input_dim = text_dim + img_dim
+        self.mlp = nn.Sequential(
+            nn.Linear(input_dim, hidden_dim),
+            nn.ReLU(),
+            nn.Dropout(0.1),
+            nn.Linear(hidden_dim, output_dim),
+        )
+        self.txt_proj = nn.Linear(text_dim, output_dim)
+        self.img_proj = nn.Linear(img_dim, output_dim)
+        self.text_dim, self.img_dim = text_dim, img_dim
+
+    def forward(self, text_emb, img_emb):
+        if self.training or not text_emb.is_cuda:
+            if not text_emb.is_cuda:
+                raise RuntimeError("FusionMLP runs on ROCm devices only; there is no CPU path")
+            return self.mlp(torch.cat([text_emb, img_emb], dim=-1))
+        return fusion_forward(text_emb, img_emb, self.mlp[0].weight, self.mlp[0].bias, self.mlp[3].weight,
+                              self.mlp[3].bias, normalize=False)
+
+
+def contrastive_fusion_loss(fused, txt_emb, img_emb, temperature=0.07):
+    """embeddings/fuse_modal.py:39-72 -> (loss, loss_txt, loss_img)."""
+    import torch.nn.functional as F
+    batch_size = fused.size(0)
+    fused_norm = F.normalize(fused, dim=-1)
+    txt_norm = F.normalize(txt_emb, dim=-1)
+    img_norm = F.normalize(img_emb, dim=-1)
+    sim_fused_txt = torch.matmul(fused_norm, txt_norm.T) / temperature
+    sim_fused_img = torch.matmul(fused_norm, img_norm.T) / temperature
+    labels = torch.arange(batch_size, device=fused.device)
+    loss_txt = F.cross_entropy(sim_fused_txt, labels)
+    loss_img = F.cross_entropy(sim_fused_img, labels)
+    loss = (loss_txt + loss_img) / 2
+    return loss, loss_txt.item(), loss_img.item()
+
+
+def train_fusion(model: FusionMLP, txt_aligned: torch.Tensor, img_aligned: torch.Tensor, epochs: int = 5,
+                 batch_size: int = 512, lr: float = 1e-3):
+    """fuse_modal.py:167-214 (tensors already on the device)."""
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    model.train()
+    history = []
+    for _ in range(epochs):
+        tot = tt = ti = 0.0
+        nb = 0
+        for i in range(0, len(txt_aligned), batch_size):
+            bt, bi = txt_aligned[i:i + batch_size], img_aligned[i:i + batch_size]
+            opt.zero_grad()
+            fused = model(bt, bi)
+            loss, lt, li = contrastive_fusion_loss(fused, model.txt_proj(bt), model.img_proj(bi))
+            loss.backward()
+            opt.step()
+            tot += loss.item(); tt += lt; ti += li
+            nb += 1
+        history.append((tot / nb, tt / nb, ti / nb))
+    return history
+
+
+def infer_fused_embeddings(model: FusionMLP, txt_emb: torch.Tensor, img_aligned: torch.Tensor,
+                           img_index: torch.Tensor, chunk: int = 1 << 17) -> torch.Tensor:
+    """fuse_modal.py:220-244: fused, L2-normalised embeddings for ALL items.
+
+    img_index[g] = row of img_aligned holding item g's image, or -1 (use the mean image
+    embedding, :211-213,231).  One fused MFMA launch per ``chunk`` items."""
+    model.eval()
+    mean_img = img_aligned.mean(dim=0)
+    out = torch.empty(txt_emb.size(0), model.mlp[3].out_features, dtype=torch.float32, device=txt_emb.device)
+    with torch.no_grad():
+        for s in range(0, txt_emb.size(0), chunk):
+            e = min(s + chunk, txt_emb.size(0))
+            out[s:e] = fusion_forward(txt_emb[s:e], img_aligned, model.mlp[0].weight, model.mlp[0].bias,
+                                      model.mlp[3].weight, model.mlp[3].bias, normalize=True,
+                                      img_index=img_index[s:e], img_fallback=mean_img)
+    return out
+
+
+def image_index_for_items(n_items: int, img_indices: np.ndarray) -> np.ndarray:
+    """fuse_modal.py:147-151: item g -> local image row (img_idx_map), -1 if none."""
+    idx = np.full(n_items, -1, np.int32)
+    idx[np.asarray(img_indices, np.int64)] = np.arange(len(img_indices), dtype=np.int32)
+    return idx

@@ -46,9 +46,12 @@ def _stub_gcs():
 
     storage.Client = Client
     cloud.storage = storage
+    aiplatform = types.ModuleType("google.cloud.aiplatform")  # imported by fuse_modal.py:14, unused by the math
+    cloud.aiplatform = aiplatform
     google.cloud = cloud
     sys.modules["google.cloud"] = cloud
     sys.modules["google.cloud.storage"] = storage
+    sys.modules["google.cloud.aiplatform"] = aiplatform
 
 
 def load_reference_custom():
@@ -190,7 +193,39 @@ def plumbing_case(ref):
     print(f"plumbing: n_users={n_users} n_items={n_items} E={ei.shape[1]} loss1={loss.item():.6f} val={val_metrics}")
 
 
+def fusion_case():
+    """FusionMLP (embeddings/fuse_modal.py:18-36), InfoNCE (:39-72) and the inference
+    normalisation (:239-241) of the real reference, imported with inert GCS/Vertex stubs."""
+    _stub_gcs()
+    spec = importlib.util.spec_from_file_location("ref_fuse_modal", REF / "embeddings" / "fuse_modal.py")
+    fm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fm)
+    torch.manual_seed(11)
+    model = fm.FusionMLP(384, 512, 128, 256)
+    rng = np.random.default_rng(11)
+    txt = rng.standard_normal((300, 384)).astype(np.float32)
+    img = rng.standard_normal((300, 512)).astype(np.float32)
+    model.eval()
+    with torch.no_grad():
+        fused = model(torch.from_numpy(txt), torch.from_numpy(img))
+        fused_n = fused / (fused.norm(dim=-1, keepdim=True) + 1e-8)
+    # one training-mode loss/grad evaluation with dropout off (RNG streams cannot match)
+    model.train()
+    model.mlp[2].p = 0.0
+    t, im = torch.from_numpy(txt[:256]), torch.from_numpy(img[:256])
+    f = model(t, im)
+    loss, lt, li = fm.contrastive_fusion_loss(f, model.txt_proj(t), model.img_proj(im))
+    loss.backward()
+    np.savez_compressed(
+        HERE / "fusion_mlp.npz", txt=txt, img=img,
+        **{"sd__" + k: v.detach().numpy() for k, v in model.state_dict().items()},
+        fused=fused.numpy(), fused_norm=fused_n.numpy(), loss=np.float32(loss.item()), loss_txt=np.float32(lt),
+        loss_img=np.float32(li), **{"grad__" + k: p.grad.numpy() for k, p in model.named_parameters()})
+    print(f"fusion: loss={loss.item():.6f} keys={list(model.state_dict().keys())}")
+
+
 def main():
+    fusion_case()
     ref = load_reference_custom()
     layer_case(ref, "small_c8", 0, 300, 3000, 8, "uniform")
     layer_case(ref, "uniform_c128", 1, 1200, 12000, 128, "uniform")

@@ -1,0 +1,81 @@
+"""A11 FusionMLP (GPU): the fused fp32-MFMA inference kernel vs the reference golden
+(embeddings/fuse_modal.py imported in make_golden.py) and vs an fp64 restatement, with the
+mean-image fallback path; InfoNCE training step vs the reference's loss and grads.
+Tolerance: max-abs error / max-abs reference <= 1e-5."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.from_numpy(np.asarray(a, np.float64))
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.from_numpy(np.asarray(b, np.float64))
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return dict(np.load(GOLDEN / "fusion_mlp.npz"))
+
+
+def _model(pkg, gold, cuda):
+    m = pkg.fusion.FusionMLP(384, 512, 128, 256)
+    sd = {k[4:]: torch.from_numpy(v) for k, v in gold.items() if k.startswith("sd__")}
+    assert sorted(sd) == sorted(m.state_dict())
+    m.load_state_dict(sd)
+    return m.to(cuda)
+
+
+def test_seeded_construction_matches_reference(pkg, gold):
+    torch.manual_seed(11)
+    m = pkg.fusion.FusionMLP(384, 512, 128, 256)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, torch.from_numpy(gold["sd__" + k])), k
+
+
+def test_fused_kernel_vs_reference_golden(pkg, gold, cuda):
+    m = _model(pkg, gold, cuda).eval()
+    txt, img = torch.from_numpy(gold["txt"]).to(cuda), torch.from_numpy(gold["img"]).to(cuda)
+    with torch.no_grad():
+        fused = m(txt, img)
+    assert rel(fused, gold["fused"]) <= 1e-5
+    idx = torch.arange(300, dtype=torch.int32, device=cuda)
+    out = pkg.fusion.fusion_forward(txt, img, m.mlp[0].weight, m.mlp[0].bias, m.mlp[3].weight, m.mlp[3].bias,
+                                    normalize=True, img_index=idx, img_fallback=img.mean(0))
+    assert rel(out, gold["fused_norm"]) <= 1e-5
+
+
+def test_infer_all_items_with_fallback_vs_fp64(pkg, oracle, gold, cuda):
+    m = _model(pkg, gold, cuda)
+    rng = np.random.default_rng(5)
+    n_items, n_img = 5000, 3100
+    txt = rng.standard_normal((n_items, 384)).astype(np.float32)
+    img_indices = np.sort(rng.choice(n_items, n_img, replace=False))       # items that have an image
+    img_aligned = rng.standard_normal((n_img, 512)).astype(np.float32)
+    idx = pkg.fusion.image_index_for_items(n_items, img_indices)
+    out = pkg.fusion.infer_fused_embeddings(m, torch.from_numpy(txt).to(cuda), torch.from_numpy(img_aligned).to(cuda),
+                                            torch.from_numpy(idx).to(cuda), chunk=1777)
+    mean_img = img_aligned.astype(np.float64).mean(0)
+    img_rows = np.where(idx[:, None] >= 0, img_aligned.astype(np.float64)[np.maximum(idx, 0)], mean_img)
+    P = {k: v.detach().double().cpu() for k, v in m.state_dict().items()}
+    ref = oracle.fusion_mlp(torch.from_numpy(txt).double(), torch.from_numpy(img_rows), P["mlp.0.weight"],
+                            P["mlp.0.bias"], P["mlp.3.weight"], P["mlp.3.bias"])
+    assert rel(out, ref) <= 1e-5
+    assert torch.allclose(out.norm(dim=-1).cpu(), torch.ones(n_items), atol=1e-5)
+
+
+def test_training_step_loss_and_grads_vs_reference(pkg, gold, cuda):
+    m = _model(pkg, gold, cuda).train()
+    m.mlp[2].p = 0.0
+    t = torch.from_numpy(gold["txt"][:256]).to(cuda)
+    im = torch.from_numpy(gold["img"][:256]).to(cuda)
+    f = m(t, im)
+    loss, lt, li = pkg.fusion.contrastive_fusion_loss(f, m.txt_proj(t), m.img_proj(im))
+    loss.backward()
+    assert abs(loss.item() - float(gold["loss"])) <= 1e-5 * float(gold["loss"])
+    for k, p in m.named_parameters():
+        assert rel(p.grad, gold["grad__" + k]) <= 1e-4, k
