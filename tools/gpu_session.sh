@@ -24,6 +24,8 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
+    bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
+    fusion) run bench_fusion 300 python tools/bench_fusion.py ;;
     prof)  (cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --steps 10 --warmup 3 --cpu-baseline-seconds 0) ;;
     pmc)   (cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o fetch -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \
            (cd /tmp && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o write -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \
