@@ -160,8 +160,17 @@ int ppgat_bwd_prologue(const float* grad_out, const float* out, const float* agg
 int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
                     const int32_t* dz_slot, int64_t n_edges, int heads, int channels, const float* h,
                     const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
-                    float dropout_p, uint64_t seed, float* grad_h, float* ds_src, float* dz,
-                    void* workspace, size_t workspace_bytes, void* stream);
+                    float dropout_p, uint64_t seed, float* grad_h, int64_t ld_grad_h, float* ds_src,
+                    int64_t ld_ds_src, float* dz, void* workspace, size_t workspace_bytes, void* stream);
+/* ds_dst[i*ld + h] = sum of dz over the CSR segment of destination i (no epilogue): with
+ * grad_h and ds_src/ds_dst written side by side into one [N, ld] buffer
+ * D = [dh_msg | ds_src | ds_dst], the projection gradients follow from two GEMMs with
+ * W_aug = [W; A_src; A_dst] (A_src[h] = sum_c att_src[h,c] W[h*C+c, :]):
+ *   dx = D W_aug,   D^T x = [dh_msg^T x ; ds_src^T x ; ds_dst^T x]  (ppgat_gemm_tn with V),
+ *   dW = dh_msg^T x + att_src (x) (ds_src^T x) + att_dst (x) (ds_dst^T x),
+ *   datt_src[h] = W_h (ds_src^T x)[h],  datt_dst[h] = W_h (ds_dst^T x)[h]. */
+int ppgat_bwd_dst_sum(const int32_t* rowptr, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
+                      int64_t ld_ds_dst, void* stream);
 int ppgat_bwd_epilogue(const int32_t* rowptr, int64_t n_nodes, int heads, int channels, const float* h,
                        const float* att_src, const float* att_dst, const float* ds_src, const float* dz,
                        float* grad_h, float* grad_att_src, float* grad_att_dst, float* part, void* stream);
@@ -194,11 +203,14 @@ int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
  * Replaces: the weight (and bias) gradient of torch.nn.Linear in GATConv.lin /
  *           SimpleGATLayer.lin (train_gat_custom.py:66,77) and PyGGAT.item_proj
  *           (train_gat_pyg.py:74,81): out[M,K] = A[N,M]^T B[N,K]; colsum[M] = sum_n A[n,:]
- *           when colsum != NULL.  fp32 in, fp32 MFMA (exact fp32 FMA), N split over
- *           workgroups with an ordered reduction of the partials (deterministic).
+ *           when colsum != NULL; vout[nv, K] = V[N, nv]^T B when nv > 0 (nv <= 16).
+ *           Row strides lda/ldb/ldv (floats; lda, ldb multiples of 4).  fp32 in, fp32 MFMA
+ *           (exact fp32 FMA), N split over workgroups with an ordered reduction of the
+ *           partials (deterministic).
  */
-int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, size_t* bytes);
-int ppgat_gemm_tn(const float* A, const float* B, int64_t n, int m, int k, float* out, float* colsum,
+int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, int nv, size_t* bytes);
+int ppgat_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t n, int m, int k, float* out,
+                  float* colsum, const float* V, int64_t ldv, int nv, float* vout,
                   void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- sampled ranking (evaluation) ------------------------------------------------

@@ -50,7 +50,8 @@ SIGNATURES = {
     "ppgat_bwd_prologue": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp,
                                    c_vp, c_vp]),
     "ppgat_bwd_edges": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
-                                c_u64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+                                c_u64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_bwd_dst_sum": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
     "ppgat_bwd_epilogue": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp]),
     "ppgat_bpr_workspace_bytes": (c_int, [c_i64, c_i64, c_int, ctypes.POINTER(c_sz)]),
@@ -58,8 +59,9 @@ SIGNATURES = {
                               c_vp, c_vp, c_sz, c_vp]),
     "ppgat_bpr_bwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                               c_vp, c_sz, c_vp]),
-    "ppgat_gemm_tn_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
-    "ppgat_gemm_tn": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_gemm_tn_workspace_bytes": (c_int, [c_i64, c_int, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_gemm_tn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp,
+                              c_vp, c_sz, c_vp]),
     "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),

@@ -11,8 +11,9 @@
                       order (so a seeded construction yields the reference's weights)
                       and keys (``lin.weight``, ``a_src``, ``a_dst``).
 
-Both run ``h = lin(x)`` through torch (a plain library GEMM) and everything on the
-edges through ``libppgat.so``.  Dropout on alpha is the counter-hash mask of
+Both run the layer as ``hip_ops.gat_layer``: ``h = lin(x)`` through the BLAS library,
+everything on the edges through ``libppgat.so``, and a backward that folds the attention
+terms into the projection GEMMs (no epilogue pass).  Dropout on alpha is the counter-hash mask of
 include/ppgat.h, drawn fresh per training forward from torch's CPU generator.
 """
 from __future__ import annotations
@@ -22,7 +23,7 @@ import math
 import torch
 
 from . import _lib
-from .hip_ops import gat_aggregate, graph_cache, linear
+from .hip_ops import gat_layer, graph_cache
 
 
 def _dropout_seed() -> int:
@@ -88,11 +89,10 @@ class GATConv(torch.nn.Module):
         if return_attention_weights:
             raise NotImplementedError("return_attention_weights not implemented")
         graph = graph_cache.get(edge_index, x.size(0))
-        h = linear(x, self.lin.weight)
         p = float(self.dropout) if self.training else 0.0
         seed = _dropout_seed() if p > 0 else 0
-        return gat_aggregate(h, self.att_src, self.att_dst, self.bias, graph, self.heads, self.out_channels,
-                             _lib.MODE_PYG, float(self.negative_slope), p, seed)
+        return gat_layer(x, self.lin.weight, self.att_src, self.att_dst, self.bias, graph, self.heads,
+                         self.out_channels, _lib.MODE_PYG, float(self.negative_slope), p, seed)
 
     def __repr__(self):
         return (f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads}, "
@@ -119,8 +119,7 @@ class SimpleGATLayer(torch.nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
         graph = graph_cache.get(edge_index, x.size(0))
-        h = linear(x, self.lin.weight)
         p = float(self.drop.p) if self.training else 0.0
         seed = _dropout_seed() if p > 0 else 0
-        return gat_aggregate(h, self.a_src, self.a_dst, None, graph, 1, self.out_dim, _lib.MODE_CUSTOM,
-                             float(self.leaky.negative_slope), p, seed)
+        return gat_layer(x, self.lin.weight, self.a_src, self.a_dst, None, graph, 1, self.out_dim, _lib.MODE_CUSTOM,
+                         float(self.leaky.negative_slope), p, seed)

@@ -249,8 +249,10 @@ int ppgat_bwd_prologue(const float* grad_out, const float* out, const float* agg
 int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
                     const int32_t* dz_slot, int64_t n_edges, int heads, int channels, const float* h,
                     const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
-                    float dropout_p, uint64_t seed, float* grad_h, float* ds_src, float* dz, void* workspace,
-                    size_t workspace_bytes, void* stream) {
+                    float dropout_p, uint64_t seed, float* grad_h, int64_t ld_grad_h, float* ds_src,
+                    int64_t ld_ds_src, float* dz, void* workspace, size_t workspace_bytes, void* stream) {
+  if (ld_grad_h < (int64_t)heads * channels || (ld_grad_h % 4) || ld_ds_src < heads)
+    return fail(PPGAT_ERR_INVALID, "bwd_edges: bad leading dimensions (ld_grad_h >= H*C, multiple of 4)");
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd_edges: unsupported channels");
   if (heads < 1 || heads > ppgat::kMaxHeads || n_edges < 0) return fail(PPGAT_ERR_INVALID, "bwd_edges: bad sizes");
   if (mode != PPGAT_MODE_PYG && mode != PPGAT_MODE_CUSTOM) return fail(PPGAT_ERR_INVALID, "unknown mode");
@@ -272,11 +274,22 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
   {
     Timed t(PPGAT_K_BWD_SRC, st);
     e = ppgat::launch_bwd_src(it, row, csc_eid, dz_slot, heads, channels, h, s_src, nstate, grad_out, mode,
-                              negative_slope, gscale, dropout_p, seed, grad_h, ds_src, dz,
+                              negative_slope, gscale, dropout_p, seed, grad_h, ld_grad_h, ds_src, ld_ds_src, dz,
                               static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
                               src_sched->n_hubs, st);
   }
   if (e != hipSuccess) return hip_fail(e, "bwd_edges");
+  return PPGAT_OK;
+}
+
+int ppgat_bwd_dst_sum(const int32_t* rowptr, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
+                      int64_t ld_ds_dst, void* stream) {
+  if (n_nodes < 0 || heads < 1 || ld_ds_dst < heads) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: bad sizes");
+  if (n_nodes > 0 && (!rowptr || !ds_dst)) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_BWD_EPI, st);
+  hipError_t e = ppgat::launch_dst_sum(rowptr, n_nodes, heads, dz, ds_dst, ld_ds_dst, st);
+  if (e != hipSuccess) return hip_fail(e, "bwd_dst_sum");
   return PPGAT_OK;
 }
 
@@ -348,8 +361,8 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
                                   grad_bias, bias_part, stream))
     return rc;
   if (int rc = ppgat_bwd_edges(sched, row, csc_eid, csc2csr, n_edges, heads, channels, h, s_src, nstate, grad_out,
-                               mode, negative_slope, dropout_p, seed, grad_h, ds_src, dz, hpart,
-                               partial_bytes(sched->n_hub_items, heads, channels), stream))
+                               mode, negative_slope, dropout_p, seed, grad_h, (int64_t)heads * channels, ds_src,
+                               heads, dz, hpart, partial_bytes(sched->n_hub_items, heads, channels), stream))
     return rc;
   return ppgat_bwd_epilogue(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, grad_att_src,
                             grad_att_dst, bpart, stream);
@@ -406,21 +419,27 @@ int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
   return PPGAT_OK;
 }
 
-int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, size_t* bytes) {
-  if (!bytes || n < 0 || m < 1 || k < 1) return fail(PPGAT_ERR_INVALID, "gemm_tn_workspace_bytes: bad arguments");
-  *bytes = ppgat::gemm_tn_workspace_bytes(n, m, k);
+int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, int nv, size_t* bytes) {
+  if (!bytes || n < 0 || m < 1 || k < 1 || nv < 0) return fail(PPGAT_ERR_INVALID, "gemm_tn_workspace_bytes: bad arguments");
+  *bytes = ppgat::gemm_tn_workspace_bytes(n, m, k, nv);
   return PPGAT_OK;
 }
 
-int ppgat_gemm_tn(const float* A, const float* B, int64_t n, int m, int k, float* out, float* colsum,
-                  void* workspace, size_t workspace_bytes, void* stream) {
-  if (n < 0 || m < 1 || k < 1) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad sizes");
-  if (!out || (n > 0 && (!A || !B))) return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
-  if (!workspace || workspace_bytes < ppgat::gemm_tn_workspace_bytes(n, m, k))
+int ppgat_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t n, int m, int k, float* out,
+                  float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* workspace,
+                  size_t workspace_bytes, void* stream) {
+  if (n < 0 || m < 1 || k < 1 || nv < 0 || nv > 16) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad sizes (nv <= 16)");
+  if (lda < m || ldb < k || (nv > 0 && ldv < nv)) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad leading dimension");
+  if ((lda % 4) || (ldb % 4) || (reinterpret_cast<uintptr_t>(A) % 16) || (reinterpret_cast<uintptr_t>(B) % 16))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: A/B rows must be 16-byte aligned");
+  if (!out || (n > 0 && (!A || !B)) || (nv > 0 && (!V || !vout)))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
+  if (!workspace || workspace_bytes < ppgat::gemm_tn_workspace_bytes(n, m, k, nv))
     return fail(PPGAT_ERR_INVALID, "gemm_tn: workspace too small");
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_GEMM_TN, st);
-  hipError_t e = ppgat::gemm_tn(A, B, n, m, k, out, colsum, workspace, st);
+  hipError_t e = ppgat::gemm_tn(A, lda, B, ldb, n, m, k, out, colsum, nv > 0 ? V : nullptr, ldv, nv, vout,
+                                workspace, st);
   if (e != hipSuccess) return hip_fail(e, "gemm_tn");
   return PPGAT_OK;
 }

@@ -32,8 +32,10 @@ hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, c
                           float* nstate, float* bias_part, int64_t blocks, hipStream_t st);
 hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
                           int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
-                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, float* ds_src,
-                          float* dz, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, int64_t ld_dh,
+                          float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
+                          const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
+hipError_t launch_dst_sum(const int32_t* rowptr, int64_t n, int heads, const float* dz, float* ds_dst, int64_t ld,
                           hipStream_t st);
 int64_t epi_blocks(int64_t n);
 hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
@@ -62,9 +64,9 @@ hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32
 hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
                    const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st);
-size_t gemm_tn_workspace_bytes(int64_t N, int M, int K);
-hipError_t gemm_tn(const float* A, const float* B, int64_t N, int M, int K, float* out, float* colsum, void* ws,
-                   hipStream_t st);
+size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv);
+hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
+                   float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st);
 
 // evaluation (ppgat_eval.hip)
 hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,

@@ -337,8 +337,8 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
                                                  const float4* __restrict__ nstate,
                                                  const float* __restrict__ grad_out, int mode, float slope,
                                                  float gscale, float p, float inv_keep, uint64_t seed,
-                                                 float* __restrict__ dh, float* __restrict__ ds_src,
-                                                 float* __restrict__ dz, float* __restrict__ partial) {
+                                                 float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
+                                                 int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
   using G = Geo<C>;
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -413,8 +413,8 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
       if (lane == 0) s[C] = ds;
       continue;
     }
-    if (sg == 0) st4(dh + (j * heads + hd) * C + sl * 4, acc);
-    if (lane == 0) ds_src[j * heads + hd] = ds;
+    if (sg == 0) st4(dh + j * ld_dh + hd * C + sl * 4, acc);
+    if (lane == 0) ds_src[j * ld_ds + hd] = ds;
   }
 }
 
@@ -422,7 +422,7 @@ template <int C>
 __global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ hub_row,
                                                    const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
                                                    const float* __restrict__ partial, float* __restrict__ dh,
-                                                   float* __restrict__ ds_src) {
+                                                   int64_t ld_dh, float* __restrict__ ds_src, int64_t ld_ds) {
   using G = Geo<C>;
   const int lane = threadIdx.x & 63;
   const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -439,8 +439,8 @@ __global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ h
       acc = add4(acc, ld4(s + sl * 4));
       ds += s[C];
     }
-    st4(dh + (j * heads + hd) * C + sl * 4, acc);
-    if (sl == 0) ds_src[j * heads + hd] = ds;
+    st4(dh + j * ld_dh + hd * C + sl * 4, acc);
+    if (sl == 0) ds_src[j * ld_ds + hd] = ds;
   }
 }
 
@@ -548,6 +548,30 @@ __global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ p
 }
 
 // ---------------------------------------------------------------------------
+// ds_dst[i, h] = sum_{k in CSR(i)} dz[k, h]: 16 lanes per (node, head), strided
+// accumulation then a fixed butterfly (deterministic).  Written with row stride ld.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_dst_sum(const int32_t* __restrict__ rowptr, int64_t pairs, int heads,
+                                                 const float* __restrict__ dz, float* __restrict__ ds_dst,
+                                                 int64_t ld) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pr = t >> 4;
+  const int l = (int)(t & 15);
+  float x = 0.f;
+  int64_t i = 0;
+  int hd = 0;
+  if (pr < pairs) {
+    i = pr / heads;
+    hd = (int)(pr % heads);
+    const int rs = rowptr[i], re = rowptr[i + 1];
+    for (int k = rs + l; k < re; k += 16) x += dz[(int64_t)k * heads + hd];
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  if (pr < pairs && l == 0) ds_dst[i * ld + hd] = x;
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers (called from ppgat_abi.cpp)
 // ---------------------------------------------------------------------------
 #define PPGAT_DISPATCH_C(C_, ...)                      \
@@ -605,20 +629,20 @@ hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, c
 
 hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
                           int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
-                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, float* ds_src,
-                          float* dz, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
-                          hipStream_t st) {
+                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, int64_t ld_dh,
+                          float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
+                          const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const Items its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   if (it.n_items > 0) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its,
                                            row, csc_eid, csc2csr, heads, h, ss,
                                            reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, p,
-                                           inv_keep, seed, dh, ds_src, dz, partial));
+                                           inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial));
   }
   if (n_hubs > 0) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,
-                                           hub_row, hub_ptr, n_hubs, heads, partial, dh, ds_src));
+                                           hub_row, hub_ptr, n_hubs, heads, partial, dh, ld_dh, ds_src, ld_ds));
   }
   return hipGetLastError();
 }
@@ -637,6 +661,14 @@ hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, co
                           int64_t blocks, hipStream_t st) {
   PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_epi<CC>, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, n, heads,
                                          h, as, ad, ds_src, dz, dh, partial));
+  return hipGetLastError();
+}
+
+hipError_t launch_dst_sum(const int32_t* rowptr, int64_t n, int heads, const float* dz, float* ds_dst, int64_t ld,
+                          hipStream_t st) {
+  const int64_t pairs = n * heads;
+  if (pairs == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dst_sum, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, rowptr, pairs, heads, dz, ds_dst, ld);
   return hipGetLastError();
 }
 

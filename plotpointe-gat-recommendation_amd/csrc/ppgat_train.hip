@@ -262,11 +262,16 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 constexpr int kTN = 128;  // output tile edge
 constexpr int kNB = 32;   // rows per LDS stage
 
-__global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, const float* __restrict__ B, int64_t N,
-                                                 int M, int K, int64_t rows_per_split, float* __restrict__ part,
-                                                 float* __restrict__ colsum_part) {
+constexpr int kMaxV = 16;  // extra row-weighted column sums V^T B (2 * heads <= 16)
+
+__global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+                                                 int64_t ldb, int64_t N, int M, int K, int64_t rows_per_split,
+                                                 float* __restrict__ part, float* __restrict__ colsum_part,
+                                                 const float* __restrict__ V, int64_t ldv, int nv,
+                                                 float* __restrict__ vpart) {
   __shared__ float sA[2][kNB][kTN];
   __shared__ float sB[2][kNB][kTN];
+  __shared__ float sV[2][kNB][kMaxV];
   const int tiles_k = (K + kTN - 1) / kTN;
   const int tile = blockIdx.x;
   const int split = blockIdx.y;
@@ -283,8 +288,14 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, co
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   float csum = 0.f;  // colsum of A for column m0 + tid (tid < 128), waves 0-1 only
-  // stage loader: 32 rows x 128 cols = 1024 float4 per operand; 256 threads x 4
-  auto load_stage = [&](int buf, int64_t n0) {
+  float vacc[kMaxV];  // (V^T B)[j][k0 + tid] for the m0 == 0 tiles
+#pragma unroll
+  for (int j = 0; j < kMaxV; ++j) vacc[j] = 0.f;
+  const bool do_v = V != nullptr && m0 == 0;
+  // register prefetch: stage s+1's global loads are in flight while stage s's MFMAs run
+  float4 ra[4], rb[4];
+  float rv[2];
+  auto load_regs = [&](int64_t n0) {
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
       const int idx = pass * 256 + tid;  // float4 index within the stage
@@ -292,28 +303,57 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, co
       const int64_t n = n0 + r;
       float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
       if (n < n_end) {
-        if (m0 + c4 + 3 < M) va = ld4(A + n * M + m0 + c4);
+        if (m0 + c4 + 3 < M) va = ld4(A + n * lda + m0 + c4);
         else {
           float t[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int e = 0; e < 4; ++e) if (m0 + c4 + e < M) t[e] = A[n * M + m0 + c4 + e];
+          for (int e = 0; e < 4; ++e) if (m0 + c4 + e < M) t[e] = A[n * lda + m0 + c4 + e];
           va = make_float4(t[0], t[1], t[2], t[3]);
         }
-        if (k0 + c4 + 3 < K) vb = ld4(B + n * K + k0 + c4);
+        if (k0 + c4 + 3 < K) vb = ld4(B + n * ldb + k0 + c4);
         else {
           float t[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int e = 0; e < 4; ++e) if (k0 + c4 + e < K) t[e] = B[n * K + k0 + c4 + e];
+          for (int e = 0; e < 4; ++e) if (k0 + c4 + e < K) t[e] = B[n * ldb + k0 + c4 + e];
           vb = make_float4(t[0], t[1], t[2], t[3]);
         }
       }
-      *reinterpret_cast<float4*>(&sA[buf][r][c4]) = va;
-      *reinterpret_cast<float4*>(&sB[buf][r][c4]) = vb;
+      ra[pass] = va;
+      rb[pass] = vb;
+    }
+    if (do_v) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int idx = q * 256 + tid;  // (row, j) of the kNB x kMaxV stage
+        const int r = idx / kMaxV, j = idx % kMaxV;
+        const int64_t n = n0 + r;
+        rv[q] = (j < nv && n < n_end) ? V[n * ldv + j] : 0.f;
+      }
+    }
+  };
+  auto store_lds = [&](int buf) {
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int idx = pass * 256 + tid;
+      const int r = idx >> 5, c4 = (idx & 31) * 4;
+      *reinterpret_cast<float4*>(&sA[buf][r][c4]) = ra[pass];
+      *reinterpret_cast<float4*>(&sB[buf][r][c4]) = rb[pass];
+    }
+    if (do_v) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int idx = q * 256 + tid;
+        sV[buf][idx / kMaxV][idx % kMaxV] = rv[q];
+      }
     }
   };
   int buf = 0;
-  if (n_beg < n_end) load_stage(0, n_beg);
+  if (n_beg < n_end) {
+    load_regs(n_beg);
+    store_lds(0);
+  }
   __syncthreads();
   for (int64_t n0 = n_beg; n0 < n_end; n0 += kNB) {
-    if (n0 + kNB < n_end) load_stage(buf ^ 1, n0 + kNB);
+    const bool has_next = n0 + kNB < n_end;
+    if (has_next) load_regs(n0 + kNB);
 #pragma unroll 4
     for (int kk = 0; kk < kNB; kk += 2) {
       const int r = kk + (lane >> 5);
@@ -329,6 +369,14 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, co
     if (colsum_part != nullptr && k0 == 0 && tid < kTN) {
       for (int r = 0; r < kNB; ++r) csum += sA[buf][r][tid];
     }
+    if (do_v && tid < kTN) {
+      for (int r = 0; r < kNB; ++r) {
+        const float b = sB[buf][r][tid];
+#pragma unroll
+        for (int j = 0; j < kMaxV; ++j) vacc[j] = fmaf(sV[buf][r][j], b, vacc[j]);
+      }
+    }
+    if (has_next) store_lds(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
@@ -346,6 +394,9 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, co
       }
   if (colsum_part != nullptr && k0 == 0 && tid < kTN && m0 + tid < M)
     colsum_part[(int64_t)split * M + m0 + tid] = csum;
+  if (do_v && tid < kTN && k0 + tid < K) {
+    for (int j = 0; j < nv; ++j) vpart[((int64_t)split * nv + j) * K + k0 + tid] = vacc[j];
+  }
 }
 
 // out[e] = sum_s part[s][e]: 8 interleaved partial sums (split s goes to sum s % 8, in
@@ -448,7 +499,7 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
 // ---- dW = A^T B ----
 static int64_t gemm_splits(int64_t N, int M, int K) {
   const int64_t tiles = (int64_t)((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
-  int64_t s = 256 / tiles;
+  int64_t s = 512 / tiles;
   if (s < 1) s = 1;
   const int64_t max_s = (N + 255) / 256;  // >= 256 rows per split
   if (s > max_s) s = max_s;
@@ -456,25 +507,32 @@ static int64_t gemm_splits(int64_t N, int M, int K) {
   return s;
 }
 
-size_t gemm_tn_workspace_bytes(int64_t N, int M, int K) {
+size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv) {
   const int64_t s = gemm_splits(N, M, K);
-  return align_up((size_t)s * M * K * 4) + align_up((size_t)s * M * 4);
+  return align_up((size_t)s * M * K * 4) + align_up((size_t)s * M * 4) + align_up((size_t)s * (nv > 0 ? nv : 1) * K * 4);
 }
 
-hipError_t gemm_tn(const float* A, const float* B, int64_t N, int M, int K, float* out, float* colsum, void* ws,
-                   hipStream_t st) {
+hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
+                   float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st) {
   const int64_t s = gemm_splits(N, M, K);
   const int64_t rows = ((N + s - 1) / s + kNB - 1) / kNB * kNB;
-  float* part = static_cast<float*>(ws);
-  float* cpart = colsum ? reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)s * M * K * 4)) : nullptr;
+  char* p = static_cast<char*>(ws);
+  float* part = reinterpret_cast<float*>(p);
+  float* cpart = colsum ? reinterpret_cast<float*>(p + align_up((size_t)s * M * K * 4)) : nullptr;
+  float* vpart = (V && nv > 0) ? reinterpret_cast<float*>(p + align_up((size_t)s * M * K * 4) +
+                                                          align_up((size_t)s * M * 4))
+                               : nullptr;
   const int tiles = ((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
-  hipLaunchKernelGGL(k_gemm_tn, dim3((unsigned)tiles, (unsigned)s), dim3(256), 0, st, A, B, N, M, K, rows, part,
-                     cpart);
+  hipLaunchKernelGGL(k_gemm_tn, dim3((unsigned)tiles, (unsigned)s), dim3(256), 0, st, A, lda, B, ldb, N, M, K, rows,
+                     part, cpart, vpart ? V : nullptr, ldv, vpart ? nv : 0, vpart);
   const int64_t elems = (int64_t)M * K;
   hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, st, part, s, elems, out);
   if (colsum)
     hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, cpart, s, (int64_t)M,
                        colsum);
+  if (vpart)
+    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)(((int64_t)nv * K + 255) / 256)), dim3(256), 0, st, vpart, s,
+                       (int64_t)nv * K, vout);
   return hipGetLastError();
 }
 

@@ -286,24 +286,134 @@ def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope
     return GATAggregate.apply(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
 
 
+def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, ld, heads, channels, mode, slope, p, seed):
+    """Pass B into D[:, :HC] (dh_msg) and D[:, HC:HC+H] (ds_src); the destination sum into
+    D[:, HC+H:HC+2H] (ds_dst).  D is [N, ld] (ld = HC + pad, pad >= 2H, ld % 4 == 0)."""
+    lib = _lib.load()
+    dev = h.device
+    N, E, HC = g.n_nodes, g.n_edges, heads * channels
+    sched = g.bwd_sched
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_fwd_workspace_bytes(sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
+               "workspace_bytes")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    dz = torch.empty(max(E, 1) * heads, dtype=torch.float32, device=dev)
+    cs = sched.cstruct()
+    st = _lib.stream_handle(dev)
+    base = D.data_ptr()
+    _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(g.row) if E else None,
+                                   _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, E, heads,
+                                   channels, h.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), grad_out.data_ptr(),
+                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), base, ld, base + 4 * HC, ld,
+                                   dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "bwd_edges")
+    _lib.check(lib.ppgat_bwd_dst_sum(g.rowptr.data_ptr(), N, heads, dz.data_ptr(), base + 4 * (HC + heads), ld, st),
+               "bwd_dst_sum")
+
+
+class GATLayer(torch.autograd.Function):
+    """One whole GAT layer x -> out with the projection inside:
+    forward  h = x W^T (BLAS), node scores, fused softmax-aggregate;
+    backward prologue, pass B and the destination sum write D = [dh_msg | ds_src | ds_dst]
+    side by side, then dx = D W_aug (BLAS) and D^T x (ppgat_gemm_tn with V) give dx, dW
+    and datt with no separate epilogue pass (include/ppgat.h ppgat_bwd_dst_sum)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, heads: int, channels: int, mode: int,
+                slope: float, dropout_p: float, seed: int):
+        x = x.contiguous()
+        h = torch.nn.functional.linear(x, weight)
+        a_s = att_src.detach().reshape(heads, channels).contiguous()
+        a_d = att_dst.detach().reshape(heads, channels).contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
+        need = any(ctx.needs_input_grad[:5])
+        out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed,
+                                     want_agg=need and heads > 1)
+        if need:
+            empty = torch.empty(0, device=x.device)
+            ctx.save_for_backward(x, weight, h, a_s, a_d, s_src, s_dst, out, m, inv_l,
+                                  agg if agg is not None else empty, b if b is not None else empty)
+        ctx.graph = graph
+        ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None)
+        ctx.att_shapes = (att_src.shape, att_dst.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        x, W, h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg, b = ctx.saved_tensors
+        heads, C, mode, slope, p, seed, has_bias, has_agg = ctx.meta
+        g = ctx.graph
+        lib = _lib.load()
+        dev = x.device
+        g_out = g_out.contiguous()
+        N, K = x.shape
+        HC = heads * C
+        ld = HC + ((2 * heads + 3) // 4) * 4
+        # prologue: packed per-node state (+ dbias)
+        want_db = has_bias and ctx.needs_input_grad[4]
+        nstate = torch.empty(N, heads, 4, dtype=torch.float32, device=dev)
+        dbias = torch.empty(C, dtype=torch.float32, device=dev) if want_db else None
+        rows = int(lib.ppgat_bwd_partial_rows(N))
+        part = torch.empty(max(rows, 1) * C, dtype=torch.float32, device=dev) if want_db else None
+        _lib.check(lib.ppgat_bwd_prologue(g_out.data_ptr(), out.data_ptr(), _lib.ptr(agg) if has_agg else None,
+                                          _lib.ptr(b) if has_bias else None, s_dst.data_ptr(), m.data_ptr(),
+                                          inv_l.data_ptr(), N, heads, C, mode, nstate.data_ptr(), _lib.ptr(dbias),
+                                          _lib.ptr(part), _lib.stream_handle(dev)), "bwd_prologue")
+        D = torch.empty(N, ld, dtype=torch.float32, device=dev)
+        _bwd_edges_dst(g, h, s_src, nstate, g_out, D, ld, heads, C, mode, slope, p, seed)
+        # W_aug = [W; A_src; A_dst],  A[hd] = sum_c att[hd, c] W[hd*C + c, :]
+        Wv = W.detach().view(heads, C, K)
+        A_s = torch.einsum("hc,hck->hk", a_s, Wv)
+        A_d = torch.einsum("hc,hck->hk", a_d, Wv)
+        Dv = D[:, :HC + 2 * heads]
+        dx = Dv @ torch.cat([W.detach(), A_s, A_d], 0) if ctx.needs_input_grad[0] else None
+        G, _, GV = gemm_tn(D[:, :HC], x, V=D[:, HC:HC + 2 * heads])
+        G_s, G_d = GV[:heads], GV[heads:2 * heads]
+        dW = (G.view(heads, C, K) + a_s[..., None] * G_s[:, None, :] + a_d[..., None] * G_d[:, None, :]).view(HC, K)
+        datt_src = torch.einsum("hck,hk->hc", Wv, G_s)
+        datt_dst = torch.einsum("hck,hk->hc", Wv, G_d)
+        return (dx, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None, None)
+
+
+def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p=0.0, seed=0):
+    """x [N, F] -> out [N, C]: lin + the fused GAT aggregation, with the fused backward."""
+    _require(x.is_cuda, "gat_layer: ppgat runs on ROCm devices only; there is no CPU path")
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise NotImplementedError("ppgat gat_layer: fp32 2-D input only")
+    return GATLayer.apply(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
+
+
 # ---------------------------------------------------------------------------
 # projection with the MFMA weight-gradient kernel, and the fused BPR/BCE loss
 # ---------------------------------------------------------------------------
-def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False):
-    """A [N,M], B [N,K] -> (A^T B [M,K], colsum(A) [M] or None), deterministic."""
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Optional[torch.Tensor] = None):
+    """A [N,M], B [N,K] (row strides may exceed the widths) -> (A^T B [M,K], colsum(A) [M]
+    or None, V^T B [nv,K] or None), deterministic."""
     lib = _lib.load()
-    _check_dev("A", A, torch.float32)
-    _check_dev("B", B, torch.float32, A.device)
-    _require(A.dim() == 2 and B.dim() == 2 and A.size(0) == B.size(0), "gemm_tn: A [N,M], B [N,K]")
+    for name, t in (("A", A), ("B", B)):
+        _require(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32,
+                 f"gemm_tn: {name} must be an fp32 ROCm tensor")
+        _require(t.dim() == 2 and t.stride(1) == 1, f"gemm_tn: {name} must be 2-D with unit column stride")
+    _require(A.size(0) == B.size(0), "gemm_tn: A [N,M], B [N,K]")
     N, M, K = A.size(0), A.size(1), B.size(1)
+    nv = 0 if V is None else V.size(1)
+    if V is not None:
+        _require(V.is_cuda and V.dtype == torch.float32 and V.dim() == 2 and V.stride(1) == 1 and V.size(0) == N,
+                 "gemm_tn: V must be fp32 [N, nv] with unit column stride")
     out = torch.empty(M, K, dtype=torch.float32, device=A.device)
     cs = torch.empty(M, dtype=torch.float32, device=A.device) if want_colsum else None
+    vout = torch.empty(max(nv, 1), K, dtype=torch.float32, device=A.device) if nv else None
     nbytes = ctypes.c_size_t(0)
-    _lib.check(lib.ppgat_gemm_tn_workspace_bytes(N, M, K, ctypes.byref(nbytes)), "gemm_tn_workspace_bytes")
+    _lib.check(lib.ppgat_gemm_tn_workspace_bytes(N, M, K, nv, ctypes.byref(nbytes)), "gemm_tn_workspace_bytes")
     ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=A.device)
-    _lib.check(lib.ppgat_gemm_tn(A.data_ptr(), B.data_ptr(), N, M, K, out.data_ptr(), _lib.ptr(cs), ws.data_ptr(),
-                                 nbytes.value, _lib.stream_handle(A.device)), "gemm_tn")
-    return out, cs
+    lda = A.stride(0) if N > 1 else max(M + (-M) % 4, 4)
+    ldb = B.stride(0) if N > 1 else max(K + (-K) % 4, 4)
+    ldv = (V.stride(0) if N > 1 else nv) if nv else 0
+    _lib.check(lib.ppgat_gemm_tn(A.data_ptr(), lda, B.data_ptr(), ldb, N, M, K, out.data_ptr(), _lib.ptr(cs),
+                                 _lib.ptr(V) if nv else None, ldv, nv, _lib.ptr(vout), ws.data_ptr(), nbytes.value,
+                                 _lib.stream_handle(A.device)), "gemm_tn")
+    return out, cs, vout
 
 
 class _Linear(torch.autograd.Function):
@@ -324,7 +434,7 @@ class _Linear(torch.autograd.Function):
         dx = g @ weight if ctx.needs_input_grad[0] else None
         dW = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dW, db = gemm_tn(g, x, want_colsum=ctx.has_bias)
+            dW, db, _ = gemm_tn(g, x, want_colsum=ctx.has_bias)
         return dx, dW, db if ctx.has_bias else None
 
 
@@ -502,8 +612,9 @@ class HipStages:
                                        _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None, E,
                                        heads, channels, h.data_ptr(), s_src.data_ptr(), nstate_full.data_ptr(),
                                        grad_out_full.data_ptr(), mode, float(slope), float(p),
-                                       int(seed) & (2**64 - 1), grad_h.data_ptr(), ds_src.data_ptr(), dz.data_ptr(),
-                                       ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "bwd_edges")
+                                       int(seed) & (2**64 - 1), grad_h.data_ptr(), heads * channels,
+                                       ds_src.data_ptr(), heads, dz.data_ptr(), ws.data_ptr(), nbytes.value,
+                                       _lib.stream_handle(dev)), "bwd_edges")
         return grad_h, ds_src
 
     def bwd_epilogue(self, v, h, att_src, att_dst, ds_src, dz, grad_h, heads, channels):

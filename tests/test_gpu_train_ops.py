@@ -21,11 +21,27 @@ def test_gemm_tn_vs_fp64(pkg, cuda, N, M, K):
     g = torch.Generator().manual_seed(N + M + K)
     A = torch.randn(N, M, generator=g, dtype=torch.float64)
     B = torch.randn(N, K, generator=g, dtype=torch.float64)
-    out, cs = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda), want_colsum=True)
+    V = torch.randn(N, 2, generator=g, dtype=torch.float64)
+    out, cs, vo = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda), want_colsum=True, V=V.float().to(cuda))
     assert rel(out, A.t() @ B) <= 1e-5
     assert rel(cs, A.sum(0)) <= 1e-5
-    out2, _ = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda))
+    assert rel(vo, V.t() @ B) <= 1e-5
+    out2, _, _ = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda))
     assert torch.equal(out, out2)
+
+
+def test_gemm_tn_strided_operands(pkg, cuda):
+    """A and V as column slices of one [N, ld] buffer (the fused backward's D = [dh | ds])."""
+    from importlib import import_module
+    ops = import_module("plotpointe-gat-recommendation_amd.hip_ops")
+    g = torch.Generator().manual_seed(9)
+    N, HC, H = 20_000, 128, 2
+    D = torch.randn(N, HC + 8, generator=g, dtype=torch.float64)
+    x = torch.randn(N, 96, generator=g, dtype=torch.float64)
+    Dd = D.float().to(cuda)
+    out, _, vo = ops.gemm_tn(Dd[:, :HC], x.float().to(cuda), V=Dd[:, HC:HC + 2 * H])
+    assert rel(out, D[:, :HC].t() @ x) <= 1e-5
+    assert rel(vo, D[:, HC:HC + 2 * H].t() @ x) <= 1e-5
 
 
 def test_linear_grads(pkg, cuda):
