@@ -162,15 +162,17 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
                     const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
                     float dropout_p, uint64_t seed, float* grad_h, int64_t ld_grad_h, float* ds_src,
                     int64_t ld_ds_src, float* dz, void* workspace, size_t workspace_bytes, void* stream);
-/* ds_dst[i*ld + h] = sum of dz over the CSR segment of destination i (no epilogue): with
+/* ds_dst[i*ld + h] = sum of dz over the CSR segment of destination i, walked with the
+ * forward (destination) schedule so hub rows are split; workspace >= n_hub_items*heads*4
+ * bytes (hub partials, added in piece order: deterministic).  With
  * grad_h and ds_src/ds_dst written side by side into one [N, ld] buffer
  * D = [dh_msg | ds_src | ds_dst], the projection gradients follow from two GEMMs with
  * W_aug = [W; A_src; A_dst] (A_src[h] = sum_c att_src[h,c] W[h*C+c, :]):
  *   dx = D W_aug,   D^T x = [dh_msg^T x ; ds_src^T x ; ds_dst^T x]  (ppgat_gemm_tn with V),
  *   dW = dh_msg^T x + att_src (x) (ds_src^T x) + att_dst (x) (ds_dst^T x),
  *   datt_src[h] = W_h (ds_src^T x)[h],  datt_dst[h] = W_h (ds_dst^T x)[h]. */
-int ppgat_bwd_dst_sum(const int32_t* rowptr, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
-                      int64_t ld_ds_dst, void* stream);
+int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
+                      int64_t ld_ds_dst, void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_bwd_epilogue(const int32_t* rowptr, int64_t n_nodes, int heads, int channels, const float* h,
                        const float* att_src, const float* att_dst, const float* ds_src, const float* dz,
                        float* grad_h, float* grad_att_src, float* grad_att_dst, float* part, void* stream);

@@ -282,13 +282,20 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
   return PPGAT_OK;
 }
 
-int ppgat_bwd_dst_sum(const int32_t* rowptr, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
-                      int64_t ld_ds_dst, void* stream) {
+int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
+                      int64_t ld_ds_dst, void* workspace, size_t workspace_bytes, void* stream) {
   if (n_nodes < 0 || heads < 1 || ld_ds_dst < heads) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: bad sizes");
-  if (n_nodes > 0 && (!rowptr || !ds_dst)) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: null pointer");
+  if (int rc = check_sched(fwd_sched, n_nodes, "bwd_dst_sum")) return rc;
+  if (n_nodes > 0 && !ds_dst) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: null pointer");
+  const size_t need = (size_t)fwd_sched->n_hub_items * heads * sizeof(float);
+  if (need > 0 && (!workspace || workspace_bytes < need))
+    return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: workspace too small");
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_BWD_EPI, st);
-  hipError_t e = ppgat::launch_dst_sum(rowptr, n_nodes, heads, dz, ds_dst, ld_ds_dst, st);
+  const ppgat::ItemsArg it{fwd_sched->item_row, fwd_sched->item_beg, fwd_sched->item_end, fwd_sched->n_items,
+                           fwd_sched->n_hub_items};
+  hipError_t e = ppgat::launch_dst_sum(it, heads, dz, ds_dst, ld_ds_dst, static_cast<float*>(workspace),
+                                       fwd_sched->hub_row, fwd_sched->hub_ptr, fwd_sched->n_hubs, st);
   if (e != hipSuccess) return hip_fail(e, "bwd_dst_sum");
   return PPGAT_OK;
 }

@@ -35,8 +35,8 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
                           int mode, float slope, float gscale, float p, uint64_t seed, float* dh, int64_t ld_dh,
                           float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
                           const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
-hipError_t launch_dst_sum(const int32_t* rowptr, int64_t n, int heads, const float* dz, float* ds_dst, int64_t ld,
-                          hipStream_t st);
+hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, float* ds_dst, int64_t ld, float* partial,
+                          const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
 int64_t epi_blocks(int64_t n);
 hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
                           const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,

@@ -548,27 +548,54 @@ __global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ p
 }
 
 // ---------------------------------------------------------------------------
-// ds_dst[i, h] = sum_{k in CSR(i)} dz[k, h]: 16 lanes per (node, head), strided
-// accumulation then a fixed butterfly (deterministic).  Written with row stride ld.
+// ds_dst[i, h] = sum_{k in CSR(i)} dz[k, h] over the forward (destination) schedule:
+// 16 lanes per (item, head), items hold <= max_edges edges, so no group waits on a hub;
+// hub pieces leave a partial that k_dst_merge adds up in piece order (deterministic).
+// Written with row stride ld.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dst_sum(const int32_t* __restrict__ rowptr, int64_t pairs, int heads,
-                                                 const float* __restrict__ dz, float* __restrict__ ds_dst,
-                                                 int64_t ld) {
+__global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const float* __restrict__ dz,
+                                                 float* __restrict__ ds_dst, int64_t ld,
+                                                 float* __restrict__ partial) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pr = t >> 4;
   const int l = (int)(t & 15);
-  float x = 0.f;
-  int64_t i = 0;
+  const bool live = pr < it.n_items * heads;
+  float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f;
+  int64_t w = 0;
   int hd = 0;
-  if (pr < pairs) {
-    i = pr / heads;
+  if (live) {
+    w = pr / heads;
     hd = (int)(pr % heads);
-    const int rs = rowptr[i], re = rowptr[i + 1];
-    for (int k = rs + l; k < re; k += 16) x += dz[(int64_t)k * heads + hd];
+    const int rs = it.beg[w], re = it.end[w];
+    int k = rs + l;
+    for (; k + 48 < re; k += 64) {
+      x0 += dz[(int64_t)k * heads + hd];
+      x1 += dz[(int64_t)(k + 16) * heads + hd];
+      x2 += dz[(int64_t)(k + 32) * heads + hd];
+      x3 += dz[(int64_t)(k + 48) * heads + hd];
+    }
+    for (; k < re; k += 16) x0 += dz[(int64_t)k * heads + hd];
   }
+  float x = (x0 + x1) + (x2 + x3);
 #pragma unroll
   for (int off = 8; off > 0; off >>= 1) x += __shfl_xor(x, off);
-  if (pr < pairs && l == 0) ds_dst[i * ld + hd] = x;
+  if (live && l == 0) {
+    if (w < it.n_hub_items) partial[w * heads + hd] = x;
+    else ds_dst[(int64_t)it.row[w] * ld + hd] = x;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dst_merge(const int32_t* __restrict__ hub_row,
+                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
+                                                   const float* __restrict__ partial, float* __restrict__ ds_dst,
+                                                   int64_t ld) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_hubs * heads) return;
+  const int64_t hb = t / heads;
+  const int hd = (int)(t % heads);
+  float x = 0.f;
+  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) x += partial[(int64_t)q * heads + hd];
+  ds_dst[(int64_t)hub_row[hb] * ld + hd] = x;
 }
 
 // ---------------------------------------------------------------------------
@@ -664,11 +691,16 @@ hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, co
   return hipGetLastError();
 }
 
-hipError_t launch_dst_sum(const int32_t* rowptr, int64_t n, int heads, const float* dz, float* ds_dst, int64_t ld,
-                          hipStream_t st) {
-  const int64_t pairs = n * heads;
+hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, float* ds_dst, int64_t ld, float* partial,
+                          const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+  const int64_t pairs = it.n_items * heads;
   if (pairs == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dst_sum, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, rowptr, pairs, heads, dz, ds_dst, ld);
+  const Items items{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  hipLaunchKernelGGL(k_dst_sum, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, ds_dst, ld,
+                     partial);
+  if (n_hubs > 0)
+    hipLaunchKernelGGL(k_dst_merge, dim3(blocks_for(n_hubs * heads)), dim3(256), 0, st, hub_row, hub_ptr, n_hubs,
+                       heads, partial, ds_dst, ld);
   return hipGetLastError();
 }
 

@@ -306,8 +306,10 @@ def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, ld, heads, channe
                                    channels, h.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), grad_out.data_ptr(),
                                    mode, float(slope), float(p), int(seed) & (2**64 - 1), base, ld, base + 4 * HC, ld,
                                    dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "bwd_edges")
-    _lib.check(lib.ppgat_bwd_dst_sum(g.rowptr.data_ptr(), N, heads, dz.data_ptr(), base + 4 * (HC + heads), ld, st),
-               "bwd_dst_sum")
+    fs = g.fwd_sched.cstruct()
+    dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), N, heads, dz.data_ptr(), base + 4 * (HC + heads), ld,
+                                     dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
 class GATLayer(torch.autograd.Function):
