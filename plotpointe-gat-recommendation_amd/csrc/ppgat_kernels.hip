@@ -27,6 +27,7 @@
 #include <math.h>
 
 #include "ppgat_internal.h"
+#include "ppgat_lanes.h"
 
 namespace ppgat {
 
@@ -46,17 +47,6 @@ __device__ __forceinline__ float dot4(float4 a, float4 b) {
 __device__ __forceinline__ float4 shfl_xor4(float4 v, int m) {
   return make_float4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-  return v;
-}
-
 // attention logit e(z) and de/dz, per mode (torch leaky_relu / clamp backward rules:
 // slope where z <= 0; clamp passes gradient where min <= e <= max).
 __device__ __forceinline__ float logit(float z, float slope, int mode) {
@@ -107,11 +97,8 @@ __global__ void __launch_bounds__(256) k_scores(const float* __restrict__ h, con
   const float4 v = valid ? ld4(h + pr * C + sl * 4) : f4(0.f);
   float x = dot4(v, ld4(att_src + hd * C + sl * 4));
   float y = dot4(v, ld4(att_dst + hd * C + sl * 4));
-#pragma unroll
-  for (int off = G::LPR / 2; off > 0; off >>= 1) {
-    x += __shfl_xor(x, off);
-    y += __shfl_xor(y, off);
-  }
+  x = group_reduce<Op::Sum, 1, G::LPR / 2>(x);
+  y = group_reduce<Op::Sum, 1, G::LPR / 2>(y);
   if (valid && sl == 0) {
     s_src[pr] = x;
     s_dst[pr] = y;
@@ -150,8 +137,9 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
                                              float* __restrict__ invl_out, float* __restrict__ agg_out,
                                              float* __restrict__ partial) {
   using G = Geo<C>;
-  const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  __shared__ int2 rec[4][64];  // per wave: chunk edges {src row, weight}
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= it.n_items) return;  // wave-uniform
   const int sg = lane / G::LPR, sl = lane % G::LPR;
   const int64_t i = it.row[w];
@@ -183,6 +171,8 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
       }
       float pw = pe;
       if (p > 0.f && valid) pw *= drop_scale(seed, (uint32_t)eid[k], (uint32_t)hd, p, inv_keep);
+      rec[wv][lane] = make_int2(j, __float_as_int(pw));
+      wave_sync();
       const int n = min(64, re - base);
       for (int q0 = 0; q0 < n; q0 += G::EPW * G::U) {
         float4 v[G::U];
@@ -190,16 +180,16 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
 #pragma unroll
         for (int u = 0; u < G::U; ++u) {
           const int q = q0 + u * G::EPW + sg;
-          const int jq = __shfl(j, q);
-          pq[u] = __shfl(pw, q);
-          v[u] = q < n ? ld4(h + ((int64_t)jq * heads + hd) * C + sl * 4) : f4(0.f);
+          const int2 r = rec[wv][q];
+          pq[u] = __int_as_float(r.y);
+          v[u] = q < n ? ld4(h + ((int64_t)r.x * heads + hd) * C + sl * 4) : f4(0.f);
         }
 #pragma unroll
         for (int u = 0; u < G::U; ++u) acc = fma4(pq[u], v[u], acc);
       }
+      wave_sync();
     }
-#pragma unroll
-    for (int off = G::LPR; off < 64; off <<= 1) acc = add4(acc, shfl_xor4(acc, off));
+    acc = across_subgroups<G::LPR>(acc);
     if (hub) {
       float* slot = partial + (w * heads + hd) * (C + 4);
       if (sg == 0) st4(slot + sl * 4, acc);
@@ -307,8 +297,7 @@ __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_
       }
       x = dot4(g, a);
     }
-#pragma unroll
-    for (int off = G::LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    x = group_reduce<Op::Sum, 1, G::LPR / 2>(x);
     if (valid && sl == 0) nstate[pr] = make_float4(s_dst[pr], m_in[pr], invl_in[pr], x * gscale);
   }
   if (bias_part == nullptr) return;
@@ -340,10 +329,17 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
                                                  float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
                                                  int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
   using G = Geo<C>;
-  const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  constexpr int GRP = G::LPR / G::U;  // lanes sharing one reduced edge value
+  // per wave, per chunk edge: {dst row, beta * gscale} and {c1, c0, CSR slot}, where
+  // dz = c1 <g_i, h_j> - c0  (c1 = alpha e' d gscale, c0 = alpha e' D_i)
+  __shared__ int2 recA[4][64];
+  __shared__ float4 recB[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= it.n_items) return;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
+  const int myu = sl / GRP;
+  const bool writer = (sl % GRP) == 0;
   const int64_t j = it.row[w];
   const int cs = it.beg[w], ce = it.end[w];
   const bool hub = w < it.n_hub_items;
@@ -356,56 +352,51 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
       const int k = base + lane;
       const bool valid = k < ce;
       const int i = valid ? row[k] : 0;
-      float alpha = 0.f, f = 0.f, Dv = 0.f, dm = 1.f;
+      float bg = 0.f, c1 = 0.f, c0 = 0.f;
       int slot = 0;
       if (valid) {
         const float4 st = nstate[(int64_t)i * heads + hd];  // {s_dst, m, inv_l, D}
         const float z = ss + st.x;
         const float e = logit(z, slope, mode);
-        f = dlogit(z, slope, mode);
-        alpha = expf(e - st.y) * st.z;
-        Dv = st.w;
+        const float af = expf(e - st.y) * st.z;
+        const float dm = p > 0.f ? drop_scale(seed, (uint32_t)csc_eid[k], (uint32_t)hd, p, inv_keep) : 1.f;
         slot = csc2csr[k];
-        if (p > 0.f) dm = drop_scale(seed, (uint32_t)csc_eid[k], (uint32_t)hd, p, inv_keep);
+        bg = af * dm * gscale;
+        const float a1 = af * dlogit(z, slope, mode);
+        c1 = a1 * dm * gscale;
+        c0 = a1 * st.w;
       }
-      const float bg = alpha * dm * gscale;  // beta * gscale
-      const float dg = dm * gscale;
+      recA[wv][lane] = make_int2(i, __float_as_int(bg));
+      recB[wv][lane] = make_float4(c1, c0, __int_as_float(slot), 0.f);
+      wave_sync();
       const int n = min(64, ce - base);
       for (int q0 = 0; q0 < n; q0 += G::EPW * G::U) {
         float4 g[G::U];
-        float part[G::U];
+        float bq[G::U], part[G::U];
 #pragma unroll
         for (int u = 0; u < G::U; ++u) {
           const int q = q0 + u * G::EPW + sg;
-          const int iq = __shfl(i, q);
-          g[u] = q < n ? ld4(grad_out + (int64_t)iq * C + sl * 4) : f4(0.f);
+          const int2 r = recA[wv][q];
+          bq[u] = __int_as_float(r.y);
+          g[u] = q < n ? ld4(grad_out + (int64_t)r.x * C + sl * 4) : f4(0.f);
         }
 #pragma unroll
         for (int u = 0; u < G::U; ++u) {
-          const int q = q0 + u * G::EPW + sg;
-          acc = fma4(__shfl(bg, q), g[u], acc);
+          acc = fma4(bq[u], g[u], acc);
           part[u] = dot4(g[u], hv);
         }
-#pragma unroll
-        for (int off = G::LPR / 2; off > 0; off >>= 1) {
-#pragma unroll
-          for (int u = 0; u < G::U; ++u) part[u] += __shfl_xor(part[u], off);
-        }
-#pragma unroll
-        for (int u = 0; u < G::U; ++u) {
-          const int q = q0 + u * G::EPW + sg;
-          const float aq = __shfl(alpha, q), Dq = __shfl(Dv, q), fq = __shfl(f, q), dq = __shfl(dg, q);
-          const int sq = __shfl(slot, q);
-          const float dzv = aq * fmaf(dq, part[u], -Dq) * fq;
-          if (sl == 0 && q < n) {
-            ds += dzv;
-            dz[(int64_t)sq * heads + hd] = dzv;
-          }
+        const float dot = transpose_reduce<G::LPR, G::U>(part, sl);
+        const int q = q0 + myu * G::EPW + sg;
+        if (writer && q < n) {
+          const float4 rb = recB[wv][q];
+          const float dzv = fmaf(rb.x, dot, -rb.y);
+          ds += dzv;
+          dz[(int64_t)__float_as_int(rb.z) * heads + hd] = dzv;
         }
       }
+      wave_sync();
     }
-#pragma unroll
-    for (int off = G::LPR; off < 64; off <<= 1) acc = add4(acc, shfl_xor4(acc, off));
+    acc = across_subgroups<G::LPR>(acc);
     ds = wave_sum(ds);
     if (hub) {
       float* s = partial + (w * heads + hd) * (C + 4);
