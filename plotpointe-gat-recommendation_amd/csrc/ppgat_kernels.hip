@@ -211,7 +211,10 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
   if (sg == 0) st4(out + i * C + sl * 4, osum);
 }
 
-// Merge the pieces of each hub row, in piece order.  One wave per hub row.
+// Merge the pieces of each hub row.  One wave per hub row: the piece maxima and
+// rescaled sums are lane-parallel (wave reductions), the C-wide partial rows are taken
+// by the subgroups in turn (piece q -> subgroup q mod EPW, two loads in flight each) and
+// combined across subgroups -- a fixed order, so the merge is deterministic.
 template <int C>
 __global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ hub_row,
                                                    const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
@@ -224,37 +227,52 @@ __global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ h
   const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (hb >= n_hubs) return;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
-  if (sg != 0) return;  // one subgroup does the (small) merge
   const int64_t i = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
   float4 osum = f4(0.f);
   for (int hd = 0; hd < heads; ++hd) {
-    float M = -INFINITY;
+    float M = 0.f;
     if (mode == kModePyg) {
-      for (int q = p0; q < p1; ++q) M = fmaxf(M, partial[((int64_t)q * heads + hd) * (C + 4) + C]);
-    } else {
-      M = 0.f;
+      M = -INFINITY;
+      for (int q = p0 + lane; q - lane < p1; q += 64)
+        M = fmaxf(M, q < p1 ? partial[((int64_t)q * heads + hd) * (C + 4) + C] : -INFINITY);
+      M = wave_max(M);
     }
     float l = 0.f;
-    float4 acc = f4(0.f);
-    for (int q = p0; q < p1; ++q) {
-      const float* slot = partial + ((int64_t)q * heads + hd) * (C + 4);
-      const float sc = expf(slot[C] - M);
-      l = fmaf(slot[C + 1], sc, l);
-      acc = fma4(sc, ld4(slot + sl * 4), acc);
+    for (int q = p0 + lane; q - lane < p1; q += 64) {
+      float t = 0.f;
+      if (q < p1) {
+        const float* slot = partial + ((int64_t)q * heads + hd) * (C + 4);
+        t = slot[C + 1] * expf(slot[C] - M);
+      }
+      l += wave_sum(t);
     }
+    float4 acc = f4(0.f), acc2 = f4(0.f);
+    int q = p0 + sg;
+    for (; q + G::EPW < p1; q += 2 * G::EPW) {
+      const float* s0 = partial + ((int64_t)q * heads + hd) * (C + 4);
+      const float* s1 = partial + ((int64_t)(q + G::EPW) * heads + hd) * (C + 4);
+      const float4 v0 = ld4(s0 + sl * 4), v1 = ld4(s1 + sl * 4);
+      acc = fma4(expf(s0[C] - M), v0, acc);
+      acc2 = fma4(expf(s1[C] - M), v1, acc2);
+    }
+    if (q < p1) {
+      const float* s0 = partial + ((int64_t)q * heads + hd) * (C + 4);
+      acc = fma4(expf(s0[C] - M), ld4(s0 + sl * 4), acc);
+    }
+    acc = across_subgroups<G::LPR>(add4(acc, acc2));
     const float invl = 1.f / (l + eps);
     const float4 a = mul4(acc, invl);
-    if (agg_out != nullptr) st4(agg_out + (i * heads + hd) * C + sl * 4, a);
+    if (agg_out != nullptr && sg == 0) st4(agg_out + (i * heads + hd) * C + sl * 4, a);
     osum = add4(osum, a);
-    if (sl == 0) {
+    if (lane == 0) {
       m_out[i * heads + hd] = M;
       invl_out[i * heads + hd] = invl;
     }
   }
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
-  st4(out + i * C + sl * 4, osum);
+  if (sg == 0) st4(out + i * C + sl * 4, osum);
 }
 
 // ---------------------------------------------------------------------------
@@ -274,31 +292,35 @@ __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_
                                                  float* __restrict__ bias_part) {
   using G = Geo<C>;
   constexpr int SPB = 256 / G::LPR;
+  constexpr int UP = 4;  // pairs per subgroup per iteration (8 row loads in flight)
   __shared__ float4 red[SPB][G::LPR];
   const int sg = threadIdx.x / G::LPR, sl = threadIdx.x % G::LPR;
   float4 bsum = f4(0.f);
-  for (int64_t pr0 = (int64_t)blockIdx.x * SPB; pr0 < pairs; pr0 += (int64_t)gridDim.x * SPB) {
-    const int64_t pr = pr0 + sg;
-    const bool valid = pr < pairs;
-    const int64_t n = valid ? pr / heads : 0;
-    float x = 0.f;
-    if (valid) {
-      const float4 g = ld4(grad_out + n * C + sl * 4);
-      if (pr % heads == 0) bsum = add4(bsum, g);
-      float4 a;
-      if (agg != nullptr) {
-        a = ld4(agg + pr * C + sl * 4);
-      } else {
-        a = ld4(out + n * C + sl * 4);
-        if (bias != nullptr) {
-          const float4 b = ld4(bias + sl * 4);
-          a = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
-        }
+  for (int64_t pr0 = (int64_t)blockIdx.x * SPB * UP; pr0 < pairs; pr0 += (int64_t)gridDim.x * SPB * UP) {
+    float4 g[UP], a[UP];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int64_t pr = pr0 + u * SPB + sg;
+      g[u] = a[u] = f4(0.f);
+      if (pr < pairs) {
+        const int64_t n = pr / heads;
+        g[u] = ld4(grad_out + n * C + sl * 4);
+        a[u] = agg != nullptr ? ld4(agg + pr * C + sl * 4) : ld4(out + n * C + sl * 4);
       }
-      x = dot4(g, a);
     }
-    x = group_reduce<Op::Sum, 1, G::LPR / 2>(x);
-    if (valid && sl == 0) nstate[pr] = make_float4(s_dst[pr], m_in[pr], invl_in[pr], x * gscale);
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const int64_t pr = pr0 + u * SPB + sg;
+      const bool valid = pr < pairs;
+      if (valid && pr % heads == 0) bsum = add4(bsum, g[u]);
+      float4 av = a[u];
+      if (agg == nullptr && bias != nullptr) {
+        const float4 b = ld4(bias + sl * 4);
+        av = make_float4(av.x - b.x, av.y - b.y, av.z - b.z, av.w - b.w);
+      }
+      float x = group_reduce<Op::Sum, 1, G::LPR / 2>(dot4(g[u], av));
+      if (valid && sl == 0) nstate[pr] = make_float4(s_dst[pr], m_in[pr], invl_in[pr], x * gscale);
+    }
   }
   if (bias_part == nullptr) return;
   red[sg][sl] = bsum;
@@ -419,19 +441,22 @@ __global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ h
   const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (hb >= n_hubs) return;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
-  if (sg != 0) return;
   const int64_t j = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
   for (int hd = 0; hd < heads; ++hd) {
-    float4 acc = f4(0.f);
     float ds = 0.f;
-    for (int q = p0; q < p1; ++q) {
-      const float* s = partial + ((int64_t)q * heads + hd) * (C + 4);
-      acc = add4(acc, ld4(s + sl * 4));
-      ds += s[C];
+    for (int q = p0 + lane; q - lane < p1; q += 64)
+      ds += wave_sum(q < p1 ? partial[((int64_t)q * heads + hd) * (C + 4) + C] : 0.f);
+    float4 acc = f4(0.f), acc2 = f4(0.f);
+    int q = p0 + sg;
+    for (; q + G::EPW < p1; q += 2 * G::EPW) {
+      acc = add4(acc, ld4(partial + ((int64_t)q * heads + hd) * (C + 4) + sl * 4));
+      acc2 = add4(acc2, ld4(partial + ((int64_t)(q + G::EPW) * heads + hd) * (C + 4) + sl * 4));
     }
-    st4(dh + j * ld_dh + hd * C + sl * 4, acc);
-    if (sl == 0) ds_src[j * ld_ds + hd] = ds;
+    if (q < p1) acc = add4(acc, ld4(partial + ((int64_t)q * heads + hd) * (C + 4) + sl * 4));
+    acc = across_subgroups<G::LPR>(add4(acc, acc2));
+    if (sg == 0) st4(dh + j * ld_dh + hd * C + sl * 4, acc);
+    if (lane == 0) ds_src[j * ld_ds + hd] = ds;
   }
 }
 

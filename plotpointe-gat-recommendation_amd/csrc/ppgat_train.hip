@@ -11,7 +11,7 @@
 //    accumulating a 128x128 tile with v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains),
 //    followed by an ordered reduction of the split partials.
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 #include <math.h>
 
@@ -60,34 +60,34 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
                                                  float2* __restrict__ coef, float* __restrict__ block_loss,
                                                  int32_t* __restrict__ bad, const int32_t* __restrict__ row_map) {
   constexpr int LPR = C / 4;
-  constexpr int SPB = 256 / LPR;  // subgroups (triples) per block
+  constexpr int SPB = 256 / LPR;  // subgroups (triples in flight) per block
   __shared__ float sl_loss[SPB];
   const int tid = threadIdx.x;
   const int sg = tid / LPR, sl = tid % LPR;
-  const int64_t t = (int64_t)blockIdx.x * SPB + sg;
-  const bool valid = t < S;
-  float pos = 0.f, neg = 0.f;
-  if (valid) {
-    const int64_t u0 = u[t], i0 = ii[t], j0 = jj[t];
-    if (bad != nullptr && sl == 0 &&
-        (u0 < 0 || u0 >= n_users || i0 < 0 || i0 >= n_items || j0 < 0 || j0 >= n_items))
-      atomicAdd(bad, 1);  // integer count; indices are clamped below, the caller raises
-    const int64_t ur = zrow(row_map, clamp_idx(u0, n_users));
-    const int64_t ir = zrow(row_map, n_users + clamp_idx(i0, n_items));
-    const int64_t jr = zrow(row_map, n_users + clamp_idx(j0, n_items));
-    const float4 a = ld4(Z + ur * C + sl * 4);
-    pos = dot4(a, ld4(Z + ir * C + sl * 4));
-    neg = dot4(a, ld4(Z + jr * C + sl * 4));
-  }
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) {
-    pos += __shfl_xor(pos, off);
-    neg += __shfl_xor(neg, off);
-  }
-  if (sl == 0) {
-    float l = 0.f;
-    float2 cf = make_float2(0.f, 0.f);
+  float lsum = 0.f;  // this subgroup's triples, in order (fixed grid => fixed partition)
+  for (int64_t t = (int64_t)blockIdx.x * SPB + sg; t - sg < S; t += (int64_t)gridDim.x * SPB) {
+    const bool valid = t < S;
+    float pos = 0.f, neg = 0.f;
     if (valid) {
+      const int64_t u0 = u[t], i0 = ii[t], j0 = jj[t];
+      if (bad != nullptr && sl == 0 &&
+          (u0 < 0 || u0 >= n_users || i0 < 0 || i0 >= n_items || j0 < 0 || j0 >= n_items))
+        atomicAdd(bad, 1);  // integer count; indices are clamped below, the caller raises
+      const int64_t ur = zrow(row_map, clamp_idx(u0, n_users));
+      const int64_t ir = zrow(row_map, n_users + clamp_idx(i0, n_items));
+      const int64_t jr = zrow(row_map, n_users + clamp_idx(j0, n_items));
+      const float4 a = ld4(Z + ur * C + sl * 4);
+      pos = dot4(a, ld4(Z + ir * C + sl * 4));
+      neg = dot4(a, ld4(Z + jr * C + sl * 4));
+    }
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) {
+      pos += __shfl_xor(pos, off);
+      neg += __shfl_xor(neg, off);
+    }
+    if (sl == 0 && valid) {
+      float l;
+      float2 cf;
       if (kind == 0) {
         const float x = pos - neg;
         const float s = 1.f / (1.f + expf(-x));
@@ -100,9 +100,10 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
         cf = make_float2((sp - 1.f) / (2.f * S), sn / (2.f * S));
       }
       coef[t] = cf;
+      lsum += l;
     }
-    sl_loss[sg] = l;
   }
+  if (sl == 0) sl_loss[sg] = lsum;
   __syncthreads();
   if (tid == 0) {
     float s = 0.f;
@@ -112,18 +113,156 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
 }
 
 // ordered sum of the block losses -> loss (mean)
-__global__ void __launch_bounds__(256) k_bpr_loss(const float* __restrict__ block_loss, int64_t nb, float denom,
-                                                  float* __restrict__ loss) {
-  __shared__ float red[256];
+__global__ void __launch_bounds__(1024) k_bpr_loss(const float* __restrict__ block_loss, int64_t nb, float denom,
+                                                   float* __restrict__ loss) {
+  __shared__ float red[1024];
   float s = 0.f;
-  for (int64_t b = threadIdx.x; b < nb; b += 256) s += block_loss[b];
+  for (int64_t b = threadIdx.x; b < nb; b += 1024) s += block_loss[b];
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = 512; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
   if (threadIdx.x == 0) loss[0] = red[0] / denom;
+}
+
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort of (key, value) int32 pairs, keys < 2^bits, for the loss backward
+// (4S contributions by destination row).  ceil(bits / 10) passes of db <= 10 bits; per pass
+//   k_rs_hist    tile digit counts (LDS int atomics: exact), digit-major [nd][tiles]
+//   exclusive scan of the counts (rocPRIM) -> global digit/tile offsets
+//   k_rs_scatter stable rank inside the tile: tile items are taken round-major (round r,
+//                wave w, lane l), a lane's same-digit peers come from db ballots, the
+//                per-(wave, digit) counts are scanned over waves in LDS, and the tile's
+//                running digit totals carry from round to round.
+// A handful of launches instead of rocPRIM's ~20-launch merge sort at this size.
+// ---------------------------------------------------------------------------
+constexpr int kRsThreads = 1024;
+constexpr int kRsWaves = kRsThreads / 64;
+constexpr int kRsRounds = 4;
+constexpr int kRsTile = kRsThreads * kRsRounds;
+
+__global__ void __launch_bounds__(kRsThreads) k_rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift, int db,
+                                                        int32_t* __restrict__ ghist, int64_t tiles) {
+  extern __shared__ int32_t h[];
+  const int nd = 1 << db;
+  for (int d = threadIdx.x; d < nd; d += kRsThreads) h[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRsTile;
+#pragma unroll
+  for (int r = 0; r < kRsRounds; ++r) {
+    const int64_t p = base + r * kRsThreads + threadIdx.x;
+    if (p < n) atomicAdd(&h[(keys[p] >> shift) & (nd - 1)], 1);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nd; d += kRsThreads) ghist[(int64_t)d * tiles + blockIdx.x] = h[d];
+}
+
+__global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const int32_t* __restrict__ kin,
+                                                           const int32_t* __restrict__ vin, int64_t n, int shift,
+                                                           int db, const int32_t* __restrict__ goff, int64_t tiles,
+                                                           int32_t* __restrict__ kout, int32_t* __restrict__ vout) {
+  extern __shared__ int32_t sm[];
+  const int nd = 1 << db;
+  int32_t* wc = sm;                   // [kRsWaves][nd]
+  int32_t* tot = sm + kRsWaves * nd;  // [nd] running position of each digit
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = threadIdx.x; d < nd; d += kRsThreads) tot[d] = goff[(int64_t)d * tiles + blockIdx.x];
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int64_t base = (int64_t)blockIdx.x * kRsTile;
+  for (int r = 0; r < kRsRounds; ++r) {
+    if (base + (int64_t)r * kRsThreads >= n) break;  // block-uniform
+    for (int q = threadIdx.x; q < kRsWaves * nd; q += kRsThreads) wc[q] = 0;
+    __syncthreads();
+    const int64_t p = base + (int64_t)r * kRsThreads + threadIdx.x;
+    const bool valid = p < n;
+    const int32_t k = valid ? kin[p] : 0;
+    const int32_t v = valid ? vin[p] : 0;
+    const int d = (k >> shift) & (nd - 1);
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < db; ++b) {
+      const bool bit = (d >> b) & 1;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const int rank = __popcll(peers & below);
+    if (valid && rank == 0) wc[w * nd + d] = __popcll(peers);
+    __syncthreads();
+    for (int dd = threadIdx.x; dd < nd; dd += kRsThreads) {
+      int32_t run = tot[dd];
+#pragma unroll
+      for (int ww = 0; ww < kRsWaves; ++ww) {
+        const int32_t t = wc[ww * nd + dd];
+        wc[ww * nd + dd] = run;
+        run += t;
+      }
+      tot[dd] = run;
+    }
+    __syncthreads();
+    if (valid) {
+      const int64_t pos = wc[w * nd + d] + rank;
+      kout[pos] = k;
+      vout[pos] = v;
+    }
+    __syncthreads();
+  }
+}
+
+struct RsPlan {
+  int passes, db;
+  int64_t tiles, cells;  // cells = nd * tiles
+  size_t scan_bytes;
+};
+
+RsPlan rs_plan(int64_t n, unsigned bits) {
+  RsPlan pl{};
+  pl.passes = (int)((bits + 9) / 10);
+  if (pl.passes < 1) pl.passes = 1;
+  pl.db = (int)((bits + pl.passes - 1) / pl.passes);
+  pl.tiles = (n + kRsTile - 1) / kRsTile;
+  if (pl.tiles < 1) pl.tiles = 1;
+  pl.cells = ((int64_t)1 << pl.db) * pl.tiles;
+  size_t b = 0;
+  (void)rocprim::exclusive_scan(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)pl.cells,
+                                rocprim::plus<int32_t>());
+  pl.scan_bytes = b;
+  return pl;
+}
+
+size_t rs_workspace_bytes(int64_t n, unsigned bits) {
+  const RsPlan pl = rs_plan(n, bits);
+  return 2 * align_up((size_t)pl.cells * 4) + align_up(pl.scan_bytes);
+}
+
+// sorts (k0, v0) using (k1, v1) as the ping-pong pair; *result_in_1 says where it ended
+hipError_t rs_sort(int32_t* k0, int32_t* v0, int32_t* k1, int32_t* v1, int64_t n, unsigned bits, void* ws,
+                   bool* result_in_1, hipStream_t st) {
+  const RsPlan pl = rs_plan(n, bits);
+  char* p = static_cast<char*>(ws);
+  int32_t* ghist = reinterpret_cast<int32_t*>(p);
+  int32_t* goff = reinterpret_cast<int32_t*>(p + align_up((size_t)pl.cells * 4));
+  void* tmp = p + 2 * align_up((size_t)pl.cells * 4);
+  size_t tmp_bytes = pl.scan_bytes;
+  const int nd = 1 << pl.db;
+  bool in1 = false;
+  for (int ps = 0; ps < pl.passes; ++ps) {
+    const int shift = ps * pl.db;
+    int32_t* ki = in1 ? k1 : k0;
+    int32_t* vi = in1 ? v1 : v0;
+    int32_t* ko = in1 ? k0 : k1;
+    int32_t* vo = in1 ? v0 : v1;
+    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)pl.tiles), dim3(kRsThreads), nd * 4, st, ki, n, shift, pl.db, ghist,
+                       pl.tiles);
+    hipError_t e = rocprim::exclusive_scan(tmp, tmp_bytes, ghist, goff, 0, (size_t)pl.cells,
+                                           rocprim::plus<int32_t>(), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)pl.tiles), dim3(kRsThreads), (kRsWaves + 1) * nd * 4, st, ki, vi,
+                       n, shift, pl.db, goff, pl.tiles, ko, vo);
+    in1 = !in1;
+  }
+  *result_in_1 = in1;
+  return hipGetLastError();
 }
 
 // contribution c = 4t + kind -> destination row (sort key)
@@ -288,9 +427,11 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   float csum = 0.f;  // colsum of A for column m0 + tid (tid < 128), waves 0-1 only
-  float vacc[kMaxV];  // (V^T B)[j][k0 + tid] for the m0 == 0 tiles
+  // (V^T B)[j][k0 + vc] for j = vg, vg + 2, ... < nv (m0 == 0 tiles): all 256 threads
+  const int vc = tid & (kTN - 1), vg = tid >> 7;
+  float vacc[kMaxV / 2];
 #pragma unroll
-  for (int j = 0; j < kMaxV; ++j) vacc[j] = 0.f;
+  for (int q = 0; q < kMaxV / 2; ++q) vacc[q] = 0.f;
   const bool do_v = V != nullptr && m0 == 0;
   // register prefetch: stage s+1's global loads are in flight while stage s's MFMAs run
   float4 ra[4], rb[4];
@@ -369,11 +510,14 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
     if (colsum_part != nullptr && k0 == 0 && tid < kTN) {
       for (int r = 0; r < kNB; ++r) csum += sA[buf][r][tid];
     }
-    if (do_v && tid < kTN) {
+    if (do_v) {
       for (int r = 0; r < kNB; ++r) {
-        const float b = sB[buf][r][tid];
+        const float b = sB[buf][r][vc];
 #pragma unroll
-        for (int j = 0; j < kMaxV; ++j) vacc[j] = fmaf(sV[buf][r][j], b, vacc[j]);
+        for (int q = 0; q < kMaxV / 2; ++q) {
+          if (vg + 2 * q >= nv) break;
+          vacc[q] = fmaf(sV[buf][r][vg + 2 * q], b, vacc[q]);
+        }
       }
     }
     if (has_next) store_lds(buf ^ 1);
@@ -394,25 +538,56 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
       }
   if (colsum_part != nullptr && k0 == 0 && tid < kTN && m0 + tid < M)
     colsum_part[(int64_t)split * M + m0 + tid] = csum;
-  if (do_v && tid < kTN && k0 + tid < K) {
-    for (int j = 0; j < nv; ++j) vpart[((int64_t)split * nv + j) * K + k0 + tid] = vacc[j];
+  if (do_v && k0 + vc < K) {
+#pragma unroll
+    for (int q = 0; q < kMaxV / 2; ++q) {
+      const int j = vg + 2 * q;
+      if (j >= nv) break;
+      vpart[((int64_t)split * nv + j) * K + k0 + vc] = vacc[q];
+    }
   }
 }
 
-// out[e] = sum_s part[s][e]: 8 interleaved partial sums (split s goes to sum s % 8, in
-// split order), then combined in a fixed order -- deterministic, 8 loads in flight.
-__global__ void __launch_bounds__(256) k_split_reduce(const float* __restrict__ part, int64_t splits, int64_t elems,
-                                                      float* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= elems) return;
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int64_t k = 0;
-  for (; k + 8 <= splits; k += 8) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] += part[(k + q) * elems + e];
+// out[e] = sum_s part[s][e] for up to three partial arrays in one launch.  A 1024-thread
+// block owns 64 consecutive elements of one array; thread group g (16 of them) sums splits
+// g, g + 16, ... with 4 interleaved accumulators, then the 16 group sums are added in
+// group order through LDS -- a fixed tree, so the result is deterministic.
+struct SplitReduceArg {
+  const float* part[3];
+  float* out[3];
+  int64_t elems[3];
+  int64_t blocks[3];  // prefix block offsets: array a owns blocks [blocks[a-1], blocks[a])
+};
+
+__global__ void __launch_bounds__(1024) k_split_reduce(SplitReduceArg arg, int64_t splits) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  int a = 0;
+  int64_t b = blockIdx.x;
+  while (a < 2 && b >= arg.blocks[a]) ++a;
+  if (a > 0) b -= arg.blocks[a - 1];
+  const float* __restrict__ part = arg.part[a];
+  const int64_t elems = arg.elems[a];
+  const int64_t e = b * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (e < elems) {
+    int64_t k = g;
+    for (; k + 48 < splits; k += 64) {
+      s0 += part[k * elems + e];
+      s1 += part[(k + 16) * elems + e];
+      s2 += part[(k + 32) * elems + e];
+      s3 += part[(k + 48) * elems + e];
+    }
+    for (; k < splits; k += 16) s0 += part[k * elems + e];
   }
-  for (int q = 0; k + q < splits; ++q) a[q] += part[(k + q) * elems + e];
-  out[e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  red[g][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && e < elems) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][lane];
+    arg.out[a][e] = t;
+  }
 }
 
 }  // namespace
@@ -428,21 +603,18 @@ __global__ void __launch_bounds__(256) k_split_reduce(const float* __restrict__ 
 
 bool bpr_channels_ok(int C) { return C == 32 || C == 64 || C == 128 || C == 256; }
 
-static int64_t bpr_fwd_blocks(int64_t S, int C) { return (S + 256 / (C / 4) - 1) / (256 / (C / 4)); }
-
-static size_t bpr_sort_temp(int64_t S, int64_t N) {
-  size_t b = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
-                                  (int32_t*)nullptr, (size_t)(4 * S > 0 ? 4 * S : 1), 0u, key_bits(N));
-  return b;
+// fixed grid (a function of S only): <= 1024 block partials for the one-block loss sum
+static int64_t bpr_fwd_blocks(int64_t S, int C) {
+  const int64_t b = (S + 256 / (C / 4) - 1) / (256 / (C / 4));
+  return b < 1024 ? b : 1024;
 }
 
-// workspace: block_loss | keys | vals | skeys | scid | slots | sort temp
+// workspace: block_loss | keys | vals | skeys | scid | slots | radix sort
 size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
   const int64_t c4 = 4 * S > 0 ? 4 * S : 1;
   const int64_t chunks = (c4 + kChunk - 1) / kChunk;
   return align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4) + 4 * align_up((size_t)c4 * 4) +
-         align_up((size_t)chunks * 2 * C * 4) + align_up(bpr_sort_temp(S, N));
+         align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N));
 }
 
 hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
@@ -460,7 +632,7 @@ hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32
                                                 block_loss, bad, row_map));
   }
   const float denom = kind == 0 ? (float)S : 2.f * (float)S;
-  hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(256), 0, st, block_loss, S > 0 ? nb : 0, denom > 0 ? denom : 1.f,
+  hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(1024), 0, st, block_loss, S > 0 ? nb : 0, denom > 0 ? denom : 1.f,
                      loss);
   return hipGetLastError();
 }
@@ -481,11 +653,17 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
   int32_t* scid = reinterpret_cast<int32_t*>(p + 3 * e4);
   float* slots = reinterpret_cast<float*>(p + 4 * e4);
   void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
-  size_t tmp_bytes = ws_bytes - (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws));
+  if (ws_bytes < (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws)) + rs_workspace_bytes(total, key_bits(N)))
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
                      n_items, row_map, keys, vals);
-  err = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, vals, scid, (size_t)total, 0u, key_bits(N), st);
+  bool in1 = false;
+  err = rs_sort(keys, vals, skeys, scid, total, key_bits(N), tmp, &in1, st);
   if (err != hipSuccess) return err;
+  if (!in1) {  // even pass count: the result is back in (keys, vals)
+    skeys = keys;
+    scid = vals;
+  }
   PPGAT_DISPATCH_LOSS_C(C, {
     constexpr int SPB = 256 / (CC / 4);
     const unsigned g = (unsigned)((chunks + SPB - 1) / SPB);
@@ -525,14 +703,22 @@ hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int
   const int tiles = ((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
   hipLaunchKernelGGL(k_gemm_tn, dim3((unsigned)tiles, (unsigned)s), dim3(256), 0, st, A, lda, B, ldb, N, M, K, rows,
                      part, cpart, vpart ? V : nullptr, ldv, vpart ? nv : 0, vpart);
-  const int64_t elems = (int64_t)M * K;
-  hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, st, part, s, elems, out);
-  if (colsum)
-    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, cpart, s, (int64_t)M,
-                       colsum);
-  if (vpart)
-    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)(((int64_t)nv * K + 255) / 256)), dim3(256), 0, st, vpart, s,
-                       (int64_t)nv * K, vout);
+  SplitReduceArg ra{};
+  int na = 0;
+  int64_t nb = 0;
+  auto add = [&](const float* pp, float* o, int64_t elems) {
+    ra.part[na] = pp;
+    ra.out[na] = o;
+    ra.elems[na] = elems;
+    nb += (elems + 63) / 64;
+    ra.blocks[na] = nb;
+    ++na;
+  };
+  add(part, out, (int64_t)M * K);
+  if (colsum) add(cpart, colsum, (int64_t)M);
+  if (vpart) add(vpart, vout, (int64_t)nv * K);
+  for (int q = na; q < 3; ++q) { ra.part[q] = ra.part[0]; ra.out[q] = ra.out[0]; ra.elems[q] = 0; ra.blocks[q] = nb; }
+  hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)nb), dim3(1024), 0, st, ra, s);
   return hipGetLastError();
 }
 

@@ -111,3 +111,18 @@ def test_bpr_bad_index_raises(pkg, cuda):
         ops.check_bpr_indices()
     pkg.bpr_loss(Z, 6, u, torch.tensor([0, 3], device=cuda), j)
     ops.check_bpr_indices()
+
+
+@pytest.mark.gpu
+def test_bpr_large_row_space(pkg, oracle, cuda):
+    """N > 2^20 rows: the contribution sort takes three radix passes (21 key bits)."""
+    rng = np.random.default_rng(7)
+    n_users, n_items, S, C = 1_100_000, 2_000, 30_000, 32
+    u = torch.from_numpy(rng.integers(0, n_users, S))
+    i = torch.from_numpy(rng.integers(0, n_items, S))
+    j = torch.from_numpy(rng.integers(0, n_items, S))
+    Z64 = torch.from_numpy(rng.standard_normal((n_users + n_items, C)) * 0.3).requires_grad_(True)
+    Zd = Z64.detach().float().to(cuda).requires_grad_(True)
+    pkg.bpr_loss(Zd, n_users, u.to(cuda), i.to(cuda), j.to(cuda)).backward()
+    oracle.bpr_loss(Z64, n_users, u, i, j).backward()
+    assert rel(Zd.grad, Z64.grad) <= 1e-5
