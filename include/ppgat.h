@@ -215,6 +215,51 @@ int ppgat_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int6
                   float* colsum, const float* V, int64_t ldv, int nv, float* vout,
                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* Same as ppgat_gemm_tn with B given as two row segments: rows [0, split) from b0 (ldb0),
+ * rows [split, n) from b1 (row - split, ldb1) -- x = cat(user_emb, item_proj(feats))
+ * (train_gat_pyg.py:79-82) without materialising the concatenation. */
+int ppgat_gemm_tn_seg(const float* A, int64_t lda, const float* b0, int64_t ldb0, const float* b1, int64_t ldb1,
+                      int64_t split, int64_t n, int m, int k, float* out, float* colsum, const float* V, int64_t ldv,
+                      int nv, float* vout, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- fused projection (matrix cores) ------------------------------------------------
+ * Replaces: h = GATConv.lin(x) (PyG Linear, no bias; train_gat_pyg.py:77) /
+ *           SimpleGATLayer.lin (train_gat_custom.py:66,77) followed by the node attention
+ *           terms (alpha_src/alpha_dst; custom :79), and PyGGAT.item_proj (train_gat_pyg.py:74,81):
+ *   y[r, :] = x_r W^T (+ bias),   x_r = x0[r] for r < split, x1[r - split] otherwise
+ *   s_src[r] = y[r] . att_src,  s_dst[r] = y[r] . att_dst   when att_src != NULL (heads = 1)
+ * W [out_cols, k] row-major (ldw); k <= 128 and k % 4 == 0; out_cols == 128.  Row strides in
+ * floats, multiples of 4, 16-byte aligned rows.  fp32 MFMA (exact fp32 FMA chains). */
+int ppgat_project_supported(int k, int out_cols);
+int ppgat_project(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int k,
+                  const float* w, int64_t ldw, int out_cols, const float* bias, const float* att_src,
+                  const float* att_dst, float* y, int64_t ldy, float* s_src, float* s_dst, void* stream);
+/* Input gradient of the layer (heads = 1), with D = [dh_msg | ds_src | ds_dst] from
+ * ppgat_bwd_edges + ppgat_bwd_dst_sum ([n, ldd], ds_src at column k, ds_dst at k + 1):
+ *   dx = D[:, :k] W + ds_src (x) (att_src W) + ds_dst (x) (att_dst W)
+ * W [k, out_cols] row-major = lin.weight; k <= 128, out_cols == 128. */
+int ppgat_project_bwd_input(const float* D, int64_t ldd, int64_t n, int k, const float* w, int64_t ldw, int out_cols,
+                            const float* att_src, const float* att_dst, float* dx, int64_t lddx, void* stream);
+/* Weight and attention-vector gradients from G = dh_msg^T x [H*C, K] and
+ * GV = [ds_src^T x ; ds_dst^T x] [2H, K] (ppgat_gemm_tn with V):
+ *   dW = G + att_src (x) GV[:H] + att_dst (x) GV[H:],  datt_src[h] = W_h GV[h],  datt_dst[h] = W_h GV[H + h]. */
+int ppgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src, const float* att_dst,
+                       int heads, int channels, int in_channels, float* dW, float* datt_src, float* datt_dst,
+                       void* stream);
+
+/* ---- optimizer -------------------------------------------------------------------------
+ * Replaces: torch.optim.Adam(model.parameters(), lr, weight_decay) .step()
+ * (train_gat_pyg.py:299,323) for fp32 dense tensors, amsgrad=False, maximize=False:
+ *   g += wd * p;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2   ((1 - b) rounded from double);
+ *   p -= step_size * m / (sqrt(v) / bias_correction2_sqrt + eps)
+ * with step_size = lr / (1 - b1^t), bias_correction2_sqrt = sqrt(1 - b2^t) per tensor
+ * (host arrays).  count <= ppgat_adam_max_tensors() tensors in one launch. */
+int ppgat_adam_max_tensors(void);
+int ppgat_adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, const int64_t* numel, const float* step_size,
+                    const float* bias_correction2_sqrt, double beta1, double beta2, float eps, float weight_decay,
+                    void* stream);
+
 /* ---- sampled ranking (evaluation) ------------------------------------------------
  * Replaces: the per-user loop of eval_sampled, scripts/train_gat_pyg.py:160-175:
  *   scores = I[cands[b]] @ U[users[b]];  rank[b] = #(scores[1:] > scores[0]) + 1
@@ -251,7 +296,9 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
 #define PPGAT_K_SCHED 7
 #define PPGAT_K_GEMM_TN 8
 #define PPGAT_K_FUSION 9
-#define PPGAT_K_COUNT 10
+#define PPGAT_K_PROJ 10
+#define PPGAT_K_ADAM 11
+#define PPGAT_K_COUNT 12
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

@@ -62,6 +62,16 @@ SIGNATURES = {
     "ppgat_gemm_tn_workspace_bytes": (c_int, [c_i64, c_int, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_gemm_tn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp,
                               c_vp, c_sz, c_vp]),
+    "ppgat_gemm_tn_seg": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_int, c_vp, c_vp,
+                                  c_vp, c_i64, c_int, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_project_supported": (c_int, [c_int, c_int]),
+    "ppgat_project": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_vp, c_vp,
+                              c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "ppgat_project_bwd_input": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "ppgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_adam_max_tensors": (c_int, []),
+    "ppgat_adam_step": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
+                                c_f, c_f, c_vp]),
     "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),
@@ -70,7 +80,8 @@ SIGNATURES = {
     "ppgat_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
 }
 
-KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6, "sched": 7, "gemm_tn": 8, "fusion": 9}
+KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6, "sched": 7,
+           "gemm_tn": 8, "fusion": 9, "proj": 10, "adam": 11}
 MODE_PYG, MODE_CUSTOM = 0, 1
 
 _lib = None

@@ -94,6 +94,15 @@ class GATConv(torch.nn.Module):
         return gat_layer(x, self.lin.weight, self.att_src, self.att_dst, self.bias, graph, self.heads,
                          self.out_channels, _lib.MODE_PYG, float(self.negative_slope), p, seed)
 
+    def forward_segments(self, x: torch.Tensor, x_items: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        """forward(cat(x, x_items), edge_index) without materialising the concatenation
+        (the model's node features, train_gat_pyg.py:79-82)."""
+        graph = graph_cache.get(edge_index, x.size(0) + x_items.size(0))
+        p = float(self.dropout) if self.training else 0.0
+        seed = _dropout_seed() if p > 0 else 0
+        return gat_layer(x, self.lin.weight, self.att_src, self.att_dst, self.bias, graph, self.heads,
+                         self.out_channels, _lib.MODE_PYG, float(self.negative_slope), p, seed, x_items=x_items)
+
     def __repr__(self):
         return (f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads}, "
                 f"backend=hip)")
@@ -123,3 +132,11 @@ class SimpleGATLayer(torch.nn.Module):
         seed = _dropout_seed() if p > 0 else 0
         return gat_layer(x, self.lin.weight, self.a_src, self.a_dst, None, graph, 1, self.out_dim, _lib.MODE_CUSTOM,
                          float(self.leaky.negative_slope), p, seed)
+
+    def forward_segments(self, x: torch.Tensor, x_items: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        """forward(cat(x, x_items), edge_index) without materialising the concatenation."""
+        graph = graph_cache.get(edge_index, x.size(0) + x_items.size(0))
+        p = float(self.drop.p) if self.training else 0.0
+        seed = _dropout_seed() if p > 0 else 0
+        return gat_layer(x, self.lin.weight, self.a_src, self.a_dst, None, graph, 1, self.out_dim, _lib.MODE_CUSTOM,
+                         float(self.leaky.negative_slope), p, seed, x_items=x_items)

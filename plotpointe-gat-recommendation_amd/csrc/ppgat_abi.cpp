@@ -426,28 +426,120 @@ int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
   return PPGAT_OK;
 }
 
+// workspace covers both GEMM variants (the choice also depends on V's alignment)
+static size_t tn_ws(int64_t n, int m, int k, int nv) {
+  const size_t a = ppgat::tn128_workspace_bytes(n), b = ppgat::gemm_tn_workspace_bytes(n, m, k, nv);
+  return (m <= 128 && k <= 128 && nv <= 2) ? (a > b ? a : b) : b;
+}
+
 int ppgat_gemm_tn_workspace_bytes(int64_t n, int m, int k, int nv, size_t* bytes) {
   if (!bytes || n < 0 || m < 1 || k < 1 || nv < 0) return fail(PPGAT_ERR_INVALID, "gemm_tn_workspace_bytes: bad arguments");
-  *bytes = ppgat::gemm_tn_workspace_bytes(n, m, k, nv);
+  *bytes = tn_ws(n, m, k, nv);
+  return PPGAT_OK;
+}
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; }
+
+int ppgat_gemm_tn_seg(const float* A, int64_t lda, const float* b0, int64_t ldb0, const float* b1, int64_t ldb1,
+                      int64_t split, int64_t n, int m, int k, float* out, float* colsum, const float* V, int64_t ldv,
+                      int nv, float* vout, void* workspace, size_t workspace_bytes, void* stream) {
+  if (n < 0 || m < 1 || k < 1 || nv < 0 || nv > 16) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad sizes (nv <= 16)");
+  if (split < 0 || split > n) return fail(PPGAT_ERR_INVALID, "gemm_tn: split outside [0, n]");
+  if (lda < m || ldb0 < k || (b1 && ldb1 < k) || (nv > 0 && ldv < nv))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn: bad leading dimension");
+  if ((lda % 4) || (ldb0 % 4) || (b1 && (ldb1 % 4)) || !al16(A) || !al16(b0) || (b1 && !al16(b1)))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: A/B rows must be 16-byte aligned");
+  if (!out || (n > 0 && (!A || !b0)) || (nv > 0 && (!V || !vout)))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
+  if (!workspace || workspace_bytes < tn_ws(n, m, k, nv))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn: workspace too small");
+  const bool fast = ppgat::tn128_shape_ok(m, k, nv, V, ldv);
+  if (!fast && b1 && split < n) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: segmented B needs m, k <= 128, nv <= 2");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = fast ? ppgat::tn128(A, lda, b0, ldb0, b1, ldb1, b1 ? split : n, n, m, k, out, colsum,
+                                     nv > 0 ? V : nullptr, ldv, nv, vout, workspace, st)
+                      : ppgat::gemm_tn(A, lda, b0, ldb0, n, m, k, out, colsum, nv > 0 ? V : nullptr, ldv, nv, vout,
+                                       workspace, st);
+  if (e != hipSuccess) return hip_fail(e, "gemm_tn");
   return PPGAT_OK;
 }
 
 int ppgat_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t n, int m, int k, float* out,
                   float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* workspace,
                   size_t workspace_bytes, void* stream) {
-  if (n < 0 || m < 1 || k < 1 || nv < 0 || nv > 16) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad sizes (nv <= 16)");
-  if (lda < m || ldb < k || (nv > 0 && ldv < nv)) return fail(PPGAT_ERR_INVALID, "gemm_tn: bad leading dimension");
-  if ((lda % 4) || (ldb % 4) || (reinterpret_cast<uintptr_t>(A) % 16) || (reinterpret_cast<uintptr_t>(B) % 16))
-    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: A/B rows must be 16-byte aligned");
-  if (!out || (n > 0 && (!A || !B)) || (nv > 0 && (!V || !vout)))
-    return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
-  if (!workspace || workspace_bytes < ppgat::gemm_tn_workspace_bytes(n, m, k, nv))
-    return fail(PPGAT_ERR_INVALID, "gemm_tn: workspace too small");
+  return ppgat_gemm_tn_seg(A, lda, B, ldb, nullptr, 0, n, n, m, k, out, colsum, V, ldv, nv, vout, workspace,
+                           workspace_bytes, stream);
+}
+
+int ppgat_project_supported(int k, int out_cols) { return ppgat::proj_shape_ok(k, out_cols) ? 1 : 0; }
+
+int ppgat_project(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int k,
+                  const float* w, int64_t ldw, int out_cols, const float* bias, const float* att_src,
+                  const float* att_dst, float* y, int64_t ldy, float* s_src, float* s_dst, void* stream) {
+  if (!ppgat::proj_shape_ok(k, out_cols)) return fail(PPGAT_ERR_UNSUPPORTED, "project: needs k <= 128, k % 4 == 0, out_cols == 128");
+  if (n < 0 || split < 0 || split > n) return fail(PPGAT_ERR_INVALID, "project: bad sizes");
+  if (ldx0 < k || (x1 && ldx1 < k) || ldw < k || ldy < out_cols || (ldx0 % 4) || (x1 && (ldx1 % 4)) || (ldw % 4))
+    return fail(PPGAT_ERR_INVALID, "project: bad leading dimension (>= width, multiple of 4)");
+  if (n > 0 && (!x0 || !w || !y || (att_src && (!att_dst || !s_src || !s_dst))))
+    return fail(PPGAT_ERR_INVALID, "project: null pointer");
+  if (!al16(x0) || (x1 && !al16(x1)) || !al16(w)) return fail(PPGAT_ERR_UNSUPPORTED, "project: rows must be 16-byte aligned");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ, st);
+  hipError_t e = ppgat::proj_fwd(x0, ldx0, x1, ldx1, x1 ? split : n, n, k, w, ldw, bias, att_src, att_dst, y, ldy,
+                                 s_src, s_dst, st);
+  if (e != hipSuccess) return hip_fail(e, "project");
+  return PPGAT_OK;
+}
+
+int ppgat_project_bwd_input(const float* D, int64_t ldd, int64_t n, int k, const float* w, int64_t ldw, int out_cols,
+                            const float* att_src, const float* att_dst, float* dx, int64_t lddx, void* stream) {
+  if (!ppgat::proj_shape_ok(k, out_cols)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_input: needs k <= 128, k % 4 == 0, out_cols == 128");
+  if (n < 0) return fail(PPGAT_ERR_INVALID, "project_bwd_input: bad sizes");
+  if (ldd < k + 2 || (ldd % 2) || (ldd % 4) || ldw < out_cols || lddx < out_cols)
+    return fail(PPGAT_ERR_INVALID, "project_bwd_input: bad leading dimension (ldd >= k + 2, multiple of 4)");
+  if (n > 0 && (!D || !w || !att_src || !att_dst || !dx)) return fail(PPGAT_ERR_INVALID, "project_bwd_input: null pointer");
+  if (!al16(D)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_input: rows must be 16-byte aligned");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ, st);
+  hipError_t e = ppgat::proj_dx(D, ldd, n, k, w, ldw, att_src, att_dst, dx, lddx, st);
+  if (e != hipSuccess) return hip_fail(e, "project_bwd_input");
+  return PPGAT_OK;
+}
+
+int ppgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src, const float* att_dst,
+                       int heads, int channels, int in_channels, float* dW, float* datt_src, float* datt_dst,
+                       void* stream) {
+  if (heads < 1 || channels < 1 || in_channels < 1) return fail(PPGAT_ERR_INVALID, "weight_grads: bad sizes");
+  if (!G || !GV || !w || !att_src || !att_dst || !dW || !datt_src || !datt_dst)
+    return fail(PPGAT_ERR_INVALID, "weight_grads: null pointer");
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_GEMM_TN, st);
-  hipError_t e = ppgat::gemm_tn(A, lda, B, ldb, n, m, k, out, colsum, nv > 0 ? V : nullptr, ldv, nv, vout,
-                                workspace, st);
-  if (e != hipSuccess) return hip_fail(e, "gemm_tn");
+  hipError_t e = ppgat::wgrad_assemble(G, GV, w, att_src, att_dst, heads, channels, in_channels, dW, datt_src,
+                                       datt_dst, st);
+  if (e != hipSuccess) return hip_fail(e, "weight_grads");
+  return PPGAT_OK;
+}
+
+int ppgat_adam_max_tensors(void) { return ppgat::adam_max_tensors(); }
+
+int ppgat_adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                    float* const* exp_avg_sq, const int64_t* numel, const float* step_size,
+                    const float* bias_correction2_sqrt, double beta1, double beta2, float eps, float weight_decay,
+                    void* stream) {
+  if (count < 0 || count > ppgat::adam_max_tensors()) return fail(PPGAT_ERR_INVALID, "adam_step: bad tensor count");
+  if (count > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel || !step_size || !bias_correction2_sqrt))
+    return fail(PPGAT_ERR_INVALID, "adam_step: null pointer");
+  for (int t = 0; t < count; ++t) {
+    if (numel[t] < 0) return fail(PPGAT_ERR_INVALID, "adam_step: negative numel");
+    if (numel[t] > 0 && (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t]))
+      return fail(PPGAT_ERR_INVALID, "adam_step: null tensor");
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_ADAM, st);
+  hipError_t e = ppgat::adam_step(count, params, grads, exp_avg, exp_avg_sq, numel, step_size, bias_correction2_sqrt,
+                                  beta1, beta2, eps, weight_decay, st);
+  if (e != hipSuccess) return hip_fail(e, "adam_step");
   return PPGAT_OK;
 }
 

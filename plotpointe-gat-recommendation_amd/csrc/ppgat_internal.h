@@ -68,6 +68,25 @@ size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv);
 hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
                    float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st);
 
+// projection GEMMs, weight gradients, optimizer (ppgat_gemm.hip)
+bool proj_shape_ok(int K, int ncols);
+hipError_t proj_fwd(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int K,
+                    const float* W, int64_t ldw, const float* bias, const float* att_src, const float* att_dst,
+                    float* y, int64_t ldy, float* s_src, float* s_dst, hipStream_t st);
+hipError_t proj_dx(const float* D, int64_t ldd, int64_t n, int K, const float* W, int64_t ldw, const float* att_src,
+                   const float* att_dst, float* y, int64_t ldy, hipStream_t st);
+bool tn128_shape_ok(int M, int K, int nv, const float* V, int64_t ldv);
+size_t tn128_workspace_bytes(int64_t N);
+hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const float* B1, int64_t ldb1, int64_t split,
+                 int64_t N, int M, int K, float* out, float* colsum, const float* V, int64_t ldv, int nv, float* vout,
+                 void* ws, hipStream_t st);
+hipError_t wgrad_assemble(const float* G, const float* GV, const float* W, const float* att_src, const float* att_dst,
+                          int heads, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st);
+int adam_max_tensors();
+hipError_t adam_step(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                     const int64_t* n, const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
+                     float eps, float wd, hipStream_t st);
+
 // evaluation (ppgat_eval.hip)
 hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                         const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,

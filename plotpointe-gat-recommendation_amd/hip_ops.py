@@ -312,43 +312,110 @@ def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, ld, heads, channe
                                      dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
+def project_supported(k: int, out_cols: int) -> bool:
+    return bool(_lib.load().ppgat_project_supported(int(k), int(out_cols)))
+
+
+def project(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+            att_src: Optional[torch.Tensor] = None, att_dst: Optional[torch.Tensor] = None,
+            x_items: Optional[torch.Tensor] = None):
+    """y = [x; x_items] W^T (+ bias) on the matrix cores (include/ppgat.h ppgat_project), with
+    s_src = y.att_src and s_dst = y.att_dst fused when att_src is given (heads = 1).
+    Returns y, or (y, s_src, s_dst)."""
+    lib = _lib.load()
+    _check_dev("x", x, torch.float32)
+    _check_dev("weight", weight, torch.float32, x.device)
+    if x_items is not None and x.size(0) == 0:
+        x, x_items = x_items, None
+    split = x.size(0)
+    n = split + (x_items.size(0) if x_items is not None else 0)
+    if x_items is not None:
+        _check_dev("x_items", x_items, torch.float32, x.device)
+    K, HC = weight.size(1), weight.size(0)
+    dev = x.device
+    y = torch.empty(n, HC, dtype=torch.float32, device=dev)
+    s_src = s_dst = None
+    if att_src is not None:
+        s_src = torch.empty(n, dtype=torch.float32, device=dev)
+        s_dst = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_project(x.data_ptr(), x.stride(0) if x.dim() == 2 and split > 1 else K, _lib.ptr(x_items),
+                                 (x_items.stride(0) if x_items.size(0) > 1 else K) if x_items is not None else 0,
+                                 split, n, K, weight.data_ptr(), weight.stride(0), HC, _lib.ptr(bias),
+                                 _lib.ptr(att_src), _lib.ptr(att_dst), y.data_ptr(), HC, _lib.ptr(s_src),
+                                 _lib.ptr(s_dst), _lib.stream_handle(dev)), "project")
+    return y if att_src is None else (y, s_src, s_dst)
+
+
+def weight_grads(G, GV, W, a_s, a_d, heads: int, C: int):
+    """dW, datt_src, datt_dst from G = dh_msg^T x and GV = [ds_src; ds_dst]^T x (ppgat_weight_grads)."""
+    lib = _lib.load()
+    HC, K = W.shape
+    dev = W.device
+    dW = torch.empty(HC, K, dtype=torch.float32, device=dev)
+    datt_src = torch.empty(heads, C, dtype=torch.float32, device=dev)
+    datt_dst = torch.empty(heads, C, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_weight_grads(G.data_ptr(), GV.data_ptr(), W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), heads,
+                                      C, K, dW.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(),
+                                      _lib.stream_handle(dev)), "weight_grads")
+    return dW, datt_src, datt_dst
+
+
 class GATLayer(torch.autograd.Function):
     """One whole GAT layer x -> out with the projection inside:
-    forward  h = x W^T (BLAS), node scores, fused softmax-aggregate;
+    forward  h = x W^T with the node scores fused (ppgat_project; BLAS + ppgat_node_scores
+             outside the fused shapes), then the fused softmax-aggregate;
     backward prologue, pass B and the destination sum write D = [dh_msg | ds_src | ds_dst]
-    side by side, then dx = D W_aug (BLAS) and D^T x (ppgat_gemm_tn with V) give dx, dW
-    and datt with no separate epilogue pass (include/ppgat.h ppgat_bwd_dst_sum)."""
+             side by side; dx = D W_aug (ppgat_project_bwd_input: the attention terms as a
+             rank-2 epilogue; BLAS with W_aug outside the fused shapes), D^T x
+             (ppgat_gemm_tn with V) and ppgat_weight_grads give dW and datt.
+    ``x_items`` (optional): the input rows [x.size(0), N) as a second tensor, so the model's
+    node features cat(user_emb, item_proj(feats)) are never concatenated."""
 
     @staticmethod
     def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, heads: int, channels: int, mode: int,
-                slope: float, dropout_p: float, seed: int):
+                slope: float, dropout_p: float, seed: int, x_items=None):
         x = x.contiguous()
-        h = torch.nn.functional.linear(x, weight)
+        x_items = x_items.contiguous() if x_items is not None else None
+        W = weight.detach().contiguous()
         a_s = att_src.detach().reshape(heads, channels).contiguous()
         a_d = att_dst.detach().reshape(heads, channels).contiguous()
         b = bias.detach().contiguous() if bias is not None else None
-        s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
-        need = any(ctx.needs_input_grad[:5])
+        K = x.size(1)
+        had_items = x_items is not None
+        split = x.size(0)
+        fused = heads == 1 and project_supported(K, heads * channels) and (x_items is None or x_items.size(1) == K)
+        if fused:
+            h, s_src, s_dst = project(x, W, att_src=a_s, att_dst=a_d, x_items=x_items)
+            s_src, s_dst = s_src.view(-1, 1), s_dst.view(-1, 1)
+        else:
+            if x_items is not None:
+                x = torch.cat([x, x_items], 0)
+                x_items = None
+            h = torch.nn.functional.linear(x, W)
+            s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
+        need = any(ctx.needs_input_grad[:5]) or (had_items and ctx.needs_input_grad[12])
         out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed,
                                      want_agg=need and heads > 1)
         if need:
             empty = torch.empty(0, device=x.device)
-            ctx.save_for_backward(x, weight, h, a_s, a_d, s_src, s_dst, out, m, inv_l,
-                                  agg if agg is not None else empty, b if b is not None else empty)
+            ctx.save_for_backward(x, x_items if x_items is not None else empty, W, h, a_s, a_d, s_src, s_dst, out, m,
+                                  inv_l, agg if agg is not None else empty, b if b is not None else empty)
         ctx.graph = graph
-        ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None)
+        ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None, fused,
+                    x_items is not None, had_items, split)
         ctx.att_shapes = (att_src.shape, att_dst.shape)
         return out
 
     @staticmethod
     def backward(ctx, g_out):
-        x, W, h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg, b = ctx.saved_tensors
-        heads, C, mode, slope, p, seed, has_bias, has_agg = ctx.meta
+        x, xi, W, h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg, b = ctx.saved_tensors
+        heads, C, mode, slope, p, seed, has_bias, has_agg, fused, seg, had_items, split = ctx.meta
         g = ctx.graph
         lib = _lib.load()
         dev = x.device
         g_out = g_out.contiguous()
-        N, K = x.shape
+        N = g.n_nodes
+        K = x.size(1)
         HC = heads * C
         ld = HC + ((2 * heads + 3) // 4) * 4
         # prologue: packed per-node state (+ dbias)
@@ -363,41 +430,58 @@ class GATLayer(torch.autograd.Function):
                                           _lib.ptr(part), _lib.stream_handle(dev)), "bwd_prologue")
         D = torch.empty(N, ld, dtype=torch.float32, device=dev)
         _bwd_edges_dst(g, h, s_src, nstate, g_out, D, ld, heads, C, mode, slope, p, seed)
-        # W_aug = [W; A_src; A_dst],  A[hd] = sum_c att[hd, c] W[hd*C + c, :]
-        Wv = W.detach().view(heads, C, K)
-        A_s = torch.einsum("hc,hck->hk", a_s, Wv)
-        A_d = torch.einsum("hc,hck->hk", a_d, Wv)
-        Dv = D[:, :HC + 2 * heads]
-        dx = Dv @ torch.cat([W.detach(), A_s, A_d], 0) if ctx.needs_input_grad[0] else None
-        G, _, GV = gemm_tn(D[:, :HC], x, V=D[:, HC:HC + 2 * heads])
-        G_s, G_d = GV[:heads], GV[heads:2 * heads]
-        dW = (G.view(heads, C, K) + a_s[..., None] * G_s[:, None, :] + a_d[..., None] * G_d[:, None, :]).view(HC, K)
-        datt_src = torch.einsum("hck,hk->hc", Wv, G_s)
-        datt_dst = torch.einsum("hck,hk->hc", Wv, G_d)
-        return (dx, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                None, None, None, None, None, None, None)
+        need_dx = ctx.needs_input_grad[0] or (had_items and ctx.needs_input_grad[12])
+        dx = None
+        if need_dx:
+            if heads == 1 and project_supported(HC, K):  # reduction over HC, K output columns
+                dx = torch.empty(N, K, dtype=torch.float32, device=dev)
+                _lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), ld, N, HC, W.data_ptr(), K, K, a_s.data_ptr(),
+                                                       a_d.data_ptr(), dx.data_ptr(), K, _lib.stream_handle(dev)),
+                           "project_bwd_input")
+            else:
+                # W_aug = [W; A_src; A_dst],  A[hd] = sum_c att[hd, c] W[hd*C + c, :]
+                Wv = W.view(heads, C, K)
+                A_s = torch.einsum("hc,hck->hk", a_s, Wv)
+                A_d = torch.einsum("hc,hck->hk", a_d, Wv)
+                dx = D[:, :HC + 2 * heads] @ torch.cat([W, A_s, A_d], 0)
+        G, _, GV = gemm_tn(D[:, :HC], x, V=D[:, HC:HC + 2 * heads], B_items=xi if seg else None)
+        dW, datt_src, datt_dst = weight_grads(G, GV, W, a_s, a_d, heads, C)
+        dx_u = dx[:split] if (dx is not None and had_items) else dx
+        dx_i = dx[split:] if (dx is not None and had_items) else None
+        return (dx_u, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None, None, dx_i)
 
 
-def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p=0.0, seed=0):
-    """x [N, F] -> out [N, C]: lin + the fused GAT aggregation, with the fused backward."""
+def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p=0.0, seed=0,
+              x_items=None):
+    """x [N, F] -> out [N, C]: lin + the fused GAT aggregation, with the fused backward.
+    With ``x_items``, the input rows are cat(x, x_items) (never materialised on the fused path)."""
     _require(x.is_cuda, "gat_layer: ppgat runs on ROCm devices only; there is no CPU path")
     if x.dtype != torch.float32 or x.dim() != 2:
         raise NotImplementedError("ppgat gat_layer: fp32 2-D input only")
-    return GATLayer.apply(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
+    if x_items is not None:
+        _require(x_items.is_cuda and x_items.dtype == torch.float32 and x_items.dim() == 2
+                 and x_items.size(1) == x.size(1), "gat_layer: x_items must match x in dtype/device/width")
+    return GATLayer.apply(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed,
+                          x_items)
 
 
 # ---------------------------------------------------------------------------
 # projection with the MFMA weight-gradient kernel, and the fused BPR/BCE loss
 # ---------------------------------------------------------------------------
-def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Optional[torch.Tensor] = None):
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Optional[torch.Tensor] = None,
+            B_items: Optional[torch.Tensor] = None):
     """A [N,M], B [N,K] (row strides may exceed the widths) -> (A^T B [M,K], colsum(A) [M]
-    or None, V^T B [nv,K] or None), deterministic."""
+    or None, V^T B [nv,K] or None), deterministic.  With ``B_items`` the B rows are
+    cat(B, B_items) (two row segments, not concatenated)."""
     lib = _lib.load()
-    for name, t in (("A", A), ("B", B)):
+    for name, t in (("A", A), ("B", B)) + ((("B_items", B_items),) if B_items is not None else ()):
         _require(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32,
                  f"gemm_tn: {name} must be an fp32 ROCm tensor")
         _require(t.dim() == 2 and t.stride(1) == 1, f"gemm_tn: {name} must be 2-D with unit column stride")
-    _require(A.size(0) == B.size(0), "gemm_tn: A [N,M], B [N,K]")
+    split = B.size(0)
+    nb = split + (B_items.size(0) if B_items is not None else 0)
+    _require(A.size(0) == nb, "gemm_tn: A [N,M], B [N,K]")
     N, M, K = A.size(0), A.size(1), B.size(1)
     nv = 0 if V is None else V.size(1)
     if V is not None:
@@ -410,11 +494,18 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     _lib.check(lib.ppgat_gemm_tn_workspace_bytes(N, M, K, nv, ctypes.byref(nbytes)), "gemm_tn_workspace_bytes")
     ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=A.device)
     lda = A.stride(0) if N > 1 else max(M + (-M) % 4, 4)
-    ldb = B.stride(0) if N > 1 else max(K + (-K) % 4, 4)
+    ldb = B.stride(0) if split > 1 else max(K + (-K) % 4, 4)
     ldv = (V.stride(0) if N > 1 else nv) if nv else 0
-    _lib.check(lib.ppgat_gemm_tn(A.data_ptr(), lda, B.data_ptr(), ldb, N, M, K, out.data_ptr(), _lib.ptr(cs),
-                                 _lib.ptr(V) if nv else None, ldv, nv, _lib.ptr(vout), ws.data_ptr(), nbytes.value,
-                                 _lib.stream_handle(A.device)), "gemm_tn")
+    if B_items is not None:
+        ldb1 = B_items.stride(0) if B_items.size(0) > 1 else max(K + (-K) % 4, 4)
+        _lib.check(lib.ppgat_gemm_tn_seg(A.data_ptr(), lda, B.data_ptr(), ldb, B_items.data_ptr(), ldb1, split, N, M,
+                                         K, out.data_ptr(), _lib.ptr(cs), _lib.ptr(V) if nv else None, ldv, nv,
+                                         _lib.ptr(vout), ws.data_ptr(), nbytes.value, _lib.stream_handle(A.device)),
+                   "gemm_tn")
+    else:
+        _lib.check(lib.ppgat_gemm_tn(A.data_ptr(), lda, B.data_ptr(), ldb, N, M, K, out.data_ptr(), _lib.ptr(cs),
+                                     _lib.ptr(V) if nv else None, ldv, nv, _lib.ptr(vout), ws.data_ptr(),
+                                     nbytes.value, _lib.stream_handle(A.device)), "gemm_tn")
     return out, cs, vout
 
 
@@ -427,6 +518,8 @@ class _Linear(torch.autograd.Function):
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        if project_supported(x.size(1), weight.size(0)) and weight.is_contiguous():
+            return project(x, weight.detach(), bias.detach().contiguous() if bias is not None else None)
         return torch.nn.functional.linear(x, weight, bias)
 
     @staticmethod

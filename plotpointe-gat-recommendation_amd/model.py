@@ -5,7 +5,9 @@ as the reference so checkpoints ({"state_dict", "config"}) load both ways:
 ``CustomGAT`` -- scripts/train_gat_custom.py:96-115 (user_emb, item_proj, layers.{l})
 
 node_features = cat(user_emb.weight, item_proj(item_feats)); L stacked layers with no
-nonlinearity in between (train_gat_pyg.py:86-87).
+nonlinearity in between (train_gat_pyg.py:86-87).  forward() hands the two row blocks to
+the first layer separately (``forward_segments``), so the concatenation is never
+materialised; ``node_features`` still returns it for callers that want it.
 """
 from __future__ import annotations
 
@@ -13,6 +15,16 @@ import torch
 
 from . import hip_ops
 from .conv import GATConv, SimpleGATLayer
+
+
+def _stack(user_w, item_proj, item_feats, layers, edge_index):
+    v = hip_ops.linear(item_feats, item_proj.weight, item_proj.bias)
+    if len(layers) == 0:
+        return torch.cat([user_w, v], dim=0)
+    x = layers[0].forward_segments(user_w, v, edge_index)
+    for layer in list(layers)[1:]:
+        x = layer(x, edge_index)
+    return x
 
 
 class PyGGAT(torch.nn.Module):
@@ -34,10 +46,7 @@ class PyGGAT(torch.nn.Module):
         return torch.cat([u, v], dim=0)
 
     def forward(self, item_feats: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
-        x = self.node_features(item_feats)
-        for conv in self.convs:
-            x = conv(x, edge_index)
-        return x
+        return _stack(self.user_emb.weight, self.item_proj, item_feats, self.convs, edge_index)
 
 
 class CustomGAT(torch.nn.Module):
@@ -55,10 +64,7 @@ class CustomGAT(torch.nn.Module):
         return torch.cat([u, v], dim=0)
 
     def forward(self, item_feats: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
-        x = self.node_features(item_feats)
-        for gat in self.layers:
-            x = gat(x, edge_index)
-        return x
+        return _stack(self.user_emb.weight, self.item_proj, item_feats, self.layers, edge_index)
 
 
 def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch.Tensor:
