@@ -44,8 +44,12 @@ def parse():
     ap.add_argument("--heads", type=int, default=1)
     ap.add_argument("--samples", type=int, default=200_000)
     ap.add_argument("--attn-dropout", type=float, default=0.1)
-    ap.add_argument("--config", type=int, choices=[2, 3], default=2,
-                    help="2: U-I graph (headline); 3: U-I + I-I kNN k=20 edges (SURVEY.md 8(d) cfg 3)")
+    ap.add_argument("--config", type=int, choices=[2, 3, 5], default=2,
+                    help="2: U-I graph (headline); 3: U-I + I-I kNN k=20 edges (SURVEY.md 8(d) cfg 3); "
+                         "5: 10M x 5M x 200M-edge synthetic, d=256, heads=4 (roofline / scaling run)")
+    ap.add_argument("--scale", type=float, default=None,
+                    help="config 5 size multiplier (default world/8: one GPU's share of the 8-GPU run, "
+                         "so the per-GPU work is the same at every N)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
@@ -132,9 +136,16 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    # ---- synthetic config-2 inputs; identical on every rank ----
-    g = data.synthetic_ui_graph(seed=42)
-    feats_np = data.synthetic_item_features(g.n_items, 128, seed=42)
+    # ---- synthetic inputs; identical on every rank ----
+    if args.config == 5:
+        scale = args.scale if args.scale is not None else world / 8.0
+        args.hidden, args.heads = 256, 4
+        g = data.synthetic_scaling_graph(scale, seed=42)
+        feats_np = data.synthetic_item_features(g.n_items, 256, seed=42)
+    else:
+        scale = None
+        g = data.synthetic_ui_graph(seed=42)
+        feats_np = data.synthetic_item_features(g.n_items, 128, seed=42)
     ei_np = g.edge_index_numpy()
     if args.config == 3:  # I-I kNN relation appended to the homogeneous edge_index (A10, "extension")
         rows, cols, _ = data.synthetic_ii_edges(g, k=20, seed=42)
@@ -145,7 +156,7 @@ def main():
     feats = torch.from_numpy(feats_np).to(dev)
     tu, ti, tj = (torch.from_numpy(a).to(dev) for a in (u, i, j))
     torch.manual_seed(42)
-    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=128, hidden=args.hidden, layers=args.layers,
+    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=feats_np.shape[1], hidden=args.hidden, layers=args.layers,
                       heads=args.heads, attn_dropout=args.attn_dropout).to(dev)
     if world > 1:
         # row-sharded graph over the ranks (dist.py): strong scaling of the fixed config-2 job
@@ -208,11 +219,23 @@ def main():
     traffic = None
     try:
         tj_ = json.loads(Path(args.traffic_json).read_text())
-        traffic = tj_.get("per_launch_bytes", {}).get(dom)
+        if tj_.get("config", 2) == args.config:  # PMC summaries are per workload
+            traffic = tj_.get("per_launch_bytes", {}).get(dom)
     except Exception:
         pass
+    if args.config == 5:
+        metric = "edges/sec GAT fwd+bwd, d=256 heads=4, 200M-edge synthetic (config 5)"
+        workload = (f"cfg5 x{scale:g}: PyGGAT train step (fwd+BPR+bwd+Adam), {g.n_users:,} users + {g.n_items:,} "
+                    f"items, {g.n_interactions:,} interactions (Zipf items), d=256, heads=4")
+        data_desc = "synthetic (config-5 scaling graph, Poisson users / Zipf items, random-init weights)"
+    else:
+        metric = "edges/sec GAT fwd+bwd, d=128, 1.69M-edge U-I graph"
+        workload = (("cfg2: PyGGAT train step (fwd+BPR+bwd+Adam), 1,689,116 interactions, "
+                     "192,403 users + 63,001 items") if args.config == 2 else
+                    "cfg3: cfg2 + I-I kNN (k=20, sim>=0.3) edges, PyGGAT train step")
+        data_desc = "synthetic (config-2 statistics-matched U-I graph, random-init weights)"
     result = {
-        "metric": "edges/sec GAT fwd+bwd, d=128, 1.69M-edge U-I graph",
+        "metric": metric,
         "value": value,
         "unit": "edges/sec",
         "n_gpus": world,
@@ -220,13 +243,11 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el / K * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "weak" if (world == 1 or args.config == 5) else "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (config-2 statistics-matched U-I graph, random-init weights)",
-        "config": {"workload": ("cfg2: PyGGAT train step (fwd+BPR+bwd+Adam), 1,689,116 interactions, "
-                                "192,403 users + 63,001 items") if args.config == 2 else
-                               "cfg3: cfg2 + I-I kNN (k=20, sim>=0.3) edges, PyGGAT train step",
+        "data": data_desc,
+        "config": {"workload": workload,
                    "edges": E, "nodes": N, "layers": args.layers, "heads": H, "hidden": C,
                    "bpr_samples": args.samples, "attn_dropout": args.attn_dropout,
                    "parallelism": f"row-sharded x{world} (RCCL all_gather/reduce_scatter)" if world > 1
@@ -239,7 +260,7 @@ def main():
         "loss": float(loss.item()),
         "optimizer": "Adam (libppgat device kernel, torch.optim.Adam semantics)",
     }
-    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0 and args.config != 5:
         result["cpu_baseline"] = cpu_baseline(g, feats_np, C, args.layers, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

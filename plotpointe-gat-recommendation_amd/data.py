@@ -347,6 +347,34 @@ def synthetic_ui_graph(n_users: int = 192_403, n_items: int = 63_001,
     return UIGraph(n_users, n_items, tptr, i_tr, val_item, test_item, n_int)
 
 
+def synthetic_scaling_graph(scale: float = 1.0, seed: int = 42, n_users: int = 10_000_000,
+                            n_items: int = 5_000_000, n_interactions: int = 100_000_000,
+                            zipf_a: float = 0.8) -> UIGraph:
+    """Config 5 of SURVEY.md 8(d) (the roofline / scaling run): 10M users x 5M items x 100M
+    interactions, symmetrised to E = 200M message edges, every size multiplied by
+    ``scale`` (scale 1/8 = one GPU's share of the 8-GPU run).  User degree 1 + Poisson(mean
+    - 1), item popularity Zipf (p(i) ~ (i + 1)^-zipf_a over the item ids), items drawn by
+    inverse CDF.  Repeated (user, item) pairs are kept (harmless for message passing; the
+    graph only has to carry config 5's size and skew).  No held-out split: every
+    interaction is a training edge."""
+    nu = max(int(round(n_users * scale)), 1)
+    ni = max(int(round(n_items * scale)), 1)
+    nt = max(int(round(n_interactions * scale)), 1)
+    rng = np.random.default_rng(seed)
+    mean = nt / nu
+    udeg = 1 + rng.poisson(max(mean - 1.0, 0.0), nu)
+    udeg = _fix_sum(udeg, nt, 1, rng)
+    w = np.arange(1, ni + 1, dtype=np.float64) ** (-zipf_a)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    items = np.searchsorted(cdf, rng.random(nt), side="right").astype(np.int64)
+    np.minimum(items, ni - 1, out=items)
+    ptr = np.zeros(nu + 1, np.int64)
+    np.cumsum(udeg, out=ptr[1:])
+    none = np.full(nu, -1, np.int64)
+    return UIGraph(nu, ni, ptr, items, none, none, nt)
+
+
 def synthetic_ii_edges(g: UIGraph, k: int = 20, seed: int = 42, min_sim: float = 0.3):
     """Config 3 I-I kNN stand-in: per item up to k neighbours drawn proportional to
     popularity, similarity U(0.3,1) kept if >= min_sim (graphs/build_ii_knn.py:91-111
