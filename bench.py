@@ -161,7 +161,9 @@ def main():
     if world > 1:
         # row-sharded graph over the ranks (dist.py): strong scaling of the fixed config-2 job
         comm = pkg.dist.Comm()
-        dg = pkg.dist.build_dist_graph(ei, N, world, rank)
+        # users and items partitioned separately: every rank holds a slice of both, so the
+        # loss only gathers item rows (dist.sharded_bpr_loss)
+        dg = pkg.dist.build_dist_graph(ei, N, world, rank, segments=[(0, g.n_users), (g.n_users, N)])
         model = pkg.dist.ShardedPyGGAT(full, dg, comm)
     else:
         model = full

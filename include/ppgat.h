@@ -184,7 +184,10 @@ int ppgat_bwd_epilogue(const int32_t* rowptr, int64_t n_nodes, int heads, int ch
  *           and its autograd (gather backward = index_put_ accumulate).
  * Z [n_rows, C]; node id v (users [0, n_users), items n_users + i) lives in row v, or in
  * row row_map[v] when row_map != NULL (int32 [n_users + n_items]; the row-sharded path keeps
- * the gathered Z in a padded per-rank layout).  u, i, j int64 [S].
+ * the gathered Z in a padded per-rank layout).  A user whose row_map entry is -1 is not held
+ * by this caller: its triples contribute nothing (loss 0, no gradient), while the mean still
+ * divides by S -- the row-sharded loss evaluates the triples of its own users only and
+ * the ranks' losses add up to the reference's.  u, i, j int64 [S].
  * Forward writes the scalar mean loss and coef [S, 2] (dloss/dpos, dloss/dneg); the
  * backward writes the full grad_Z [N, C] (zero rows included) = grad_loss * sum of the
  * per-triple contributions, deterministically (sorted contributions, ordered sums).

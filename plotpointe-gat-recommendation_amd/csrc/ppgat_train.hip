@@ -68,24 +68,28 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
   for (int64_t t = (int64_t)blockIdx.x * SPB + sg; t - sg < S; t += (int64_t)gridDim.x * SPB) {
     const bool valid = t < S;
     float pos = 0.f, neg = 0.f;
+    bool skip = false;  // row_map -1: user not held here (row-sharded loss), triple contributes 0
     if (valid) {
       const int64_t u0 = u[t], i0 = ii[t], j0 = jj[t];
-      if (bad != nullptr && sl == 0 &&
-          (u0 < 0 || u0 >= n_users || i0 < 0 || i0 >= n_items || j0 < 0 || j0 >= n_items))
-        atomicAdd(bad, 1);  // integer count; indices are clamped below, the caller raises
+      const bool oob = u0 < 0 || u0 >= n_users || i0 < 0 || i0 >= n_items || j0 < 0 || j0 >= n_items;
       const int64_t ur = zrow(row_map, clamp_idx(u0, n_users));
       const int64_t ir = zrow(row_map, n_users + clamp_idx(i0, n_items));
       const int64_t jr = zrow(row_map, n_users + clamp_idx(j0, n_items));
-      const float4 a = ld4(Z + ur * C + sl * 4);
-      pos = dot4(a, ld4(Z + ir * C + sl * 4));
-      neg = dot4(a, ld4(Z + jr * C + sl * 4));
+      skip = ur < 0;
+      if (!skip) {
+        const float4 a = ld4(Z + ur * C + sl * 4);
+        pos = dot4(a, ld4(Z + ir * C + sl * 4));
+        neg = dot4(a, ld4(Z + jr * C + sl * 4));
+      }
+      if (bad != nullptr && sl == 0 && oob) atomicAdd(bad, 1);  // indices were clamped; the caller raises
     }
 #pragma unroll
     for (int off = LPR / 2; off > 0; off >>= 1) {
       pos += __shfl_xor(pos, off);
       neg += __shfl_xor(neg, off);
     }
-    if (sl == 0 && valid) {
+    if (sl == 0 && valid && skip) coef[t] = make_float2(0.f, 0.f);
+    if (sl == 0 && valid && !skip) {
       float l;
       float2 cf;
       if (kind == 0) {
@@ -266,9 +270,11 @@ hipError_t rs_sort(int32_t* k0, int32_t* v0, int32_t* k1, int32_t* v1, int64_t n
 }
 
 // contribution c = 4t + kind -> destination row (sort key)
+// (contributions of triples whose user row is -1 -- not held here -- get the sentinel key
+// n_rows: they sort last and are never written)
 __global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
                            const int64_t* __restrict__ jj, int64_t S, int64_t n_users, int64_t n_items,
-                           const int32_t* __restrict__ row_map, int32_t* __restrict__ key,
+                           const int32_t* __restrict__ row_map, int64_t n_rows, int32_t* __restrict__ key,
                            int32_t* __restrict__ val) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= 4 * S) return;
@@ -278,7 +284,8 @@ __global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restr
   if (kd < 2) d = clamp_idx(u[t], n_users);
   else if (kd == 2) d = n_users + clamp_idx(ii[t], n_items);
   else d = n_users + clamp_idx(jj[t], n_items);
-  key[c] = (int32_t)zrow(row_map, d);
+  const bool skip = zrow(row_map, clamp_idx(u[t], n_users)) < 0;
+  key[c] = skip ? (int32_t)n_rows : (int32_t)zrow(row_map, d);
   val[c] = (int32_t)c;
 }
 
@@ -298,7 +305,7 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
                                                     const int32_t* __restrict__ row_map,
                                                     const float2* __restrict__ coef,
                                                     const float* __restrict__ grad_loss, const float* __restrict__ Z,
-                                                    float* __restrict__ dZ, float* __restrict__ slots) {
+                                                    int64_t n_rows, float* __restrict__ dZ, float* __restrict__ slots) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   __shared__ int32_t s_src[SPB][kChunk];
@@ -320,9 +327,11 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
         const int kd = c & 3;
         const float2 tc = coef[t];
         dst = skey[p];
-        if (kd == 0) { src = (int32_t)zrow(row_map, n_users + clamp_idx(ii[t], n_items)); cf = tc.x; }
-        else if (kd == 1) { src = (int32_t)zrow(row_map, n_users + clamp_idx(jj[t], n_items)); cf = tc.y; }
-        else { src = (int32_t)zrow(row_map, clamp_idx(u[t], n_users)); cf = kd == 2 ? tc.x : tc.y; }
+        if (dst < n_rows) {
+          if (kd == 0) { src = (int32_t)zrow(row_map, n_users + clamp_idx(ii[t], n_items)); cf = tc.x; }
+          else if (kd == 1) { src = (int32_t)zrow(row_map, n_users + clamp_idx(jj[t], n_items)); cf = tc.y; }
+          else { src = (int32_t)zrow(row_map, clamp_idx(u[t], n_users)); cf = kd == 2 ? tc.x : tc.y; }
+        }
       }
       s_src[sg][q] = src;
       s_dst[sg][q] = dst;
@@ -355,7 +364,7 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
         const bool first = seg_start == 0, last = q == len - 1;
         if (first && starts_before) st4(slots + (ch * 2 + 0) * C + sl * 4, acc);
         else if (last && ends_after) st4(slots + (ch * 2 + 1) * C + sl * 4, acc);
-        else st4(dZ + (int64_t)r * C + sl * 4, acc);
+        else if (r < n_rows) st4(dZ + (int64_t)r * C + sl * 4, acc);
         acc = make_float4(0.f, 0.f, 0.f, 0.f);
         seg_start = q + 1;
       }
@@ -367,7 +376,8 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
 // head slots of the following chunks, in chunk order, and writes the row.
 template <int C>
 __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ skey, int64_t total,
-                                                   const float* __restrict__ slots, float* __restrict__ dZ) {
+                                                   const float* __restrict__ slots, int64_t n_rows,
+                                                   float* __restrict__ dZ) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
@@ -377,7 +387,7 @@ __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ s
   const int64_t b1 = min(b0 + kChunk, total);
   if (b1 >= total) return;
   const int32_t r = skey[b1 - 1];
-  if (skey[b1] != r) return;                           // last segment does not continue
+  if (skey[b1] != r || r >= n_rows) return;            // last segment does not continue / sentinel
   if (skey[b0] == r && b0 > 0 && skey[b0 - 1] == r) return;  // segment started in an earlier chunk
   float4 acc = ld4(slots + (ch * 2 + 1) * C + sl * 4);
   for (int64_t c2 = ch + 1;; ++c2) {
@@ -614,7 +624,7 @@ size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
   const int64_t c4 = 4 * S > 0 ? 4 * S : 1;
   const int64_t chunks = (c4 + kChunk - 1) / kChunk;
   return align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4) + 4 * align_up((size_t)c4 * 4) +
-         align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N));
+         align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N + 1));
 }
 
 hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
@@ -653,12 +663,12 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
   int32_t* scid = reinterpret_cast<int32_t*>(p + 3 * e4);
   float* slots = reinterpret_cast<float*>(p + 4 * e4);
   void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
-  if (ws_bytes < (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws)) + rs_workspace_bytes(total, key_bits(N)))
+  if (ws_bytes < (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws)) + rs_workspace_bytes(total, key_bits(N + 1)))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
-                     n_items, row_map, keys, vals);
+                     n_items, row_map, N, keys, vals);
   bool in1 = false;
-  err = rs_sort(keys, vals, skeys, scid, total, key_bits(N), tmp, &in1, st);
+  err = rs_sort(keys, vals, skeys, scid, total, key_bits(N + 1), tmp, &in1, st);
   if (err != hipSuccess) return err;
   if (!in1) {  // even pass count: the result is back in (keys, vals)
     skeys = keys;
@@ -668,8 +678,8 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
     constexpr int SPB = 256 / (CC / 4);
     const unsigned g = (unsigned)((chunks + SPB - 1) / SPB);
     hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, skeys, scid, total, u, i, j, n_users, n_items,
-                       row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, dZ, slots);
-    hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, dZ);
+                       row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, slots);
+    hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, N, dZ);
   });
   return hipGetLastError();
 }

@@ -1,9 +1,12 @@
 """Row-sharded multi-GPU GAT: one process per GPU, RCCL over xGMI.
 
-Partition.  Node ids [0, N) are cut into `world` contiguous ranges balanced by
-in-degree + out-degree + a per-node constant.  Every range is padded to R rows so all
-per-node tensors are [R, ...] per rank and [world*R, ...] gathered ("padded space";
-node n lives at row owner(n)*R + n - lo(owner)).  The graph is static: the global
+Partition.  The node ids are cut into segments (default: one, [0, N); the recommender
+uses two, users [0, n_users) and items [n_users, N)) and every segment into `world`
+contiguous ranges balanced by in-degree + out-degree + a per-node constant, so each rank
+holds a slice of every segment.  A rank's block is its segment slices, each padded to
+that segment's largest slice, R rows in all; per-node tensors are [R, ...] per rank and
+[world*R, ...] gathered ("padded space"; node n of segment s owned by rank r lives at row
+r*R + off_s + n - lo_s(r)).  The graph is static: the global
 CSR/CSC in padded space is built once on every rank (device radix sort) and each rank
 keeps slices of it:
   forward : CSR rows of its own destinations (col indexes the gathered padded space)
@@ -17,8 +20,10 @@ Per layer.
             sources (complete dh for them: no reverse exchange) -> reduce_scatter(dz)
             (every slot is written by exactly one rank, so the sum is exact) -> epilogue
             on own rows.
-Loss: all_gather of Z, each rank evaluates its contiguous share of the BPR triples, the
-gradient returns by reduce_scatter.  Dense parameters (lin, att, bias, item_proj) are
+Loss: with the (users, items) segments a rank evaluates the triples of its own users
+against an all_gather of the item rows only (n_items x C instead of N x C), and the
+item-row gradients return by reduce_scatter; with one segment, all_gather of Z and a
+contiguous share of the triples.  Dense parameters (lin, att, bias, item_proj) are
 replicated and all-reduced once per step; user-embedding rows are owner-held.
 On a locality-free graph the halo is ~all nodes, so all_gather is the natural collective
 here (a per-peer all-to-all index list would carry the same rows).
@@ -141,11 +146,15 @@ class DistGraph:
     rank: int
     n_nodes: int
     n_edges: int
-    bounds: np.ndarray
+    bounds: np.ndarray          # segment 0's range bounds (the only segment by default)
     R: int
     row_map: torch.Tensor       # [N] int32, node id -> padded row
     e_max: int
     view: LocalView
+    seg_bounds: list = None     # per segment: [world + 1] range bounds (node ids)
+    seg_R: list = None          # per segment: padded rows per rank
+    seg_off: list = None        # per segment: row offset inside a rank's block
+    loss_map: Optional[torch.Tensor] = None  # lazily built by sharded_bpr_loss
 
     @property
     def lo(self) -> int:
@@ -158,6 +167,19 @@ class DistGraph:
     @property
     def P(self) -> int:
         return self.world * self.R
+
+    def owned(self, rank: Optional[int] = None):
+        """[(lo, hi, row offset in the block, padded rows)] per segment of a rank."""
+        r = self.rank if rank is None else rank
+        return [(int(b[r]), int(b[r + 1]), off, Rs) for b, off, Rs in zip(self.seg_bounds, self.seg_off, self.seg_R)]
+
+    def owned_users(self, n_users: int, rank: Optional[int] = None):
+        """(u0, u1): the rank's users (one contiguous range at the top of its block)."""
+        rng = [(max(lo, 0), min(hi, n_users), off) for lo, hi, off, _ in self.owned(rank) if min(hi, n_users) > lo]
+        if not rng:
+            return 0, 0
+        assert len(rng) == 1 and rng[0][2] == 0, "users must be one range at the top of the block"
+        return rng[0][0], rng[0][1]
 
 
 def _hip_csr(ei, P):
@@ -172,17 +194,31 @@ def _hip_sched(ptr, E):
 
 def build_dist_graph(edge_index: torch.Tensor, n_nodes: int, world: int, rank: int,
                      csr_builder: Callable = _hip_csr, sched_builder: Optional[Callable] = _hip_sched,
-                     node_weight: float = 4.0) -> DistGraph:
+                     node_weight: float = 4.0, segments=None) -> DistGraph:
     """Every rank calls this with the same global edge_index (LongTensor [2, E], original
-    node ids) and gets its own slices.  Deterministic: all ranks agree on every array."""
+    node ids) and gets its own slices.  ``segments``: contiguous node-id ranges covering
+    [0, N) in order, each split over the ranks (default one segment).  Deterministic: all
+    ranks agree on every array."""
     dev = edge_index.device
     N = int(n_nodes)
     E = int(edge_index.size(1))
+    segs = [(0, N)] if segments is None else [(int(a), int(b)) for a, b in segments]
+    assert segs[0][0] == 0 and segs[-1][1] == N and all(segs[k][1] == segs[k + 1][0] for k in range(len(segs) - 1))
     deg = (torch.bincount(edge_index[1], minlength=N) + torch.bincount(edge_index[0], minlength=N)).cpu().numpy()
-    bounds = partition_bounds(deg.astype(np.float64) + node_weight, world)
-    R = max(int(np.max(np.diff(bounds))), 1)
-    owner = np.repeat(np.arange(world), np.diff(bounds))
-    row_map_np = (owner * R + (np.arange(N) - bounds[owner])).astype(np.int64)
+    seg_bounds, seg_R, seg_off = [], [], []
+    off = 0
+    for a, b in segs:
+        bnd = a + partition_bounds(deg[a:b].astype(np.float64) + node_weight, world)
+        seg_bounds.append(bnd)
+        Rs = max(int(np.max(np.diff(bnd))), 1 if len(segs) == 1 else 0)
+        seg_R.append(Rs)
+        seg_off.append(off)
+        off += Rs
+    R = max(off, 1)
+    row_map_np = np.empty(N, np.int64)
+    for (a, b), bnd, o in zip(segs, seg_bounds, seg_off):
+        owner = np.repeat(np.arange(world), np.diff(bnd))
+        row_map_np[a:b] = owner * R + o + (np.arange(a, b) - bnd[owner])
     row_map = torch.from_numpy(row_map_np).to(dev)
     ei_p = row_map[edge_index]                       # [2, E] padded ids
     P = world * R
@@ -207,7 +243,8 @@ def build_dist_graph(edge_index: torch.Tensor, n_nodes: int, world: int, rank: i
     if sched_builder is not None:
         view.fwd_sched = sched_builder(v_rowptr, e1 - e0)
         view.bwd_sched = sched_builder(v_colptr, c1 - c0)
-    return DistGraph(world, rank, N, E, bounds, R, row_map.to(torch.int32), e_max, view)
+    return DistGraph(world, rank, N, E, seg_bounds[0], R, row_map.to(torch.int32), e_max, view,
+                     seg_bounds, seg_R, seg_off)
 
 
 # ---------------------------------------------------------------------------
@@ -271,10 +308,7 @@ class ShardedPyGGAT(torch.nn.Module):
         self.stages = stages if stages is not None else HipStages()
         self.n_users, self.n_items = full.n_users, full.n_items
         nu = self.n_users
-        lo, hi = dg.lo, dg.hi
-        self.u0, self.u1 = min(max(lo, 0), nu), min(max(hi, 0), nu)
-        self.i0, self.i1 = min(max(lo - nu, 0), self.n_items), min(max(hi - nu, 0), self.n_items)
-        self.pad = dg.R - (hi - lo)
+        self.u0, self.u1 = dg.owned_users(nu)
         self.user_emb_local = torch.nn.Parameter(full.user_emb.weight.detach()[self.u0:self.u1].clone())
         self.item_proj = full.item_proj
         self.convs = full.convs
@@ -283,10 +317,25 @@ class ShardedPyGGAT(torch.nn.Module):
         return [p for n, p in self.named_parameters() if n != "user_emb_local"]
 
     def node_features(self, item_feats):
-        v = self.stages.linear(item_feats[self.i0:self.i1].contiguous(), self.item_proj.weight, self.item_proj.bias)
-        parts = [self.user_emb_local, v]
-        if self.pad:
-            parts.append(torch.zeros(self.pad, v.size(1), dtype=v.dtype, device=v.device))
+        """The rank's block: per segment, its users (user_emb rows) then its items
+        (item_proj of the feature rows), padded to the segment's row count."""
+        nu = self.n_users
+        parts = []
+        for lo, hi, _, Rs in self.dg.owned():
+            n = 0
+            if min(hi, nu) > lo:
+                parts.append(self.user_emb_local[max(lo, 0) - self.u0:min(hi, nu) - self.u0])
+                n += min(hi, nu) - lo
+            a, b = max(lo, nu), hi
+            if b > a:
+                parts.append(self.stages.linear(item_feats[a - nu:b - nu].contiguous(), self.item_proj.weight,
+                                                self.item_proj.bias))
+                n += b - a
+            if Rs > n:
+                parts.append(torch.zeros(Rs - n, self.user_emb_local.size(1), dtype=self.user_emb_local.dtype,
+                                         device=self.user_emb_local.device))
+        if self.u1 == self.u0:  # no users here: keep user_emb_local in the graph (a defined, empty grad)
+            parts.insert(0, self.user_emb_local[:0])
         return torch.cat(parts, 0)
 
     def forward(self, item_feats):
@@ -301,9 +350,12 @@ class ShardedPyGGAT(torch.nn.Module):
 
     def allreduce_grads(self):
         """One flat all-reduce of every dense parameter gradient (replicated params)."""
-        ps = [p for p in self.dense_parameters() if p.grad is not None]
-        if not ps or self.comm.world == 1:
+        if self.comm.world == 1:
             return
+        ps = self.dense_parameters()
+        for p in ps:  # a rank whose block has no items never touched item_proj: its share is 0
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
         flat = torch.cat([p.grad.reshape(-1) for p in ps])
         self.comm.all_reduce_(flat)
         off = 0
@@ -321,8 +373,7 @@ class ShardedPyGGAT(torch.nn.Module):
         allb = self.comm.all_gather_rows(blk)
         rows = []
         for r in range(self.dg.world):
-            lo, hi = int(self.dg.bounds[r]), int(self.dg.bounds[r + 1])
-            u0, u1 = min(lo, self.n_users), min(hi, self.n_users)
+            u0, u1 = self.dg.owned_users(self.n_users, r)
             rows.append(allb[r * self.dg.R: r * self.dg.R + (u1 - u0)])
         sd = {"user_emb.weight": torch.cat(rows, 0)}
         for k, v in self.state_dict().items():
@@ -331,14 +382,39 @@ class ShardedPyGGAT(torch.nn.Module):
         return sd
 
 
+def _item_loss_map(dg: DistGraph, n_users: int) -> torch.Tensor:
+    """Node id -> row of [own block's user rows ; all_gather of every rank's item slice]:
+    own users -> their block row, other users -> -1 (triple skipped), items -> gathered row."""
+    if dg.loss_map is None:
+        (ub, ib), (RU, RI) = dg.seg_bounds, dg.seg_R
+        N = dg.n_nodes
+        m = np.full(N, -1, np.int64)
+        u0, u1 = int(ub[dg.rank]), int(ub[dg.rank + 1])
+        m[u0:u1] = np.arange(u1 - u0)
+        owner = np.repeat(np.arange(dg.world), np.diff(ib))
+        m[n_users:] = RU + owner * RI + (np.arange(n_users, N) - ib[owner])
+        dg.loss_map = torch.from_numpy(m).to(torch.int32).to(dg.row_map.device)
+    return dg.loss_map
+
+
 def sharded_bpr_loss(Z_local, dg: DistGraph, comm: Comm, u, i, j, n_users: int, n_items: int, loss: str = "bpr",
                      stages=None):
-    """This rank's contiguous share of the S triples over the all-gathered Z; the returned
-    value is weighted so that the sum over ranks is the reference's mean loss."""
+    """The BPR/BCE loss of train_gat_pyg.py:313-322 over row-sharded Z; the ranks' returned
+    values add up to the reference's mean loss.
+
+    (users, items) segments: every rank evaluates the triples of its own users against
+    the all-gathered item rows (n_items x C), item gradients return by reduce_scatter.
+    Otherwise: all_gather of Z and a contiguous share of the triples."""
     if stages is None:
         from .hip_ops import HipStages
         stages = HipStages()
     S = int(u.numel())
+    segs = dg.seg_bounds
+    if len(segs) == 2 and int(segs[0][0]) == 0 and int(segs[0][-1]) == n_users:
+        RU, RI = dg.seg_R
+        I_full = all_gather_rows(Z_local[RU:RU + RI], comm)
+        Zl = torch.cat([Z_local[:RU], I_full], 0)
+        return stages.bpr(Zl, n_users, n_items, _item_loss_map(dg, n_users), u, i, j, loss)
     a, b = S * comm.rank // comm.world, S * (comm.rank + 1) // comm.world
     Z_full = all_gather_rows(Z_local, comm)
     part = stages.bpr(Z_full, n_users, n_items, dg.row_map, u[a:b], i[a:b], j[a:b], loss)

@@ -46,9 +46,16 @@ class CpuStages:
         return torch.nn.functional.linear(x, W, b)
 
     def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss):
+        """Triples whose user maps to -1 are not held by this rank: they contribute 0 and
+        the mean stays over all S triples (include/ppgat.h ppgat_bpr_fwd)."""
         rm = row_map.long()
-        Zn = Z.index_select(0, rm)          # node-id order
-        return O.bpr_loss(Zn, n_users, u, i, j, loss)
+        held = torch.nonzero(rm >= 0).squeeze(1)
+        Zn = Z.new_zeros(rm.numel(), Z.size(1)).index_copy(0, held, Z.index_select(0, rm[held]))  # node-id order
+        keep = rm[u.long()] >= 0
+        S = u.numel()
+        if int(keep.sum()) == 0:
+            return Z.sum() * 0
+        return O.bpr_loss(Zn, n_users, u[keep], i[keep], j[keep], loss) * (float(keep.sum()) / S)
 
     def scores(self, h, a_s, a_d, H, C):
         hv = h.view(-1, H, C)

@@ -41,7 +41,7 @@ def _setup(n_users=300, n_items=120, n_int=3000, heads=1, C=32):
     return pkg, g, ei, feats, full, [torch.from_numpy(a) for a in (u, i, j)]
 
 
-def _worker(rank, world, port, out_dir, heads):
+def _worker(rank, world, port, out_dir, heads, segmented):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -52,7 +52,9 @@ def _worker(rank, world, port, out_dir, heads):
     pkg, g, ei, feats, full, (u, i, j) = _setup(heads=heads)
     dmod = pkg.dist
     comm = dmod.Comm()
-    dg = dmod.build_dist_graph(ei, g.n_nodes, world, rank, csr_builder=csr_builder, sched_builder=None)
+    segs = [(0, g.n_users), (g.n_users, g.n_nodes)] if segmented else None
+    dg = dmod.build_dist_graph(ei, g.n_nodes, world, rank, csr_builder=csr_builder, sched_builder=None,
+                               segments=segs)
     st = CpuStages()
     model = dmod.ShardedPyGGAT(full, dg, comm, stages=st).train()
     torch.manual_seed(123)
@@ -96,10 +98,12 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("world,heads", [(2, 1), (3, 2)])
-def test_sharded_matches_unsharded(tmp_path, world, heads):
+@pytest.mark.parametrize("world,heads,segmented", [(2, 1, False), (3, 2, False), (2, 1, True), (3, 2, True)])
+def test_sharded_matches_unsharded(tmp_path, world, heads, segmented):
+    """segmented: users and items partitioned separately (every rank holds both), the loss
+    over the rank's own users with only the item rows gathered."""
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path), heads), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), heads, segmented), nprocs=world, join=True,
                        start_method="spawn")
     res = torch.load(tmp_path / "res.pt", weights_only=False)
     Zr, lr, gr, full = _reference(heads)

@@ -39,12 +39,13 @@ def _setup(dev, heads=1):
     return pkg, g, ei, feats, full, [torch.from_numpy(a).to(dev) for a in (u, i, j)]
 
 
-def _sharded(rank, world, out_dir, heads):
+def _sharded(rank, world, out_dir, heads, segmented=True):
     dev = torch.device("cuda", 0)
     pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads)
     D = pkg.dist
     comm = D.Comm()
-    dg = D.build_dist_graph(ei, g.n_nodes, world, rank)
+    segs = [(0, g.n_users), (g.n_users, g.n_nodes)] if segmented else None
+    dg = D.build_dist_graph(ei, g.n_nodes, world, rank, segments=segs)
     model = D.ShardedPyGGAT(full, dg, comm).train()
     torch.manual_seed(123)
     Z = model(feats)
@@ -66,13 +67,13 @@ def _sharded(rank, world, out_dir, heads):
                    os.path.join(out_dir, f"sharded_{world}.pt"))
 
 
-def _worker(rank, world, port, out_dir, heads):
+def _worker(rank, world, port, out_dir, heads, segmented=True):
     sys.path.insert(0, str(ROOT))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _sharded(rank, world, out_dir, heads)
+        _sharded(rank, world, out_dir, heads, segmented)
     finally:
         dist.destroy_process_group()
 
@@ -102,18 +103,20 @@ def _check(res, ref):
         assert _rel(v, grads[k]) <= (1e-5 if v.dim() == 2 and "att" not in k else 1e-4), k
 
 
-@pytest.mark.parametrize("heads", [1, 2])
-def test_sharded_world1_rccl(cuda, tmp_path, heads):
+@pytest.mark.parametrize("heads,segmented", [(1, True), (2, False)])
+def test_sharded_world1_rccl(cuda, tmp_path, heads, segmented):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
     try:
-        _sharded(0, 1, str(tmp_path), heads)
+        _sharded(0, 1, str(tmp_path), heads, segmented)
     finally:
         dist.destroy_process_group()
     _check(torch.load(tmp_path / "sharded_1.pt", weights_only=False), _unsharded(cuda, heads))
 
 
-def test_sharded_world2_shared_gpu(cuda, tmp_path):
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), 1), nprocs=2, join=True, start_method="spawn")
+@pytest.mark.parametrize("segmented", [True, False])
+def test_sharded_world2_shared_gpu(cuda, tmp_path, segmented):
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), 1, segmented), nprocs=2, join=True,
+                       start_method="spawn")
     _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), _unsharded(cuda, 1))

@@ -16,7 +16,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"k_fwd<": "fwd", "k_bwd_src<": "bwd_src", "k_bwd_epi<": "bwd_epi", "k_bwd_pro<": "bwd_pro",
-           "k_scores<": "scores", "k_gemm_tn": "gemm_tn", "k_bpr_chunks<": "bpr_chunks", "k_bpr_fwd<": "bpr_fwd"}
+           "k_scores<": "scores", "k_gemm_tn": "gemm_tn", "k_bpr_chunks<": "bpr_chunks", "k_bpr_fwd<": "bpr_fwd",
+           "k_proj<0>": "proj_fwd", "k_proj<1>": "proj_dx", "k_tn128<": "tn128", "k_adam": "adam"}
 
 
 def load(d, counter):
@@ -35,11 +36,12 @@ def load(d, counter):
 
 def main():
     fd, wd, out = sys.argv[1:4]
+    config = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     fetch = load(fd, "FETCH_SIZE")
     write = load(wd, "WRITE_SIZE")
     res = {"note": "per-launch HBM-side bytes (L2 fabric requests, Infinity-Cache hits included); "
                    "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes",
-           "per_launch_bytes": {}, "raw_kib": {}}
+           "config": config, "per_launch_bytes": {}, "raw_kib": {}}
     for k in sorted(set(fetch) | set(write)):
         f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1)
         w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
