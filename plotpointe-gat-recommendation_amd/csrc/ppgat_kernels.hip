@@ -431,6 +431,161 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pass B for heads > 1: the same decomposition as k_bwd_src, but every head of an edge is
+// handled in one pass, so each grad_out row g_i (C floats, shared by the heads: the output
+// is the head mean) is gathered ONCE per edge instead of once per edge and head.  Per
+// chunk of 64 edges a lane builds the records of one edge for all heads; per group of
+// U x EPW edges the lane reduces U x H partial dots <g_i, h_j^hd> over its subgroup with a
+// transposing butterfly (mh_reduce).  Requires C >= 32.
+// ---------------------------------------------------------------------------
+// V per-lane values, each summed over the LPR lanes of a subgroup.  Transposing steps at
+// offsets LPR/2 .. 8 (while more than one value is left), then a DPP reduction over the
+// 8-lane octet for the R values left.  Returns R; v[t] (t < R) holds the sum of value
+// index base + t, base = sum over steps of (lane bit set ? half the values then : 0).
+template <int OFF, int N>
+__device__ __forceinline__ int mh_transpose(float (&v)[16], int sl, int& base) {
+  if constexpr (OFF >= 8 && N > 1) {
+    constexpr int Hh = N / 2;
+    const bool bit = (sl & OFF) != 0;
+#pragma unroll
+    for (int t = 0; t < Hh; ++t) {
+      if constexpr (OFF >= 16) {
+        float r0, r1;
+        row_swap<OFF>(v[t], v[Hh + t], r0, r1);
+        v[t] = r0 + r1;
+      } else {
+        const float send = bit ? v[t] : v[Hh + t];
+        const float keep = bit ? v[Hh + t] : v[t];
+        v[t] = keep + dpp<0x128>(send);
+      }
+    }
+    if (bit) base += Hh;
+    return mh_transpose<OFF / 2, Hh>(v, sl, base);
+  } else {
+#pragma unroll
+    for (int t = 0; t < N; ++t) v[t] = group_reduce<Op::Sum, 1, 4>(v[t]);
+    return N;
+  }
+}
+
+template <int C, int H>
+__global__ void __launch_bounds__(256) k_bwd_src_mh(Items it, const int32_t* __restrict__ row,
+                                                    const int32_t* __restrict__ csc_eid,
+                                                    const int32_t* __restrict__ csc2csr,
+                                                    const float* __restrict__ h, const float* __restrict__ s_src,
+                                                    const float4* __restrict__ nstate,
+                                                    const float* __restrict__ grad_out, int mode, float slope,
+                                                    float gscale, float p, float inv_keep, uint64_t seed,
+                                                    float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
+                                                    int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
+  using G = Geo<C>;
+  static_assert(C >= 32, "k_bwd_src_mh: C >= 32");
+  constexpr int U = G::U * H > 16 ? (16 / H > 0 ? 16 / H : 1) : G::U;  // <= 16 partial dots per lane
+  constexpr int V = U * H;
+  static_assert(V <= 16, "values per lane");
+  static_assert(64 % (G::EPW * U) == 0, "chunk tiling");
+  __shared__ int2 recA[4][64];       // {dst row, CSR slot}
+  __shared__ float4 recH[4][H][64];  // per head {beta * gscale, c1, c0, -}
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (w >= it.n_items) return;
+  const int sg = lane / G::LPR, sl = lane % G::LPR;
+  const int64_t j = it.row[w];
+  const int cs = it.beg[w], ce = it.end[w];
+  const bool hub = w < it.n_hub_items;
+  float ss[H];
+  float4 hv[H], acc[H];
+  float dsa[H];
+#pragma unroll
+  for (int hd = 0; hd < H; ++hd) {
+    ss[hd] = s_src[j * H + hd];
+    hv[hd] = ld4(h + (j * H + hd) * C + sl * 4);
+    acc[hd] = f4(0.f);
+    dsa[hd] = 0.f;
+  }
+  for (int base = cs; base < ce; base += 64) {
+    const int k = base + lane;
+    const bool valid = k < ce;
+    const int i = valid ? row[k] : 0;
+    const int slot = valid ? csc2csr[k] : 0;
+    const uint32_t eid = (valid && p > 0.f) ? (uint32_t)csc_eid[k] : 0u;
+#pragma unroll
+    for (int hd = 0; hd < H; ++hd) {
+      float bg = 0.f, c1 = 0.f, c0 = 0.f;
+      if (valid) {
+        const float4 st = nstate[(int64_t)i * H + hd];  // {s_dst, m, inv_l, D}
+        const float z = ss[hd] + st.x;
+        const float e = logit(z, slope, mode);
+        const float af = expf(e - st.y) * st.z;
+        const float dm = p > 0.f ? drop_scale(seed, eid, (uint32_t)hd, p, inv_keep) : 1.f;
+        bg = af * dm * gscale;
+        const float a1 = af * dlogit(z, slope, mode);
+        c1 = a1 * dm * gscale;
+        c0 = a1 * st.w;
+      }
+      recH[wv][hd][lane] = make_float4(bg, c1, c0, 0.f);
+    }
+    recA[wv][lane] = make_int2(i, slot);
+    wave_sync();
+    const int n = min(64, ce - base);
+    for (int q0 = 0; q0 < n; q0 += G::EPW * U) {
+      float4 g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u * G::EPW + sg;
+        g[u] = q < n ? ld4(grad_out + (int64_t)recA[wv][q].x * C + sl * 4) : f4(0.f);
+      }
+      float part[16];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u * G::EPW + sg;
+#pragma unroll
+        for (int hd = 0; hd < H; ++hd) {
+          acc[hd] = fma4(recH[wv][hd][q].x, g[u], acc[hd]);
+          part[u * H + hd] = dot4(g[u], hv[hd]);
+        }
+      }
+#pragma unroll
+      for (int t = V; t < 16; ++t) part[t] = 0.f;
+      int vbase = 0;
+      const int R = mh_transpose<G::LPR / 2, V>(part, sl, vbase);
+      const int t = sl & 7;
+      if (t < R) {
+        float dot = part[0];
+#pragma unroll
+        for (int x = 1; x < 8; ++x)
+          if (x == t) dot = part[x];
+        const int vi = vbase + t;
+        const int u = vi / H, hd = vi % H;
+        const int q = q0 + u * G::EPW + sg;
+        if (q < n) {
+          const float4 rb = recH[wv][hd][q];
+          const float dzv = fmaf(rb.y, dot, -rb.z);
+#pragma unroll
+          for (int x = 0; x < H; ++x)
+            if (x == hd) dsa[x] += dzv;
+          dz[(int64_t)recA[wv][q].y * H + hd] = dzv;
+        }
+      }
+    }
+    wave_sync();
+  }
+#pragma unroll
+  for (int hd = 0; hd < H; ++hd) {
+    const float4 a = across_subgroups<G::LPR>(acc[hd]);
+    const float ds = wave_sum(dsa[hd]);
+    if (hub) {
+      float* sp = partial + (w * H + hd) * (C + 4);
+      if (sg == 0) st4(sp + sl * 4, a);
+      if (lane == 0) sp[C] = ds;
+    } else {
+      if (sg == 0) st4(dh + j * ld_dh + hd * C + sl * 4, a);
+      if (lane == 0) ds_src[j * ld_ds + hd] = ds;
+    }
+  }
+}
+
 template <int C>
 __global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ hub_row,
                                                    const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
@@ -678,10 +833,22 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const Items its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   if (it.n_items > 0) {
-    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its,
-                                           row, csc_eid, csc2csr, heads, h, ss,
-                                           reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, p,
-                                           inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial));
+    const bool mh = heads > 1 && C >= 32 && (heads == 2 || heads == 4 || heads == 8);
+    if (mh) {  // every head of an edge in one pass (one grad_out gather per edge)
+#define PPGAT_MH(HH)                                                                                           \
+  PPGAT_DISPATCH_C(C, if constexpr (CC >= 32) {                                                             \
+    hipLaunchKernelGGL((k_bwd_src_mh<CC, HH>), dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its, row,   \
+                       csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, \
+                       p, inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial);                             \
+  })
+      if (heads == 2) { PPGAT_MH(2); } else if (heads == 4) { PPGAT_MH(4); } else { PPGAT_MH(8); }
+#undef PPGAT_MH
+    } else {
+      PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its,
+                                             row, csc_eid, csc2csr, heads, h, ss,
+                                             reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, p,
+                                             inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial));
+    }
   }
   if (n_hubs > 0) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,

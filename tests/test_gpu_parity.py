@@ -158,6 +158,8 @@ def _pyg_case(pkg, oracle, cuda, n, e, cin, C, heads, kind, p, seed, training):
     (2000, 20_000, 64, 64, 2, "uniform"),
     (1500, 15_000, 64, 256, 4, "skewed"),
     (800, 6000, 32, 32, 8, "uniform"),
+    (1200, 12_000, 64, 128, 8, "skewed"),
+    (1000, 9000, 32, 64, 4, "skewed"),
     (300, 2000, 4, 4, 1, "uniform"),
 ])
 def test_pyg_gatconv_vs_oracle_eval(pkg, oracle, cuda, n, e, cin, C, heads, kind):
