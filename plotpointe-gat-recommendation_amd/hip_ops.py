@@ -484,6 +484,13 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     _require(A.size(0) == nb, "gemm_tn: A [N,M], B [N,K]")
     N, M, K = A.size(0), A.size(1), B.size(1)
     nv = 0 if V is None else V.size(1)
+    if B_items is None and M * K > 128 * 128 and N >= 65536:
+        # beyond one 128 x 128 tile (config 5: 1024 x 256 over 1.9M rows) the library GEMM
+        # (hipBLASLt, ~130 TF at these shapes) beats the split-N kernel; still one pass each
+        out = torch.mm(A.t(), B)
+        cs = A.sum(0) if want_colsum else None
+        vout = torch.mm(V.t(), B) if nv else None
+        return out, cs, vout
     if V is not None:
         _require(V.is_cuda and V.dtype == torch.float32 and V.dim() == 2 and V.stride(1) == 1 and V.size(0) == N,
                  "gemm_tn: V must be fp32 [N, nv] with unit column stride")

@@ -157,3 +157,20 @@ def test_fused_layer_equals_unfused(pkg, cuda):
     assert rel(out_a, out_b) <= 1e-5
     for a, b in zip(ga, gb):
         assert rel(a, b) <= 1e-4
+
+
+def test_gemm_tn_large_shape_deterministic(pkg, cuda):
+    """Beyond one 128 x 128 tile gemm_tn goes through the library GEMM: fp32-accurate and
+    bitwise reproducible run to run (config 5's 1024 x 256 weight gradient, scaled down)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(21)
+    N = 100_000
+    A = torch.randn(N, 1032, generator=g, dtype=torch.float64)
+    B = torch.randn(N, 256, generator=g, dtype=torch.float64)
+    Ad, Bd = A.float().to(cuda), B.float().to(cuda)
+    out, cs, vo = ops.gemm_tn(Ad[:, :1024], Bd, want_colsum=True, V=Ad[:, 1024:1032])
+    assert rel(out, A[:, :1024].t() @ B) <= 1e-5
+    assert rel(cs, A[:, :1024].sum(0)) <= 1e-5
+    assert rel(vo, A[:, 1024:1032].t() @ B) <= 1e-5
+    out2, cs2, vo2 = ops.gemm_tn(Ad[:, :1024], Bd, want_colsum=True, V=Ad[:, 1024:1032])
+    assert torch.equal(out, out2) and torch.equal(cs, cs2) and torch.equal(vo, vo2)
