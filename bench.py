@@ -198,6 +198,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    t_host = time.perf_counter() - t0  # host time to enqueue the K steps (launch overhead check)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -244,6 +245,7 @@ def main():
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": el / K * 1e3,
+        "host_enqueue_ms_per_step": t_host / K * 1e3,
         "higher_is_better": True,
         "scaling": "weak" if (world == 1 or args.config == 5) else "strong",
         "vs_baseline": None,

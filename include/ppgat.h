@@ -237,12 +237,14 @@ int ppgat_project_supported(int k, int out_cols);
 int ppgat_project(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int k,
                   const float* w, int64_t ldw, int out_cols, const float* bias, const float* att_src,
                   const float* att_dst, float* y, int64_t ldy, float* s_src, float* s_dst, void* stream);
-/* Input gradient of the layer (heads = 1), with D = [dh_msg | ds_src | ds_dst] from
- * ppgat_bwd_edges + ppgat_bwd_dst_sum ([n, ldd], ds_src at column k, ds_dst at k + 1):
- *   dx = D[:, :k] W + ds_src (x) (att_src W) + ds_dst (x) (att_dst W)
+/* Input gradient of the layer (heads = 1), from the message gradient D [n, k] (ldd) and the
+ * node logit gradients S [n, 2] = {ds_src, ds_dst} (lds) of ppgat_bwd_edges +
+ * ppgat_bwd_dst_sum:
+ *   dx = D W + ds_src (x) (att_src W) + ds_dst (x) (att_dst W)
  * W [k, out_cols] row-major = lin.weight; k <= 128, out_cols == 128. */
 int ppgat_project_bwd_input(const float* D, int64_t ldd, int64_t n, int k, const float* w, int64_t ldw, int out_cols,
-                            const float* att_src, const float* att_dst, float* dx, int64_t lddx, void* stream);
+                            const float* att_src, const float* att_dst, const float* S, int64_t lds, float* dx,
+                            int64_t lddx, void* stream);
 /* Weight and attention-vector gradients from G = dh_msg^T x [H*C, K] and
  * GV = [ds_src^T x ; ds_dst^T x] [2H, K] (ppgat_gemm_tn with V):
  *   dW = G + att_src (x) GV[:H] + att_dst (x) GV[H:],  datt_src[h] = W_h GV[h],  datt_dst[h] = W_h GV[H + h]. */

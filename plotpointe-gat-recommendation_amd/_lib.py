@@ -67,7 +67,8 @@ SIGNATURES = {
     "ppgat_project_supported": (c_int, [c_int, c_int]),
     "ppgat_project": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_vp, c_vp,
                               c_vp, c_i64, c_vp, c_vp, c_vp]),
-    "ppgat_project_bwd_input": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "ppgat_project_bwd_input": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                        c_i64, c_vp]),
     "ppgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_adam_max_tensors": (c_int, []),
     "ppgat_adam_step": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,

@@ -493,16 +493,17 @@ int ppgat_project(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1, 
 }
 
 int ppgat_project_bwd_input(const float* D, int64_t ldd, int64_t n, int k, const float* w, int64_t ldw, int out_cols,
-                            const float* att_src, const float* att_dst, float* dx, int64_t lddx, void* stream) {
+                            const float* att_src, const float* att_dst, const float* S, int64_t lds, float* dx,
+                            int64_t lddx, void* stream) {
   if (!ppgat::proj_shape_ok(k, out_cols)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_input: needs k <= 128, k % 4 == 0, out_cols == 128");
   if (n < 0) return fail(PPGAT_ERR_INVALID, "project_bwd_input: bad sizes");
-  if (ldd < k + 2 || (ldd % 2) || (ldd % 4) || ldw < out_cols || lddx < out_cols)
-    return fail(PPGAT_ERR_INVALID, "project_bwd_input: bad leading dimension (ldd >= k + 2, multiple of 4)");
-  if (n > 0 && (!D || !w || !att_src || !att_dst || !dx)) return fail(PPGAT_ERR_INVALID, "project_bwd_input: null pointer");
-  if (!al16(D)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_input: rows must be 16-byte aligned");
+  if (ldd < k || (ldd % 4) || ldw < out_cols || lddx < out_cols || lds < 2 || (lds % 2))
+    return fail(PPGAT_ERR_INVALID, "project_bwd_input: bad leading dimension (ldd >= k and % 4, lds >= 2 and even)");
+  if (n > 0 && (!D || !w || !att_src || !att_dst || !S || !dx)) return fail(PPGAT_ERR_INVALID, "project_bwd_input: null pointer");
+  if (!al16(D) || (reinterpret_cast<uintptr_t>(S) % 8)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_input: D rows 16-byte, S rows 8-byte aligned");
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_PROJ, st);
-  hipError_t e = ppgat::proj_dx(D, ldd, n, k, w, ldw, att_src, att_dst, dx, lddx, st);
+  hipError_t e = ppgat::proj_dx(D, ldd, n, k, w, ldw, att_src, att_dst, S, lds, dx, lddx, st);
   if (e != hipSuccess) return hip_fail(e, "project_bwd_input");
   return PPGAT_OK;
 }

@@ -7,7 +7,7 @@
 //    terms s_src = h.att_src, s_dst = h.att_dst (PyG alpha_src/alpha_dst; custom :79) in the
 //    epilogue, so h is never re-read for them.  x may come from two row segments (users from
 //    user_emb, items from the item projection: train_gat_pyg.py:79-82) -- no concatenation.
-//  * k_proj<1>: dx = D[:, :HC] W + ds_src (x) A_src + ds_dst (x) A_dst (heads = 1), the input
+//  * k_proj<1>: dx = D W + ds_src (x) A_src + ds_dst (x) A_dst (heads = 1), the input
 //    gradient of the layer with the attention-logit terms folded in as a rank-2 epilogue
 //    (A = att W, computed per workgroup from W in LDS).
 //  * k_tn128: out = A^T B for A [N, M<=128], B [N, K<=128] (dW of every projection), one
@@ -714,11 +714,11 @@ hipError_t proj_fwd(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1
 }
 
 hipError_t proj_dx(const float* D, int64_t ldd, int64_t n, int K, const float* W, int64_t ldw, const float* att_src,
-                   const float* att_dst, float* y, int64_t ldy, hipStream_t st) {
+                   const float* att_dst, const float* S, int64_t lds, float* y, int64_t ldy, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   ProjArg a{};
   a.x0 = D; a.ldx0 = ldd; a.x1 = D; a.ldx1 = ldd; a.split = n; a.n = n; a.K = K; a.W = W; a.ldw = ldw;
-  a.att_src = att_src; a.att_dst = att_dst; a.ds = D + K; a.ldds = ldd; a.y = y; a.ldy = ldy;
+  a.att_src = att_src; a.att_dst = att_dst; a.ds = S; a.ldds = lds; a.y = y; a.ldy = ldy;
   hipLaunchKernelGGL(k_proj<1>, dim3(proj_grid(n)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -74,7 +74,7 @@ hipError_t proj_fwd(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1
                     const float* W, int64_t ldw, const float* bias, const float* att_src, const float* att_dst,
                     float* y, int64_t ldy, float* s_src, float* s_dst, hipStream_t st);
 hipError_t proj_dx(const float* D, int64_t ldd, int64_t n, int K, const float* W, int64_t ldw, const float* att_src,
-                   const float* att_dst, float* y, int64_t ldy, hipStream_t st);
+                   const float* att_dst, const float* S, int64_t lds, float* y, int64_t ldy, hipStream_t st);
 bool tn128_shape_ok(int M, int K, int nv, const float* V, int64_t ldv);
 size_t tn128_workspace_bytes(int64_t N);
 hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const float* B1, int64_t ldb1, int64_t split,

@@ -286,9 +286,10 @@ def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope
     return GATAggregate.apply(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
 
 
-def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, ld, heads, channels, mode, slope, p, seed):
-    """Pass B into D[:, :HC] (dh_msg) and D[:, HC:HC+H] (ds_src); the destination sum into
-    D[:, HC+H:HC+2H] (ds_dst).  D is [N, ld] (ld = HC + pad, pad >= 2H, ld % 4 == 0)."""
+def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channels, mode, slope, p, seed):
+    """Pass B into D [N, HC] (dh_msg) and S[:, :H] (ds_src); the destination sum into
+    S[:, H:2H] (ds_dst).  S [N, 2H] is compact (its scattered per-node writes stay in L2)
+    and D keeps whole 512-B rows for the GEMMs that read it."""
     lib = _lib.load()
     dev = h.device
     N, E, HC = g.n_nodes, g.n_edges, heads * channels
@@ -300,15 +301,15 @@ def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, ld, heads, channe
     dz = torch.empty(max(E, 1) * heads, dtype=torch.float32, device=dev)
     cs = sched.cstruct()
     st = _lib.stream_handle(dev)
-    base = D.data_ptr()
     _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(g.row) if E else None,
                                    _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, E, heads,
                                    channels, h.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), grad_out.data_ptr(),
-                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), base, ld, base + 4 * HC, ld,
-                                   dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "bwd_edges")
+                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), D.data_ptr(), HC,
+                                   S.data_ptr(), 2 * heads, dz.data_ptr(), ws.data_ptr(), nbytes.value, st),
+               "bwd_edges")
     fs = g.fwd_sched.cstruct()
     dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), N, heads, dz.data_ptr(), base + 4 * (HC + heads), ld,
+    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), N, heads, dz.data_ptr(), S.data_ptr() + 4 * heads, 2 * heads,
                                      dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
@@ -364,10 +365,11 @@ class GATLayer(torch.autograd.Function):
     """One whole GAT layer x -> out with the projection inside:
     forward  h = x W^T with the node scores fused (ppgat_project; BLAS + ppgat_node_scores
              outside the fused shapes), then the fused softmax-aggregate;
-    backward prologue, pass B and the destination sum write D = [dh_msg | ds_src | ds_dst]
-             side by side; dx = D W_aug (ppgat_project_bwd_input: the attention terms as a
-             rank-2 epilogue; BLAS with W_aug outside the fused shapes), D^T x
-             (ppgat_gemm_tn with V) and ppgat_weight_grads give dW and datt.
+    backward prologue, pass B and the destination sum write D = dh_msg [N, HC] and the
+             compact S = [ds_src | ds_dst] [N, 2H]; dx = D W + S [A_src; A_dst]
+             (ppgat_project_bwd_input: the attention terms as a rank-2 epilogue; BLAS outside
+             the fused shapes), D^T x and S^T x (ppgat_gemm_tn with V) and
+             ppgat_weight_grads give dW and datt.
     ``x_items`` (optional): the input rows [x.size(0), N) as a second tensor, so the model's
     node features cat(user_emb, item_proj(feats)) are never concatenated."""
 
@@ -417,7 +419,6 @@ class GATLayer(torch.autograd.Function):
         N = g.n_nodes
         K = x.size(1)
         HC = heads * C
-        ld = HC + ((2 * heads + 3) // 4) * 4
         # prologue: packed per-node state (+ dbias)
         want_db = has_bias and ctx.needs_input_grad[4]
         nstate = torch.empty(N, heads, 4, dtype=torch.float32, device=dev)
@@ -428,23 +429,24 @@ class GATLayer(torch.autograd.Function):
                                           _lib.ptr(b) if has_bias else None, s_dst.data_ptr(), m.data_ptr(),
                                           inv_l.data_ptr(), N, heads, C, mode, nstate.data_ptr(), _lib.ptr(dbias),
                                           _lib.ptr(part), _lib.stream_handle(dev)), "bwd_prologue")
-        D = torch.empty(N, ld, dtype=torch.float32, device=dev)
-        _bwd_edges_dst(g, h, s_src, nstate, g_out, D, ld, heads, C, mode, slope, p, seed)
+        D = torch.empty(N, HC, dtype=torch.float32, device=dev)
+        S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
+        _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed)
         need_dx = ctx.needs_input_grad[0] or (had_items and ctx.needs_input_grad[12])
         dx = None
         if need_dx:
             if heads == 1 and project_supported(HC, K):  # reduction over HC, K output columns
                 dx = torch.empty(N, K, dtype=torch.float32, device=dev)
-                _lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), ld, N, HC, W.data_ptr(), K, K, a_s.data_ptr(),
-                                                       a_d.data_ptr(), dx.data_ptr(), K, _lib.stream_handle(dev)),
-                           "project_bwd_input")
+                _lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), HC, N, HC, W.data_ptr(), K, K, a_s.data_ptr(),
+                                                       a_d.data_ptr(), S.data_ptr(), 2, dx.data_ptr(), K,
+                                                       _lib.stream_handle(dev)), "project_bwd_input")
             else:
                 # W_aug = [W; A_src; A_dst],  A[hd] = sum_c att[hd, c] W[hd*C + c, :]
                 Wv = W.view(heads, C, K)
                 A_s = torch.einsum("hc,hck->hk", a_s, Wv)
                 A_d = torch.einsum("hc,hck->hk", a_d, Wv)
-                dx = D[:, :HC + 2 * heads] @ torch.cat([W, A_s, A_d], 0)
-        G, _, GV = gemm_tn(D[:, :HC], x, V=D[:, HC:HC + 2 * heads], B_items=xi if seg else None)
+                dx = torch.addmm(S @ torch.cat([A_s, A_d], 0), D, W)
+        G, _, GV = gemm_tn(D, x, V=S, B_items=xi if seg else None)
         dW, datt_src, datt_dst = weight_grads(G, GV, W, a_s, a_d, heads, C)
         dx_u = dx[:split] if (dx is not None and had_items) else dx
         dx_i = dx[split:] if (dx is not None and had_items) else None

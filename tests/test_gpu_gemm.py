@@ -56,17 +56,18 @@ def test_project_bias(pkg, cuda):
 def test_project_bwd_input_vs_fp64(pkg, cuda, N):
     lib = pkg._lib.load()
     g = torch.Generator().manual_seed(N)
-    HC, K, ld = 128, 128, 132
-    D = torch.randn(N, ld, generator=g, dtype=torch.float64)
+    HC, K = 128, 128
+    D = torch.randn(N, HC, generator=g, dtype=torch.float64)
+    S = torch.randn(N, 2, generator=g, dtype=torch.float64)
     W = torch.randn(HC, K, generator=g, dtype=torch.float64) / 11
     a_s = torch.randn(HC, generator=g, dtype=torch.float64)
     a_d = torch.randn(HC, generator=g, dtype=torch.float64)
-    Dd, Wd, asd, add = (t.float().to(cuda).contiguous() for t in (D, W, a_s, a_d))
+    Dd, Sd, Wd, asd, add = (t.float().to(cuda).contiguous() for t in (D, S, W, a_s, a_d))
     dx = torch.empty(N, K, device=cuda)
-    pkg._lib.check(lib.ppgat_project_bwd_input(Dd.data_ptr(), ld, N, HC, Wd.data_ptr(), K, K, asd.data_ptr(),
-                                               add.data_ptr(), dx.data_ptr(), K,
+    pkg._lib.check(lib.ppgat_project_bwd_input(Dd.data_ptr(), HC, N, HC, Wd.data_ptr(), K, K, asd.data_ptr(),
+                                               add.data_ptr(), Sd.data_ptr(), 2, dx.data_ptr(), K,
                                                pkg._lib.stream_handle(cuda)), "project_bwd_input")
-    ref = D[:, :HC] @ W + D[:, HC:HC + 1] * (a_s @ W)[None] + D[:, HC + 1:HC + 2] * (a_d @ W)[None]
+    ref = D @ W + S[:, :1] * (a_s @ W)[None] + S[:, 1:2] * (a_d @ W)[None]
     assert rel(dx, ref) <= 1e-5
 
 

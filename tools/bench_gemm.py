@@ -43,19 +43,20 @@ def main():
     W = torch.randn(128, 128, device=dev, generator=g)
     a_s = torch.randn(128, device=dev, generator=g)
     a_d = torch.randn(128, device=dev, generator=g)
-    D = torch.randn(N, 132, device=dev, generator=g)
+    D = torch.randn(N, 128, device=dev, generator=g)
+    S = torch.randn(N, 2, device=dev, generator=g)
     dx = torch.empty(N, 128, device=dev)
     st = pkg._lib.stream_handle(dev)
     res = {}
     cases = {
         "proj_fwd_scores": lambda: ops.project(x, W, att_src=a_s, att_dst=a_d),
-        "proj_dx": lambda: pkg._lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), 132, N, 128, W.data_ptr(), 128, 128,
-                                                                      a_s.data_ptr(), a_d.data_ptr(), dx.data_ptr(),
-                                                                      128, st), "dx"),
-        "tn_dW_V": lambda: ops.gemm_tn(D[:, :128], x, V=D[:, 128:130]),
-        "tn_plain": lambda: ops.gemm_tn(D[:, :128], x),
+        "proj_dx": lambda: pkg._lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), 128, N, 128, W.data_ptr(), 128, 128,
+                                                                      a_s.data_ptr(), a_d.data_ptr(), S.data_ptr(), 2,
+                                                                      dx.data_ptr(), 128, st), "dx"),
+        "tn_dW_V": lambda: ops.gemm_tn(D, x, V=S),
+        "tn_plain": lambda: ops.gemm_tn(D, x),
         "blas_fwd": lambda: torch.nn.functional.linear(x, W),
-        "blas_dx": lambda: D[:, :130] @ torch.randn(130, 128, device=dev),
+        "blas_dx": lambda: D @ torch.randn(128, 128, device=dev),
     }
     for k, fn in cases.items():
         if args.only and k not in args.only.split(","):
