@@ -453,7 +453,9 @@ int ppgat_gemm_tn_seg(const float* A, int64_t lda, const float* b0, int64_t ldb0
     return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
   if (!workspace || workspace_bytes < tn_ws(n, m, k, nv))
     return fail(PPGAT_ERR_INVALID, "gemm_tn: workspace too small");
-  const bool fast = ppgat::tn128_shape_ok(m, k, nv, V, ldv);
+  // the register-accumulator kernel pays a fixed per-wave ramp/epilogue: below ~1e5 rows the
+  // LDS-staged split-N kernel is faster (item_proj's 63k rows: 30 vs 46 us)
+  const bool fast = ppgat::tn128_shape_ok(m, k, nv, V, ldv) && (n >= 100000 || (b1 && split < n));
   if (!fast && b1 && split < n) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: segmented B needs m, k <= 128, nv <= 2");
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_GEMM_TN, st);

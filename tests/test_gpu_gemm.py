@@ -74,7 +74,7 @@ def test_project_bwd_input_vs_fp64(pkg, cuda, N):
 def test_gemm_tn_segments(pkg, cuda):
     ops = _ops()
     g = torch.Generator().manual_seed(11)
-    N, split = 70_001, 50_000
+    N, split = 130_001, 100_000  # >= 1e5 rows: both calls take the register-accumulator kernel
     A = torch.randn(N, 132, generator=g, dtype=torch.float64)
     B = torch.randn(N, 128, generator=g, dtype=torch.float64)
     Ad, Bd = A.float().to(cuda), B.float().to(cuda)
