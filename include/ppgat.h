@@ -265,6 +265,18 @@ int ppgat_adam_step(int count, float* const* params, const float* const* grads, 
                     const float* bias_correction2_sqrt, double beta1, double beta2, float eps, float weight_decay,
                     void* stream);
 
+/* ---- I-I kNN graph (config 3's second relation) ------------------------------------
+ * Replaces: the per-item selection loop of graphs/build_ii_knn.py:76-99 (self excluded as
+ * -inf, argpartition top-k, sorted descending, kept where sim >= min_similarity).  S is a
+ * block of the cosine-similarity matrix: rows = query items q0 .. q0 + rows - 1, columns =
+ * all n_cols items (row stride ld floats).  Writes, per row, the k best (item, similarity)
+ * sorted by similarity descending with ties by smaller item index (out_idx / out_sim
+ * [rows, k]; -1 / -inf where fewer than k items exist) and out_cnt[row] = how many of them
+ * reach min_sim (a prefix).  k <= ppgat_knn_max_k().  Deterministic. */
+int ppgat_knn_max_k(void);
+int ppgat_knn_topk(const float* S, int64_t ld, int64_t rows, int64_t n_cols, int64_t q0, int k, float min_sim,
+                   int32_t* out_idx, float* out_sim, int32_t* out_cnt, void* stream);
+
 /* ---- sampled ranking (evaluation) ------------------------------------------------
  * Replaces: the per-user loop of eval_sampled, scripts/train_gat_pyg.py:160-175:
  *   scores = I[cands[b]] @ U[users[b]];  rank[b] = #(scores[1:] > scores[0]) + 1

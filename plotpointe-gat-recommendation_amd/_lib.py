@@ -73,6 +73,8 @@ SIGNATURES = {
     "ppgat_adam_max_tensors": (c_int, []),
     "ppgat_adam_step": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
                                 c_f, c_f, c_vp]),
+    "ppgat_knn_max_k": (c_int, []),
+    "ppgat_knn_topk": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),

@@ -546,6 +546,20 @@ int ppgat_adam_step(int count, float* const* params, const float* const* grads, 
   return PPGAT_OK;
 }
 
+int ppgat_knn_max_k(void) { return ppgat::knn_max_k(); }
+
+int ppgat_knn_topk(const float* S, int64_t ld, int64_t rows, int64_t n_cols, int64_t q0, int k, float min_sim,
+                   int32_t* out_idx, float* out_sim, int32_t* out_cnt, void* stream) {
+  if (k < 1 || k > ppgat::knn_max_k()) return fail(PPGAT_ERR_UNSUPPORTED, "knn_topk: k must be in [1, 64]");
+  if (rows < 0 || n_cols < 1 || ld < n_cols || q0 < 0) return fail(PPGAT_ERR_INVALID, "knn_topk: bad sizes");
+  if (n_cols > INT32_MAX) return fail(PPGAT_ERR_UNSUPPORTED, "knn_topk: item ids must fit int32");
+  if (rows > 0 && (!S || !out_idx || !out_sim || !out_cnt)) return fail(PPGAT_ERR_INVALID, "knn_topk: null pointer");
+  hipError_t e = ppgat::knn_topk(S, ld, rows, n_cols, q0, k, min_sim, out_idx, out_sim, out_cnt,
+                                 static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "knn_topk");
+  return PPGAT_OK;
+}
+
 int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
                        int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
                        int32_t* rank, void* stream) {

@@ -55,28 +55,6 @@ __device__ __forceinline__ int acc_row(int q, int hf) { return (q & 3) + 8 * (q 
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-// 16 per-lane partial values, each to be summed over the 32 lanes of its half-wave.  On
-// return v[t] (t < 4) holds the full sum of value index ((l >> 4) & 1) * 8 + ((l >> 3) & 1) * 4 + t,
-// the same on all 8 lanes of the lane's octet (transposing butterfly: 8 + 4 exchanges,
-// then 3 DPP steps per value; see ppgat_lanes.h).
-__device__ __forceinline__ void reduce16_over32(float (&v)[16], int lane) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    float r0, r1;
-    row_swap<16>(v[t], v[8 + t], r0, r1);
-    v[t] = r0 + r1;
-  }
-  const bool b8 = (lane & 8) != 0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const float send = b8 ? v[t] : v[4 + t];
-    const float keep = b8 ? v[4 + t] : v[t];
-    v[t] = keep + dpp<0x128>(send);
-  }
-#pragma unroll
-  for (int t = 0; t < 4; ++t) v[t] = group_reduce<Op::Sum, 1, 4>(v[t]);
-}
-
 // ---------------------------------------------------------------------------
 // projection GEMM with fused epilogues
 // ---------------------------------------------------------------------------

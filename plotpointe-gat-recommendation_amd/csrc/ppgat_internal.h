@@ -87,6 +87,11 @@ hipError_t adam_step(int count, float* const* p, const float* const* g, float* c
                      const int64_t* n, const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
                      float eps, float wd, hipStream_t st);
 
+// I-I kNN neighbour selection (ppgat_knn.hip)
+int knn_max_k();
+hipError_t knn_topk(const float* S, int64_t ld, int64_t rows, int64_t n_cols, int64_t q0, int k, float min_sim,
+                    int32_t* out_idx, float* out_sim, int32_t* out_cnt, hipStream_t st);
+
 // evaluation (ppgat_eval.hip)
 hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                         const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,

@@ -1,0 +1,45 @@
+"""I-I kNN graph on the GPU -- graphs/build_ii_knn.py (the second relation of config 3).
+
+``build_ii_knn(embeddings, k=20, min_similarity=0.3)`` returns the reference's COO triplet
+(rows = item, cols = neighbour, sims = cosine) in the reference's order (items ascending,
+neighbours by similarity descending), for ``scipy.sparse.coo_matrix((sims, (rows, cols)))``
+and ``save_npz`` exactly as build_ii_knn.py:104-116 writes it.
+
+Steps (build_ii_knn.py line refs): rows normalised as e / (||e|| + 1e-8) (:57-59) and again
+by sklearn's cosine_similarity (:76); per block of query rows the similarity block
+E_q E^T is one library GEMM (hipBLASLt, fp32); the selection -- self excluded, top-k,
+sorted, thresholded (:79-95) -- is libppgat's ``ppgat_knn_topk`` kernel.  The full n x n
+matrix is never materialised (block_rows x n at a time).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def build_ii_knn(embeddings: torch.Tensor, k: int = 20, min_similarity: float = 0.3, block_rows: int = 8192):
+    lib = _lib.load()
+    if not (isinstance(embeddings, torch.Tensor) and embeddings.is_cuda and embeddings.dim() == 2):
+        raise RuntimeError("build_ii_knn: embeddings must be a 2-D ROCm tensor (there is no CPU path)")
+    if k < 1 or k > int(lib.ppgat_knn_max_k()):
+        raise NotImplementedError(f"build_ii_knn: k={k} outside [1, {int(lib.ppgat_knn_max_k())}]")
+    e = embeddings.to(torch.float32).contiguous()
+    n = e.size(0)
+    dev = e.device
+    en = e / (torch.linalg.vector_norm(e, dim=1, keepdim=True) + 1e-8)
+    n2 = torch.linalg.vector_norm(en, dim=1, keepdim=True)
+    ex = en / torch.where(n2 == 0, torch.ones_like(n2), n2)  # sklearn.preprocessing.normalize
+    idx = torch.empty(n, k, dtype=torch.int32, device=dev)
+    sim = torch.empty(n, k, dtype=torch.float32, device=dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    st = _lib.stream_handle(dev)
+    for q0 in range(0, n, block_rows):
+        q1 = min(q0 + block_rows, n)
+        S = ex[q0:q1] @ ex.t()
+        _lib.check(lib.ppgat_knn_topk(S.data_ptr(), n, q1 - q0, n, q0, k, float(min_similarity),
+                                      idx[q0:].data_ptr(), sim[q0:].data_ptr(), cnt[q0:].data_ptr(), st),
+                   "knn_topk")
+    keep = torch.arange(k, device=dev)[None, :] < cnt[:, None].to(torch.int64)
+    rows = torch.arange(n, device=dev, dtype=torch.int32)[:, None].expand(n, k)[keep]
+    return rows, idx[keep], sim[keep]

@@ -13,6 +13,8 @@ reference's outputs), written as .npz / .json next to this script:
 
   layer_<name>.npz   SimpleGATLayer (train_gat_custom.py:63-93) forward in eval mode and
                      the gradients of sum(out * G) for a fixed upstream G.
+  knn_small.npz      graphs/build_ii_knn.py main() (k=20, min_sim 0.3) on clustered
+                     synthetic embeddings, GCS replaced by local files.
   plumbing_cfg1.npz  config-1 synthetic interactions -> build_splits (:148-162),
                      build_edge_index (:166-175), sample_bpr_epoch (:213-224, seed 42),
                      CustomGAT (:96-115) init at seed 42, eval forward Z, one BPR+Adam
@@ -224,7 +226,78 @@ def fusion_case():
     print(f"fusion: loss={loss.item():.6f} keys={list(model.state_dict().keys())}")
 
 
+def knn_case():
+    """graphs/build_ii_knn.py main() on clustered synthetic embeddings, GCS replaced by local
+    files (download copies our .npy, uploads are no-ops); the reference's own output npz
+    (scipy COO: rows = item, cols = neighbour, data = cosine) becomes the fixture."""
+    import os
+    import shutil
+    import tempfile
+    from scipy.sparse import load_npz
+
+    rng = np.random.default_rng(11)
+    n, d, n_cl = 2000, 64, 40
+    centers = rng.standard_normal((n_cl, d)).astype(np.float32)
+    lab = rng.integers(0, n_cl, n)
+    emb = (centers[lab] + 0.9 * rng.standard_normal((n, d))).astype(np.float32)
+    noisy = rng.random(n) < 0.15  # weakly clustered rows: some of their top-20 fall below 0.3
+    emb[noisy] = (0.35 * centers[lab[noisy]] + rng.standard_normal((int(noisy.sum()), d))).astype(np.float32)
+    emb[7] = 0.0  # a zero row (norm 0): the reference's +1e-8 guard
+    _stub_gcs()
+    storage = sys.modules["google.cloud.storage"]
+
+    class _Blob:
+        def __init__(self, src):
+            self.src = src
+
+        def download_to_filename(self, path):
+            shutil.copy(self.src, path)
+
+        def upload_from_filename(self, path):
+            pass
+
+    class _Bucket:
+        def __init__(self, src):
+            self.src = src
+
+        def blob(self, name):
+            return _Blob(self.src)
+
+    work = Path(tempfile.mkdtemp())
+    np.save(work / "emb.npy", emb)
+
+    class _Client:
+        def __init__(self, *a, **k):
+            pass
+
+        def bucket(self, name):
+            return _Bucket(str(work / "emb.npy"))
+
+    old_client = storage.Client
+    storage.Client = _Client
+    spec = importlib.util.spec_from_file_location("ref_build_ii_knn", REF / "graphs" / "build_ii_knn.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    argv, cwd = sys.argv, os.getcwd()
+    try:
+        os.chdir(work)
+        sys.argv = ["build_ii_knn.py", "--project-id", "x", "--embeddings-path", "gs://b/emb.npy",
+                    "--output-prefix", "gs://b/out", "--output-name", "ii", "--k", "20", "--min-similarity", "0.3",
+                    "--batch-size", "300"]
+        mod.main()
+        m = load_npz(work / "tmp" / "ii.npz").tocoo()
+    finally:
+        sys.argv = argv
+        os.chdir(cwd)
+        storage.Client = old_client
+        shutil.rmtree(work, ignore_errors=True)
+    np.savez_compressed(HERE / "knn_small.npz", emb=emb, rows=m.row.astype(np.int32), cols=m.col.astype(np.int32),
+                        sims=m.data.astype(np.float32), k=20, min_sim=0.3)
+    print(f"knn: {m.nnz} edges over {n} items")
+
+
 def main():
+    knn_case()
     fusion_case()
     ref = load_reference_custom()
     layer_case(ref, "small_c8", 0, 300, 3000, 8, "uniform")
