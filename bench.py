@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the N>1 flow with "
+                         "several ranks on one GPU (tests/test_gpu_dist.py)")
     return ap.parse_args()
 
 
@@ -131,8 +134,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        local = local if args.dist_backend == "nccl" else 0  # gloo rehearsal: ranks share GPU 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -205,7 +212,8 @@ def main():
     el = time.perf_counter() - t0
     _lib.profile_enable(False)
     if world > 1:
-        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        tt = torch.tensor([el], dtype=torch.float64)
+        tt = tt.to(dev) if args.dist_backend == "nccl" else tt
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         el = float(tt.item())
     K = args.steps

@@ -120,3 +120,22 @@ def test_sharded_world2_shared_gpu(cuda, tmp_path, segmented):
     mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), 1, segmented), nprocs=2, join=True,
                        start_method="spawn")
     _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), _unsharded(cuda, 1))
+
+
+def test_bench_two_ranks_rehearsal(cuda, tmp_path):
+    """The N>1 flow of bench.py (torch.distributed.run launch, row-sharded model, sharded
+    loss, grad all-reduce, Adam, max-over-ranks timing, one JSON line from rank 0), two
+    ranks sharing this box's GPU over gloo -- the driver's 2/4/8-GPU runs use RCCL."""
+    import json
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--dist-backend", "gloo"]
+    p = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong" and res["value"] > 0
+    assert res["config"]["parallelism"].startswith("row-sharded x2")
