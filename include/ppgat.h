@@ -277,6 +277,26 @@ int ppgat_knn_max_k(void);
 int ppgat_knn_topk(const float* S, int64_t ld, int64_t rows, int64_t n_cols, int64_t q0, int k, float min_sim,
                    int32_t* out_idx, float* out_sim, int32_t* out_cnt, void* stream);
 
+/* ---- BPR triple sampler ---------------------------------------------------------------
+ * Replaces: sample_bpr_epoch, scripts/train_gat_pyg.py:179-190 (Python loop per epoch):
+ *   u uniform over users with >= 1 train item; i uniform over the positions of u's train
+ *   list (random.choice); j uniform over [0, n_items), redrawn while j is one of u's items.
+ * Same distribution, a counter-based stream instead of Python's Mersenne twister: every
+ * draw hashes (seed, t0 + s, draw number), so a triple does not depend on how the S
+ * triples are split over calls (oracle/sampler_oracle.py restates the stream bit for bit).
+ * prepare (once per graph): user_ptr [n_users+1] int64 CSR over user_items [nnz] int32 item
+ * ids (any order within a user) -> items_sorted [nnz] (each user's items ascending),
+ * eligible [n_users] (ids of users with items, ascending) and *n_eligible (device int64).
+ * sample: u, i, j [S] int64; *bad (device) = 1 if no user has items, 2 if some user's
+ * negative was not found in 1024 draws (the user holds ~all items; the reference loops). */
+int ppgat_bpr_sampler_workspace_bytes(int64_t n_users, int64_t nnz, size_t* bytes);
+int ppgat_bpr_sampler_prepare(const int64_t* user_ptr, const int32_t* user_items, int64_t n_users, int64_t nnz,
+                              int32_t* items_sorted, int32_t* eligible, int64_t* n_eligible, void* workspace,
+                              size_t workspace_bytes, void* stream);
+int ppgat_bpr_sample(const int64_t* user_ptr, const int32_t* items_sorted, const int32_t* eligible,
+                     const int64_t* n_eligible, int64_t n_items, int64_t n_triples, uint64_t seed, int64_t t0,
+                     int64_t* u, int64_t* i, int64_t* j, int32_t* bad, void* stream);
+
 /* ---- sampled ranking (evaluation) ------------------------------------------------
  * Replaces: the per-user loop of eval_sampled, scripts/train_gat_pyg.py:160-175:
  *   scores = I[cands[b]] @ U[users[b]];  rank[b] = #(scores[1:] > scores[0]) + 1
@@ -315,7 +335,8 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
 #define PPGAT_K_FUSION 9
 #define PPGAT_K_PROJ 10
 #define PPGAT_K_ADAM 11
-#define PPGAT_K_COUNT 12
+#define PPGAT_K_SAMPLE 12
+#define PPGAT_K_COUNT 13
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

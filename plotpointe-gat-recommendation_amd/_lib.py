@@ -75,6 +75,9 @@ SIGNATURES = {
                                 c_f, c_f, c_vp]),
     "ppgat_knn_max_k": (c_int, []),
     "ppgat_knn_topk": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_bpr_sampler_workspace_bytes": (c_int, [c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "ppgat_bpr_sampler_prepare": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_bpr_sample": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_u64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),
@@ -84,7 +87,8 @@ SIGNATURES = {
 }
 
 KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6, "sched": 7,
-           "gemm_tn": 8, "fusion": 9, "proj": 10, "adam": 11}
+           "gemm_tn": 8, "fusion": 9, "proj": 10, "adam": 11,
+           "sample": 12}
 MODE_PYG, MODE_CUSTOM = 0, 1
 
 _lib = None

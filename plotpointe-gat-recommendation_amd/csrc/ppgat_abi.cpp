@@ -560,6 +560,47 @@ int ppgat_knn_topk(const float* S, int64_t ld, int64_t rows, int64_t n_cols, int
   return PPGAT_OK;
 }
 
+int ppgat_bpr_sampler_workspace_bytes(int64_t n_users, int64_t nnz, size_t* bytes) {
+  if (!bytes || n_users < 0 || nnz < 0) return fail(PPGAT_ERR_INVALID, "bpr_sampler_workspace_bytes: bad arguments");
+  if (n_users > INT32_MAX || nnz > UINT32_MAX)
+    return fail(PPGAT_ERR_UNSUPPORTED, "bpr_sampler: users must fit int32 and nnz uint32");
+  *bytes = ppgat::bpr_sampler_workspace_bytes(n_users, nnz);
+  return PPGAT_OK;
+}
+
+int ppgat_bpr_sampler_prepare(const int64_t* user_ptr, const int32_t* user_items, int64_t n_users, int64_t nnz,
+                              int32_t* items_sorted, int32_t* eligible, int64_t* n_eligible, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  if (n_users < 0 || nnz < 0) return fail(PPGAT_ERR_INVALID, "bpr_sampler_prepare: bad sizes");
+  if (n_users > INT32_MAX || nnz > UINT32_MAX)
+    return fail(PPGAT_ERR_UNSUPPORTED, "bpr_sampler: users must fit int32 and nnz uint32");
+  if (!user_ptr || !n_eligible || (n_users > 0 && (!eligible || !workspace)) || (nnz > 0 && (!user_items || !items_sorted)))
+    return fail(PPGAT_ERR_INVALID, "bpr_sampler_prepare: null pointer");
+  if (workspace_bytes < ppgat::bpr_sampler_workspace_bytes(n_users, nnz))
+    return fail(PPGAT_ERR_INVALID, "bpr_sampler_prepare: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_SAMPLE, st);
+  hipError_t e = ppgat::bpr_sampler_prepare(user_ptr, user_items, n_users, nnz, items_sorted, eligible, n_eligible,
+                                            workspace, workspace_bytes, st);
+  if (e != hipSuccess) return hip_fail(e, "bpr_sampler_prepare");
+  return PPGAT_OK;
+}
+
+int ppgat_bpr_sample(const int64_t* user_ptr, const int32_t* items_sorted, const int32_t* eligible,
+                     const int64_t* n_eligible, int64_t n_items, int64_t n_triples, uint64_t seed, int64_t t0,
+                     int64_t* u, int64_t* i, int64_t* j, int32_t* bad, void* stream) {
+  if (n_items < 0 || n_items > INT32_MAX || n_triples < 0 || t0 < 0)
+    return fail(PPGAT_ERR_INVALID, "bpr_sample: bad sizes");
+  if (!bad || (n_triples > 0 && (!user_ptr || !eligible || !n_eligible || !u || !i || !j)))
+    return fail(PPGAT_ERR_INVALID, "bpr_sample: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_SAMPLE, st);
+  hipError_t e = ppgat::bpr_sample(user_ptr, items_sorted, eligible, n_eligible, n_items, n_triples, seed, t0, u, i,
+                                   j, bad, st);
+  if (e != hipSuccess) return hip_fail(e, "bpr_sample");
+  return PPGAT_OK;
+}
+
 int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
                        int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
                        int32_t* rank, void* stream) {

@@ -92,6 +92,15 @@ int knn_max_k();
 hipError_t knn_topk(const float* S, int64_t ld, int64_t rows, int64_t n_cols, int64_t q0, int k, float min_sim,
                     int32_t* out_idx, float* out_sim, int32_t* out_cnt, hipStream_t st);
 
+// BPR triple sampler (ppgat_sample.hip)
+size_t bpr_sampler_workspace_bytes(int64_t n_users, int64_t nnz);
+hipError_t bpr_sampler_prepare(const int64_t* ptr, const int32_t* items, int64_t n_users, int64_t nnz,
+                               int32_t* items_sorted, int32_t* eligible, int64_t* n_eligible, void* ws,
+                               size_t ws_bytes, hipStream_t st);
+hipError_t bpr_sample(const int64_t* ptr, const int32_t* items_sorted, const int32_t* eligible,
+                      const int64_t* n_eligible, int64_t n_items, int64_t S, uint64_t seed, int64_t t0, int64_t* u,
+                      int64_t* i, int64_t* j, int32_t* bad, hipStream_t st);
+
 // evaluation (ppgat_eval.hip)
 hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                         const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,

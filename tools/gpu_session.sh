@@ -23,6 +23,8 @@ for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     gemm) run pytest_gemm 300 python -u -m pytest tests/test_gpu_gemm.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
+    sampler) run pytest_sampler 300 python -u -m pytest tests/test_sampler.py "tests/test_gpu_eval.py::test_trainer_device_sampler" -m gpu -q -rf --timeout 120 --timeout-method thread ;;
+    bsampler) run bench_sampler 300 python tools/bench_sampler.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
