@@ -2,12 +2,12 @@
 // layer's per-node work fused into their epilogues, the weight-gradient GEMM, the
 // weight-gradient assembly and the optimizer update (gfx950 / MI355X).
 //
-//  * k_proj<0>: h = x W^T (+ bias) for x [N, K<=128], W [128, K]  -- GATConv.lin / item_proj
+//  * k_proj16<0>: h = x W^T (+ bias) for x [N, K<=128], W [128, K]  -- GATConv.lin / item_proj
 //    (scripts/train_gat_pyg.py:74,77,81; train_gat_custom.py:66,77), with the node attention
 //    terms s_src = h.att_src, s_dst = h.att_dst (PyG alpha_src/alpha_dst; custom :79) in the
 //    epilogue, so h is never re-read for them.  x may come from two row segments (users from
 //    user_emb, items from the item projection: train_gat_pyg.py:79-82) -- no concatenation.
-//  * k_proj<1>: dx = D W + ds_src (x) A_src + ds_dst (x) A_dst (heads = 1), the input
+//  * k_proj16<1>: dx = D W + ds_src (x) A_src + ds_dst (x) A_dst (heads = 1), the input
 //    gradient of the layer with the attention-logit terms folded in as a rank-2 epilogue
 //    (A = att W, computed per workgroup from W in LDS).
 //  * k_tn128: out = A^T B for A [N, M<=128], B [N, K<=128] (dW of every projection), one
@@ -19,8 +19,9 @@
 //  * k_adam: torch.optim.Adam's update (L2 weight decay, bias corrections; the arithmetic of
 //    ATen's fused Adam) over up to 16 tensors per launch.
 //
-// MFMA: v_mfma_f32_32x32x2_f32, exact fp32 FMA chains (MI355X_MICROARCH.md: 157 TF peak,
-// 64 cycles per instruction per SIMD).  Lane maps (l = lane, r = l & 31, hf = l >> 5):
+// MFMA: v_mfma_f32_16x16x4_f32 (projections) and v_mfma_f32_32x32x2_f32 (k_tn128), exact
+// fp32 FMA chains (MI355X_MICROARCH.md: 157 TF peak; 32 / 64 cycles per instruction per
+// SIMD).  32x32x2 lane maps (l = lane, r = l & 31, hf = l >> 5):
 //   A operand A'[i = r][kk = hf], B operand B'[kk = hf][j = r],
 //   accumulator register q: row (q & 3) + 8 (q >> 2) + 4 hf, column r.
 // The reduction index of each MFMA is free to permute as long as A and B agree, which is
@@ -32,8 +33,13 @@
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
 
+// Projection kernel occupancy: 2 waves per SIMD (256 VGPRs, two workgroups per CU).
+#ifndef PPGAT_PROJ16_OCC
+#define PPGAT_PROJ16_OCC 2
+#endif
 // Experiment hook for tools/bench_gemm.py (0 in every product build): bit 0 skips the x
-// loads of the projection kernel, bit 1 its MFMAs, bit 2 its epilogue stores.
+// loads of the projection kernel, bit 1 its MFMAs, bit 2 its epilogue stores, bit 3 its LDS
+// reads of W.
 #ifndef PPGAT_PROJ_VARIANT
 #define PPGAT_PROJ_VARIANT 0
 #endif
@@ -55,11 +61,28 @@ __device__ __forceinline__ int acc_row(int q, int hf) { return (q & 3) + 8 * (q 
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+// wave-uniform 64-bit value forced into scalar registers
+__device__ __forceinline__ int64_t sgpr(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// ... and as a global-address-space pointer (plain loads, not flat ones that also count
+// against the LDS wait counter)
+using gfloat = __attribute__((address_space(1))) const float;
+__device__ __forceinline__ gfloat* sgpr(const float* p) {
+  return (gfloat*)(uintptr_t)sgpr((int64_t)reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ float4 ld4(gfloat* p) {
+  using v4 = __attribute__((ext_vector_type(4))) float;
+  const v4 v = *(__attribute__((address_space(1))) const v4*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // ---------------------------------------------------------------------------
 // projection GEMM with fused epilogues
 // ---------------------------------------------------------------------------
 constexpr int kPT = 128;       // output columns (one tile)
-constexpr int kPLd = kPT + 4;  // LDS row stride: 16 lanes of a ds_read_b128 hit 64 distinct banks
 
 struct ProjArg {
   const float* x0;  // rows [0, split)
@@ -82,63 +105,79 @@ struct ProjArg {
   float* s_dst;
 };
 
-// 8 per-lane partial values, each summed over the 32 lanes of its half-wave.  On return
-// v[t] (t < 2) holds the full sum of value index ((l >> 4) & 1) * 4 + ((l >> 3) & 1) * 2 + t.
-__device__ __forceinline__ void reduce8_over32(float (&v)[8], int lane) {
+// ---------------------------------------------------------------------------
+// projection GEMM, one wave per 16-row tile (v_mfma_f32_16x16x4_f32)
+//
+// Every wave owns whole output rows: a 16 x 128 tile with the full reduction (K <= 128), so
+// no partial tiles are exchanged and the waves never synchronise after the prologue.  W is
+// staged once per workgroup in LDS as B'[j][k] (row stride 132 floats: the 16 lanes of a
+// ds_read_b128 row hit 64 distinct banks) and re-read per tile, one ds_read_b128 per four
+// MFMAs.  Lane l = (jl = l & 15, kq = l >> 4): A operand x[row jl][k = 32 kq + s], B operand
+// B'[col 16 cb + jl][k = 32 kq + s] (the reduction index is permuted: each lane reads 128
+// contiguous bytes of its x row), accumulator q = row 4 kq + q, column 16 cb + jl.
+// Software pipeline per iteration (tile t): x (and ds) of tile t + nw in flight; the MFMAs
+// of tile t; the epilogue of tile t - nw (its raw accumulators kept from the previous
+// iteration) -- bias / rank-2 terms, node scores, stores clipped by buffer descriptors --
+// scheduled into the MFMA shadows.
+// ---------------------------------------------------------------------------
+constexpr int kP16Ld = kPT + 4;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// 8 per-lane values (index v = 4 h + q), each summed over the 16 lanes of a row.  On return
+// lane jl holds the full sum for index 4 ((jl >> 3) & 1) + 2 ((jl >> 2) & 1) + ((jl >> 1) & 1)
+// (lanes jl and jl ^ 1 agree).  Pairing: ror 8, half-row mirror, xor 2, xor 1 -- every final
+// value covers all 16 lanes exactly once.
+__device__ __forceinline__ float reduce8_over16(float (&v)[8], int jl) {
+  const bool b3 = (jl & 8) != 0, b2 = (jl & 4) != 0, b1 = (jl & 2) != 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    float r0, r1;
-    row_swap<16>(v[t], v[4 + t], r0, r1);
-    v[t] = r0 + r1;
-  }
-  const bool b8 = (lane & 8) != 0;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const float send = b8 ? v[t] : v[2 + t];
-    const float keep = b8 ? v[2 + t] : v[t];
+    const float send = b3 ? v[t] : v[4 + t];
+    const float keep = b3 ? v[4 + t] : v[t];
     v[t] = keep + dpp<0x128>(send);
   }
 #pragma unroll
-  for (int t = 0; t < 2; ++t) v[t] = group_reduce<Op::Sum, 1, 4>(v[t]);
+  for (int t = 0; t < 2; ++t) {
+    const float send = b2 ? v[t] : v[2 + t];
+    const float keep = b2 ? v[2 + t] : v[t];
+    v[t] = keep + dpp<0x141>(send);
+  }
+  {
+    const float send = b1 ? v[0] : v[1];
+    const float keep = b1 ? v[1] : v[0];
+    v[0] = keep + dpp<0x4E>(send);
+  }
+  return v[0] + dpp<0xB1>(v[0]);
 }
 
-// Workgroup = 4 waves = 2 pairs, one workgroup per CU, persistent over 32-row tiles.  The two
-// waves of a pair split the reduction (k) in halves and keep their half of B in registers
-// for the whole launch (128 VGPRs: 4 column blocks x 32 k-steps), so the MFMA loop reads no
-// LDS; x rows stream from HBM with the next tile in flight.  Per tile both waves publish
-// their partial 32 x 128 tile row-major to LDS, then each finalises 16 rows: the two
-// partials added in a fixed order, epilogue, float4 stores of whole row segments, scores.
-// k mapping: step s of wave half kh, lane half hf covers k = 64 kh + 32 hf + s.
-constexpr int kXLd = kPT + 8;  // exchange row stride: rows 4 apart land 32 banks apart
-constexpr int kXTile = 32 * kXLd;
-constexpr int kProjLds = 2 * 2 * 2 * kXTile;  // [slot][pair][half] partial tiles (floats)
-static_assert(kProjLds >= kPT * kPLd, "the W staging image aliases the exchange buffers");
-
 template <int MODE>
-__global__ void __launch_bounds__(256, 1) k_proj(ProjArg a) {
-  __shared__ float4 lds4[kProjLds / 4];
+__global__ void __launch_bounds__(256, PPGAT_PROJ16_OCC) k_proj16(ProjArg a) {
+  __shared__ float4 sW4[kPT * kP16Ld / 4];
   __shared__ float sV[2][kPT];  // att (mode 0) / A = att W (mode 1)
-  float* lds = reinterpret_cast<float*>(lds4);
-  float (*sW)[kPLd] = reinterpret_cast<float (*)[kPLd]>(lds);  // W as stored (prologue only)
+  float* sW = reinterpret_cast<float*>(sW4);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: buffer descriptors stay in SGPRs
-  const int r = lane & 31, hf = lane >> 5;
-  const int kh = w & 1, pr = w >> 1;
+  const int jl = lane & 15, kq = lane >> 4;
   const int K = a.K;
-  // ---- stage W (zero-padded to 128 x 128), the attention vectors ----
+  // ---- stage B'[j][k] (zero-padded to 128 x 128) and the attention vectors ----
   if (MODE == 0) {
     for (int idx = tid; idx < kPT * 32; idx += 256) {
       const int j = idx >> 5, k4 = (idx & 31) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k4 < K) v = ld4(a.W + (int64_t)j * a.ldw + k4);
-      st4(&sW[j][k4], v);
+      st4(&sW[j * kP16Ld + k4], v);
     }
   } else {
     for (int idx = tid; idx < kPT * 32; idx += 256) {
       const int k = idx >> 5, j4 = (idx & 31) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k < K) v = ld4(a.W + (int64_t)k * a.ldw + j4);
-      st4(&sW[k][j4], v);
+      sW[(j4 + 0) * kP16Ld + k] = v.x;
+      sW[(j4 + 1) * kP16Ld + k] = v.y;
+      sW[(j4 + 2) * kP16Ld + k] = v.z;
+      sW[(j4 + 3) * kP16Ld + k] = v.w;
     }
   }
   const bool vec = a.att_src != nullptr;
@@ -150,152 +189,142 @@ __global__ void __launch_bounds__(256, 1) k_proj(ProjArg a) {
   if (MODE == 1 && vec) {  // A[j] = sum_k att[k] W[k][j]
     float s = 0.f;
     const int j = tid & 127, v = tid >> 7;
-    for (int k = 0; k < kPT; ++k) s = fmaf(sV[v][k], sW[k][j], s);
+    for (int k = 0; k < kPT; ++k) s = fmaf(sV[v][k], sW[j * kP16Ld + k], s);
     __syncthreads();
     sV[v][j] = s;
+    __syncthreads();
   }
-  // ---- B fragments into registers: bq[nb][s] = B[k = 64 kh + 32 hf + s][j = 32 nb + r] ----
-  float bq[4][32];
-  const int kb = 64 * kh + 32 * hf;
+  float va[8], vb[8], bias[8];
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-    for (int s4 = 0; s4 < 32; s4 += 4) {
-      if (MODE == 0) {
-        const float4 v = *reinterpret_cast<const float4*>(&sW[nb * 32 + r][kb + s4]);
-        bq[nb][s4] = v.x; bq[nb][s4 + 1] = v.y; bq[nb][s4 + 2] = v.z; bq[nb][s4 + 3] = v.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bq[nb][s4 + e] = sW[kb + s4 + e][nb * 32 + r];
-      }
-    }
-  __syncthreads();  // sW is dead from here on: its bytes become the exchange buffers
-  // epilogue lane map: lane owns columns c4 .. c4 + 3 of rows 16 kh + 2 i + hf (i < 8)
-  const int c4 = 4 * r;
-  float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va, bias4 = va;
-  if (vec) {
-    va = make_float4(sV[0][c4], sV[0][c4 + 1], sV[0][c4 + 2], sV[0][c4 + 3]);
-    vb = make_float4(sV[1][c4], sV[1][c4 + 1], sV[1][c4 + 2], sV[1][c4 + 3]);
+  for (int cb = 0; cb < 8; ++cb) {
+    const int c = 16 * cb + jl;
+    va[cb] = vec ? sV[0][c] : 0.f;
+    vb[cb] = vec ? sV[1][c] : 0.f;
+    bias[cb] = (MODE == 0 && a.bias) ? a.bias[c] : 0.f;
   }
-  if (MODE == 0 && a.bias) bias4 = ld4(a.bias + c4);
+  gfloat* const x0 = sgpr(a.x0);
+  gfloat* const x1 = sgpr(a.x1);
+  const int64_t ldx0 = sgpr(a.ldx0), ldx1 = sgpr(a.ldx1), split = sgpr(a.split), n = sgpr(a.n);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t tiles = (n + 15) / 16;
+  const int64_t iters = (tiles + nw - 1) / nw;  // the same for every wave
+  const float* sWl = sW + jl * kP16Ld + 32 * kq;
 
-  const int64_t tiles = (a.n + 31) / 32;
-  const int64_t iters = (tiles + 2 * (int64_t)gridDim.x - 1) / (2 * (int64_t)gridDim.x);  // same for every wave
-  // x loads are unconditional (a select on a loaded value makes the compiler wait for the
-  // load right there, which would serialise the prefetch): rows past n read row n - 1 (their
-  // outputs are never stored), columns past K read in-row columns < K that meet zero B rows.
+  // x loads are unconditional (a select on a loaded value makes hipcc wait for the load right
+  // there, serialising the prefetch): rows past n read row n - 1 (never stored), columns
+  // past K read in-row columns < K that meet zero rows of B'
   auto load_x = [&](int64_t tile, float4 (&xv)[8]) {
     if (PPGAT_PROJ_VARIANT & 1) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) xv[q] = make_float4(tile, q, r, 1.f);
+      for (int q = 0; q < 8; ++q) xv[q] = make_float4(tile, q, jl, 1.f);
       return;
     }
-    int64_t row = tile * 32 + r;
-    row = row < a.n ? row : a.n - 1;
-    const float* src = row < a.split ? a.x0 + row * a.ldx0 : a.x1 + (row - a.split) * a.ldx1;
+    int64_t row = tile * 16 + jl;
+    row = row < n ? row : n - 1;
+    gfloat* src = row < split ? x0 + row * ldx0 : x1 + (row - split) * ldx1;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int c = kb + 4 * q;
+      const int c = 32 * kq + 4 * q;
       xv[q] = ld4(src + (c < K ? c : K - 4));
     }
   };
-  // Finalise tile tt from exchange slot sl: rows 16 kh + 2 i + hf, columns c4..c4+3.  Branch
-  // free so hipcc can interleave it with the next tile's MFMAs: stores go through buffer
-  // descriptors whose record count clips rows past n (and a whole tile past the last one).
-  auto finalize = [&](int64_t tt, int sl) {
-    const float* X = lds + ((sl * 2 + pr) * 2) * kXTile;
-    const int64_t row0 = tt * 32;
-    // rows of this tile that exist (0 for tt < 0 or past the last tile), min/max only: a
-    // branch here would split the basic block the MFMAs share with this code
-    const int64_t live = min(min(max(a.n - row0, (int64_t)0), (int64_t)32), max(row0 + 32, (int64_t)0));
-    const int64_t base = max(row0, (int64_t)0);
-    const auto ry = __builtin_amdgcn_make_buffer_rsrc(a.y + base * a.ldy, 0,
-                                                      (int)(live * a.ldy * 4), 0x00020000);
-    float4 y[8];
-    float ps[8], pd[8];
+  auto load_d = [&](int64_t tile, float2 (&dv)[4]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rr = 16 * kh + 2 * i + hf;
-      const float4 p0 = *reinterpret_cast<const float4*>(X + rr * kXLd + c4);
-      const float4 p1 = *reinterpret_cast<const float4*>(X + kXTile + rr * kXLd + c4);
-      float4 v = make_float4(p0.x + p1.x, p0.y + p1.y, p0.z + p1.z, p0.w + p1.w);
-      if (MODE == 1) {
-        const int64_t row = min(max(row0 + rr, (int64_t)0), a.n - 1);
-        const float2 d = *reinterpret_cast<const float2*>(a.ds + row * a.ldds);
-        v.x = fmaf(d.y, vb.x, fmaf(d.x, va.x, v.x));
-        v.y = fmaf(d.y, vb.y, fmaf(d.x, va.y, v.y));
-        v.z = fmaf(d.y, vb.z, fmaf(d.x, va.z, v.z));
-        v.w = fmaf(d.y, vb.w, fmaf(d.x, va.w, v.w));
-      } else {
-        ps[i] = fmaf(v.w, va.w, fmaf(v.z, va.z, fmaf(v.y, va.y, v.x * va.x)));
-        pd[i] = fmaf(v.w, vb.w, fmaf(v.z, vb.z, fmaf(v.y, vb.y, v.x * vb.x)));
-        v = make_float4(v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w);
-      }
-      y[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rr = 16 * kh + 2 * i + hf;
-      if (!(PPGAT_PROJ_VARIANT & 4) || y[i].x == 12345.f)
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(y[i].x), __float_as_uint(y[i].y),
-                                                      __float_as_uint(y[i].z), __float_as_uint(y[i].w)},
-                                               ry, (int)((rr * a.ldy + c4) * 4), 0, 0);
-    }
-    if (MODE == 0 && vec) {
-      reduce8_over32(ps, lane);
-      reduce8_over32(pd, lane);
-      const int o = lane & 7;
-      const int i = ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + (o & 1);
-      const int off = o < 2 ? (16 * kh + 2 * i + hf) * 4 : 0x40000000;  // non-writers fall outside
-      const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.s_src + base, 0, (int)(live * 4), 0x00020000);
-      const auto rd = __builtin_amdgcn_make_buffer_rsrc(a.s_dst + base, 0, (int)(live * 4), 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((o & 1) ? ps[1] : ps[0]), rs, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((o & 1) ? pd[1] : pd[0]), rd, off, 0, 0);
+    for (int q = 0; q < 4; ++q) {
+      int64_t row = tile * 16 + 4 * kq + q;
+      row = min(max(row, (int64_t)0), n - 1);
+      dv[q] = *reinterpret_cast<const float2*>(a.ds + row * a.ldds);
     }
   };
+  // epilogue of tile tt from its raw accumulators (a no-op store-wise for tt < 0 or past
+  // the last tile: the descriptors then hold no records)
+  auto finalize = [&](int64_t tt, const f32x4 (&ac)[8], const float2 (&dv)[4]) {
+    const int64_t row0 = tt * 16;
+    const int64_t live = min(min(max(n - row0, (int64_t)0), (int64_t)16), max(row0 + 16, (int64_t)0));
+    const int64_t base = max(row0, (int64_t)0);
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc(a.y + base * a.ldy, 0, (int)(live * a.ldy * 4), 0x00020000);
+    float ps[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { ps[q] = 0.f; ps[4 + q] = 0.f; }
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = ac[cb][q];
+        if (MODE == 1) {
+          v = fmaf(dv[q].y, vb[cb], fmaf(dv[q].x, va[cb], v));
+        } else {
+          ps[q] = fmaf(v, va[cb], ps[q]);
+          ps[4 + q] = fmaf(v, vb[cb], ps[4 + q]);
+          v += bias[cb];
+        }
+        if (!(PPGAT_PROJ_VARIANT & 4) || v == 12345.f)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry,
+                                                (int)(((4 * kq + q) * a.ldy + 16 * cb + jl) * 4), 0, 0);
+      }
+    if (MODE == 0 && vec) {
+      const float sv = reduce8_over16(ps, jl);
+      const int rr = 4 * kq + 2 * ((jl >> 2) & 1) + ((jl >> 1) & 1);
+      const bool wr = (jl & 1) == 0, dst = (jl & 8) != 0;
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.s_src + base, 0, (int)(live * 4), 0x00020000);
+      const auto rd = __builtin_amdgcn_make_buffer_rsrc(a.s_dst + base, 0, (int)(live * 4), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), rs, (wr && !dst) ? rr * 4 : 0x40000000, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), rd, (wr && dst) ? rr * 4 : 0x40000000, 0, 0);
+    }
+  };
+
   float4 xr[8];
-  load_x((int64_t)blockIdx.x * 2 + pr, xr);
-  // iteration it: MFMAs of tile it interleaved with the finalisation of tile it - 1 (a no-op
-  // at it = 0: its descriptors have no records), then the partial of tile it is published;
-  // one barrier per iteration (two exchange slots).  No branches inside, so the scheduler
-  // can fill the MFMA shadows with the finalisation.
+  float2 dcur[4], dprev[4];
+  f32x4 accp[8];
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) accp[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dcur[q] = dprev[q] = make_float2(0.f, 0.f);
+  load_x(wave, xr);
+  if (MODE == 1) load_d(wave, dcur);
   for (int64_t it = 0; it < iters; ++it) {
-    const int64_t t = (it * gridDim.x + blockIdx.x) * 2 + pr;
+    const int64_t t = wave + it * nw;
     float4 xn[8];
-    load_x(t + 2 * (int64_t)gridDim.x, xn);  // next tile in flight
-    f32x16 acc[4];
+    float2 dn[4];
+    load_x(t + nw, xn);  // next tile in flight
+    if (MODE == 1) load_d(t + nw, dn);
+    f32x4 acc[8];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
+    for (int cb = 0; cb < 8; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[nb][q] = 0.f;
-    if (!(PPGAT_PROJ_VARIANT & 2)) {
+    for (int s4 = 0; s4 < 8; ++s4) {
+      float4 bf[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int cb = 0; cb < 8; ++cb)
+        bf[cb] = (PPGAT_PROJ_VARIANT & 8) ? make_float4(va[cb], vb[cb], s4, cb)
+                                          : *reinterpret_cast<const float4*>(sWl + cb * 16 * kP16Ld + 4 * s4);
+      if (!(PPGAT_PROJ_VARIANT & 2)) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma(comp(xr[q], e), bq[nb][4 * q + e], acc[nb]);
-    } else {
+          for (int cb = 0; cb < 8; ++cb) acc[cb] = mfma16(comp(xr[s4], e), comp(bf[cb], e), acc[cb]);
+      } else {
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) acc[nb][0] = xr[nb].x + bq[nb][0];
+        for (int cb = 0; cb < 8; ++cb) acc[cb][0] += xr[s4].x * bf[cb].y;
+      }
     }
-    finalize(t - 2 * (int64_t)gridDim.x, (int)((it + 1) & 1));
+    finalize(t - nw, accp, dprev);
 #pragma unroll
-    for (int g = 0; g < 128; ++g) {
+    for (int g = 0; g < 256; ++g) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x366, 2, 0);  // then up to two VALU/SALU/DS/VMEM
+      __builtin_amdgcn_sched_group_barrier(0x3F6, 2, 0);  // then up to two other instructions
     }
-    // ---- publish the partial tile row-major: X[slot][pr][kh][row][col] ----
-    float* mine = lds + (((int)(it & 1) * 2 + pr) * 2 + kh) * kXTile;
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) mine[acc_row(q, hf) * kXLd + nb * 32 + r] = acc[nb][q];
-    __syncthreads();
+    for (int cb = 0; cb < 8; ++cb) accp[cb] = acc[cb];
 #pragma unroll
     for (int q = 0; q < 8; ++q) xr[q] = xn[q];
+    if (MODE == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { dprev[q] = dcur[q]; dcur[q] = dn[q]; }
+    }
   }
-  finalize(((iters - 1) * gridDim.x + blockIdx.x) * 2 + pr, (int)((iters - 1) & 1));
+  finalize(wave + (iters - 1) * nw, accp, dprev);
 }
 
 // ---------------------------------------------------------------------------
@@ -672,10 +701,10 @@ __global__ void __launch_bounds__(256) k_adam(AdamArg a) {
 // ---- host launchers ----
 bool proj_shape_ok(int K, int ncols) { return K >= 4 && K <= kPT && K % 4 == 0 && ncols == kPT; }
 
-static unsigned proj_grid(int64_t n) {
-  const int64_t tiles = (n + 31) / 32;
-  int64_t g = (tiles + 1) / 2;
-  if (g > 256) g = 256;  // one workgroup per CU, persistent over the row tiles
+static unsigned proj16_grid(int64_t n) {
+  const int64_t tiles = (n + 15) / 16;
+  int64_t g = (tiles + 3) / 4;
+  if (g > 256 * PPGAT_PROJ16_OCC) g = 256 * PPGAT_PROJ16_OCC;  // persistent over the 16-row tiles
   return (unsigned)(g < 1 ? 1 : g);
 }
 
@@ -687,7 +716,7 @@ hipError_t proj_fwd(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1
   a.x0 = x0; a.ldx0 = ldx0; a.x1 = x1 ? x1 : x0; a.ldx1 = x1 ? ldx1 : ldx0; a.split = x1 ? split : n; a.n = n;
   a.K = K; a.W = W; a.ldw = ldw; a.bias = bias; a.att_src = att_src; a.att_dst = att_dst;
   a.y = y; a.ldy = ldy; a.s_src = s_src; a.s_dst = s_dst;
-  hipLaunchKernelGGL(k_proj<0>, dim3(proj_grid(n)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_proj16<0>, dim3(proj16_grid(n)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -697,7 +726,7 @@ hipError_t proj_dx(const float* D, int64_t ldd, int64_t n, int K, const float* W
   ProjArg a{};
   a.x0 = D; a.ldx0 = ldd; a.x1 = D; a.ldx1 = ldd; a.split = n; a.n = n; a.K = K; a.W = W; a.ldw = ldw;
   a.att_src = att_src; a.att_dst = att_dst; a.ds = S; a.ldds = lds; a.y = y; a.ldy = ldy;
-  hipLaunchKernelGGL(k_proj<1>, dim3(proj_grid(n)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_proj16<1>, dim3(proj16_grid(n)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
