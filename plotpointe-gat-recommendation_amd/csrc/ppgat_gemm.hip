@@ -46,6 +46,25 @@
 
 namespace ppgat {
 
+#if PPGAT_CLOCK_PROBE
+// Diagnostic builds only (tools/build_variants.sh -DPPGAT_CLOCK_PROBE=1): per-wave shader
+// clock and 100 MHz real-time deltas of the projection / weight-gradient kernels, read by
+// ppgat_debug_clock_mhz.  Nothing else reads these words.
+__device__ unsigned long long g_probe[2][4096][2];
+#define PPGAT_PROBE_BEGIN                                            \
+  const unsigned long long probe_t0 = __builtin_amdgcn_s_memtime(); \
+  const unsigned long long probe_r0 = __builtin_amdgcn_s_memrealtime();
+#define PPGAT_PROBE_END(SLOT, WAVE)                                                            \
+  if ((threadIdx.x & 63) == 0 && (WAVE) < 4096) {                                              \
+    volatile unsigned long long* pp = &g_probe[SLOT][WAVE][0];                                 \
+    pp[0] = __builtin_amdgcn_s_memtime() - probe_t0;                                           \
+    pp[1] = __builtin_amdgcn_s_memrealtime() - probe_r0;                                       \
+  }
+#else
+#define PPGAT_PROBE_BEGIN
+#define PPGAT_PROBE_END(SLOT, WAVE)
+#endif
+
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -121,6 +140,12 @@ struct ProjArg {
 // scheduled into the MFMA shadows.
 // ---------------------------------------------------------------------------
 constexpr int kP16Ld = kPT + 4;
+// LDS column of reduction index k in a B' row: the 32-wide k chunks 1 and 2 trade places, so
+// the two k chunks met by each 16-lane group of a ds_read_b128 ({0-3,12-15,20-27}, ...) start
+// on the same bank slot and the group's 16 lanes cover 16 distinct slots (no 2-way conflict)
+__host__ __device__ constexpr int p16_col(int k) {
+  return ((k >> 5) == 1 ? 64 : (k >> 5) == 2 ? 32 : (k & ~31)) + (k & 31);
+}
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -167,17 +192,18 @@ __global__ void __launch_bounds__(256, PPGAT_PROJ16_OCC) k_proj16(ProjArg a) {
       const int j = idx >> 5, k4 = (idx & 31) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k4 < K) v = ld4(a.W + (int64_t)j * a.ldw + k4);
-      st4(&sW[j * kP16Ld + k4], v);
+      st4(&sW[j * kP16Ld + p16_col(k4)], v);
     }
   } else {
     for (int idx = tid; idx < kPT * 32; idx += 256) {
       const int k = idx >> 5, j4 = (idx & 31) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k < K) v = ld4(a.W + (int64_t)k * a.ldw + j4);
-      sW[(j4 + 0) * kP16Ld + k] = v.x;
-      sW[(j4 + 1) * kP16Ld + k] = v.y;
-      sW[(j4 + 2) * kP16Ld + k] = v.z;
-      sW[(j4 + 3) * kP16Ld + k] = v.w;
+      const int c = p16_col(k);
+      sW[(j4 + 0) * kP16Ld + c] = v.x;
+      sW[(j4 + 1) * kP16Ld + c] = v.y;
+      sW[(j4 + 2) * kP16Ld + c] = v.z;
+      sW[(j4 + 3) * kP16Ld + c] = v.w;
     }
   }
   const bool vec = a.att_src != nullptr;
@@ -189,11 +215,12 @@ __global__ void __launch_bounds__(256, PPGAT_PROJ16_OCC) k_proj16(ProjArg a) {
   if (MODE == 1 && vec) {  // A[j] = sum_k att[k] W[k][j]
     float s = 0.f;
     const int j = tid & 127, v = tid >> 7;
-    for (int k = 0; k < kPT; ++k) s = fmaf(sV[v][k], sW[j * kP16Ld + k], s);
+    for (int k = 0; k < kPT; ++k) s = fmaf(sV[v][k], sW[j * kP16Ld + p16_col(k)], s);
     __syncthreads();
     sV[v][j] = s;
     __syncthreads();
   }
+  PPGAT_PROBE_BEGIN
   float va[8], vb[8], bias[8];
 #pragma unroll
   for (int cb = 0; cb < 8; ++cb) {
@@ -209,7 +236,7 @@ __global__ void __launch_bounds__(256, PPGAT_PROJ16_OCC) k_proj16(ProjArg a) {
   const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t tiles = (n + 15) / 16;
   const int64_t iters = (tiles + nw - 1) / nw;  // the same for every wave
-  const float* sWl = sW + jl * kP16Ld + 32 * kq;
+  const float* sWl = sW + jl * kP16Ld + p16_col(32 * kq);
 
   // x loads are unconditional (a select on a loaded value makes hipcc wait for the load right
   // there, serialising the prefetch): rows past n read row n - 1 (never stored), columns
@@ -325,12 +352,22 @@ __global__ void __launch_bounds__(256, PPGAT_PROJ16_OCC) k_proj16(ProjArg a) {
     }
   }
   finalize(wave + (iters - 1) * nw, accp, dprev);
+  PPGAT_PROBE_END(0, wave)
 }
 
 // ---------------------------------------------------------------------------
 // out[M, K] = A^T B (+ V^T B, colsum A), M, K <= 128
+//
+// Workgroup = 8 waves = 4 pairs, one workgroup per CU (two waves per SIMD).  A pair owns a
+// contiguous range of rows; its wave mh accumulates the m-half [64 mh, 64 mh + 64) of the
+// 128 x 128 output (128 accumulation registers), streaming float2 of A and float4 of B per
+// lane straight from HBM into the MFMA operand layout: lane (r, hf) takes row base + 2p + hf,
+// A'[m = 64 mh + 2 r + i][kk = hf], B'[kk = hf][k = 4 r + j].  Wave mh also forms V[:, mh]^T B
+// (on the VALU) and colsum over its m-half.  Pair partials are summed through LDS in pair
+// order, then an ordered split reduction across workgroups (deterministic).
 // ---------------------------------------------------------------------------
-constexpr int kTnPairs = 8;  // row pairs per prefetch batch
+constexpr int kTnPairs = 4;  // row pairs per prefetch batch
+constexpr int kTnWaves = 8;
 
 struct TnArg {
   const float* A;
@@ -345,80 +382,77 @@ struct TnArg {
   int nv;
   int64_t n;
   int M, K;
-  int64_t rows_per_wave;  // even
+  int64_t rows_per_pair;  // even
   float* part;   // [gridDim.x][128][128] (m-major)
   float* vpart;  // [gridDim.x][2][128]
   float* cpart;  // nullable: [gridDim.x][128]
 };
 
 // One batch of kTnPairs row pairs: lane (r, hf) takes row base + 2p + hf.
-template <int NV, bool MASK>
+template <bool MASK>
 __device__ __forceinline__ void tn_load(const float* pa, const float* pb, const float* pv, int64_t sa, int64_t sb,
-                                        int64_t sv, bool am, bool bk, float4 (&av)[kTnPairs], float4 (&bv)[kTnPairs],
-                                        float2 (&vv)[kTnPairs]) {
+                                        int64_t sv, bool am, bool bk, float2 (&av)[kTnPairs], float4 (&bv)[kTnPairs],
+                                        float (&vv)[kTnPairs]) {
 #pragma unroll
   for (int p = 0; p < kTnPairs; ++p) {
-    av[p] = ld4(pa + p * sa);
+    av[p] = *reinterpret_cast<const float2*>(pa + p * sa);
     bv[p] = ld4(pb + p * sb);
-    if (NV == 2) vv[p] = *reinterpret_cast<const float2*>(pv + p * sv);
-    else if (NV == 1) vv[p] = make_float2(pv[p * sv], 0.f);
-    else vv[p] = make_float2(0.f, 0.f);
+    vv[p] = pv[p * sv];
     if (MASK) {
-      if (!am) av[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!am) av[p] = make_float2(0.f, 0.f);
       if (!bk) bv[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
 
-template <int NV>
-__device__ __forceinline__ void tn_compute(f32x16 (&acc)[4][4], float4& vacc0, float4& vacc1, float4& csum,
-                                           const float4 (&av)[kTnPairs], const float4 (&bv)[kTnPairs],
-                                           const float2 (&vv)[kTnPairs]) {
+template <bool HASV>
+__device__ __forceinline__ void tn_compute(f32x16 (&acc)[2][4], float4& vacc, float2& csum,
+                                           const float2 (&av)[kTnPairs], const float4 (&bv)[kTnPairs],
+                                           const float (&vv)[kTnPairs]) {
 #pragma unroll
   for (int p = 0; p < kTnPairs; ++p) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma(comp(av[p], i), comp(bv[p], j), acc[i][j]);
-    if (NV > 0) {
-      vacc0.x = fmaf(vv[p].x, bv[p].x, vacc0.x);
-      vacc0.y = fmaf(vv[p].x, bv[p].y, vacc0.y);
-      vacc0.z = fmaf(vv[p].x, bv[p].z, vacc0.z);
-      vacc0.w = fmaf(vv[p].x, bv[p].w, vacc0.w);
-    }
-    if (NV > 1) {
-      vacc1.x = fmaf(vv[p].y, bv[p].x, vacc1.x);
-      vacc1.y = fmaf(vv[p].y, bv[p].y, vacc1.y);
-      vacc1.z = fmaf(vv[p].y, bv[p].z, vacc1.z);
-      vacc1.w = fmaf(vv[p].y, bv[p].w, vacc1.w);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma(i ? av[p].y : av[p].x, comp(bv[p], j), acc[i][j]);
+    if (HASV) {
+      vacc.x = fmaf(vv[p], bv[p].x, vacc.x);
+      vacc.y = fmaf(vv[p], bv[p].y, vacc.y);
+      vacc.z = fmaf(vv[p], bv[p].z, vacc.z);
+      vacc.w = fmaf(vv[p], bv[p].w, vacc.w);
     }
     csum.x += av[p].x;
     csum.y += av[p].y;
-    csum.z += av[p].z;
-    csum.w += av[p].w;
   }
 }
 
 template <int NV, bool MASK>
-__global__ void __launch_bounds__(256, 1) k_tn128(TnArg a) {
+__global__ void __launch_bounds__(64 * kTnWaves, 1) k_tn128(TnArg a) {
   __shared__ float sR[kPT][kPT + 4];
-  __shared__ float sVr[4][2][kPT];
-  __shared__ float sC[4][kPT];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ float sVr[kTnWaves / 2][2][kPT];
+  __shared__ float sC[kTnWaves / 2][kPT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + w;
-  const int64_t n_beg = wid * a.rows_per_wave;
-  const int64_t n_end = min(a.n, n_beg + a.rows_per_wave);
-  const bool am = !MASK || 4 * r < a.M, bk = !MASK || 4 * r < a.K;
-  const int acol = am ? 4 * r : 0, bcol = bk ? 4 * r : 0;  // masked lanes read column 0, zeroed after
-  f32x16 acc[4][4];
+  const int mh = w & 1, pr = w >> 1;
+  const int64_t pid = (int64_t)blockIdx.x * (kTnWaves / 2) + pr;
+  const int64_t n_beg = pid * a.rows_per_pair;
+  const int64_t n_end = min(a.n, n_beg + a.rows_per_pair);
+  const int mcol = 64 * mh + 2 * r;
+  const bool am = !MASK || mcol < a.M, bk = !MASK || 4 * r < a.K;
+  const int acol = am ? mcol : 0, bcol = bk ? 4 * r : 0;  // masked lanes read column 0, zeroed after
+  const bool hasv = mh < NV;
+  const int vcol = hasv ? mh : 0;
+  f32x16 acc[2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-  float4 vacc0 = make_float4(0.f, 0.f, 0.f, 0.f), vacc1 = vacc0, csum = vacc0;
+  float4 vacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 csum = make_float2(0.f, 0.f);
+  PPGAT_PROBE_BEGIN
   // two B segments: rows [n_beg, split) from B, [split, n_end) from B1
   for (int seg = 0; seg < 2; ++seg) {
     const int64_t r0 = seg == 0 ? n_beg : max(n_beg, a.split);
@@ -431,20 +465,22 @@ __global__ void __launch_bounds__(256, 1) k_tn128(TnArg a) {
     const int64_t full = (r1 - r0) / (2 * kTnPairs);
     const float* pa = a.A + (r0 + hf) * a.lda + acol;
     const float* pb = bbase + (r0 - boff + hf) * ldb + bcol;
-    const float* pv = a.V + (r0 + hf) * a.ldv;
-    float4 av[kTnPairs], bv[kTnPairs];
-    float2 vv[kTnPairs];
+    const float* pv = a.V + (r0 + hf) * a.ldv + vcol;
+    float2 av[kTnPairs];
+    float4 bv[kTnPairs];
+    float vv[kTnPairs];
     if (full > 0) {
-      tn_load<NV, MASK>(pa, pb, pv, sa, sb, sv, am, bk, av, bv, vv);
+      tn_load<MASK>(pa, pb, pv, sa, sb, sv, am, bk, av, bv, vv);
       for (int64_t bt = 1; bt < full; ++bt) {
         pa += kTnPairs * sa;
         pb += kTnPairs * sb;
         pv += kTnPairs * sv;
-        float4 an[kTnPairs], bn[kTnPairs];
-        float2 vn[kTnPairs];
-        tn_load<NV, MASK>(pa, pb, pv, sa, sb, sv, am, bk, an, bn, vn);  // in flight during the MFMAs
+        float2 an[kTnPairs];
+        float4 bn[kTnPairs];
+        float vn[kTnPairs];
+        tn_load<MASK>(pa, pb, pv, sa, sb, sv, am, bk, an, bn, vn);  // in flight during the MFMAs
         __builtin_amdgcn_sched_barrier(0);
-        tn_compute<NV>(acc, vacc0, vacc1, csum, av, bv, vv);
+        tn_compute<NV != 0>(acc, vacc, csum, av, bv, vv);
 #pragma unroll
         for (int p = 0; p < kTnPairs; ++p) {
           av[p] = an[p];
@@ -452,7 +488,7 @@ __global__ void __launch_bounds__(256, 1) k_tn128(TnArg a) {
           vv[p] = vn[p];
         }
       }
-      tn_compute<NV>(acc, vacc0, vacc1, csum, av, bv, vv);
+      tn_compute<NV != 0>(acc, vacc, csum, av, bv, vv);
     }
     // tail (< 2 kTnPairs rows): out-of-range pairs read the segment's first row, zeroed
     const int64_t t0 = r0 + full * 2 * kTnPairs;
@@ -461,26 +497,25 @@ __global__ void __launch_bounds__(256, 1) k_tn128(TnArg a) {
       for (int p = 0; p < kTnPairs; ++p) {
         const bool ok = t0 + 2 * p + hf < r1;
         const int64_t row = ok ? t0 + 2 * p + hf : r0;
-        const float4 va = ld4(a.A + row * a.lda + acol);
+        const float2 va = *reinterpret_cast<const float2*>(a.A + row * a.lda + acol);
         const float4 vb = ld4(bbase + (row - boff) * ldb + bcol);
-        av[p] = (ok && am) ? va : make_float4(0.f, 0.f, 0.f, 0.f);
+        av[p] = (ok && am) ? va : make_float2(0.f, 0.f);
         bv[p] = (ok && bk) ? vb : make_float4(0.f, 0.f, 0.f, 0.f);
-        float2 v = make_float2(0.f, 0.f);
-        if (NV == 2) v = *reinterpret_cast<const float2*>(a.V + row * a.ldv);
-        if (NV == 1) v.x = a.V[row * a.ldv];
-        vv[p] = ok ? v : make_float2(0.f, 0.f);
+        const float v = NV > 0 ? a.V[row * a.ldv + vcol] : 0.f;
+        vv[p] = ok ? v : 0.f;
       }
-      tn_compute<NV>(acc, vacc0, vacc1, csum, av, bv, vv);
+      tn_compute<NV != 0>(acc, vacc, csum, av, bv, vv);
     }
   }
-  // ---- workgroup reduction through LDS, waves in order 0..3 ----
-  // acc[i][j][q]: m = 4 * acc_row(q, hf) + i, k = 4 * r + j
+  PPGAT_PROBE_END(1, blockIdx.x * kTnWaves + w)
+  // ---- workgroup reduction through LDS, pairs in order 0..3 ----
+  // acc[i][j][q]: m = 64 mh + 2 acc_row(q, hf) + i, k = 4 r + j
   auto put = [&](bool add) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int m = 4 * acc_row(q, hf) + i;
+        const int m = 64 * mh + 2 * acc_row(q, hf) + i;
         float4 v = make_float4(acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]);
         float* dst = &sR[m][4 * r];
         if (add) {
@@ -490,50 +525,50 @@ __global__ void __launch_bounds__(256, 1) k_tn128(TnArg a) {
         st4(dst, v);
       }
   };
-  // (no loop over turns: a loop lets the compiler hoist all 256 accumulator reads)
-  if (w == 0) put(false);
+  // (no loop over turns: a loop lets the compiler hoist all accumulator reads)
+  if (pr == 0) put(false);
   __syncthreads();
-  if (w == 1) put(true);
+  if (pr == 1) put(true);
   __syncthreads();
-  if (w == 2) put(true);
+  if (pr == 2) put(true);
   __syncthreads();
-  if (w == 3) put(true);
-  __syncthreads();
-  // V and colsum: combine the two half-waves (lane, lane ^ 32), then the waves in order
+  if (pr == 3) put(true);
+  // V and colsum: combine the two half-waves (lane, lane ^ 32), then the pairs in order
   {
-    float t0[4] = {vacc0.x, vacc0.y, vacc0.z, vacc0.w}, t1[4] = {vacc1.x, vacc1.y, vacc1.z, vacc1.w};
-    float c[4] = {csum.x, csum.y, csum.z, csum.w};
+    float t[4] = {vacc.x, vacc.y, vacc.z, vacc.w};
+    float c[2] = {csum.x, csum.y};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x0, x1;
-      row_swap<32>(t0[e], t0[e], x0, x1);
-      t0[e] = x0 + x1;
-      row_swap<32>(t1[e], t1[e], x0, x1);
-      t1[e] = x0 + x1;
+      row_swap<32>(t[e], t[e], x0, x1);
+      t[e] = x0 + x1;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float x0, x1;
       row_swap<32>(c[e], c[e], x0, x1);
       c[e] = x0 + x1;
     }
     if (hf == 0) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sVr[w][0][4 * r + e] = t0[e];
-        sVr[w][1][4 * r + e] = t1[e];
-        sC[w][4 * r + e] = c[e];
-      }
+      for (int e = 0; e < 4; ++e) sVr[pr][mh][4 * r + e] = hasv ? t[e] : 0.f;
+      sC[pr][mcol] = c[0];
+      sC[pr][mcol + 1] = c[1];
     }
   }
   __syncthreads();
   float* P = a.part + (int64_t)blockIdx.x * kPT * kPT;
-  for (int idx = tid; idx < kPT * kPT / 4; idx += 256) {
+  for (int idx = tid; idx < kPT * kPT / 4; idx += 64 * kTnWaves) {
     const int m = idx >> 5, k4 = (idx & 31) * 4;
     st4(P + m * kPT + k4, *reinterpret_cast<const float4*>(&sR[m][k4]));
   }
-  {
+  if (tid < 2 * kPT) {
     const int v = tid >> 7, k = tid & 127;
     a.vpart[((int64_t)blockIdx.x * 2 + v) * kPT + k] =
         ((sVr[0][v][k] + sVr[1][v][k]) + sVr[2][v][k]) + sVr[3][v][k];
-    if (a.cpart && tid < kPT)
-      a.cpart[(int64_t)blockIdx.x * kPT + tid] = ((sC[0][tid] + sC[1][tid]) + sC[2][tid]) + sC[3][tid];
+  } else if (a.cpart && tid < 3 * kPT) {
+    const int m = tid - 2 * kPT;
+    a.cpart[(int64_t)blockIdx.x * kPT + m] = ((sC[0][m] + sC[1][m]) + sC[2][m]) + sC[3][m];
   }
 }
 
@@ -736,9 +771,9 @@ bool tn128_shape_ok(int M, int K, int nv, const float* V, int64_t ldv) {
 }
 
 static int64_t tn_blocks(int64_t N) {
-  int64_t b = 256;                     // one workgroup (4 waves) per CU
-  const int64_t min_rows = 16;         // >= 16 rows per wave
-  while (b > 1 && b * 4 * min_rows > N) b /= 2;
+  int64_t b = 256;                     // one workgroup (4 wave pairs) per CU
+  const int64_t min_rows = 16;         // >= 16 rows per pair
+  while (b > 1 && b * (kTnWaves / 2) * min_rows > N) b /= 2;
   return b;
 }
 
@@ -762,18 +797,17 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
   a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.B1 = B1 ? B1 : B; a.ldb1 = B1 ? ldb1 : ldb; a.split = B1 ? split : N;
   a.V = nv > 0 ? V : A; a.ldv = nv > 0 ? ldv : lda; a.nv = nv; a.n = N;
   a.M = M; a.K = K;
-  const int64_t waves = nb * 4;
-  a.rows_per_wave = ((N + waves - 1) / waves + 1) / 2 * 2;
+  const int64_t pairs = nb * (kTnWaves / 2);
+  a.rows_per_pair = ((N + pairs - 1) / pairs + 1) / 2 * 2;
   a.part = reinterpret_cast<float*>(p);
   a.vpart = reinterpret_cast<float*>(p + align_up((size_t)nb * kPT * kPT * 4));
   a.cpart = colsum ? reinterpret_cast<float*>(p + align_up((size_t)nb * kPT * kPT * 4) +
                                               align_up((size_t)nb * 2 * kPT * 4))
                    : nullptr;
   const bool mask = M != kPT || K != kPT;
-  const bool v2 = nv == 2 && (a.ldv % 2) == 0 && (reinterpret_cast<uintptr_t>(a.V) % 8) == 0;
-  const int NVk = nv == 0 ? 0 : (nv == 1 || !v2) ? 1 : 2;
-  if (nv == 2 && !v2) return hipErrorInvalidValue;  // caller guarantees 8-byte aligned V pairs
-#define PPGAT_TN(NV_, MASK_) hipLaunchKernelGGL((k_tn128<NV_, MASK_>), dim3((unsigned)nb), dim3(256), 0, st, a)
+  const int NVk = nv;
+#define PPGAT_TN(NV_, MASK_) \
+  hipLaunchKernelGGL((k_tn128<NV_, MASK_>), dim3((unsigned)nb), dim3(64 * kTnWaves), 0, st, a)
   if (mask) {
     if (NVk == 0) PPGAT_TN(0, true); else if (NVk == 1) PPGAT_TN(1, true); else PPGAT_TN(2, true);
   } else {
@@ -819,3 +853,20 @@ hipError_t adam_step(int count, float* const* p, const float* const* g, float* c
 }
 
 }  // namespace ppgat
+
+#if PPGAT_CLOCK_PROBE
+// median over waves of (shader cycles / real time) in MHz for slot 0 (k_proj16) / 1 (k_tn128)
+extern "C" int ppgat_debug_clock_mhz(int slot, int waves, double* mhz) {
+  static unsigned long long h[2][4096][2];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(ppgat::g_probe), sizeof(h)) != hipSuccess) return 3;
+  double v[4096];
+  int n = 0;
+  for (int w = 0; w < waves && w < 4096; ++w)
+    if (h[slot][w][1] > 0) v[n++] = (double)h[slot][w][0] / (double)h[slot][w][1] * 100.0;
+  if (n == 0) return 1;
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && v[j - 1] > v[j]; --j) { const double t = v[j]; v[j] = v[j - 1]; v[j - 1] = t; }
+  *mhz = v[n / 2];
+  return 0;
+}
+#endif

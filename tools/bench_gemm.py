@@ -63,7 +63,15 @@ def main():
             continue
         res[k] = timeit(fn, args.iters)
     flop = 2 * N * 128 * 128
-    print(json.dumps({k: {"us": v, "tflops": flop / v / 1e6} for k, v in res.items()}, indent=1))
+    out = {k: {"us": v, "tflops": flop / v / 1e6} for k, v in res.items()}
+    if hasattr(lib, "ppgat_debug_clock_mhz"):  # diagnostic build (-DPPGAT_CLOCK_PROBE=1)
+        import ctypes
+        lib.ppgat_debug_clock_mhz.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        for slot, name in ((0, "proj16"), (1, "tn128")):
+            mhz = ctypes.c_double(0.0)
+            if lib.ppgat_debug_clock_mhz(slot, 4096, ctypes.byref(mhz)) == 0:
+                out[f"clock_mhz_{name}"] = mhz.value
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
