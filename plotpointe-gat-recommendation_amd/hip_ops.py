@@ -8,6 +8,7 @@ fp32/int64 ROCm tensor of the expected shape -- there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -361,6 +362,73 @@ def weight_grads(G, GV, W, a_s, a_d, heads: int, C: int):
     return dW, datt_src, datt_dst
 
 
+# ---------------------------------------------------------------------------
+# weight gradients on a side stream
+# ---------------------------------------------------------------------------
+# A layer's dW = D^T x (+ S^T x) is independent of everything the backward does after it
+# (dx, the next layer's edge passes), so it can run on a second HIP stream, overlapping the
+# memory-bound edge kernels of the layer below.  Off by default (PPGAT_ASYNC_WGRAD=1 turns it
+# on): at config 2 the persistent GEMM grid holds whole CUs the edge kernels then lack, and
+# the step measured 2.47 ms against 2.42 ms in order (profiles/r01/v10_async_wgrad_bench.log).
+# The main stream waits for it
+# in a callback queued on the autograd engine, which runs once the whole backward pass has
+# been enqueued -- before anything (optimizer, host reads) can consume the gradients.  Only
+# used when the parameters' .grad are None and carry no hooks: accumulating into an existing
+# .grad, or a hook, would read the gradient on the main stream before it exists.
+_SIDE_STREAMS = {}
+_PENDING_JOINS = []
+
+
+def _async_wgrad_enabled() -> bool:
+    return os.environ.get("PPGAT_ASYNC_WGRAD", "0") == "1"
+
+
+def _grad_free(params) -> bool:
+    for p in params:
+        if p is None:
+            continue
+        if p.grad is not None or getattr(p, "_backward_hooks", None) or \
+                getattr(p, "_post_accumulate_grad_hooks", None):
+            return False
+    return True
+
+
+def _join_side_streams():
+    while _PENDING_JOINS:
+        main, ev = _PENDING_JOINS.pop()
+        main.wait_event(ev)
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _SIDE_STREAMS[dev.index] = s
+    return s
+
+
+def _run_on_side(dev, inputs, fn):
+    """fn() on the side stream after the main stream's work so far; returns fn's tensors,
+    registered for use on the main stream, with the join queued on the autograd engine."""
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    for t in inputs:
+        if t is not None and t.numel() > 0:
+            t.record_stream(side)
+    with torch.cuda.stream(side):
+        outs = fn()
+    for t in outs:
+        if t is not None:
+            t.record_stream(main)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    if not _PENDING_JOINS:
+        torch.autograd.Variable._execution_engine.queue_callback(_join_side_streams)
+    _PENDING_JOINS.append((main, ev))
+    return outs
+
+
 class GATLayer(torch.autograd.Function):
     """One whole GAT layer x -> out with the projection inside:
     forward  h = x W^T with the node scores fused (ppgat_project; BLAS + ppgat_node_scores
@@ -403,6 +471,7 @@ class GATLayer(torch.autograd.Function):
             ctx.save_for_backward(x, x_items if x_items is not None else empty, W, h, a_s, a_d, s_src, s_dst, out, m,
                                   inv_l, agg if agg is not None else empty, b if b is not None else empty)
         ctx.graph = graph
+        ctx.params = (weight, att_src, att_dst)
         ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None, fused,
                     x_items is not None, had_items, split)
         ctx.att_shapes = (att_src.shape, att_dst.shape)
@@ -446,8 +515,14 @@ class GATLayer(torch.autograd.Function):
                 A_s = torch.einsum("hc,hck->hk", a_s, Wv)
                 A_d = torch.einsum("hc,hck->hk", a_d, Wv)
                 dx = torch.addmm(S @ torch.cat([A_s, A_d], 0), D, W)
-        G, _, GV = gemm_tn(D, x, V=S, B_items=xi if seg else None)
-        dW, datt_src, datt_dst = weight_grads(G, GV, W, a_s, a_d, heads, C)
+        def wgrad():
+            G, _, GV = gemm_tn(D, x, V=S, B_items=xi if seg else None)
+            return weight_grads(G, GV, W, a_s, a_d, heads, C)
+
+        if _async_wgrad_enabled() and _grad_free(ctx.params):
+            dW, datt_src, datt_dst = _run_on_side(dev, (D, S, x, xi, W, a_s, a_d), wgrad)
+        else:
+            dW, datt_src, datt_dst = wgrad()
         dx_u = dx[:split] if (dx is not None and had_items) else dx
         dx_i = dx[split:] if (dx is not None and had_items) else None
         return (dx_u, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,

@@ -126,3 +126,36 @@ def test_bpr_large_row_space(pkg, oracle, cuda):
     pkg.bpr_loss(Zd, n_users, u.to(cuda), i.to(cuda), j.to(cuda)).backward()
     oracle.bpr_loss(Z64, n_users, u, i, j).backward()
     assert rel(Zd.grad, Z64.grad) <= 1e-5
+
+
+def _two_layer_grads(pkg, cuda, steps=1, zero=True):
+    g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
+    ei = torch.from_numpy(g.edge_index_numpy()).to(cuda)
+    feats = torch.from_numpy(pkg.data.synthetic_item_features(g.n_items, 64, seed=5)).to(cuda)
+    torch.manual_seed(0)
+    model = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=64, hidden=128, layers=2, heads=1,
+                       attn_dropout=0.1).to(cuda).train()
+    u, i, j = (torch.from_numpy(a).to(cuda) for a in pkg.data.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items,
+                                                                                 20_000, seed=1))
+    for s in range(steps):
+        if zero:
+            model.zero_grad(set_to_none=True)
+        torch.manual_seed(100 + s)
+        pkg.bpr_loss(model(feats, ei), g.n_users, u, i, j).backward()
+    return {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+
+
+def test_side_stream_weight_grads_bitwise(pkg, cuda, monkeypatch):
+    """Layer weight gradients on the side stream (joined at the end of backward) equal the
+    in-order path bit for bit, read straight after backward() without a sync; a second
+    backward into existing .grad takes the in-order path (accumulation)."""
+    monkeypatch.setenv("PPGAT_ASYNC_WGRAD", "0")
+    ref = _two_layer_grads(pkg, cuda)
+    acc_ref = _two_layer_grads(pkg, cuda, steps=2, zero=False)
+    monkeypatch.setenv("PPGAT_ASYNC_WGRAD", "1")
+    got = _two_layer_grads(pkg, cuda)
+    acc = _two_layer_grads(pkg, cuda, steps=2, zero=False)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
+        assert torch.equal(acc[k], acc_ref[k]), k
+    assert pkg.hip_ops._PENDING_JOINS == []
