@@ -46,7 +46,7 @@ extern "C" {
 #define PPGAT_MODE_PYG 0
 #define PPGAT_MODE_CUSTOM 1
 
-/* Library identification. */
+/* Library identification: 2 = ppgat_schedule carries n_long_items (schedule counts int32[4]). */
 int ppgat_version(void);
 const char* ppgat_last_error(void);
 
@@ -74,9 +74,12 @@ int ppgat_csr_build(const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
  * pieces listed first (hubs in row order, pieces merged deterministically afterwards),
  * then every other row as one item in descending-degree order (longest work first).
  * Capacities: items <= ppgat_schedule_capacity(), hub_row <= N, hub_ptr <= N+1.
- * counts (device int32[3]) receives {n_hubs, n_hub_items, n_items}; the caller reads it
- * once (a one-time host sync per static graph) to fill a ppgat_schedule.
+ * counts (device int32[4]) receives {n_hubs, n_hub_items, n_items, n_long_rows}, n_long_rows
+ * = rows that are not hubs and have more than PPGAT_SHORT_ITEM_EDGES edges; the caller
+ * reads it once (a one-time host sync per static graph) to fill a ppgat_schedule, with
+ * n_long_items = n_hub_items + n_long_rows.
  */
+#define PPGAT_SHORT_ITEM_EDGES 16
 typedef struct ppgat_schedule {
   const int32_t* item_row;  /* [n_items] row (dst for CSR, src for CSC) */
   const int32_t* item_beg;  /* [n_items] first edge slot */
@@ -86,6 +89,9 @@ typedef struct ppgat_schedule {
   const int32_t* hub_row;   /* [n_hubs] */
   const int32_t* hub_ptr;   /* [n_hubs+1] piece (= item) ranges per hub */
   int64_t n_hubs;
+  int64_t n_long_items;     /* items [0, n_long_items) have > PPGAT_SHORT_ITEM_EDGES edges; the
+                               rest (descending degree) are run four per wavefront (heads = 1).
+                               -1: unknown (every item takes the one-per-wavefront path) */
 } ppgat_schedule;
 
 int64_t ppgat_schedule_capacity(int64_t n_nodes, int64_t n_edges, int32_t max_edges);

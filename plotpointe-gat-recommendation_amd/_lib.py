@@ -21,7 +21,8 @@ c_int, c_i64, c_u64, c_f, c_vp, c_sz = (ctypes.c_int, ctypes.c_int64, ctypes.c_u
 class Schedule(ctypes.Structure):
     """include/ppgat.h ppgat_schedule"""
     _fields_ = [("item_row", c_vp), ("item_beg", c_vp), ("item_end", c_vp), ("n_items", c_i64),
-                ("n_hub_items", c_i64), ("hub_row", c_vp), ("hub_ptr", c_vp), ("n_hubs", c_i64)]
+                ("n_hub_items", c_i64), ("hub_row", c_vp), ("hub_ptr", c_vp), ("n_hubs", c_i64),
+                ("n_long_items", c_i64)]
 
 
 SP = ctypes.POINTER(Schedule)

@@ -89,7 +89,7 @@ struct Timed {
 
 extern "C" {
 
-int ppgat_version(void) { return 1; }
+int ppgat_version(void) { return 2; }
 
 const char* ppgat_last_error(void) { return g_err.c_str(); }
 
@@ -148,10 +148,13 @@ int ppgat_schedule_build(const int32_t* ptr, int64_t n_nodes, int64_t n_edges, i
   return PPGAT_OK;
 }
 
+static_assert(ppgat::kShortItemEdges == PPGAT_SHORT_ITEM_EDGES, "short-item bound");
+
 static int check_sched(const ppgat_schedule* s, int64_t n_nodes, const char* who) {
   if (!s) return fail(PPGAT_ERR_INVALID, std::string(who) + ": null schedule");
   if (s->n_items < 0 || s->n_hub_items < 0 || s->n_hubs < 0 || s->n_hub_items > s->n_items ||
-      s->n_items < n_nodes - s->n_hubs)
+      s->n_items < n_nodes - s->n_hubs ||
+      (s->n_long_items != -1 && (s->n_long_items < s->n_hub_items || s->n_long_items > s->n_items)))
     return fail(PPGAT_ERR_INVALID, std::string(who) + ": inconsistent schedule counts");
   if (s->n_items > 0 && (!s->item_row || !s->item_beg || !s->item_end))
     return fail(PPGAT_ERR_INVALID, std::string(who) + ": null schedule arrays");
@@ -209,7 +212,8 @@ int ppgat_fwd(const ppgat_schedule* sched, const int32_t* col, const int32_t* cs
     return fail(PPGAT_ERR_INVALID, "fwd: workspace too small");
   const float eps = mode == PPGAT_MODE_PYG ? 1e-16f : 1e-9f;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const ppgat::ItemsArg it{sched->item_row, sched->item_beg, sched->item_end, sched->n_items, sched->n_hub_items};
+  const ppgat::ItemsArg it{sched->item_row, sched->item_beg, sched->item_end, sched->n_items, sched->n_hub_items,
+                           sched->n_long_items};
   Timed t(PPGAT_K_FWD, st);
   hipError_t e = ppgat::launch_fwd(it, col, csr_eid, heads, channels, h, s_src, s_dst, bias, mode, negative_slope,
                                    eps, dropout_p, seed, out, m, inv_l, agg, static_cast<float*>(workspace),
@@ -269,7 +273,7 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
   const float gscale = mode == PPGAT_MODE_PYG ? 1.f / (float)heads : 1.f;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const ppgat::ItemsArg it{src_sched->item_row, src_sched->item_beg, src_sched->item_end, src_sched->n_items,
-                           src_sched->n_hub_items};
+                           src_sched->n_hub_items, src_sched->n_long_items};
   hipError_t e;
   {
     Timed t(PPGAT_K_BWD_SRC, st);
@@ -293,7 +297,7 @@ int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int head
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_BWD_EPI, st);
   const ppgat::ItemsArg it{fwd_sched->item_row, fwd_sched->item_beg, fwd_sched->item_end, fwd_sched->n_items,
-                           fwd_sched->n_hub_items};
+                           fwd_sched->n_hub_items, fwd_sched->n_long_items};
   hipError_t e = ppgat::launch_dst_sum(it, heads, dz, ds_dst, ld_ds_dst, static_cast<float*>(workspace),
                                        fwd_sched->hub_row, fwd_sched->hub_ptr, fwd_sched->n_hubs, st);
   if (e != hipSuccess) return hip_fail(e, "bwd_dst_sum");

@@ -125,19 +125,27 @@ hipError_t csr_build(const int64_t* ei, int64_t E, int64_t N, int32_t* rowptr, i
 // ---------------------------------------------------------------------------
 // Work schedule for the fused edge kernels (see ppgat_kernels.hip "Work items"):
 // rows with deg > T become ceil(deg/T) hub pieces, listed first (hubs in row order);
-// the other rows follow in descending degree (stable).  counts = {n_hubs, n_hub_items, n_items}.
+// the other rows follow in descending degree (stable).
+// counts = {n_hubs, n_hub_items, n_items, non-hub rows with more than kShortItemEdges edges}.
 // ---------------------------------------------------------------------------
 int64_t schedule_capacity(int64_t N, int64_t E, int32_t T) { return N + (E + T - 1) / T + 1; }
 
 __global__ void k_sched_keys(const int32_t* __restrict__ ptr, int64_t N, int32_t T, int32_t* __restrict__ key,
                              int32_t* __restrict__ iota, int32_t* __restrict__ counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  const int32_t deg = ptr[i + 1] - ptr[i];
-  const bool hub = deg > T;
-  key[i] = hub ? 0 : (T + 1 - deg);
-  iota[i] = (int32_t)i;
-  if (hub) atomicAdd(&counts[0], 1);
+  const int32_t deg = i < N ? ptr[i + 1] - ptr[i] : 0;
+  const bool hub = i < N && deg > T;
+  const bool lng = i < N && !hub && deg > kShortItemEdges;
+  if (i < N) {
+    key[i] = hub ? 0 : (T + 1 - deg);
+    iota[i] = (int32_t)i;
+  }
+  // one atomic per wave and counter (tens of thousands of rows count as long)
+  const uint64_t bh = __ballot(hub), bl = __ballot(lng);
+  if ((threadIdx.x & 63) == 0) {
+    if (bh) atomicAdd(&counts[0], (int32_t)__popcll(bh));
+    if (bl) atomicAdd(&counts[3], (int32_t)__popcll(bl));
+  }
 }
 
 __global__ void k_sched_np(const int32_t* __restrict__ order, const int32_t* __restrict__ ptr, int64_t N, int32_t T,
@@ -204,7 +212,7 @@ hipError_t schedule_build(const int32_t* ptr, int64_t N, int32_t T, int32_t* ite
                           int32_t* item_end, int32_t* hub_row, int32_t* hub_ptr, int32_t* counts, void* ws,
                           size_t ws_bytes, hipStream_t st) {
   if (T < 1 || T >= (1 << 20) - 2 || ws_bytes < schedule_workspace_bytes(N)) return hipErrorInvalidValue;
-  hipError_t err = hipMemsetAsync(counts, 0, 3 * sizeof(int32_t), st);
+  hipError_t err = hipMemsetAsync(counts, 0, 4 * sizeof(int32_t), st);
   if (err != hipSuccess) return err;
   err = hipMemsetAsync(hub_ptr, 0, sizeof(int32_t), st);
   if (err != hipSuccess) return err;

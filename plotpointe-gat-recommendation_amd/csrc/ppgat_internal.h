@@ -10,6 +10,7 @@ constexpr int kModePyg = 0;
 constexpr int kModeCustom = 1;
 constexpr int kMaxHeads = 8;
 constexpr int64_t kEpiMaxBlocks = 1024;
+constexpr int kShortItemEdges = 16;  // include/ppgat.h PPGAT_SHORT_ITEM_EDGES
 
 // host-side view of a work schedule (see include/ppgat.h ppgat_schedule)
 struct ItemsArg {
@@ -18,6 +19,7 @@ struct ItemsArg {
   const int32_t* end;
   int64_t n_items;
   int64_t n_hub_items;
+  int64_t n_long_items;  // -1: unknown (no four-per-wave short-item path)
 };
 
 hipError_t launch_scores(const float* h, const float* as, const float* ad, int64_t n, int heads, int C, float* ss,

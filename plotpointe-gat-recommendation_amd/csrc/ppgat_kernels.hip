@@ -29,6 +29,10 @@
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
 
+#ifndef PPGAT_SHORT_U
+#define PPGAT_SHORT_U 4  // neighbour rows in flight per short item (per 16-lane row)
+#endif
+
 namespace ppgat {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -209,6 +213,88 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
   if (sg == 0) st4(out + i * C + sl * 4, osum);
+}
+
+// ---------------------------------------------------------------------------
+// Short items (<= kShortItemEdges edges, heads = 1): four items per wave, one per 16-lane
+// row of the wave.  With one item per wave a short row leaves the wave waiting on a chain
+// of dependent loads (item -> edge -> node terms -> neighbour rows) for a handful of
+// edges; four per wave put four times the neighbour rows in flight (4 rows x 4 items per
+// wave).  Lane ql of a 16-lane row takes the edge rs + ql for the softmax terms (16-lane
+// DPP reductions) and the float4 columns ql, ql + 16, ... of every neighbour row.
+// ---------------------------------------------------------------------------
+constexpr int kSU = PPGAT_SHORT_U;
+static_assert(kSU == 4 || kSU == 8 || kSU == 16, "short-item unroll");
+
+template <int C>
+__global__ void __launch_bounds__(256) k_fwd_short(Items it, int64_t first, const int32_t* __restrict__ col,
+                                                   const int32_t* __restrict__ eid, const float* __restrict__ h,
+                                                   const float* __restrict__ s_src, const float* __restrict__ s_dst,
+                                                   const float* __restrict__ bias, int mode, float slope, float eps,
+                                                   float p, float inv_keep, uint64_t seed, float* __restrict__ out,
+                                                   float* __restrict__ m_out, float* __restrict__ invl_out,
+                                                   float* __restrict__ agg_out) {
+  constexpr int NV = C / 64;  // float4 columns per lane
+  static_assert(NV >= 1, "k_fwd_short: C >= 64");
+  __shared__ int2 rec[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int qr = lane >> 4, ql = lane & 15;
+  const int64_t item = first + ((int64_t)blockIdx.x * 4 + wv) * 4 + qr;
+  const bool live = item < it.n_items;
+  const int64_t ic = live ? item : first;
+  const int64_t i = it.row[ic];
+  const int rs = it.beg[ic], re = live ? it.end[ic] : rs;
+  const bool pyg = mode == kModePyg;
+  const int k = rs + ql;
+  const bool valid = k < re;
+  const int j = valid ? col[k] : 0;
+  const float e = valid ? logit(s_src[j] + s_dst[i], slope, mode) : -INFINITY;
+  float m = 0.f, pe;
+  if (pyg) {
+    m = group_reduce<Op::Max, 1, 8>(e);
+    pe = valid ? expf(e - m) : 0.f;
+  } else {
+    pe = valid ? expf(e) : 0.f;
+  }
+  const float l = group_reduce<Op::Sum, 1, 8>(pe);
+  float pw = pe;
+  if (p > 0.f && valid) pw *= drop_scale(seed, (uint32_t)eid[k], 0u, p, inv_keep);
+  rec[wv][lane] = make_int2(j, __float_as_int(pw));
+  wave_sync();
+  const int2* rq = &rec[wv][qr * 16];
+  const int n = re - rs;
+  float4 acc[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) acc[c] = f4(0.f);
+  for (int t0 = 0; t0 < n; t0 += kSU) {
+    float4 v[kSU][NV];
+    float wt[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int t = t0 + u;
+      const int2 r = rq[t & 15];
+      wt[u] = t < n ? __int_as_float(r.y) : 0.f;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) v[u][c] = t < n ? ld4(h + (int64_t)r.x * C + (ql + 16 * c) * 4) : f4(0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kSU; ++u)
+#pragma unroll
+      for (int c = 0; c < NV; ++c) acc[c] = fma4(wt[u], v[u][c], acc[c]);
+  }
+  if (!live) return;
+  const float invl = 1.f / (l + eps);
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col4 = (ql + 16 * c) * 4;
+    const float4 a = mul4(acc[c], invl);
+    if (agg_out != nullptr) st4(agg_out + i * C + col4, a);
+    st4(out + i * C + col4, bias != nullptr ? add4(a, ld4(bias + col4)) : a);
+  }
+  if (ql == 0) {
+    m_out[i] = (pyg && re > rs) ? m : 0.f;
+    invl_out[i] = invl;
+  }
 }
 
 // Merge the pieces of each hub row.  One wave per hub row: the piece maxima and
@@ -429,6 +515,98 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
     if (sg == 0) st4(dh + j * ld_dh + hd * C + sl * 4, acc);
     if (lane == 0) ds_src[j * ld_ds + hd] = ds;
   }
+}
+
+// Pass B for short items (<= kShortItemEdges edges, heads = 1): four source rows per wave,
+// one per 16-lane row, as k_fwd_short.  Lane ql builds the record of edge rs + ql and, after
+// the 16-lane reduction of <g_i, h_j> for its edge, writes that edge's dz.
+template <int C>
+__global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, const int32_t* __restrict__ row,
+                                                       const int32_t* __restrict__ csc_eid,
+                                                       const int32_t* __restrict__ csc2csr,
+                                                       const float* __restrict__ h, const float* __restrict__ s_src,
+                                                       const float4* __restrict__ nstate,
+                                                       const float* __restrict__ grad_out, int mode, float slope,
+                                                       float gscale, float p, float inv_keep, uint64_t seed,
+                                                       float* __restrict__ dh, int64_t ld_dh,
+                                                       float* __restrict__ ds_src, int64_t ld_ds,
+                                                       float* __restrict__ dz) {
+  constexpr int NV = C / 64;
+  static_assert(NV >= 1, "k_bwd_src_short: C >= 64");
+  __shared__ int2 rec[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int qr = lane >> 4, ql = lane & 15;
+  const int64_t item = first + ((int64_t)blockIdx.x * 4 + wv) * 4 + qr;
+  const bool live = item < it.n_items;
+  const int64_t ic = live ? item : first;
+  const int64_t j = it.row[ic];
+  const int rs = it.beg[ic], re = live ? it.end[ic] : rs;
+  const float ss = s_src[j];
+  float4 hv[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) hv[c] = ld4(h + j * C + (ql + 16 * c) * 4);
+  const int k = rs + ql;
+  const bool valid = k < re;
+  const int i = valid ? row[k] : 0;
+  float bg = 0.f, c1 = 0.f, c0 = 0.f;
+  int slot = 0;
+  if (valid) {
+    const float4 st = nstate[i];  // {s_dst, m, inv_l, D}
+    const float z = ss + st.x;
+    const float af = expf(logit(z, slope, mode) - st.y) * st.z;
+    const float dm = p > 0.f ? drop_scale(seed, (uint32_t)csc_eid[k], 0u, p, inv_keep) : 1.f;
+    slot = csc2csr[k];
+    bg = af * dm * gscale;
+    const float a1 = af * dlogit(z, slope, mode);
+    c1 = a1 * dm * gscale;
+    c0 = a1 * st.w;
+  }
+  rec[wv][lane] = make_int2(i, __float_as_int(bg));
+  wave_sync();
+  const int2* rq = &rec[wv][qr * 16];
+  const int n = re - rs;
+  float4 acc[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) acc[c] = f4(0.f);
+  float ds = 0.f;
+  for (int t0 = 0; t0 < n; t0 += kSU) {
+    float4 g[kSU][NV];
+    float bq[kSU], part[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int t = t0 + u;
+      const int2 r = rq[t & 15];
+      bq[u] = t < n ? __int_as_float(r.y) : 0.f;
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        g[u][c] = t < n ? ld4(grad_out + (int64_t)r.x * C + (ql + 16 * c) * 4) : f4(0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      part[u] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        acc[c] = fma4(bq[u], g[u][c], acc[c]);
+        part[u] += dot4(g[u][c], hv[c]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) part[u] = group_reduce<Op::Sum, 1, 8>(part[u]);
+    const int my = ql - t0;
+    if (valid && my >= 0 && my < kSU) {
+      float dot = part[0];
+#pragma unroll
+      for (int u = 1; u < kSU; ++u) dot = my == u ? part[u] : dot;
+      const float dzv = fmaf(c1, dot, -c0);
+      ds += dzv;
+      dz[slot] = dzv;
+    }
+  }
+  ds = group_reduce<Op::Sum, 1, 8>(ds);
+  if (!live) return;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) st4(dh + j * ld_dh + (ql + 16 * c) * 4, acc[c]);
+  if (ql == 0) ds_src[j * ld_ds] = ds;
 }
 
 // ---------------------------------------------------------------------------
@@ -795,17 +973,39 @@ hipError_t launch_scores(const float* h, const float* as, const float* ad, int64
   return hipGetLastError();
 }
 
+// First item of the four-per-wave short path, or n_items when every item takes the
+// one-per-wave kernel (heads > 1, C < 64, or a schedule without n_long_items).
+static int64_t short_begin(const ItemsArg& it, int heads, int C) {
+  if (heads != 1 || (C != 64 && C != 128 && C != 256)) return it.n_items;
+  if (it.n_long_items < it.n_hub_items || it.n_long_items > it.n_items) return it.n_items;
+  return it.n_long_items;
+}
+
+#define PPGAT_DISPATCH_C64(C, ...)                             \
+  do {                                                         \
+    if ((C) == 64) { constexpr int CC = 64; __VA_ARGS__; }     \
+    else if ((C) == 128) { constexpr int CC = 128; __VA_ARGS__; } \
+    else { constexpr int CC = 256; __VA_ARGS__; }              \
+  } while (0)
+
 hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, int heads, int C,
                       const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
                       float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
                       float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                       hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const Items its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-  if (it.n_items > 0) {
-    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its, col,
+  const int64_t n_long = short_begin(it, heads, C);
+  const Items its{it.row, it.beg, it.end, n_long, it.n_hub_items};
+  if (n_long > 0) {
+    PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd<CC>, dim3(blocks_for(n_long * 64)), dim3(256), 0, st, its, col,
                                            eid, heads, h, ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m,
                                            invl, agg, partial));
+  }
+  if (n_long < it.n_items) {
+    const Items all{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+    const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16);  // 4 waves x 4 items per block
+    PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_fwd_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, col, eid, h,
+                                             ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m, invl, agg));
   }
   if (n_hubs > 0) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,
@@ -831,20 +1031,28 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
                           float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
                           const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const Items its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-  if (it.n_items > 0) {
+  const int64_t n_long = short_begin(it, heads, C);
+  const Items its{it.row, it.beg, it.end, n_long, it.n_hub_items};
+  if (n_long < it.n_items) {
+    const Items all{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+    const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16);
+    PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_bwd_src_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, row,
+                                             csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go,
+                                             mode, slope, gscale, p, inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz));
+  }
+  if (n_long > 0) {
     const bool mh = heads > 1 && C >= 32 && (heads == 2 || heads == 4 || heads == 8);
     if (mh) {  // every head of an edge in one pass (one grad_out gather per edge)
 #define PPGAT_MH(HH)                                                                                           \
   PPGAT_DISPATCH_C(C, if constexpr (CC >= 32) {                                                             \
-    hipLaunchKernelGGL((k_bwd_src_mh<CC, HH>), dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its, row,   \
+    hipLaunchKernelGGL((k_bwd_src_mh<CC, HH>), dim3(blocks_for(n_long * 64)), dim3(256), 0, st, its, row,      \
                        csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, \
                        p, inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial);                             \
   })
       if (heads == 2) { PPGAT_MH(2); } else if (heads == 4) { PPGAT_MH(4); } else { PPGAT_MH(8); }
 #undef PPGAT_MH
     } else {
-      PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(it.n_items * 64)), dim3(256), 0, st, its,
+      PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(n_long * 64)), dim3(256), 0, st, its,
                                              row, csc_eid, csc2csr, heads, h, ss,
                                              reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, p,
                                              inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial));

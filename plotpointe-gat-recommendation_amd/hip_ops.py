@@ -50,15 +50,16 @@ class Schedule:
     n_hub_items: int
     n_hubs: int
     max_edges: int
+    n_long_items: int = -1  # items [0, n_long_items) have > 16 edges (-1: unknown)
 
     def cstruct(self) -> "_lib.Schedule":
         return _lib.Schedule(self.item_row.data_ptr(), self.item_beg.data_ptr(), self.item_end.data_ptr(),
                              self.n_items, self.n_hub_items, self.hub_row.data_ptr(), self.hub_ptr.data_ptr(),
-                             self.n_hubs)
+                             self.n_hubs, self.n_long_items)
 
 
 def schedule_build(ptr: torch.Tensor, n_edges: int, max_edges: int = MAX_EDGES_PER_ITEM) -> Schedule:
-    """Work items over ptr[N+1] (one host sync to read the three counts)."""
+    """Work items over ptr[N+1] (one host sync to read the four counts)."""
     lib = _lib.load()
     _check_dev("ptr", ptr, torch.int32)
     N = ptr.numel() - 1
@@ -71,7 +72,7 @@ def schedule_build(ptr: torch.Tensor, n_edges: int, max_edges: int = MAX_EDGES_P
     item_end = torch.empty(max(cap, 1), **i32)
     hub_row = torch.empty(max(N, 1), **i32)
     hub_ptr = torch.empty(N + 1, **i32)
-    counts = torch.empty(3, **i32)
+    counts = torch.empty(4, **i32)
     nbytes = ctypes.c_size_t(0)
     _lib.check(lib.ppgat_schedule_workspace_bytes(N, ctypes.byref(nbytes)), "schedule_workspace_bytes")
     ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
@@ -79,8 +80,9 @@ def schedule_build(ptr: torch.Tensor, n_edges: int, max_edges: int = MAX_EDGES_P
                                         item_beg.data_ptr(), item_end.data_ptr(), hub_row.data_ptr(),
                                         hub_ptr.data_ptr(), counts.data_ptr(), ws.data_ptr(), nbytes.value,
                                         _lib.stream_handle(dev)), "schedule_build")
-    n_hubs, n_hub_items, n_items = (int(v) for v in counts.cpu().tolist())
-    return Schedule(item_row, item_beg, item_end, hub_row, hub_ptr, n_items, n_hub_items, n_hubs, max_edges)
+    n_hubs, n_hub_items, n_items, n_long_rows = (int(v) for v in counts.cpu().tolist())
+    return Schedule(item_row, item_beg, item_end, hub_row, hub_ptr, n_items, n_hub_items, n_hubs, max_edges,
+                    n_hub_items + n_long_rows)
 
 
 @dataclass

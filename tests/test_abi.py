@@ -24,7 +24,7 @@ def test_all_header_symbols_exported(pkg):
 
 def test_version_and_channels(pkg):
     lib = pkg._lib.load()
-    assert lib.ppgat_version() == 1
+    assert lib.ppgat_version() == 2
     assert [c for c in range(1, 300) if lib.ppgat_supported_channels(c)] == [4, 8, 16, 32, 64, 128, 256]
 
 

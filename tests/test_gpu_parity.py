@@ -54,6 +54,8 @@ def test_schedule_bit_exact(pkg, oracle, cuda, T):
         for sched, ptr in ((g.fwd_sched, g.rowptr), (g.bwd_sched, g.colptr)):
             row, beg, end, hub_row, hub_ptr, nhi = oracle.work_schedule(ptr.cpu().numpy(), T)
             assert sched.n_items == len(row) and sched.n_hub_items == nhi and sched.n_hubs == len(hub_row)
+            deg = np.diff(ptr.cpu().numpy().astype(np.int64))
+            assert sched.n_long_items == nhi + int(((deg <= T) & (deg > 16)).sum())
             k = sched.n_items
             assert np.array_equal(sched.item_row[:k].cpu().numpy(), row)
             assert np.array_equal(sched.item_beg[:k].cpu().numpy(), beg)

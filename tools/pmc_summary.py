@@ -15,9 +15,12 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_fwd<": "fwd", "k_bwd_src<": "bwd_src", "k_bwd_epi<": "bwd_epi", "k_bwd_pro<": "bwd_pro",
+KERNELS = {"k_fwd<": "fwd_long", "k_fwd_short<": "fwd_short", "k_bwd_src<": "bwd_src_long",
+           "k_bwd_src_short<": "bwd_src_short", "k_bwd_epi<": "bwd_epi", "k_bwd_pro<": "bwd_pro",
            "k_scores<": "scores", "k_gemm_tn": "gemm_tn", "k_bpr_chunks<": "bpr_chunks", "k_bpr_fwd<": "bpr_fwd",
-           "k_proj<0>": "proj_fwd", "k_proj<1>": "proj_dx", "k_tn128<": "tn128", "k_adam": "adam"}
+           "k_proj16<0>": "proj_fwd", "k_proj16<1>": "proj_dx", "k_tn128<": "tn128", "k_adam": "adam"}
+# one edge pass = its one-item-per-wave kernel + its four-items-per-wave short-item kernel
+PASSES = {"fwd": ("fwd_long", "fwd_short"), "bwd_src": ("bwd_src_long", "bwd_src_short")}
 
 
 def load(d, counter):
@@ -47,6 +50,9 @@ def main():
         w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
         res["raw_kib"][k] = {"fetch": f, "write": w, "launches": len(fetch.get(k, []))}
         res["per_launch_bytes"][k] = (2 * f + w) * 1024
+    for k, parts in PASSES.items():
+        if any(q in res["per_launch_bytes"] for q in parts):
+            res["per_launch_bytes"][k] = sum(res["per_launch_bytes"].get(q, 0.0) for q in parts)
     json.dump(res, open(out, "w"), indent=2)
     print(json.dumps(res, indent=2))
 
