@@ -9,7 +9,10 @@ namespace ppgat {
 constexpr int kModePyg = 0;
 constexpr int kModeCustom = 1;
 constexpr int kMaxHeads = 8;
-constexpr int64_t kEpiMaxBlocks = 1024;
+#ifndef PPGAT_EPI_BLOCKS
+#define PPGAT_EPI_BLOCKS 1024
+#endif
+constexpr int64_t kEpiMaxBlocks = PPGAT_EPI_BLOCKS;
 constexpr int kShortItemEdges = 16;  // include/ppgat.h PPGAT_SHORT_ITEM_EDGES
 
 // host-side view of a work schedule (see include/ppgat.h ppgat_schedule)

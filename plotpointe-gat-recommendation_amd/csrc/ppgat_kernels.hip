@@ -29,6 +29,9 @@
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
 
+#ifndef PPGAT_PRO_UP
+#define PPGAT_PRO_UP 4
+#endif
 #ifndef PPGAT_SHORT_U
 #define PPGAT_SHORT_U 4  // neighbour rows in flight per short item (per 16-lane row)
 #endif
@@ -378,7 +381,7 @@ __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_
                                                  float* __restrict__ bias_part) {
   using G = Geo<C>;
   constexpr int SPB = 256 / G::LPR;
-  constexpr int UP = 4;  // pairs per subgroup per iteration (8 row loads in flight)
+  constexpr int UP = PPGAT_PRO_UP;  // pairs per subgroup per iteration (2 UP row loads in flight)
   __shared__ float4 red[SPB][G::LPR];
   const int sg = threadIdx.x / G::LPR, sl = threadIdx.x % G::LPR;
   float4 bsum = f4(0.f);
