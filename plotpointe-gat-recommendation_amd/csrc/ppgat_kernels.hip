@@ -929,8 +929,7 @@ __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const floa
     for (; k < re; k += 16) x0 += dz[(int64_t)k * heads + hd];
   }
   float x = (x0 + x1) + (x2 + x3);
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  x = group_reduce<Op::Sum, 1, 8>(x);  // the 16 lanes of a DPP row
   if (live && l == 0) {
     if (w < it.n_hub_items) partial[w * heads + hd] = x;
     else ds_dst[(int64_t)it.row[w] * ld + hd] = x;

@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include "ppgat_internal.h"
+#include "ppgat_lanes.h"
 
 namespace ppgat {
 
@@ -83,11 +84,8 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
       }
       if (bad != nullptr && sl == 0 && oob) atomicAdd(bad, 1);  // indices were clamped; the caller raises
     }
-#pragma unroll
-    for (int off = LPR / 2; off > 0; off >>= 1) {
-      pos += __shfl_xor(pos, off);
-      neg += __shfl_xor(neg, off);
-    }
+    pos = group_reduce<Op::Sum, 1, LPR / 2>(pos);  // DPP / permlane steps, no LDS round trips
+    neg = group_reduce<Op::Sum, 1, LPR / 2>(neg);
     if (sl == 0 && valid && skip) coef[t] = make_float2(0.f, 0.f);
     if (sl == 0 && valid && !skip) {
       float l;
