@@ -98,9 +98,13 @@ def _check(res, ref):
     assert _rel(res["user_grad"], grads["user_emb.weight"]) <= 1e-5
     # vector-valued grads (att_*, bias, item_proj.bias) are sums over every node with
     # cancellation, and the two sides sum in different orders: same 1e-4 bound as the
-    # attention-vector grads of test_gpu_parity.py
+    # attention-vector grads of test_gpu_parity.py against the oracle.  Here BOTH sides are
+    # fp32 sums in different orders, so their errors vs the exact value can add: 2x that
+    # bound for the attention vectors (measured 1.2e-4 on convs.1.att_dst once the
+    # destination-sum reductions changed order; each side stays within 1e-4 of the oracle)
     for k, v in res["grads"].items():
-        assert _rel(v, grads[k]) <= (1e-5 if v.dim() == 2 and "att" not in k else 1e-4), k
+        tol = 1e-5 if v.dim() == 2 and "att" not in k else (2e-4 if "att" in k else 1e-4)
+        assert _rel(v, grads[k]) <= tol, k
 
 
 @pytest.mark.parametrize("heads,segmented", [(1, True), (2, False)])
