@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
+    ap.add_argument("--partition", choices=["auto", "replicated", "rows"], default="auto",
+                    help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
+                         "'rows' = users and items row-sharded with all_gather halos (dist.build_dist_graph); "
+                         "auto = replicated for configs 2/3, rows for config 5")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the N>1 flow with "
                          "several ranks on one GPU (tests/test_gpu_dist.py)")
@@ -165,8 +169,15 @@ def main():
     torch.manual_seed(42)
     full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=feats_np.shape[1], hidden=args.hidden, layers=args.layers,
                       heads=args.heads, attn_dropout=args.attn_dropout).to(dev)
-    if world > 1:
-        # row-sharded graph over the ranks (dist.py): strong scaling of the fixed config-2 job
+    part = args.partition if args.partition != "auto" else ("rows" if args.config == 5 else "replicated")
+    if world > 1 and part == "replicated":
+        # strong scaling of the fixed config-2 job: users sharded, the 63k item rows on every
+        # rank, every edge homed with its user; item rows merged by all_reduce (dist.py)
+        comm = pkg.dist.Comm()
+        dg = pkg.dist.build_replicated_graph(ei, N, g.n_users, world, rank)
+        model = pkg.dist.ReplicatedPyGGAT(full, dg, comm)
+    elif world > 1:
+        # row-sharded graph over the ranks (dist.py)
         comm = pkg.dist.Comm()
         # users and items partitioned separately: every rank holds a slice of both, so the
         # loss only gathers item rows (dist.sharded_bpr_loss)
@@ -182,7 +193,8 @@ def main():
         model.train()
         if world > 1:
             Z = model(feats)
-            loss = pkg.dist.sharded_bpr_loss(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
+            loss_fn = pkg.dist.replicated_bpr_loss if part == "replicated" else pkg.dist.sharded_bpr_loss
+            loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
             opt.zero_grad(set_to_none=True)
             loss.backward()
             model.allreduce_grads()
@@ -262,8 +274,10 @@ def main():
         "config": {"workload": workload,
                    "edges": E, "nodes": N, "layers": args.layers, "heads": H, "hidden": C,
                    "bpr_samples": args.samples, "attn_dropout": args.attn_dropout,
-                   "parallelism": f"row-sharded x{world} (RCCL all_gather/reduce_scatter)" if world > 1
-                   else "single"},
+                   "parallelism": ("single" if world == 1 else
+                                   f"user-sharded x{world}, item rows replicated (RCCL all_reduce)"
+                                   if part == "replicated" else
+                                   f"row-sharded x{world} (RCCL all_gather/reduce_scatter)")},
         "fused_kernel_edges_per_sec": E * args.layers * K / (fused_ms / 1e3) if fused_ms else None,
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -83,15 +83,15 @@ class Comm:
         dist.reduce_scatter_tensor(out, t, group=self.group)
         return out
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
         if self.world == 1:
             return t
         if self._host(t):
             h = t.cpu()
-            dist.all_reduce(h, group=self.group)
+            dist.all_reduce(h, op=op, group=self.group)
             t.copy_(h)
             return t
-        dist.all_reduce(t, group=self.group)
+        dist.all_reduce(t, op=op, group=self.group)
         return t
 
 
@@ -425,3 +425,216 @@ def gather_rows_to_global(Z_local, dg: DistGraph, comm: Comm) -> torch.Tensor:
     """[R, C] own rows -> [N, C] in node-id order (every rank gets the full matrix)."""
     Z_full = comm.all_gather_rows(Z_local.contiguous())
     return Z_full.index_select(0, dg.row_map.to(torch.int64))
+
+
+# ---------------------------------------------------------------------------
+# replicated-item partition: users sharded, the (small) item segment on every rank
+# ---------------------------------------------------------------------------
+# The U-I graph is bipartite (train_gat_pyg.py:139-147: every column joins a user and an
+# item).  Sharding only the users and keeping every item row on every rank gives each
+# edge exactly one home -- the owner of its user endpoint -- with every row it touches
+# local, so no node features are gathered at all:
+#   forward : user destinations are complete locally; an item destination sees the in-edges
+#             of the rank's users only, so its softmax is split over the ranks.  Each rank
+#             runs the fused kernel on its local graph, then the item rows are merged
+#             exactly: all_reduce(MAX) of the per-rank maxima, all_reduce(SUM) of
+#             [c_r * agg_r | c_r] with c_r = l_r * exp(m_r - m) (the log-sum-exp merge of
+#             the hub pieces in ppgat_fwd, across ranks).  The merged rows (and their m,
+#             1/l) are bitwise identical on every rank.
+#   backward: item-row gradients arrive as per-rank partial sums (each rank's loss covers
+#             its own users' triples; each rank's edges feed its share of dx), so each
+#             layer's backward starts with one all_reduce of the item rows of grad_out;
+#             after that every quantity of the layer backward is a sum over the rank's own
+#             edges (dh, ds_src, ds_dst of item rows, datt, dW) and is left partial for
+#             the next all_reduce (item rows) or the dense-gradient all_reduce.
+# Per layer and step: 2 all_reduces of n_items x (C+1) floats (32.5 MB at config 2)
+# against 2 all_gathers of N x C (131 MB) for the row-sharded scheme above.  Item-item
+# columns (config 3's kNN relation) have no user endpoint: they go to the rank owning the
+# destination item's contiguous share.  User-user columns would need a user halo and are
+# refused.
+@dataclass
+class RepGraph:
+    world: int
+    rank: int
+    n_nodes: int
+    n_edges: int
+    n_users: int
+    n_items: int
+    user_bounds: np.ndarray     # [world + 1] user-id range bounds
+    RU: int                     # user rows per rank (padded to the largest share)
+    view: LocalView             # local CSR/CSC over [RU user rows | n_items item rows]
+    loss_map: torch.Tensor      # [N] int32: node id -> local row, -1 for other ranks' users
+    item_live: torch.Tensor     # [n_items] bool: item rows with local in-edges
+    bounds: np.ndarray = None   # = user_bounds (the DistGraph field the tests read)
+
+    @property
+    def R(self) -> int:
+        return self.RU + self.n_items
+
+    def owned_users(self, n_users: int, rank: Optional[int] = None):
+        r = self.rank if rank is None else rank
+        return int(self.user_bounds[r]), int(self.user_bounds[r + 1])
+
+
+def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,
+                           csr_builder: Callable = _hip_csr, sched_builder: Optional[Callable] = _hip_sched,
+                           node_weight: float = 4.0) -> RepGraph:
+    """Every rank calls this with the same global edge_index (LongTensor [2, E], node ids
+    users [0, n_users), items [n_users, N)); users are cut into `world` contiguous ranges
+    balanced by degree + node_weight.  Deterministic: all ranks agree on every array."""
+    dev = edge_index.device
+    N, nu = int(n_nodes), int(n_users)
+    ni = N - nu
+    E = int(edge_index.size(1))
+    src, dst = edge_index[0], edge_index[1]
+    su, du = src < nu, dst < nu
+    if bool((su & du).any()):
+        raise NotImplementedError("replicated-item partition: user-user columns need a user halo")
+    uend = torch.where(su, src, dst)
+    deg = torch.bincount(uend[su | du], minlength=nu).cpu().numpy().astype(np.float64)
+    ub = partition_bounds(deg + node_weight, world)
+    RU = int(np.max(np.diff(ub))) if nu else 0
+    ub_t = torch.from_numpy(ub).to(dev)
+    owner = torch.bucketize(uend, ub_t[1:-1], right=True)            # the user endpoint's rank
+    ii_owner = torch.div((dst - nu).clamp_min(0) * world, max(ni, 1), rounding_mode="floor")
+    owner = torch.where(su | du, owner, ii_owner)
+    local = torch.nonzero(owner == rank).squeeze(1)
+    u0, u1 = int(ub[rank]), int(ub[rank + 1])
+    rm = np.full(N, -1, np.int64)
+    rm[u0:u1] = np.arange(u1 - u0)
+    rm[nu:] = RU + np.arange(ni)
+    row_map = torch.from_numpy(rm).to(dev)
+    R = RU + ni
+    ei_l = row_map[edge_index[:, local]]
+    El = int(local.numel())
+    G = csr_builder(ei_l, R)
+    lid = local.to(torch.int32)
+    orig = (lambda t: lid[t.long()].contiguous()) if El else (lambda t: t[:0].contiguous())
+    view = LocalView(R, G.rowptr.contiguous(), G.col[:El].contiguous(), orig(G.csr_eid[:El]), El,
+                     G.colptr.contiguous(), G.row[:El].contiguous(), orig(G.csc_eid[:El]),
+                     G.csc2csr[:El].contiguous(), El)
+    if sched_builder is not None:
+        view.fwd_sched = sched_builder(view.rowptr, El)
+        view.bwd_sched = sched_builder(view.colptr, El)
+    rp = G.rowptr.to(torch.int64)
+    item_live = (rp[RU + 1:] - rp[RU:-1]) > 0
+    return RepGraph(world, rank, N, E, nu, ni, ub, RU, view, row_map.to(torch.int32), item_live, ub)
+
+
+def _merge_item_rows(rg: RepGraph, comm: Comm, out, m, inv_l, agg, bias, heads: int, C: int):
+    """Exact cross-rank softmax merge of the item destination rows (PyG mode, eps 1e-16),
+    in place on out / m / inv_l / agg."""
+    eps = 1e-16
+    RU = rg.RU
+    live = rg.item_live[:, None]
+    mi = m[RU:]
+    mx = torch.where(live, mi, torch.full_like(mi, -float("inf")))
+    comm.all_reduce_(mx, dist.ReduceOp.MAX)
+    c = torch.where(live, (1.0 / inv_l[RU:] - eps) * torch.exp(mi - torch.where(live, mx, mi)), torch.zeros_like(mi))
+    if agg is not None:
+        a = agg[RU:]
+    else:
+        a = (out[RU:] - bias if bias is not None else out[RU:]).view(-1, 1, C)
+    pack = torch.cat([a * c[..., None], c[..., None]], -1).contiguous()   # [n_items, H, C + 1]
+    comm.all_reduce_(pack)
+    L = pack[..., C]
+    ag = pack[..., :C] / (L + eps)[..., None]
+    inv_l[RU:] = 1.0 / (L + eps)
+    m[RU:] = torch.where(L > 0, mx, torch.zeros_like(mx))
+    if agg is not None:
+        agg[RU:] = ag
+    o = ag.mean(1)
+    out[RU:] = o + bias if bias is not None else o
+
+
+class _ReplicatedGAT(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, att_src, att_dst, bias, rg: RepGraph, comm: Comm, stages, heads: int, C: int, mode: int,
+                slope: float, p: float, seed: int):
+        h = h.contiguous()
+        a_s = att_src.detach().reshape(heads, C).contiguous()
+        a_d = att_dst.detach().reshape(heads, C).contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        s_src, s_dst = stages.scores(h, a_s, a_d, heads, C)
+        out, m, inv_l, agg = stages.fwd(rg.view, h, s_src, s_dst, b, heads, C, mode, slope, p, seed, heads > 1)
+        if comm.world > 1:
+            _merge_item_rows(rg, comm, out, m, inv_l, agg, b, heads, C)
+        if any(ctx.needs_input_grad[:4]):
+            empty = torch.empty(0, device=h.device)
+            ctx.save_for_backward(h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg if agg is not None else empty,
+                                  b if b is not None else empty)
+        ctx.rg, ctx.comm, ctx.stages = rg, comm, stages
+        ctx.meta = (heads, C, mode, slope, p, seed, bias is not None, agg is not None)
+        ctx.att_shapes = (att_src.shape, att_dst.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg, b = ctx.saved_tensors
+        heads, C, mode, slope, p, seed, has_bias, has_agg = ctx.meta
+        rg, comm, st = ctx.rg, ctx.comm, ctx.stages
+        RU = rg.RU
+        g = g.contiguous()
+        if comm.world > 1:  # item rows: per-rank partial sums -> the full gradient on every rank
+            g = g.clone()
+            gi = g[RU:].contiguous()
+            comm.all_reduce_(gi)
+            g[RU:] = gi
+        nstate, _ = st.bwd_prologue(g, out, agg if has_agg else None, b if has_bias else None, s_dst, m, inv_l,
+                                    heads, C, mode, False)
+        dz = torch.zeros(max(rg.view.n_bwd_edges, 1) * heads, dtype=h.dtype, device=h.device)
+        grad_h, ds_src = st.bwd_edges(rg.view, h, s_src, nstate, g, dz, heads, C, mode, slope, p, seed)
+        datt_src, datt_dst = st.bwd_epilogue(rg.view, h, a_s, a_d, ds_src, dz, grad_h, heads, C)
+        dbias = None
+        if has_bias and ctx.needs_input_grad[3]:
+            dbias = g[:RU].sum(0)  # own users; the replicated item rows are counted on rank 0 only
+            if comm.rank == 0:
+                dbias = dbias + g[RU:].sum(0)
+        return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None, None, None, None)
+
+
+class ReplicatedPyGGAT(ShardedPyGGAT):
+    """PyGGAT with the users sharded and the item rows replicated (see above).  Local rows:
+    [own users | pad to RU | every item]; ``forward`` returns them (Z's item rows are the
+    same on every rank)."""
+
+    def node_features(self, item_feats):
+        rg = self.dg
+        parts = [self.user_emb_local]
+        pad = rg.RU - (self.u1 - self.u0)
+        if pad > 0:
+            parts.append(self.user_emb_local.new_zeros(pad, self.user_emb_local.size(1)))
+        parts.append(self.stages.linear(item_feats.contiguous(), self.item_proj.weight, self.item_proj.bias))
+        return torch.cat(parts, 0)
+
+    def forward(self, item_feats):
+        x = self.node_features(item_feats)
+        for conv in self.convs:
+            h = self.stages.linear(x, conv.lin.weight, None)
+            p = float(conv.dropout) if self.training else 0.0
+            seed = _dropout_seed() if p > 0 else 0
+            x = _ReplicatedGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, self.dg, self.comm, self.stages,
+                                     conv.heads, conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p,
+                                     seed)
+        return x
+
+
+def replicated_bpr_loss(Z_local, rg: RepGraph, comm: Comm, u, i, j, n_users: int, n_items: int,
+                        loss: str = "bpr", stages=None):
+    """The BPR/BCE loss of train_gat_pyg.py:313-322: each rank takes the triples of its own
+    users against its (replicated) item rows -- no exchange; the ranks' values add up to
+    the reference's mean loss and their item-row gradients are partial sums (merged by the
+    next layer backward's all_reduce)."""
+    if stages is None:
+        from .hip_ops import HipStages
+        stages = HipStages()
+    return stages.bpr(Z_local, n_users, n_items, rg.loss_map, u, i, j, loss)
+
+
+def replicated_rows_to_global(Z_local, rg: RepGraph, comm: Comm) -> torch.Tensor:
+    """[RU + n_items, C] local rows -> [N, C] in node-id order (every rank gets it)."""
+    users = comm.all_gather_rows(Z_local[:rg.RU].contiguous())
+    ub = rg.user_bounds
+    idx = np.concatenate([r * rg.RU + np.arange(ub[r + 1] - ub[r]) for r in range(rg.world)]).astype(np.int64)
+    return torch.cat([users.index_select(0, torch.from_numpy(idx).to(users.device)), Z_local[rg.RU:]], 0)

@@ -44,6 +44,8 @@ def _sharded(rank, world, out_dir, heads, segmented=True):
     pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads)
     D = pkg.dist
     comm = D.Comm()
+    if segmented == "replicated":
+        return _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, (u, i, j), comm)
     segs = [(0, g.n_users), (g.n_users, g.n_nodes)] if segmented else None
     dg = D.build_dist_graph(ei, g.n_nodes, world, rank, segments=segs)
     model = D.ShardedPyGGAT(full, dg, comm).train()
@@ -63,6 +65,33 @@ def _sharded(rank, world, out_dir, heads, segmented=True):
     rows = [ug[r * dg.R: r * dg.R + (min(int(dg.bounds[r + 1]), g.n_users) - min(int(dg.bounds[r]), g.n_users))]
             for r in range(world)]
     if rank == 0:
+        torch.save({"Z": Zg.cpu(), "loss": tot.cpu(), "grads": grads, "user_grad": torch.cat(rows)},
+                   os.path.join(out_dir, f"sharded_{world}.pt"))
+
+
+def _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, uij, comm):
+    """Users sharded, item rows on every rank (dist.build_replicated_graph)."""
+    D = pkg.dist
+    u, i, j = uij
+    rg = D.build_replicated_graph(ei, g.n_nodes, g.n_users, world, rank)
+    model = D.ReplicatedPyGGAT(full, rg, comm).train()
+    torch.manual_seed(123)
+    Z = model(feats)
+    loss = D.replicated_bpr_loss(Z, rg, comm, u, i, j, g.n_users, g.n_items)
+    loss.backward()
+    model.allreduce_grads()
+    tot = loss.detach().clone()
+    comm.all_reduce_(tot)
+    Zg = D.replicated_rows_to_global(Z.detach(), rg, comm)
+    items = comm.all_gather_rows(Z.detach()[rg.RU:].contiguous()).view(world, g.n_items, -1)
+    grads = {n: p.grad.detach().cpu() for n, p in model.named_parameters() if n != "user_emb_local"}
+    blk = torch.zeros(rg.RU, model.user_emb_local.size(1), device=dev)
+    blk[:model.u1 - model.u0] = model.user_emb_local.grad
+    ug = comm.all_gather_rows(blk).cpu()
+    ub = rg.user_bounds
+    rows = [ug[r * rg.RU: r * rg.RU + int(ub[r + 1] - ub[r])] for r in range(world)]
+    if rank == 0:
+        assert all(torch.equal(items[r], items[0]) for r in range(world)), "item replicas differ"
         torch.save({"Z": Zg.cpu(), "loss": tot.cpu(), "grads": grads, "user_grad": torch.cat(rows)},
                    os.path.join(out_dir, f"sharded_{world}.pt"))
 
@@ -107,7 +136,7 @@ def _check(res, ref):
         assert _rel(v, grads[k]) <= tol, k
 
 
-@pytest.mark.parametrize("heads,segmented", [(1, True), (2, False)])
+@pytest.mark.parametrize("heads,segmented", [(1, True), (2, False), (1, "replicated"), (2, "replicated")])
 def test_sharded_world1_rccl(cuda, tmp_path, heads, segmented):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
@@ -119,7 +148,7 @@ def test_sharded_world1_rccl(cuda, tmp_path, heads, segmented):
     _check(torch.load(tmp_path / "sharded_1.pt", weights_only=False), _unsharded(cuda, heads))
 
 
-@pytest.mark.parametrize("segmented", [True, False])
+@pytest.mark.parametrize("segmented", [True, False, "replicated"])
 def test_sharded_world2_shared_gpu(cuda, tmp_path, segmented):
     mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), 1, segmented), nprocs=2, join=True,
                        start_method="spawn")
@@ -142,4 +171,4 @@ def test_bench_two_ranks_rehearsal(cuda, tmp_path):
     assert len(lines) == 1, p.stdout[-2000:]
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["scaling"] == "strong" and res["value"] > 0
-    assert res["config"]["parallelism"].startswith("row-sharded x2")
+    assert res["config"]["parallelism"].startswith("user-sharded x2")
