@@ -57,6 +57,11 @@ def parse():
                     help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
                          "'rows' = users and items row-sharded with all_gather halos (dist.build_dist_graph); "
                          "auto = replicated for configs 2/3, rows for config 5")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="capture the training step once in a hipGraph and replay it (auto: on for N>1 over RCCL, "
+                         "where the per-rank step is short enough for host launch overhead to dominate)")
+    ap.add_argument("--dist-at-1", action="store_true",
+                    help="rehearsal: run the N>1 code path (process group, partition, collectives) with one rank")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the N>1 flow with "
                          "several ranks on one GPU (tests/test_gpu_dist.py)")
@@ -136,7 +141,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dist_path = world > 1 or args.dist_at_1
+    if args.dist_at_1:
+        os.environ.setdefault("PPGAT_COMM_ALWAYS", "1")
+        for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517")):
+            os.environ.setdefault(k, v)
+    if dist_path:
         import torch.distributed as dist
         local = local if args.dist_backend == "nccl" else 0  # gloo rehearsal: ranks share GPU 0
         torch.cuda.set_device(local)
@@ -170,13 +180,13 @@ def main():
     full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=feats_np.shape[1], hidden=args.hidden, layers=args.layers,
                       heads=args.heads, attn_dropout=args.attn_dropout).to(dev)
     part = args.partition if args.partition != "auto" else ("rows" if args.config == 5 else "replicated")
-    if world > 1 and part == "replicated":
+    if dist_path and part == "replicated":
         # strong scaling of the fixed config-2 job: users sharded, the 63k item rows on every
         # rank, every edge homed with its user; item rows merged by all_reduce (dist.py)
         comm = pkg.dist.Comm()
         dg = pkg.dist.build_replicated_graph(ei, N, g.n_users, world, rank)
         model = pkg.dist.ReplicatedPyGGAT(full, dg, comm)
-    elif world > 1:
+    elif dist_path:
         # row-sharded graph over the ranks (dist.py)
         comm = pkg.dist.Comm()
         # users and items partitioned separately: every rank holds a slice of both, so the
@@ -187,11 +197,15 @@ def main():
         model = full
         pkg.graph_cache.get(ei, N)  # one-time CSR/CSC build (not timed)
     # same Adam update as train_gat_pyg.py:299 (lr 1e-3, L2 1e-4): libppgat's device Adam (optim.py)
-    opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    use_graph = (args.graph == "on" or
+                 (args.graph == "auto" and dist_path and args.dist_backend == "nccl" and world > 1))
+    opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=use_graph)
 
     def step():
         model.train()
-        if world > 1:
+        if use_graph:
+            _lib.dropout_advance(dev)  # fresh dropout masks on every replay
+        if dist_path:
             Z = model(feats)
             loss_fn = pkg.dist.replicated_bpr_loss if part == "replicated" else pkg.dist.sharded_bpr_loss
             loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
@@ -206,24 +220,57 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
+    graph = None
+    if use_graph:
+        # warm up on a side stream (allocator pools, RCCL communicators, lazy inits), then
+        # capture one whole step -- forward, loss, backward, collectives, Adam -- and replay it
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            loss_static = step()
+        graph.replay()  # the capture itself ran nothing: one replay so every rank starts from a replayed step
+        torch.cuda.synchronize()
+    else:
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     _lib.profile_reset()
-    _lib.profile_enable(True)
-    if world > 1:
+    _lib.profile_enable(graph is None)  # per-kernel events in eager mode only (not capturable)
+    if dist_path:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        if graph is not None:
+            graph.replay()
+        else:
+            loss = step()
     t_host = time.perf_counter() - t0  # host time to enqueue the K steps (launch overhead check)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_path:
         torch.distributed.barrier()
     el = time.perf_counter() - t0
     _lib.profile_enable(False)
-    if world > 1:
+    kern_src = "HIP events on the launch stream inside the timed region"
+    if graph is not None:
+        loss = loss_static
+        # graph replays carry no per-kernel events: time the same step eagerly for the
+        # kernel breakdown and the roofline (after the timed region; not part of value)
+        torch.cuda.synchronize()
+        _lib.profile_reset()
+        _lib.profile_enable(True)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        _lib.profile_enable(False)
+        kern_src = "HIP events, eager replay of the same step after the timed graph replays"
+    if dist_path:
         tt = torch.tensor([el], dtype=torch.float64)
         tt = tt.to(dev) if args.dist_backend == "nccl" else tt
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -274,10 +321,12 @@ def main():
         "config": {"workload": workload,
                    "edges": E, "nodes": N, "layers": args.layers, "heads": H, "hidden": C,
                    "bpr_samples": args.samples, "attn_dropout": args.attn_dropout,
-                   "parallelism": ("single" if world == 1 else
+                   "parallelism": ("single" if not dist_path else
                                    f"user-sharded x{world}, item rows replicated (RCCL all_reduce)"
                                    if part == "replicated" else
                                    f"row-sharded x{world} (RCCL all_gather/reduce_scatter)")},
+        "hip_graph": graph is not None,
+        "kernel_timing": kern_src,
         "fused_kernel_edges_per_sec": E * args.layers * K / (fused_ms / 1e3) if fused_ms else None,
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -290,7 +339,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(g, feats_np, C, args.layers, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_path:
         torch.distributed.destroy_process_group()
 
 

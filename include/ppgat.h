@@ -270,6 +270,24 @@ int ppgat_adam_step(int count, float* const* params, const float* const* grads, 
                     float* const* exp_avg_sq, const int64_t* numel, const float* step_size,
                     const float* bias_correction2_sqrt, double beta1, double beta2, float eps, float weight_decay,
                     void* stream);
+/* Graph-capturable variant: the step count t is read on the device from *step (a float the
+ * caller increments on the same stream before the launch), step_size = lr / (1 - beta1^t)
+ * and bias_correction2_sqrt = sqrt(1 - beta2^t) are formed in double in the kernel and
+ * rounded once -- the values the host path passes.  Same replacement as ppgat_adam_step
+ * (torch.optim.Adam(capturable=True) semantics); one launch per <= max_tensors tensors. */
+int ppgat_adam_step_device(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                           float* const* exp_avg_sq, const int64_t* numel, const float* step, double lr, double beta1,
+                           double beta2, float eps, float weight_decay, void* stream);
+
+/* ---- dropout epoch (hipGraph replays) ------------------------------------------------------
+ * Every dropout mask of ppgat_fwd / ppgat_bwd_edges uses seed' = seed + epoch * 0xD1B54A32D192ED03
+ * (mod 2^64), epoch a device-side counter (0 at load: seeds are used as passed).  A training
+ * step captured once in a hipGraph bakes its host seeds in; enqueueing ppgat_dropout_advance
+ * at the top of the captured step gives every replay fresh masks (the reference draws new
+ * F.dropout masks per call, train_gat_pyg.py:77 attn dropout).  Stream-ordered.
+ * Replaces: nothing in the reference (eager PyTorch draws from its generator each call). */
+int ppgat_dropout_advance(void* stream);
+int ppgat_dropout_set_epoch(uint64_t epoch, void* stream);
 
 /* ---- I-I kNN graph (config 3's second relation) ------------------------------------
  * Replaces: the per-item selection loop of graphs/build_ii_knn.py:76-99 (self excluded as

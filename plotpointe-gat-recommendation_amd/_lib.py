@@ -74,6 +74,10 @@ SIGNATURES = {
     "ppgat_adam_max_tensors": (c_int, []),
     "ppgat_adam_step": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
                                 c_f, c_f, c_vp]),
+    "ppgat_adam_step_device": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, c_f, c_f, c_vp]),
+    "ppgat_dropout_advance": (c_int, [c_vp]),
+    "ppgat_dropout_set_epoch": (c_int, [ctypes.c_uint64, c_vp]),
     "ppgat_knn_max_k": (c_int, []),
     "ppgat_knn_topk": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_bpr_sampler_workspace_bytes": (c_int, [c_i64, c_i64, ctypes.POINTER(c_sz)]),
@@ -157,3 +161,19 @@ def profile_read(kernel: str):
     n = ctypes.c_int64(0)
     check(lib.ppgat_profile_read(KERNELS[kernel], ctypes.byref(ms), ctypes.byref(n)), "profile_read")
     return ms.value, n.value
+
+
+def dropout_advance(device=None):
+    """Enqueue the dropout-epoch increment (include/ppgat.h ppgat_dropout_advance) on the
+    current stream: call once at the top of a training step that is captured in a graph."""
+    import torch
+    lib = load()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    check(lib.ppgat_dropout_advance(stream_handle(dev)), "dropout_advance")
+
+
+def dropout_set_epoch(epoch: int, device=None):
+    import torch
+    lib = load()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    check(lib.ppgat_dropout_set_epoch(int(epoch) & (2**64 - 1), stream_handle(dev)), "dropout_set_epoch")

@@ -545,8 +545,40 @@ int ppgat_adam_step(int count, float* const* params, const float* const* grads, 
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_ADAM, st);
   hipError_t e = ppgat::adam_step(count, params, grads, exp_avg, exp_avg_sq, numel, step_size, bias_correction2_sqrt,
-                                  beta1, beta2, eps, weight_decay, st);
+                                  beta1, beta2, eps, weight_decay, nullptr, 0.0, st);
   if (e != hipSuccess) return hip_fail(e, "adam_step");
+  return PPGAT_OK;
+}
+
+int ppgat_adam_step_device(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                           float* const* exp_avg_sq, const int64_t* numel, const float* step, double lr, double beta1,
+                           double beta2, float eps, float weight_decay, void* stream) {
+  if (count < 0 || count > ppgat::adam_max_tensors())
+    return fail(PPGAT_ERR_INVALID, "adam_step_device: bad tensor count");
+  if (count > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel || !step))
+    return fail(PPGAT_ERR_INVALID, "adam_step_device: null pointer");
+  for (int t = 0; t < count; ++t) {
+    if (numel[t] < 0) return fail(PPGAT_ERR_INVALID, "adam_step_device: negative numel");
+    if (numel[t] > 0 && (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t]))
+      return fail(PPGAT_ERR_INVALID, "adam_step_device: null tensor");
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_ADAM, st);
+  hipError_t e = ppgat::adam_step(count, params, grads, exp_avg, exp_avg_sq, numel, nullptr, nullptr, beta1, beta2,
+                                  eps, weight_decay, step, lr, st);
+  if (e != hipSuccess) return hip_fail(e, "adam_step_device");
+  return PPGAT_OK;
+}
+
+int ppgat_dropout_advance(void* stream) {
+  hipError_t e = ppgat::dropout_epoch(0, 0, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "dropout_advance");
+  return PPGAT_OK;
+}
+
+int ppgat_dropout_set_epoch(uint64_t epoch, void* stream) {
+  hipError_t e = ppgat::dropout_epoch(1, epoch, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "dropout_set_epoch");
   return PPGAT_OK;
 }
 

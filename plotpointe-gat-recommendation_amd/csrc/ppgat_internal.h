@@ -88,9 +88,10 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
 hipError_t wgrad_assemble(const float* G, const float* GV, const float* W, const float* att_src, const float* att_dst,
                           int heads, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st);
 int adam_max_tensors();
+hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st);
 hipError_t adam_step(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
                      const int64_t* n, const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
-                     float eps, float wd, hipStream_t st);
+                     float eps, float wd, const float* tstep, double lr, hipStream_t st);
 
 // I-I kNN neighbour selection (ppgat_knn.hip)
 int knn_max_k();

@@ -68,6 +68,16 @@ __device__ __forceinline__ float dlogit(float z, float slope, int mode) {
   return d;
 }
 
+// Dropout epoch: a device-side counter folded into every dropout seed, so a step captured
+// once in a hipGraph draws fresh masks on each replay (ppgat_dropout_advance enqueues the
+// increment on the stream; 0 -- the default -- leaves the seeds as passed).  The effective
+// seed is seed + epoch * kDropEpochMul (mod 2^64), restated in oracle/gat_oracle.py.
+__device__ uint64_t g_drop_epoch = 0;
+constexpr uint64_t kDropEpochMul = 0xD1B54A32D192ED03ull;
+__device__ __forceinline__ uint64_t epoch_seed(uint64_t seed) {
+  return seed + *(volatile const uint64_t*)&g_drop_epoch * kDropEpochMul;
+}
+
 // Counter-based dropout mask on alpha (restated in oracle/gat_oracle.py:dropout_scale).
 __device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t eid, uint32_t head, float p,
                                             float inv_keep) {
@@ -143,6 +153,7 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
                                              uint64_t seed, float* __restrict__ out, float* __restrict__ m_out,
                                              float* __restrict__ invl_out, float* __restrict__ agg_out,
                                              float* __restrict__ partial) {
+  if (p > 0.f) seed = epoch_seed(seed);
   using G = Geo<C>;
   __shared__ int2 rec[4][64];  // per wave: chunk edges {src row, weight}
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -237,6 +248,7 @@ __global__ void __launch_bounds__(256) k_fwd_short(Items it, int64_t first, cons
                                                    float p, float inv_keep, uint64_t seed, float* __restrict__ out,
                                                    float* __restrict__ m_out, float* __restrict__ invl_out,
                                                    float* __restrict__ agg_out) {
+  if (p > 0.f) seed = epoch_seed(seed);
   constexpr int NV = C / 64;  // float4 columns per lane
   static_assert(NV >= 1, "k_fwd_short: C >= 64");
   __shared__ int2 rec[4][64];
@@ -439,6 +451,7 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
                                                  float gscale, float p, float inv_keep, uint64_t seed,
                                                  float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
                                                  int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
+  if (p > 0.f) seed = epoch_seed(seed);
   using G = Geo<C>;
   constexpr int GRP = G::LPR / G::U;  // lanes sharing one reduced edge value
   // per wave, per chunk edge: {dst row, beta * gscale} and {c1, c0, CSR slot}, where
@@ -534,6 +547,7 @@ __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, 
                                                        float* __restrict__ dh, int64_t ld_dh,
                                                        float* __restrict__ ds_src, int64_t ld_ds,
                                                        float* __restrict__ dz) {
+  if (p > 0.f) seed = epoch_seed(seed);
   constexpr int NV = C / 64;
   static_assert(NV >= 1, "k_bwd_src_short: C >= 64");
   __shared__ int2 rec[4][64];
@@ -660,6 +674,7 @@ __global__ void __launch_bounds__(256) k_bwd_src_mh(Items it, const int32_t* __r
                                                     float gscale, float p, float inv_keep, uint64_t seed,
                                                     float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
                                                     int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
+  if (p > 0.f) seed = epoch_seed(seed);
   using G = Geo<C>;
   static_assert(C >= 32, "k_bwd_src_mh: C >= 32");
   constexpr int U = G::U * H > 16 ? (16 / H > 0 ? 16 / H : 1) : G::U;  // <= 16 partial dots per lane
@@ -1101,6 +1116,17 @@ hipError_t launch_col_reduce(const float* partial, int64_t rows, int cols, int s
                              hipStream_t st) {
   hipLaunchKernelGGL(k_col_reduce, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, partial, rows, cols, split,
                      out_a, out_b);
+  return hipGetLastError();
+}
+
+namespace {
+__global__ void k_drop_epoch(int set, uint64_t value) {
+  if (threadIdx.x == 0) g_drop_epoch = set ? value : g_drop_epoch + 1;
+}
+}  // namespace
+
+hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st) {
+  hipLaunchKernelGGL(k_drop_epoch, dim3(1), dim3(64), 0, st, set, value);
   return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ here (a per-peer all-to-all index list would carry the same rows).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -53,13 +54,16 @@ class Comm:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.backend = dist.get_backend(group)
+        # active: run the collectives (world > 1, or PPGAT_COMM_ALWAYS=1 to rehearse the RCCL
+        # calls -- e.g. their hipGraph capture -- on a single-GPU box)
+        self.active = self.world > 1 or os.environ.get("PPGAT_COMM_ALWAYS") == "1"
 
     def _host(self, t):
         return self.backend == "gloo" and t.is_cuda
 
     def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
         t = t.contiguous()
-        if self.world == 1:
+        if not self.active:
             return t
         if self.backend == "gloo":
             src = t.cpu() if t.is_cuda else t
@@ -72,7 +76,7 @@ class Comm:
 
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
         t = t.contiguous()
-        if self.world == 1:
+        if not self.active:
             return t
         R = t.size(0) // self.world
         if self.backend == "gloo":
@@ -84,7 +88,7 @@ class Comm:
         return out
 
     def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-        if self.world == 1:
+        if not self.active:
             return t
         if self._host(t):
             h = t.cpu()
@@ -350,7 +354,7 @@ class ShardedPyGGAT(torch.nn.Module):
 
     def allreduce_grads(self):
         """One flat all-reduce of every dense parameter gradient (replicated params)."""
-        if self.comm.world == 1:
+        if not self.comm.active:
             return
         ps = self.dense_parameters()
         for p in ps:  # a rank whose block has no items never touched item_proj: its share is 0
@@ -557,7 +561,7 @@ class _ReplicatedGAT(torch.autograd.Function):
         b = bias.detach().contiguous() if bias is not None else None
         s_src, s_dst = stages.scores(h, a_s, a_d, heads, C)
         out, m, inv_l, agg = stages.fwd(rg.view, h, s_src, s_dst, b, heads, C, mode, slope, p, seed, heads > 1)
-        if comm.world > 1:
+        if comm.active:
             _merge_item_rows(rg, comm, out, m, inv_l, agg, b, heads, C)
         if any(ctx.needs_input_grad[:4]):
             empty = torch.empty(0, device=h.device)
@@ -575,7 +579,7 @@ class _ReplicatedGAT(torch.autograd.Function):
         rg, comm, st = ctx.rg, ctx.comm, ctx.stages
         RU = rg.RU
         g = g.contiguous()
-        if comm.world > 1:  # item rows: per-rank partial sums -> the full gradient on every rank
+        if comm.active:  # item rows: per-rank partial sums -> the full gradient on every rank
             g = g.clone()
             gi = g[RU:].contiguous()
             comm.all_reduce_(gi)

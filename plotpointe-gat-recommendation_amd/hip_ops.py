@@ -637,6 +637,8 @@ class _BadIndex:
 
     @classmethod
     def track(cls, bad: torch.Tensor):
+        if torch.cuda.is_current_stream_capturing():  # a captured step: no host copy / event query
+            return
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)
         host.copy_(bad, non_blocking=True)
         ev = torch.cuda.Event()
@@ -645,6 +647,8 @@ class _BadIndex:
 
     @classmethod
     def raise_pending(cls, wait: bool = False):
+        if torch.cuda.is_current_stream_capturing():
+            return
         keep = []
         for ev, host in cls.pending:
             if wait:

@@ -6,6 +6,13 @@ hyper-parameters, the same per-parameter state keys (``step``, ``exp_avg``,
 ``exp_avg_sq``) and the same update rule (L2 weight decay added to the gradient, bias
 corrections, eps after the square root), so optimizer state_dicts move between the two.
 Supported: fp32 dense tensors on one ROCm device, amsgrad=False, maximize=False.
+
+``capturable=True`` (torch.optim.Adam's flag of the same name): the step count lives on
+the device (one float per param group, shared by its parameters' ``state["step"]``) and is
+incremented and turned into the bias corrections on the stream
+(``ppgat_adam_step_device``), so ``step()`` can be captured in a hipGraph and replayed.
+All parameters of a group are assumed to step together (a parameter with no gradient is
+skipped, but the group's count still advances).
 """
 from __future__ import annotations
 
@@ -19,7 +26,7 @@ from . import _lib
 
 class Adam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 amsgrad: bool = False, maximize: bool = False):
+                 amsgrad: bool = False, maximize: bool = False, capturable: bool = False):
         if amsgrad or maximize:
             raise NotImplementedError("ppgat Adam: amsgrad / maximize not implemented")
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
@@ -27,7 +34,7 @@ class Adam(torch.optim.Optimizer):
         if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError(f"invalid betas {betas}")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
-                                      maximize=False))
+                                      maximize=False, capturable=bool(capturable)))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -40,6 +47,9 @@ class Adam(torch.optim.Optimizer):
         for group in self.param_groups:
             b1, b2 = group["betas"]
             batch = []
+            if group.get("capturable", False):
+                self._step_device(lib, cap, group)
+                continue
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -64,6 +74,43 @@ class Adam(torch.optim.Optimizer):
             if batch:
                 self._launch(lib, batch, group, b1, b2)
         return loss
+
+    def _step_device(self, lib, cap, group):
+        b1, b2 = group["betas"]
+        ps = [p for p in group["params"] if p.grad is not None]
+        if not ps:
+            return
+        tstep = None
+        for p in group["params"]:
+            st = self.state[p]
+            if "step" in st:
+                tstep = st["step"]
+                break
+        for p in ps:
+            g = p.grad
+            if g.is_sparse or not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous()
+                                   and g.dtype == torch.float32):
+                raise RuntimeError("ppgat Adam: fp32 contiguous dense ROCm parameters and gradients only")
+            st = self.state[p]
+            if len(st) == 0:
+                if tstep is None:
+                    tstep = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["step"] = tstep
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        tstep.add_(1.0)  # on the stream: graph replays advance it
+        for k in range(0, len(ps), cap):
+            chunk = ps[k:k + cap]
+            n = len(chunk)
+            dev = chunk[0].device
+            P = (ctypes.c_void_p * n)(*[p.data_ptr() for p in chunk])
+            G = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p in chunk])
+            M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in chunk])
+            V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in chunk])
+            NE = (ctypes.c_int64 * n)(*[p.numel() for p in chunk])
+            _lib.check(lib.ppgat_adam_step_device(n, P, G, M, V, NE, tstep.data_ptr(), float(group["lr"]), float(b1),
+                                                  float(b2), float(group["eps"]), float(group["weight_decay"]),
+                                                  _lib.stream_handle(dev)), "adam_step_device")
 
     @staticmethod
     def _launch(lib, batch, group, b1, b2):

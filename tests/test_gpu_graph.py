@@ -1,0 +1,125 @@
+"""hipGraph capture of the training step (bench.py --graph): the dropout epoch
+(include/ppgat.h ppgat_dropout_advance), the device-step Adam (ppgat_adam_step_device) and
+a captured forward + BPR + backward + Adam step replayed against the same step run eagerly."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def test_dropout_epoch_moves_the_seed(pkg, oracle, cuda):
+    """Under epoch e the masks are those of seed + e * 0xD1B54A32D192ED03 (oracle.epoch_seed)."""
+    from importlib import import_module
+    _lib = import_module("plotpointe-gat-recommendation_amd._lib")
+    conv_mod = import_module("plotpointe-gat-recommendation_amd.conv")
+    g = pkg.data.synthetic_ui_graph(n_users=400, n_items=150, n_interactions=4000, seed=2)
+    ei = torch.from_numpy(g.edge_index_numpy()).to(cuda)
+    torch.manual_seed(0)
+    conv = pkg.GATConv(128, 128, heads=1, concat=False, dropout=0.3, add_self_loops=False).to(cuda).train()
+    x = torch.randn(g.n_nodes, 128, device=cuda)
+    try:
+        _lib.dropout_set_epoch(0, cuda)
+        torch.manual_seed(7)
+        out0 = conv(x, ei)
+        _lib.dropout_set_epoch(5, cuda)
+        torch.manual_seed(7)
+        out5 = conv(x, ei)
+    finally:
+        _lib.dropout_set_epoch(0, cuda)
+    torch.manual_seed(7)
+    seed = conv_mod._dropout_seed()
+    ref = oracle.pyg_gat_conv(x.double().cpu(), ei.cpu(), conv.lin.weight.double().cpu(), conv.att_src.double().cpu(),
+                              conv.att_dst.double().cpu(), conv.bias.double().cpu(), 1, dropout_p=0.3,
+                              seed=oracle.epoch_seed(seed, 5))
+    assert rel(out5, ref) <= 1e-5
+    assert rel(out0, ref) > 1e-3  # a different mask
+
+
+def test_adam_device_step_matches_host(pkg, cuda):
+    torch.manual_seed(0)
+    shapes = [(1000, 128), (128,), (3, 5), (70_001,)]
+    ps_h = [torch.randn(s, device=cuda) for s in shapes]
+    ps_d = [p.clone() for p in ps_h]
+    for p in ps_h + ps_d:
+        p.requires_grad_(True)
+    oh = pkg.optim.Adam(ps_h, lr=1e-3, weight_decay=1e-4)
+    od = pkg.optim.Adam(ps_d, lr=1e-3, weight_decay=1e-4, capturable=True)
+    for k in range(4):
+        grads = [torch.randn(s, device=cuda) for s in shapes]
+        for a, b, gr in zip(ps_h, ps_d, grads):
+            a.grad, b.grad = gr.clone(), gr.clone()
+        oh.step()
+        od.step()
+    for a, b in zip(ps_h, ps_d):
+        assert rel(b, a) <= 1e-6
+    assert float(od.state[ps_d[0]]["step"]) == 4.0
+
+
+def test_graph_replay_equals_eager_steps(pkg, cuda):
+    """Warm up, snapshot, capture one step, replay it 3 times; restore the snapshot and run
+    the same 3 steps eagerly (same host seeds, same dropout epochs): same parameters."""
+    from importlib import import_module
+    _lib = import_module("plotpointe-gat-recommendation_amd._lib")
+    g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
+    ei = torch.from_numpy(g.edge_index_numpy()).to(cuda)
+    feats = torch.from_numpy(pkg.data.synthetic_item_features(g.n_items, 64, seed=5)).to(cuda)
+    torch.manual_seed(0)
+    model = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=64, hidden=128, layers=2, heads=1,
+                       attn_dropout=0.2).to(cuda).train()
+    u, i, j = (torch.from_numpy(a).to(cuda) for a in pkg.data.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items,
+                                                                                 20_000, seed=1))
+    opt = pkg.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-4, capturable=True)
+
+    def step():
+        _lib.dropout_advance(cuda)
+        loss = pkg.bpr_loss(model(feats, ei), g.n_users, u, i, j)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    try:
+        side = torch.cuda.Stream(cuda)
+        side.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream(cuda).wait_stream(side)
+        torch.cuda.synchronize()
+        snap_p = [p.detach().clone() for p in model.parameters()]
+        snap_s = {k: (v["exp_avg"].clone(), v["exp_avg_sq"].clone(), v["step"].clone()) for k, v in opt.state.items()}
+        graph = torch.cuda.CUDAGraph()
+        torch.manual_seed(99)
+        with torch.cuda.graph(graph):
+            loss_static = step()
+        _lib.dropout_set_epoch(1000, cuda)
+        losses_g = []
+        for _ in range(3):
+            graph.replay()
+            losses_g.append(float(loss_static))
+        got = [p.detach().clone() for p in model.parameters()]
+        with torch.no_grad():
+            for p, s in zip(model.parameters(), snap_p):
+                p.copy_(s)
+            for k, (m, v, t) in snap_s.items():
+                opt.state[k]["exp_avg"].copy_(m)
+                opt.state[k]["exp_avg_sq"].copy_(v)
+                opt.state[k]["step"].copy_(t)
+        _lib.dropout_set_epoch(1000, cuda)
+        losses_e = []
+        for _ in range(3):
+            torch.manual_seed(99)  # the host seeds the capture baked in
+            losses_e.append(float(step()))
+        torch.cuda.synchronize()
+    finally:
+        _lib.dropout_set_epoch(0, cuda)
+    assert len(set(losses_g)) == 3  # parameters and masks move between replays
+    np.testing.assert_allclose(losses_g, losses_e, rtol=1e-6)
+    for a, b in zip(got, model.parameters()):
+        assert rel(a, b) <= 1e-6
