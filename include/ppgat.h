@@ -279,6 +279,21 @@ int ppgat_adam_step_device(int count, float* const* params, const float* const* 
                            float* const* exp_avg_sq, const int64_t* numel, const float* step, double lr, double beta1,
                            double beta2, float eps, float weight_decay, void* stream);
 
+/* ---- replicated-item partition: cross-rank merge of item destination rows -----------------
+ * Replaces: nothing one-to-one -- in the reference every destination's softmax sees all of
+ * its in-edges (PyG softmax over edge_index, train_gat_pyg.py:77); with users sharded over
+ * ranks and the item rows replicated (dist.py), an item's in-edges are split over the ranks,
+ * so each rank's ppgat_fwd output for item rows is merged exactly (PyG mode, eps 1e-16):
+ *   phase 0: mx[i,h] = m[i,h] if row i has local in-edges else -inf      -> all_reduce(MAX, mx)
+ *   phase 1: pack = [c * a | c], c = (1/inv_l - eps) * exp(m - mx) (0 for rows without local
+ *            in-edges), a = agg (heads > 1) or out - bias (heads = 1)     -> all_reduce(SUM, pack)
+ *   phase 2: agg = pack_a / (pack_c + eps), out = mean_h agg + bias, inv_l = 1/(pack_c + eps),
+ *            m = pack_c > 0 ? mx : 0   (in place on the item rows)
+ * item_rowptr: the local CSR rowptr at the first item row (n_items + 1 entries); out/agg/m/inv_l
+ * point at the first item row; pack holds n_items*heads*(channels + 1) floats ([a] then [c]). */
+int ppgat_rep_merge(int phase, const int32_t* item_rowptr, int64_t n_items, int heads, int channels, float* out,
+                    float* agg, const float* bias, float* m, float* inv_l, float* mx, float* pack, void* stream);
+
 /* ---- dropout epoch (hipGraph replays) ------------------------------------------------------
  * Every dropout mask of ppgat_fwd / ppgat_bwd_edges uses seed' = seed + epoch * 0xD1B54A32D192ED03
  * (mod 2^64), epoch a device-side counter (0 at load: seeds are used as passed).  A training

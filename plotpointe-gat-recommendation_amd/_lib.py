@@ -77,6 +77,7 @@ SIGNATURES = {
     "ppgat_adam_step_device": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double, c_f, c_f, c_vp]),
     "ppgat_dropout_advance": (c_int, [c_vp]),
+    "ppgat_rep_merge": (c_int, [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_dropout_set_epoch": (c_int, [ctypes.c_uint64, c_vp]),
     "ppgat_knn_max_k": (c_int, []),
     "ppgat_knn_topk": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp]),

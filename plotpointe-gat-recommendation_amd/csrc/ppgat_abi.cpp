@@ -570,6 +570,22 @@ int ppgat_adam_step_device(int count, float* const* params, const float* const* 
   return PPGAT_OK;
 }
 
+int ppgat_rep_merge(int phase, const int32_t* item_rowptr, int64_t n_items, int heads, int channels, float* out,
+                    float* agg, const float* bias, float* m, float* inv_l, float* mx, float* pack, void* stream) {
+  if (phase < 0 || phase > 2) return fail(PPGAT_ERR_INVALID, "rep_merge: phase must be 0, 1 or 2");
+  if (n_items < 0 || heads < 1 || heads > ppgat::kMaxHeads || channels < 4 || channels % 4 != 0)
+    return fail(PPGAT_ERR_INVALID, "rep_merge: bad sizes");
+  if (n_items > 0 && (!item_rowptr || !out || !m || !inv_l || !mx || !pack))
+    return fail(PPGAT_ERR_INVALID, "rep_merge: null pointer");
+  if (n_items > 0 && heads > 1 && !agg) return fail(PPGAT_ERR_INVALID, "rep_merge: heads > 1 needs agg");
+  if (heads == 1) agg = nullptr;
+  float* pack_c = pack + n_items * heads * channels;
+  hipError_t e = ppgat::rep_merge(phase, item_rowptr, n_items, heads, channels, 1e-16f, out, agg, bias, m, inv_l, mx,
+                                  pack, pack_c, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "rep_merge");
+  return PPGAT_OK;
+}
+
 int ppgat_dropout_advance(void* stream) {
   hipError_t e = ppgat::dropout_epoch(0, 0, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "dropout_advance");

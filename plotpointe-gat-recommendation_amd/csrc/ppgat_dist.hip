@@ -1,0 +1,113 @@
+// ppgat_dist.hip -- cross-rank merge of the replicated item rows (dist.py, replicated-item
+// partition).  Each rank's fused forward (ppgat_fwd) leaves, for every item destination,
+// the softmax state of the in-edges it holds (those of its own users): max m_r, sum l_r
+// (as 1/(l_r + eps)) and the normalised aggregate a_r.  The exact merged row is the
+// log-sum-exp combination the single-GPU kernel forms over all in-edges:
+//   m = max_r m_r,  c_r = l_r exp(m_r - m),  L = sum_r c_r,  a = sum_r c_r a_r / (L + eps)
+//   out = mean_h a + bias,  1/l = 1 / (L + eps)
+// with the two sums taken by all_reduce(MAX) of m' and all_reduce(SUM) of [c a | c].
+// Elementwise over [n_items, heads, C]: HBM-bound, one float4 per thread.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "ppgat_internal.h"
+
+namespace ppgat {
+namespace {
+
+__device__ __forceinline__ bool live_row(const int32_t* rowptr, int64_t i) { return rowptr[i + 1] > rowptr[i]; }
+
+// phase 0: mx = live ? m : -inf
+__global__ void __launch_bounds__(256) k_rep_max(const float* __restrict__ m, const int32_t* __restrict__ rowptr,
+                                                 int64_t n, int heads, float* __restrict__ mx) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * heads) return;
+  mx[t] = live_row(rowptr, t / heads) ? m[t] : -INFINITY;
+}
+
+// phase 1: pack_a[i, h, :] = c a_r,  pack_c[i, h] = c  (after all_reduce MAX of mx).
+// One thread per float4 of the [n * heads, C] pack: consecutive threads, consecutive
+// 16-B columns (C/4 threads per (row, head)).
+__global__ void __launch_bounds__(256) k_rep_pack(const float* __restrict__ out, const float* __restrict__ agg,
+                                                  const float* __restrict__ bias, const float* __restrict__ m,
+                                                  const float* __restrict__ invl, const int32_t* __restrict__ rowptr,
+                                                  const float* __restrict__ mx, int64_t n, int heads, int C, float eps,
+                                                  float* __restrict__ pack_a, float* __restrict__ pack_c) {
+  const int Q = C / 4;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * heads * Q) return;
+  const int64_t w = t / Q;  // (row, head)
+  const int q = (int)(t % Q);
+  const int64_t i = w / heads;
+  float c = 0.f;
+  if (live_row(rowptr, i)) c = (1.f / invl[w] - eps) * expf(m[w] - mx[w]);
+  float4 v = agg != nullptr ? reinterpret_cast<const float4*>(agg + w * C)[q]
+                            : reinterpret_cast<const float4*>(out + i * C)[q];
+  if (agg == nullptr && bias != nullptr) {
+    const float4 b = reinterpret_cast<const float4*>(bias)[q];
+    v.x -= b.x; v.y -= b.y; v.z -= b.z; v.w -= b.w;
+  }
+  v.x *= c; v.y *= c; v.z *= c; v.w *= c;
+  reinterpret_cast<float4*>(pack_a + w * C)[q] = v;
+  if (q == 0) pack_c[w] = c;
+}
+
+// phase 2 (after all_reduce SUM of the pack): the merged rows; one thread per float4 of
+// the [n, C] output, looping over the heads
+__global__ void __launch_bounds__(256) k_rep_finish(const float* __restrict__ pack_a, const float* __restrict__ pack_c,
+                                                    const float* __restrict__ mx, const float* __restrict__ bias,
+                                                    int64_t n, int heads, int C, float eps, float* __restrict__ out,
+                                                    float* __restrict__ m, float* __restrict__ invl,
+                                                    float* __restrict__ agg) {
+  const int Q = C / 4;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * Q) return;
+  const int64_t i = t / Q;
+  const int q = (int)(t % Q);
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int hd = 0; hd < heads; ++hd) {
+    const int64_t w = i * heads + hd;
+    const float L = pack_c[w];
+    const float r = 1.f / (L + eps);
+    float4 v = reinterpret_cast<const float4*>(pack_a + w * C)[q];
+    v.x *= r; v.y *= r; v.z *= r; v.w *= r;
+    if (agg != nullptr) reinterpret_cast<float4*>(agg + w * C)[q] = v;
+    o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+    if (q == 0) {
+      invl[w] = r;
+      m[w] = L > 0.f ? mx[w] : 0.f;
+    }
+  }
+  if (heads > 1) {
+    const float inv_h = 1.f / (float)heads;
+    o.x *= inv_h; o.y *= inv_h; o.z *= inv_h; o.w *= inv_h;
+  }
+  if (bias != nullptr) {
+    const float4 b = reinterpret_cast<const float4*>(bias)[q];
+    o.x += b.x; o.y += b.y; o.z += b.z; o.w += b.w;
+  }
+  reinterpret_cast<float4*>(out + i * C)[q] = o;
+}
+
+}  // namespace
+
+hipError_t rep_merge(int phase, const int32_t* rowptr, int64_t n, int heads, int C, float eps, float* out, float* agg,
+                     const float* bias, float* m, float* invl, float* mx, float* pack_a, float* pack_c,
+                     hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t rows = n * heads;
+  if (phase == 0) {
+    hipLaunchKernelGGL(k_rep_max, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, m, rowptr, n, heads, mx);
+  } else if (phase == 1) {
+    const int64_t th = rows * (C / 4);
+    hipLaunchKernelGGL(k_rep_pack, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, out, agg, bias, m, invl,
+                       rowptr, mx, n, heads, C, eps, pack_a, pack_c);
+  } else {
+    const int64_t th = n * (C / 4);
+    hipLaunchKernelGGL(k_rep_finish, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, pack_a, pack_c, mx, bias,
+                       n, heads, C, eps, out, m, invl, agg);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ppgat

@@ -89,6 +89,10 @@ hipError_t wgrad_assemble(const float* G, const float* GV, const float* W, const
                           int heads, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st);
 int adam_max_tensors();
 hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st);
+// replicated-item merge (ppgat_dist.hip): phase 0 max, 1 pack, 2 finish
+hipError_t rep_merge(int phase, const int32_t* rowptr, int64_t n, int heads, int C, float eps, float* out, float* agg,
+                     const float* bias, float* m, float* invl, float* mx, float* pack_a, float* pack_c,
+                     hipStream_t st);
 hipError_t adam_step(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
                      const int64_t* n, const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
                      float eps, float wd, const float* tstep, double lr, hipStream_t st);

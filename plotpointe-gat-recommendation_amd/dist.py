@@ -362,11 +362,12 @@ class ShardedPyGGAT(torch.nn.Module):
                 p.grad = torch.zeros_like(p)
         flat = torch.cat([p.grad.reshape(-1) for p in ps])
         self.comm.all_reduce_(flat)
-        off = 0
+        views, off = [], 0
         for p in ps:
             n = p.grad.numel()
-            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            views.append(flat[off:off + n].view_as(p.grad))
             off += n
+        torch._foreach_copy_([p.grad for p in ps], views)  # one multi-tensor launch, not one copy per tensor
 
     def full_state_dict(self):
         """Reference-keyed state_dict (user_emb gathered from the owners)."""
@@ -465,11 +466,13 @@ class RepGraph:
     n_users: int
     n_items: int
     user_bounds: np.ndarray     # [world + 1] user-id range bounds
-    RU: int                     # user rows per rank (padded to the largest share)
+    RU: int                     # this rank's user rows (the top of its local row space)
+    RU_max: int                 # the largest RU over the ranks (block size of user-row gathers)
     view: LocalView             # local CSR/CSC over [RU user rows | n_items item rows]
     loss_map: torch.Tensor      # [N] int32: node id -> local row, -1 for other ranks' users
     item_live: torch.Tensor     # [n_items] bool: item rows with local in-edges
     bounds: np.ndarray = None   # = user_bounds (the DistGraph field the tests read)
+    graph: object = None        # the local view as a hip_ops.CSRGraph (fused layer path)
 
     @property
     def R(self) -> int:
@@ -497,7 +500,8 @@ def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int,
     uend = torch.where(su, src, dst)
     deg = torch.bincount(uend[su | du], minlength=nu).cpu().numpy().astype(np.float64)
     ub = partition_bounds(deg + node_weight, world)
-    RU = int(np.max(np.diff(ub))) if nu else 0
+    RU_max = int(np.max(np.diff(ub))) if nu else 0
+    RU = int(ub[rank + 1] - ub[rank])
     ub_t = torch.from_numpy(ub).to(dev)
     owner = torch.bucketize(uend, ub_t[1:-1], right=True)            # the user endpoint's rank
     ii_owner = torch.div((dst - nu).clamp_min(0) * world, max(ni, 1), rounding_mode="floor")
@@ -517,12 +521,50 @@ def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int,
     view = LocalView(R, G.rowptr.contiguous(), G.col[:El].contiguous(), orig(G.csr_eid[:El]), El,
                      G.colptr.contiguous(), G.row[:El].contiguous(), orig(G.csc_eid[:El]),
                      G.csc2csr[:El].contiguous(), El)
+    graph = None
     if sched_builder is not None:
         view.fwd_sched = sched_builder(view.rowptr, El)
         view.bwd_sched = sched_builder(view.colptr, El)
+        from .hip_ops import CSRGraph
+        graph = CSRGraph(R, El, view.rowptr, view.col, view.csr_eid, view.colptr, view.row, view.csc_eid,
+                         view.dz_slot, view.fwd_sched, view.bwd_sched)
     rp = G.rowptr.to(torch.int64)
     item_live = (rp[RU + 1:] - rp[RU:-1]) > 0
-    return RepGraph(world, rank, N, E, nu, ni, ub, RU, view, row_map.to(torch.int32), item_live, ub)
+    return RepGraph(world, rank, N, E, nu, ni, ub, RU, RU_max, view, row_map.to(torch.int32), item_live, ub, graph)
+
+
+class RepHooks:
+    """The two exchange points of the fused layer (hip_ops.GATLayer ``rep``): the item-row
+    merge after the forward kernel (ppgat_rep_merge + 2 all_reduces) and the item-row
+    all_reduce of grad_out before the backward."""
+
+    def __init__(self, rg: RepGraph, comm: Comm):
+        self.rg, self.comm = rg, comm
+        self.RU, self.rank = rg.RU, comm.rank
+
+    def merge_fwd(self, out, m, inv_l, agg, bias, heads: int, C: int):
+        if not self.comm.active:
+            return
+        lib = _lib.load()
+        rg, RU = self.rg, self.RU
+        n = rg.n_items
+        dev = out.device
+        mx = torch.empty(n, heads, dtype=torch.float32, device=dev)
+        pack = torch.empty(n * heads * (C + 1), dtype=torch.float32, device=dev)
+        rp = rg.view.rowptr[RU:]
+        args = (rp.data_ptr(), n, heads, C, out.data_ptr() + 4 * RU * C,
+                agg.data_ptr() + 4 * RU * heads * C if agg is not None else None, _lib.ptr(bias),
+                m.data_ptr() + 4 * RU * heads, inv_l.data_ptr() + 4 * RU * heads, mx.data_ptr(), pack.data_ptr(),
+                _lib.stream_handle(dev))
+        _lib.check(lib.ppgat_rep_merge(0, *args), "rep_merge")
+        self.comm.all_reduce_(mx, dist.ReduceOp.MAX)
+        _lib.check(lib.ppgat_rep_merge(1, *args), "rep_merge")
+        self.comm.all_reduce_(pack)
+        _lib.check(lib.ppgat_rep_merge(2, *args), "rep_merge")
+
+    def reduce_grad(self, g):
+        if self.comm.active:
+            self.comm.all_reduce_(g[self.RU:])
 
 
 def _merge_item_rows(rg: RepGraph, comm: Comm, out, m, inv_l, agg, bias, heads: int, C: int):
@@ -600,19 +642,32 @@ class _ReplicatedGAT(torch.autograd.Function):
 
 class ReplicatedPyGGAT(ShardedPyGGAT):
     """PyGGAT with the users sharded and the item rows replicated (see above).  Local rows:
-    [own users | pad to RU | every item]; ``forward`` returns them (Z's item rows are the
-    same on every rank)."""
+    [own users | every item]; ``forward`` returns them (Z's item rows are the same on every
+    rank).  With the HIP stages (default) each layer is the fused hip_ops.GATLayer on the
+    local graph with RepHooks at its two exchange points; other stages objects (the CPU
+    restatement of the tests) run the staged _ReplicatedGAT."""
+
+    def __init__(self, full, dg, comm: Comm, stages=None):
+        super().__init__(full, dg, comm, stages)
+        self.fused = stages is None
+        self.hooks = RepHooks(dg, comm)
 
     def node_features(self, item_feats):
-        rg = self.dg
-        parts = [self.user_emb_local]
-        pad = rg.RU - (self.u1 - self.u0)
-        if pad > 0:
-            parts.append(self.user_emb_local.new_zeros(pad, self.user_emb_local.size(1)))
-        parts.append(self.stages.linear(item_feats.contiguous(), self.item_proj.weight, self.item_proj.bias))
-        return torch.cat(parts, 0)
+        x_items = self.stages.linear(item_feats.contiguous(), self.item_proj.weight, self.item_proj.bias)
+        return torch.cat([self.user_emb_local, x_items], 0)
 
     def forward(self, item_feats):
+        if self.fused:
+            from .hip_ops import gat_layer
+            x_items = self.stages.linear(item_feats.contiguous(), self.item_proj.weight, self.item_proj.bias)
+            x = self.user_emb_local
+            for li, conv in enumerate(self.convs):
+                p = float(conv.dropout) if self.training else 0.0
+                seed = _dropout_seed() if p > 0 else 0
+                x = gat_layer(x, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, self.dg.graph, conv.heads,
+                              conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p, seed,
+                              x_items=x_items if li == 0 else None, rep=self.hooks)
+            return x
         x = self.node_features(item_feats)
         for conv in self.convs:
             h = self.stages.linear(x, conv.lin.weight, None)
@@ -622,6 +677,25 @@ class ReplicatedPyGGAT(ShardedPyGGAT):
                                      conv.heads, conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p,
                                      seed)
         return x
+
+
+def _replicated_full_state_dict(self):
+    """Reference-keyed state_dict (user_emb gathered from the owners)."""
+    rg = self.dg
+    C = self.user_emb_local.size(1)
+    blk = torch.zeros(rg.RU_max, C, dtype=torch.float32, device=self.user_emb_local.device)
+    blk[:rg.RU] = self.user_emb_local.detach()
+    allb = self.comm.all_gather_rows(blk)
+    ub = rg.user_bounds
+    sd = {"user_emb.weight": torch.cat([allb[r * rg.RU_max: r * rg.RU_max + int(ub[r + 1] - ub[r])]
+                                        for r in range(rg.world)], 0)}
+    for k, v in self.state_dict().items():
+        if k != "user_emb_local":
+            sd[k] = v
+    return sd
+
+
+ReplicatedPyGGAT.full_state_dict = _replicated_full_state_dict
 
 
 def replicated_bpr_loss(Z_local, rg: RepGraph, comm: Comm, u, i, j, n_users: int, n_items: int,
@@ -638,7 +712,9 @@ def replicated_bpr_loss(Z_local, rg: RepGraph, comm: Comm, u, i, j, n_users: int
 
 def replicated_rows_to_global(Z_local, rg: RepGraph, comm: Comm) -> torch.Tensor:
     """[RU + n_items, C] local rows -> [N, C] in node-id order (every rank gets it)."""
-    users = comm.all_gather_rows(Z_local[:rg.RU].contiguous())
+    blk = Z_local.new_zeros(rg.RU_max, Z_local.size(1))
+    blk[:rg.RU] = Z_local[:rg.RU]
+    users = comm.all_gather_rows(blk)
     ub = rg.user_bounds
-    idx = np.concatenate([r * rg.RU + np.arange(ub[r + 1] - ub[r]) for r in range(rg.world)]).astype(np.int64)
+    idx = np.concatenate([r * rg.RU_max + np.arange(ub[r + 1] - ub[r]) for r in range(rg.world)]).astype(np.int64)
     return torch.cat([users.index_select(0, torch.from_numpy(idx).to(users.device)), Z_local[rg.RU:]], 0)

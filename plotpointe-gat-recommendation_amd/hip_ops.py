@@ -445,7 +445,7 @@ class GATLayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, heads: int, channels: int, mode: int,
-                slope: float, dropout_p: float, seed: int, x_items=None):
+                slope: float, dropout_p: float, seed: int, x_items=None, rep=None):
         x = x.contiguous()
         x_items = x_items.contiguous() if x_items is not None else None
         W = weight.detach().contiguous()
@@ -467,12 +467,15 @@ class GATLayer(torch.autograd.Function):
             s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
         need = any(ctx.needs_input_grad[:5]) or (had_items and ctx.needs_input_grad[12])
         out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed,
-                                     want_agg=need and heads > 1)
+                                     want_agg=(need or rep is not None) and heads > 1)
+        if rep is not None:  # replicated item rows (dist.py): merge their softmax over the ranks
+            rep.merge_fwd(out, m, inv_l, agg, b, heads, channels)
         if need:
             empty = torch.empty(0, device=x.device)
             ctx.save_for_backward(x, x_items if x_items is not None else empty, W, h, a_s, a_d, s_src, s_dst, out, m,
                                   inv_l, agg if agg is not None else empty, b if b is not None else empty)
         ctx.graph = graph
+        ctx.rep = rep
         ctx.params = (weight, att_src, att_dst)
         ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None, fused,
                     x_items is not None, had_items, split)
@@ -490,16 +493,34 @@ class GATLayer(torch.autograd.Function):
         N = g.n_nodes
         K = x.size(1)
         HC = heads * C
+        rep = ctx.rep
+        if rep is not None:  # item rows of grad_out: per-rank partial sums -> the full gradient
+            rep.reduce_grad(g_out)
         # prologue: packed per-node state (+ dbias)
         want_db = has_bias and ctx.needs_input_grad[4]
         nstate = torch.empty(N, heads, 4, dtype=torch.float32, device=dev)
         dbias = torch.empty(C, dtype=torch.float32, device=dev) if want_db else None
-        rows = int(lib.ppgat_bwd_partial_rows(N))
-        part = torch.empty(max(rows, 1) * C, dtype=torch.float32, device=dev) if want_db else None
-        _lib.check(lib.ppgat_bwd_prologue(g_out.data_ptr(), out.data_ptr(), _lib.ptr(agg) if has_agg else None,
-                                          _lib.ptr(b) if has_bias else None, s_dst.data_ptr(), m.data_ptr(),
-                                          inv_l.data_ptr(), N, heads, C, mode, nstate.data_ptr(), _lib.ptr(dbias),
-                                          _lib.ptr(part), _lib.stream_handle(dev)), "bwd_prologue")
+
+        def prologue(r0, r1, db):
+            n = r1 - r0
+            rows = int(lib.ppgat_bwd_partial_rows(n))
+            part = torch.empty(max(rows, 1) * C, dtype=torch.float32, device=dev) if db is not None else None
+            _lib.check(lib.ppgat_bwd_prologue(g_out.data_ptr() + 4 * r0 * C, out.data_ptr() + 4 * r0 * C,
+                                              agg.data_ptr() + 4 * r0 * HC if has_agg else None,
+                                              _lib.ptr(b) if has_bias else None, s_dst.data_ptr() + 4 * r0 * heads,
+                                              m.data_ptr() + 4 * r0 * heads, inv_l.data_ptr() + 4 * r0 * heads, n,
+                                              heads, C, mode, nstate.data_ptr() + 16 * r0 * heads, _lib.ptr(db),
+                                              _lib.ptr(part), _lib.stream_handle(dev)), "bwd_prologue")
+
+        if rep is None:
+            prologue(0, N, dbias)
+        else:  # the replicated item rows enter dbias on one rank only
+            RU = rep.RU
+            db_i = torch.empty(C, dtype=torch.float32, device=dev) if (want_db and rep.rank == 0) else None
+            prologue(0, RU, dbias)
+            prologue(RU, N, db_i)
+            if db_i is not None:
+                dbias = dbias + db_i
         D = torch.empty(N, HC, dtype=torch.float32, device=dev)
         S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
         _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed)
@@ -528,11 +549,11 @@ class GATLayer(torch.autograd.Function):
         dx_u = dx[:split] if (dx is not None and had_items) else dx
         dx_i = dx[split:] if (dx is not None and had_items) else None
         return (dx_u, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                None, None, None, None, None, None, None, dx_i)
+                None, None, None, None, None, None, None, dx_i, None)
 
 
 def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p=0.0, seed=0,
-              x_items=None):
+              x_items=None, rep=None):
     """x [N, F] -> out [N, C]: lin + the fused GAT aggregation, with the fused backward.
     With ``x_items``, the input rows are cat(x, x_items) (never materialised on the fused path)."""
     _require(x.is_cuda, "gat_layer: ppgat runs on ROCm devices only; there is no CPU path")
@@ -542,7 +563,7 @@ def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, s
         _require(x_items.is_cuda and x_items.dtype == torch.float32 and x_items.dim() == 2
                  and x_items.size(1) == x.size(1), "gat_layer: x_items must match x in dtype/device/width")
     return GATLayer.apply(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed,
-                          x_items)
+                          x_items, rep)
 
 
 # ---------------------------------------------------------------------------

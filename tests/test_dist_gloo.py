@@ -150,11 +150,11 @@ def _rep_worker(rank, world, port, out_dir, heads, ii):
     items = comm.all_gather_rows(Z.detach()[rg.RU:].contiguous())   # replicas must agree bitwise
     sd = model.full_state_dict()
     grads = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
-    ublk = torch.zeros(rg.RU, model.user_emb_local.size(1), dtype=torch.float64)
+    ublk = torch.zeros(rg.RU_max, model.user_emb_local.size(1), dtype=torch.float64)
     ublk[:model.u1 - model.u0] = model.user_emb_local.grad
     ug = comm.all_gather_rows(ublk)
     ub = rg.user_bounds
-    urows = [ug[r * rg.RU: r * rg.RU + int(ub[r + 1] - ub[r])] for r in range(world)]
+    urows = [ug[r * rg.RU_max: r * rg.RU_max + int(ub[r + 1] - ub[r])] for r in range(world)]
     if rank == 0:
         torch.save({"Z": Zg, "loss": tot, "grads": grads, "user_grad": torch.cat(urows), "sd": sd,
                     "items": items.view(world, g.n_items, -1), "n_local_edges": rg.view.n_fwd_edges},

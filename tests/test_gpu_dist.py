@@ -44,8 +44,9 @@ def _sharded(rank, world, out_dir, heads, segmented=True):
     pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads)
     D = pkg.dist
     comm = D.Comm()
-    if segmented == "replicated":
-        return _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, (u, i, j), comm)
+    if str(segmented).startswith("replicated"):
+        return _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, (u, i, j), comm,
+                           staged=segmented == "replicated-staged")
     segs = [(0, g.n_users), (g.n_users, g.n_nodes)] if segmented else None
     dg = D.build_dist_graph(ei, g.n_nodes, world, rank, segments=segs)
     model = D.ShardedPyGGAT(full, dg, comm).train()
@@ -69,12 +70,13 @@ def _sharded(rank, world, out_dir, heads, segmented=True):
                    os.path.join(out_dir, f"sharded_{world}.pt"))
 
 
-def _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, uij, comm):
-    """Users sharded, item rows on every rank (dist.build_replicated_graph)."""
+def _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, uij, comm, staged=False):
+    """Users sharded, item rows on every rank (dist.build_replicated_graph); the fused
+    layer with RepHooks, or (staged) the stage-by-stage path the CPU tests also run."""
     D = pkg.dist
     u, i, j = uij
     rg = D.build_replicated_graph(ei, g.n_nodes, g.n_users, world, rank)
-    model = D.ReplicatedPyGGAT(full, rg, comm).train()
+    model = D.ReplicatedPyGGAT(full, rg, comm, stages=pkg.hip_ops.HipStages() if staged else None).train()
     torch.manual_seed(123)
     Z = model(feats)
     loss = D.replicated_bpr_loss(Z, rg, comm, u, i, j, g.n_users, g.n_items)
@@ -85,11 +87,11 @@ def _replicated(rank, world, out_dir, dev, pkg, g, ei, feats, full, uij, comm):
     Zg = D.replicated_rows_to_global(Z.detach(), rg, comm)
     items = comm.all_gather_rows(Z.detach()[rg.RU:].contiguous()).view(world, g.n_items, -1)
     grads = {n: p.grad.detach().cpu() for n, p in model.named_parameters() if n != "user_emb_local"}
-    blk = torch.zeros(rg.RU, model.user_emb_local.size(1), device=dev)
+    blk = torch.zeros(rg.RU_max, model.user_emb_local.size(1), device=dev)
     blk[:model.u1 - model.u0] = model.user_emb_local.grad
     ug = comm.all_gather_rows(blk).cpu()
     ub = rg.user_bounds
-    rows = [ug[r * rg.RU: r * rg.RU + int(ub[r + 1] - ub[r])] for r in range(world)]
+    rows = [ug[r * rg.RU_max: r * rg.RU_max + int(ub[r + 1] - ub[r])] for r in range(world)]
     if rank == 0:
         assert all(torch.equal(items[r], items[0]) for r in range(world)), "item replicas differ"
         torch.save({"Z": Zg.cpu(), "loss": tot.cpu(), "grads": grads, "user_grad": torch.cat(rows)},
@@ -136,7 +138,8 @@ def _check(res, ref):
         assert _rel(v, grads[k]) <= tol, k
 
 
-@pytest.mark.parametrize("heads,segmented", [(1, True), (2, False), (1, "replicated"), (2, "replicated")])
+@pytest.mark.parametrize("heads,segmented", [(1, True), (2, False), (1, "replicated"), (2, "replicated"),
+                                             (1, "replicated-staged")])
 def test_sharded_world1_rccl(cuda, tmp_path, heads, segmented):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
@@ -148,7 +151,7 @@ def test_sharded_world1_rccl(cuda, tmp_path, heads, segmented):
     _check(torch.load(tmp_path / "sharded_1.pt", weights_only=False), _unsharded(cuda, heads))
 
 
-@pytest.mark.parametrize("segmented", [True, False, "replicated"])
+@pytest.mark.parametrize("segmented", [True, False, "replicated", "replicated-staged"])
 def test_sharded_world2_shared_gpu(cuda, tmp_path, segmented):
     mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), 1, segmented), nprocs=2, join=True,
                        start_method="spawn")

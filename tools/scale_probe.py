@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--partition", choices=["replicated", "rows"], default="replicated")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph (as bench.py for N>1)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = data.synthetic_ui_graph(seed=42)
@@ -69,10 +70,12 @@ def main():
         model = D.ShardedPyGGAT(full, dg, comm)
         loss_fn = D.sharded_bpr_loss
         n_edges = dg.view.n_fwd_edges
-    opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=args.graph)
 
     def step():
         model.train()
+        if args.graph:
+            _lib.dropout_advance(dev)
         Z = model(feats)
         loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
         opt.zero_grad(set_to_none=True)
@@ -80,21 +83,34 @@ def main():
         model.allreduce_grads()
         opt.step()
 
+    run = step
+    if args.graph:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
     for _ in range(args.warmup):
-        step()
+        run()
     torch.cuda.synchronize()
     _lib.profile_reset()
-    _lib.profile_enable(True)
+    _lib.profile_enable(not args.graph)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     th = time.perf_counter() - t0
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     _lib.profile_enable(False)
     kern = {k: _lib.profile_read(k)[0] / args.steps for k in ("fwd", "bwd_pro", "bwd_src", "bwd_epi", "proj",
                                                                "gemm_tn", "adam")}
-    print(json.dumps({"partition": args.partition, "world": args.world, "rank": args.rank,
+    print(json.dumps({"partition": args.partition, "graph": args.graph, "world": args.world, "rank": args.rank,
                       "rows": int(dg.R), "local_edges": int(n_edges), "global_edges": int(ei.size(1)),
                       "ms_per_step": el / args.steps * 1e3, "host_enqueue_ms_per_step": th / args.steps * 1e3,
                       "kernel_ms_per_step": kern}), flush=True)
