@@ -231,11 +231,17 @@ def main():
                 step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            loss_static = step()
-        graph.replay()  # the capture itself ran nothing: one replay so every rank starts from a replayed step
-        torch.cuda.synchronize()
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                loss_static = step()
+            graph.replay()  # the capture itself ran nothing: one replay so every rank starts from a replayed step
+            torch.cuda.synchronize()
+        except Exception as exc:  # capture refused (driver / RCCL): time the same step eagerly instead
+            print(f"bench: hipGraph capture failed ({type(exc).__name__}: {exc}); running eagerly", file=sys.stderr,
+                  flush=True)
+            graph = None
+            torch.cuda.synchronize()
     else:
         for _ in range(args.warmup):
             step()
