@@ -290,10 +290,18 @@ def main():
     dom = max(("fwd", "bwd_src", "bwd_epi"), key=lambda k: kern[k][0])
     dom_ms, dom_n = kern[dom]
     avg_s = dom_ms / max(dom_n, 1) / 1e3
-    ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0)
+    if dist_path:
+        # rank 0's kernels run over its local graph: price them on its own rows and edges
+        v = dg.view
+        ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
+                        args.attn_dropout > 0)
+    else:
+        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0)
     achieved = ab / avg_s / 1e9
     traffic = None
     try:
+        if dist_path:
+            raise LookupError("the committed PMC summary is for the unsharded graph")
         tj_ = json.loads(Path(args.traffic_json).read_text())
         if tj_.get("config", 2) == args.config:  # PMC summaries are per workload
             traffic = tj_.get("per_launch_bytes", {}).get(dom)
