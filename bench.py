@@ -44,8 +44,9 @@ def parse():
     ap.add_argument("--heads", type=int, default=1)
     ap.add_argument("--samples", type=int, default=200_000)
     ap.add_argument("--attn-dropout", type=float, default=0.1)
-    ap.add_argument("--config", type=int, choices=[2, 3, 5], default=2,
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="2: U-I graph (headline); 3: U-I + I-I kNN k=20 edges (SURVEY.md 8(d) cfg 3); "
+                         "4: config 2 row-sharded with the all_to_all halo (N>1); "
                          "5: 10M x 5M x 200M-edge synthetic, d=256, heads=4 (roofline / scaling run)")
     ap.add_argument("--scale", type=float, default=None,
                     help="config 5 size multiplier (default world/8: one GPU's share of the 8-GPU run, "
@@ -53,10 +54,10 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
-    ap.add_argument("--partition", choices=["auto", "replicated", "rows"], default="auto",
+    ap.add_argument("--partition", choices=["auto", "replicated", "halo"], default="auto",
                     help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
-                         "'rows' = users and items row-sharded with all_gather halos (dist.build_dist_graph); "
-                         "auto = replicated for configs 2/3, rows for config 5")
+                         "'halo' = users and items row-sharded, RCCL all_to_all of the halo rows per layer "
+                         "(dist.build_halo_graph); auto = replicated for configs 2/3, halo for configs 4/5")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="capture the training step once in a hipGraph and replay it (auto: on for N>1 over RCCL, "
                          "where the per-rank step is short enough for host launch overhead to dominate)")
@@ -90,11 +91,25 @@ def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool) -> fl
     return 0.0
 
 
+def host_cores() -> int:
+    """CPU cores this process may run on: the affinity mask, further capped by a cgroup CPU
+    quota when one is set (a GPU box's share of its host is smaller than os.cpu_count())."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except Exception:
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(g: data.UIGraph, feats: np.ndarray, hidden: int, layers: int, budget_s: float):
     """Oracle (torch CPU restatement of PyG GATConv, oracle/gat_oracle.py) fwd+bwd of the
-    L GAT layers, on a bounded prefix sample of the same graph."""
+    L GAT layers, on a bounded prefix sample of the same graph: median of 5 timed
+    iterations after one warm-up, on every core the process may use."""
     from oracle import gat_oracle
-    threads = min(os.cpu_count() or 1, 16)
+    threads = host_cores()
     torch.set_num_threads(threads)
     # sample: the first n_u users (all their train edges) -> ~400k directed edges
     target_e = 400_000
@@ -123,17 +138,19 @@ def cpu_baseline(g: data.UIGraph, feats: np.ndarray, hidden: int, layers: int, b
         h.square().mean().backward()
 
     once()  # warm-up
-    iters, t0 = 0, time.perf_counter()
-    while True:
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
         once()
-        iters += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or iters >= 50:
-            break
-    return {"value": E * layers * iters / el, "unit": "edges/sec", "cores": threads, "kind": "port",
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": E * layers / med, "unit": "edges/sec", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(),
             "sample": f"oracle pyg_gat_conv x{layers} layers fwd+bwd (no lin/loss/Adam), first {n_u} users' "
                       f"train edges = {E} of {2 * len(g.user_items)} directed edges over all {N} nodes, d={hidden}, "
-                      f"{iters} timed iterations, {el:.1f}s, torch {torch.__version__} CPU"}
+                      f"median of 5 iterations ({min(times):.2f}-{max(times):.2f} s each) after 1 warm-up, "
+                      f"{threads} threads (affinity/cgroup share of {os.cpu_count()} host CPUs), "
+                      f"torch {torch.__version__} CPU"}
 
 
 def main():
@@ -179,7 +196,7 @@ def main():
     torch.manual_seed(42)
     full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=feats_np.shape[1], hidden=args.hidden, layers=args.layers,
                       heads=args.heads, attn_dropout=args.attn_dropout).to(dev)
-    part = args.partition if args.partition != "auto" else ("rows" if args.config == 5 else "replicated")
+    part = args.partition if args.partition != "auto" else ("halo" if args.config in (4, 5) else "replicated")
     if dist_path and part == "replicated":
         # strong scaling of the fixed config-2 job: users sharded, the 63k item rows on every
         # rank, every edge homed with its user; item rows merged by all_reduce (dist.py)
@@ -187,18 +204,18 @@ def main():
         dg = pkg.dist.build_replicated_graph(ei, N, g.n_users, world, rank)
         model = pkg.dist.ReplicatedPyGGAT(full, dg, comm)
     elif dist_path:
-        # row-sharded graph over the ranks (dist.py)
+        # users and items row-sharded, edges homed at their destination's rank, one RCCL
+        # all_to_all of the halo rows per layer and direction (dist.py)
         comm = pkg.dist.Comm()
-        # users and items partitioned separately: every rank holds a slice of both, so the
-        # loss only gathers item rows (dist.sharded_bpr_loss)
-        dg = pkg.dist.build_dist_graph(ei, N, world, rank, segments=[(0, g.n_users), (g.n_users, N)])
-        model = pkg.dist.ShardedPyGGAT(full, dg, comm)
+        dg = pkg.dist.build_halo_graph(ei, N, g.n_users, world, rank)
+        model = pkg.dist.HaloPyGGAT(full, dg, comm)
     else:
         model = full
         pkg.graph_cache.get(ei, N)  # one-time CSR/CSC build (not timed)
     # same Adam update as train_gat_pyg.py:299 (lr 1e-3, L2 1e-4): libppgat's device Adam (optim.py)
-    use_graph = (args.graph == "on" or
-                 (args.graph == "auto" and dist_path and args.dist_backend == "nccl" and world > 1))
+    # hipGraph replay by default (one captured step: ~150 launches enqueued once), except the
+    # gloo rehearsal whose collectives run on the host
+    use_graph = args.graph == "on" or (args.graph == "auto" and not (dist_path and args.dist_backend == "gloo"))
     opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=use_graph)
 
     def step():
@@ -207,7 +224,7 @@ def main():
             _lib.dropout_advance(dev)  # fresh dropout masks on every replay
         if dist_path:
             Z = model(feats)
-            loss_fn = pkg.dist.replicated_bpr_loss if part == "replicated" else pkg.dist.sharded_bpr_loss
+            loss_fn = pkg.dist.replicated_bpr_loss if part == "replicated" else pkg.dist.halo_bpr_loss
             loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
             opt.zero_grad(set_to_none=True)
             loss.backward()
@@ -231,17 +248,29 @@ def main():
                 step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize()
+        ok = 1
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 loss_static = step()
-            graph.replay()  # the capture itself ran nothing: one replay so every rank starts from a replayed step
-            torch.cuda.synchronize()
         except Exception as exc:  # capture refused (driver / RCCL): time the same step eagerly instead
-            print(f"bench: hipGraph capture failed ({type(exc).__name__}: {exc}); running eagerly", file=sys.stderr,
-                  flush=True)
-            graph = None
-            torch.cuda.synchronize()
+            print(f"bench: hipGraph capture failed ({type(exc).__name__}: {exc})", file=sys.stderr, flush=True)
+            graph, ok = None, 0
+        torch.cuda.synchronize()
+        if dist_path:
+            # one shared decision: replay only if every rank captured (a rank running eagerly
+            # beside replaying ranks would pair its collectives with different calls)
+            flag = torch.tensor([ok], dtype=torch.int32, device=dev if args.dist_backend == "nccl" else "cpu")
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                graph = None
+        if graph is not None:
+            graph.replay()  # the capture itself ran nothing: one replay so every rank starts from a replayed step
+        else:
+            print("bench: running the step eagerly", file=sys.stderr, flush=True)
+            for _ in range(max(args.warmup, 1)):
+                step()
+        torch.cuda.synchronize()
     else:
         for _ in range(args.warmup):
             step()
@@ -292,7 +321,10 @@ def main():
     avg_s = dom_ms / max(dom_n, 1) / 1e3
     if dist_path:
         # rank 0's kernels run over its local graph: price them on its own rows and edges
-        v = dg.view
+        if part == "replicated":
+            v = dg.view
+        else:
+            v = dg.fwd_view if dom == "fwd" else dg.bwd_view
         ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
                         args.attn_dropout > 0)
     else:
@@ -316,6 +348,8 @@ def main():
         metric = "edges/sec GAT fwd+bwd, d=128, 1.69M-edge U-I graph"
         workload = (("cfg2: PyGGAT train step (fwd+BPR+bwd+Adam), 1,689,116 interactions, "
                      "192,403 users + 63,001 items") if args.config == 2 else
+                    ("cfg4: the cfg2 train step, users and items row-sharded (all_to_all halo)")
+                    if args.config == 4 else
                     "cfg3: cfg2 + I-I kNN (k=20, sim>=0.3) edges, PyGGAT train step")
         data_desc = "synthetic (config-2 statistics-matched U-I graph, random-init weights)"
     result = {
@@ -338,7 +372,7 @@ def main():
                    "parallelism": ("single" if not dist_path else
                                    f"user-sharded x{world}, item rows replicated (RCCL all_reduce)"
                                    if part == "replicated" else
-                                   f"row-sharded x{world} (RCCL all_gather/reduce_scatter)")},
+                                   f"row-sharded x{world}, RCCL all_to_all halo + grad all_reduce")},
         "hip_graph": graph is not None,
         "kernel_timing": kern_src,
         "fused_kernel_edges_per_sec": E * args.layers * K / (fused_ms / 1e3) if fused_ms else None,

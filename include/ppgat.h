@@ -46,7 +46,9 @@ extern "C" {
 #define PPGAT_MODE_PYG 0
 #define PPGAT_MODE_CUSTOM 1
 
-/* Library identification: 2 = ppgat_schedule carries n_long_items (schedule counts int32[4]). */
+/* Library identification: 2 = ppgat_schedule carries n_long_items (schedule counts int32[4]);
+ * 3 = ppgat_fwd / ppgat_bwd / ppgat_bwd_edges carry seed_used, ppgat_adam_step_device takes one
+ * step pointer per tensor. */
 int ppgat_version(void);
 const char* ppgat_last_error(void);
 
@@ -118,12 +120,16 @@ int ppgat_node_scores(const float* h, const float* att_src, const float* att_dst
  * per-(node,head) softmax state m [N,H] and inv_l = 1/(l+eps) [N,H] (saved for the
  * backward), and agg [N,H,C] (per-head aggregate) when agg != NULL (required for heads > 1
  * training).  workspace: hub-piece partials, ppgat_fwd_workspace_bytes().
+ * seed_used (device uint64[1], nullable; written when dropout_p > 0): the effective mask seed
+ * (seed folded with the dropout epoch at the time the forward runs).  Passing it to the
+ * backward below makes the backward regenerate exactly the forward's mask even if the epoch
+ * advances in between (ppgat_dropout_advance from another replayed graph, a recompute).
  */
 int ppgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int channels, size_t* bytes);
 int ppgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid,
               int64_t n_nodes, int64_t n_edges, int heads, int channels,
               const float* h, const float* s_src, const float* s_dst, const float* bias,
-              int mode, float negative_slope, float dropout_p, uint64_t seed,
+              int mode, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
               float* out, float* m, float* inv_l, float* agg,
               void* workspace, size_t workspace_bytes, void* stream);
 
@@ -135,7 +141,8 @@ int ppgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t
  * ds_dst (x) att_dst), grad_att_src/grad_att_dst [H,C] and, when grad_bias != NULL,
  * grad_bias [C] = column sums of grad_out.  Atomic-free and
  * deterministic (segment-owned sums in a fixed order).  agg may be NULL when heads == 1
- * (out - bias is used).
+ * (out - bias is used).  seed_used: the forward's ppgat_fwd seed_used (nullable: then seed is
+ * folded with the current dropout epoch).
  */
 int ppgat_bwd_workspace_bytes(int64_t n_nodes, int64_t n_edges, int64_t n_hub_items, int heads, int channels,
                               size_t* bytes);
@@ -146,7 +153,7 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
               const float* att_src, const float* att_dst, const float* bias,
               const float* out, const float* agg, const float* m, const float* inv_l,
               const float* grad_out,
-              int mode, float negative_slope, float dropout_p, uint64_t seed,
+              int mode, float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
               float* grad_h, float* grad_att_src, float* grad_att_dst, float* grad_bias,
               void* workspace, size_t workspace_bytes, void* stream);
 
@@ -166,7 +173,8 @@ int ppgat_bwd_prologue(const float* grad_out, const float* out, const float* agg
 int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
                     const int32_t* dz_slot, int64_t n_edges, int heads, int channels, const float* h,
                     const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
-                    float dropout_p, uint64_t seed, float* grad_h, int64_t ld_grad_h, float* ds_src,
+                    float dropout_p, uint64_t seed, const uint64_t* seed_used, float* grad_h, int64_t ld_grad_h,
+                    float* ds_src,
                     int64_t ld_ds_src, float* dz, void* workspace, size_t workspace_bytes, void* stream);
 /* ds_dst[i*ld + h] = sum of dz over the CSR segment of destination i, walked with the
  * forward (destination) schedule so hub rows are split; workspace >= n_hub_items*heads*4
@@ -270,13 +278,15 @@ int ppgat_adam_step(int count, float* const* params, const float* const* grads, 
                     float* const* exp_avg_sq, const int64_t* numel, const float* step_size,
                     const float* bias_correction2_sqrt, double beta1, double beta2, float eps, float weight_decay,
                     void* stream);
-/* Graph-capturable variant: the step count t is read on the device from *step (a float the
- * caller increments on the same stream before the launch), step_size = lr / (1 - beta1^t)
+/* Graph-capturable variant: tensor k's step count t is read on the device from *step[k] (one
+ * float per parameter, as torch.optim.Adam(capturable=True) keeps it; the caller increments
+ * them on the same stream before the launch), step_size = lr / (1 - beta1^t)
  * and bias_correction2_sqrt = sqrt(1 - beta2^t) are formed in double in the kernel and
  * rounded once -- the values the host path passes.  Same replacement as ppgat_adam_step
  * (torch.optim.Adam(capturable=True) semantics); one launch per <= max_tensors tensors. */
 int ppgat_adam_step_device(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                           float* const* exp_avg_sq, const int64_t* numel, const float* step, double lr, double beta1,
+                           float* const* exp_avg_sq, const int64_t* numel, const float* const* step, double lr,
+                           double beta1,
                            double beta2, float eps, float weight_decay, void* stream);
 
 /* ---- replicated-item partition: cross-rank merge of item destination rows -----------------
@@ -293,6 +303,19 @@ int ppgat_adam_step_device(int count, float* const* params, const float* const* 
  * point at the first item row; pack holds n_items*heads*(channels + 1) floats ([a] then [c]). */
 int ppgat_rep_merge(int phase, const int32_t* item_rowptr, int64_t n_items, int heads, int channels, float* out,
                     float* agg, const float* bias, float* m, float* inv_l, float* mx, float* pack, void* stream);
+
+/* ---- row-sharded partition: halo exchange rows ------------------------------------------
+ * Replaces: nothing one-to-one -- the reference is one process on one GPU; with nodes
+ * row-sharded over ranks (dist.py ExchangePlan) every layer all_to_all's the rows the peers'
+ * edges read, and the backward returns their gradients to the owner.
+ *   ppgat_rows_gather:     dst[r, :] = src[idx[r], :]      (pack the all_to_all send buffer)
+ *   ppgat_rows_return_add: dst[o, :] += sum_{k = ret_ptr[o]}^{ret_ptr[o+1]-1} ret[ret_pos[k], :]
+ *                          (returned halo gradients, added in peer order: deterministic)
+ * Rows of `cols` floats with row strides ld_* (floats). */
+int ppgat_rows_gather(const float* src, int64_t ld_src, const int64_t* idx, int64_t n_rows, int cols, float* dst,
+                      int64_t ld_dst, void* stream);
+int ppgat_rows_return_add(float* dst, int64_t ld_dst, const float* ret, int64_t ld_ret, const int32_t* ret_ptr,
+                          const int32_t* ret_pos, int64_t n_rows, int cols, void* stream);
 
 /* ---- dropout epoch (hipGraph replays) ------------------------------------------------------
  * Every dropout mask of ppgat_fwd / ppgat_bwd_edges uses seed' = seed + epoch * 0xD1B54A32D192ED03

@@ -42,16 +42,16 @@ SIGNATURES = {
     "ppgat_node_scores": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp]),
     "ppgat_fwd_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_fwd": (c_int, [SP, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
-                          c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+                          c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_bwd_workspace_bytes": (c_int, [c_i64, c_i64, c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_bwd": (c_int, [SP, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                          c_sz, c_vp]),
+                          c_vp, c_sz, c_vp]),
     "ppgat_bwd_partial_rows": (c_i64, [c_i64]),
     "ppgat_bwd_prologue": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp,
                                    c_vp, c_vp]),
     "ppgat_bwd_edges": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
-                                c_u64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
+                                c_u64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_bwd_dst_sum": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_vp, c_sz, c_vp]),
     "ppgat_bwd_epilogue": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp]),
@@ -79,6 +79,8 @@ SIGNATURES = {
     "ppgat_dropout_advance": (c_int, [c_vp]),
     "ppgat_rep_merge": (c_int, [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_dropout_set_epoch": (c_int, [ctypes.c_uint64, c_vp]),
+    "ppgat_rows_gather": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
+    "ppgat_rows_return_add": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_vp]),
     "ppgat_knn_max_k": (c_int, []),
     "ppgat_knn_topk": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_bpr_sampler_workspace_bytes": (c_int, [c_i64, c_i64, ctypes.POINTER(c_sz)]),

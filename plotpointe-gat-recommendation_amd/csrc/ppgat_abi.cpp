@@ -89,7 +89,7 @@ struct Timed {
 
 extern "C" {
 
-int ppgat_version(void) { return 2; }
+int ppgat_version(void) { return 3; }
 
 const char* ppgat_last_error(void) { return g_err.c_str(); }
 
@@ -198,8 +198,8 @@ int ppgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int channels, size
 
 int ppgat_fwd(const ppgat_schedule* sched, const int32_t* col, const int32_t* csr_eid, int64_t n_nodes,
               int64_t n_edges, int heads, int channels, const float* h, const float* s_src, const float* s_dst,
-              const float* bias, int mode, float negative_slope, float dropout_p, uint64_t seed, float* out, float* m,
-              float* inv_l, float* agg, void* workspace, size_t workspace_bytes, void* stream) {
+              const float* bias, int mode, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
+              float* out, float* m, float* inv_l, float* agg, void* workspace, size_t workspace_bytes, void* stream) {
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "fwd: unsupported channels");
   if (heads < 1 || n_nodes < 0 || n_edges < 0) return fail(PPGAT_ERR_INVALID, "fwd: bad sizes");
   if (int rc = check_mode(mode, heads, bias, dropout_p)) return rc;
@@ -216,7 +216,8 @@ int ppgat_fwd(const ppgat_schedule* sched, const int32_t* col, const int32_t* cs
                            sched->n_long_items};
   Timed t(PPGAT_K_FWD, st);
   hipError_t e = ppgat::launch_fwd(it, col, csr_eid, heads, channels, h, s_src, s_dst, bias, mode, negative_slope,
-                                   eps, dropout_p, seed, out, m, inv_l, agg, static_cast<float*>(workspace),
+                                   eps, dropout_p, seed, dropout_p > 0.f ? seed_used : nullptr, out, m, inv_l, agg,
+                                   static_cast<float*>(workspace),
                                    sched->hub_row, sched->hub_ptr, sched->n_hubs, st);
   if (e != hipSuccess) return hip_fail(e, "fwd");
   return PPGAT_OK;
@@ -253,8 +254,9 @@ int ppgat_bwd_prologue(const float* grad_out, const float* out, const float* agg
 int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
                     const int32_t* dz_slot, int64_t n_edges, int heads, int channels, const float* h,
                     const float* s_src, const float* nstate, const float* grad_out, int mode, float negative_slope,
-                    float dropout_p, uint64_t seed, float* grad_h, int64_t ld_grad_h, float* ds_src,
-                    int64_t ld_ds_src, float* dz, void* workspace, size_t workspace_bytes, void* stream) {
+                    float dropout_p, uint64_t seed, const uint64_t* seed_used, float* grad_h, int64_t ld_grad_h,
+                    float* ds_src, int64_t ld_ds_src, float* dz, void* workspace, size_t workspace_bytes,
+                    void* stream) {
   if (ld_grad_h < (int64_t)heads * channels || (ld_grad_h % 4) || ld_ds_src < heads)
     return fail(PPGAT_ERR_INVALID, "bwd_edges: bad leading dimensions (ld_grad_h >= H*C, multiple of 4)");
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd_edges: unsupported channels");
@@ -278,7 +280,8 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
   {
     Timed t(PPGAT_K_BWD_SRC, st);
     e = ppgat::launch_bwd_src(it, row, csc_eid, dz_slot, heads, channels, h, s_src, nstate, grad_out, mode,
-                              negative_slope, gscale, dropout_p, seed, grad_h, ld_grad_h, ds_src, ld_ds_src, dz,
+                              negative_slope, gscale, dropout_p, seed, seed_used, grad_h, ld_grad_h, ds_src,
+                              ld_ds_src, dz,
                               static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
                               src_sched->n_hubs, st);
   }
@@ -347,8 +350,9 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
               const int32_t* csc2csr, int64_t n_nodes, int64_t n_edges, int heads, int channels, const float* h,
               const float* s_src, const float* s_dst, const float* att_src, const float* att_dst, const float* bias,
               const float* out, const float* agg, const float* m, const float* inv_l, const float* grad_out, int mode,
-              float negative_slope, float dropout_p, uint64_t seed, float* grad_h, float* grad_att_src,
-              float* grad_att_dst, float* grad_bias, void* workspace, size_t workspace_bytes, void* stream) {
+              float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used, float* grad_h,
+              float* grad_att_src, float* grad_att_dst, float* grad_bias, void* workspace, size_t workspace_bytes,
+              void* stream) {
   if (!channels_ok(channels)) return fail(PPGAT_ERR_UNSUPPORTED, "bwd: unsupported channels");
   if (heads < 1 || n_nodes < 0 || n_edges < 0) return fail(PPGAT_ERR_INVALID, "bwd: bad sizes");
   if (int rc = check_mode(mode, heads, bias, dropout_p)) return rc;
@@ -372,7 +376,8 @@ int ppgat_bwd(const ppgat_schedule* sched, const int32_t* rowptr, const int32_t*
                                   grad_bias, bias_part, stream))
     return rc;
   if (int rc = ppgat_bwd_edges(sched, row, csc_eid, csc2csr, n_edges, heads, channels, h, s_src, nstate, grad_out,
-                               mode, negative_slope, dropout_p, seed, grad_h, (int64_t)heads * channels, ds_src,
+                               mode, negative_slope, dropout_p, seed, seed_used, grad_h, (int64_t)heads * channels,
+                               ds_src,
                                heads, dz, hpart, partial_bytes(sched->n_hub_items, heads, channels), stream))
     return rc;
   return ppgat_bwd_epilogue(rowptr, n_nodes, heads, channels, h, att_src, att_dst, ds_src, dz, grad_h, grad_att_src,
@@ -551,7 +556,8 @@ int ppgat_adam_step(int count, float* const* params, const float* const* grads, 
 }
 
 int ppgat_adam_step_device(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                           float* const* exp_avg_sq, const int64_t* numel, const float* step, double lr, double beta1,
+                           float* const* exp_avg_sq, const int64_t* numel, const float* const* step, double lr,
+                           double beta1,
                            double beta2, float eps, float weight_decay, void* stream) {
   if (count < 0 || count > ppgat::adam_max_tensors())
     return fail(PPGAT_ERR_INVALID, "adam_step_device: bad tensor count");
@@ -559,6 +565,7 @@ int ppgat_adam_step_device(int count, float* const* params, const float* const* 
     return fail(PPGAT_ERR_INVALID, "adam_step_device: null pointer");
   for (int t = 0; t < count; ++t) {
     if (numel[t] < 0) return fail(PPGAT_ERR_INVALID, "adam_step_device: negative numel");
+    if (!step[t]) return fail(PPGAT_ERR_INVALID, "adam_step_device: null step pointer");
     if (numel[t] > 0 && (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t]))
       return fail(PPGAT_ERR_INVALID, "adam_step_device: null tensor");
   }
@@ -583,6 +590,27 @@ int ppgat_rep_merge(int phase, const int32_t* item_rowptr, int64_t n_items, int 
   hipError_t e = ppgat::rep_merge(phase, item_rowptr, n_items, heads, channels, 1e-16f, out, agg, bias, m, inv_l, mx,
                                   pack, pack_c, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "rep_merge");
+  return PPGAT_OK;
+}
+
+int ppgat_rows_gather(const float* src, int64_t ld_src, const int64_t* idx, int64_t n_rows, int cols, float* dst,
+                      int64_t ld_dst, void* stream) {
+  if (n_rows < 0 || cols < 0 || ld_src < cols || ld_dst < cols) return fail(PPGAT_ERR_INVALID, "rows_gather: bad sizes");
+  if (n_rows > 0 && cols > 0 && (!src || !idx || !dst)) return fail(PPGAT_ERR_INVALID, "rows_gather: null pointer");
+  hipError_t e = ppgat::rows_gather(src, ld_src, idx, n_rows, cols, dst, ld_dst, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "rows_gather");
+  return PPGAT_OK;
+}
+
+int ppgat_rows_return_add(float* dst, int64_t ld_dst, const float* ret, int64_t ld_ret, const int32_t* ret_ptr,
+                          const int32_t* ret_pos, int64_t n_rows, int cols, void* stream) {
+  if (n_rows < 0 || cols < 0 || ld_dst < cols || ld_ret < cols)
+    return fail(PPGAT_ERR_INVALID, "rows_return_add: bad sizes");
+  if (n_rows > 0 && cols > 0 && (!dst || !ret_ptr || (!ret && ret_pos)))
+    return fail(PPGAT_ERR_INVALID, "rows_return_add: null pointer");
+  hipError_t e = ppgat::rows_return_add(dst, ld_dst, ret, ld_ret, ret_ptr, ret_pos, n_rows, cols,
+                                        static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "rows_return_add");
   return PPGAT_OK;
 }
 

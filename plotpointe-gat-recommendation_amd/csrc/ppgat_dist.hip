@@ -7,6 +7,12 @@
 //   out = mean_h a + bias,  1/l = 1 / (L + eps)
 // with the two sums taken by all_reduce(MAX) of m' and all_reduce(SUM) of [c a | c].
 // Elementwise over [n_items, heads, C]: HBM-bound, one float4 per thread.
+//
+// Halo exchange of the row-sharded partition (dist.py ExchangePlan): the send buffer of an
+// all_to_all_single is packed from the rank's own rows (k_rows_gather), and the gradients
+// the peers return for those rows are added back in a fixed order (k_rows_return_add):
+// row o gets its returned copies in peer order, so the sum is deterministic.  Both are
+// row copies of `cols` floats (16-B vectors when aligned), HBM-bound.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -89,7 +95,75 @@ __global__ void __launch_bounds__(256) k_rep_finish(const float* __restrict__ pa
   reinterpret_cast<float4*>(out + i * C)[q] = o;
 }
 
+// dst[r, :] = src[idx[r], :]; one 64-lane wave per row, float4 per lane when cols % 4 == 0
+__global__ void __launch_bounds__(256) k_rows_gather(const float* __restrict__ src, int64_t lds,
+                                                     const int64_t* __restrict__ idx, int64_t n, int cols,
+                                                     float* __restrict__ dst, int64_t ldd, int vec) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const float* s = src + idx[r] * lds;
+  float* d = dst + r * ldd;
+  if (vec) {
+    for (int c = lane * 4; c < cols; c += 256)
+      *reinterpret_cast<float4*>(d + c) = *reinterpret_cast<const float4*>(s + c);
+  } else {
+    for (int c = lane; c < cols; c += 64) d[c] = s[c];
+  }
+}
+
+// dst[o, :] += sum_{k in [ptr[o], ptr[o+1])} ret[pos[k], :], k ascending (peer order)
+__global__ void __launch_bounds__(256) k_rows_return_add(float* __restrict__ dst, int64_t ldd,
+                                                         const float* __restrict__ ret, int64_t ldr,
+                                                         const int32_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ pos, int64_t n, int cols,
+                                                         int vec) {
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= n) return;
+  const int k0 = ptr[o], k1 = ptr[o + 1];
+  if (k0 == k1) return;
+  const int lane = threadIdx.x & 63;
+  float* d = dst + o * ldd;
+  if (vec) {
+    for (int c = lane * 4; c < cols; c += 256) {
+      float4 a = *reinterpret_cast<const float4*>(d + c);
+      for (int k = k0; k < k1; ++k) {
+        const float4 b = *reinterpret_cast<const float4*>(ret + (int64_t)pos[k] * ldr + c);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      *reinterpret_cast<float4*>(d + c) = a;
+    }
+  } else {
+    for (int c = lane; c < cols; c += 64) {
+      float a = d[c];
+      for (int k = k0; k < k1; ++k) a += ret[(int64_t)pos[k] * ldr + c];
+      d[c] = a;
+    }
+  }
+}
+
 }  // namespace
+
+static bool vec_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int cols) {
+  return cols % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(a) % 16) == 0 &&
+         (reinterpret_cast<uintptr_t>(b) % 16) == 0;
+}
+
+hipError_t rows_gather(const float* src, int64_t lds, const int64_t* idx, int64_t n, int cols, float* dst,
+                       int64_t ldd, hipStream_t st) {
+  if (n <= 0 || cols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows_gather, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd,
+                     vec_ok(src, lds, dst, ldd, cols) ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t rows_return_add(float* dst, int64_t ldd, const float* ret, int64_t ldr, const int32_t* ptr,
+                           const int32_t* pos, int64_t n, int cols, hipStream_t st) {
+  if (n <= 0 || cols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows_return_add, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, dst, ldd, ret, ldr, ptr, pos,
+                     n, cols, vec_ok(dst, ldd, ret, ldr, cols) ? 1 : 0);
+  return hipGetLastError();
+}
 
 hipError_t rep_merge(int phase, const int32_t* rowptr, int64_t n, int heads, int C, float eps, float* out, float* agg,
                      const float* bias, float* m, float* invl, float* mx, float* pack_a, float* pack_c,

@@ -682,7 +682,7 @@ struct AdamArg {
   float bc2_sqrt[kAdamMax];
   int count;
   float beta1, beta2, omb1, omb2, eps, wd;  // omb = 1 - beta, rounded once from double on the host
-  const float* tstep;  // non-null: step_size / bc2_sqrt from the device step count t (graph replays)
+  const float* tstep[kAdamMax];  // non-null: step_size / bc2_sqrt from tensor t's device step count (graph replays)
   double lr, b1d, b2d;
 };
 
@@ -706,8 +706,8 @@ __global__ void __launch_bounds__(256) k_adam(AdamArg a) {
   float* __restrict__ V = a.v[ti];
   const int64_t n = a.n[ti];
   float ss = a.step_size[ti], bc = a.bc2_sqrt[ti];
-  if (a.tstep != nullptr) {  // the host formulas of optim.Adam, in double, rounded once
-    const double t = (double)*a.tstep;
+  if (a.tstep[ti] != nullptr) {  // the host formulas of optim.Adam, in double, rounded once
+    const double t = (double)*a.tstep[ti];
     ss = (float)(a.lr / (1.0 - pow(a.b1d, t)));
     bc = (float)sqrt(1.0 - pow(a.b2d, t));
   }
@@ -842,15 +842,16 @@ int adam_max_tensors() { return kAdamMax; }
 
 hipError_t adam_step(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
                      const int64_t* n, const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
-                     float eps, float wd, const float* tstep, double lr, hipStream_t st) {
+                     float eps, float wd, const float* const* tstep, double lr, hipStream_t st) {
   AdamArg a{};
   a.count = count;
-  a.tstep = tstep; a.lr = lr; a.b1d = beta1; a.b2d = beta2;
+  a.lr = lr; a.b1d = beta1; a.b2d = beta2;
   a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.omb1 = (float)(1.0 - beta1); a.omb2 = (float)(1.0 - beta2);
   a.eps = eps; a.wd = wd;
   int64_t blocks = 0;
   for (int t = 0; t < count; ++t) {
     a.p[t] = p[t]; a.g[t] = g[t]; a.m[t] = m[t]; a.v[t] = v[t]; a.n[t] = n[t];
+    a.tstep[t] = tstep ? tstep[t] : nullptr;
     a.step_size[t] = step_size ? step_size[t] : 0.f; a.bc2_sqrt[t] = bc2_sqrt ? bc2_sqrt[t] : 1.f;
     blocks += (n[t] + kAdamPerBlock - 1) / kAdamPerBlock;
     a.blk_end[t] = blocks;

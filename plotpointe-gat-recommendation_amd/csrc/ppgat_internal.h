@@ -29,15 +29,16 @@ hipError_t launch_scores(const float* h, const float* as, const float* ad, int64
                          float* sd, hipStream_t st);
 hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, int heads, int C,
                       const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
-                      float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
-                      float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                      float eps, float p, uint64_t seed, uint64_t* seed_out, float* out, float* m, float* invl,
+                      float* agg, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                       hipStream_t st);
 hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
                           const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
                           float* nstate, float* bias_part, int64_t blocks, hipStream_t st);
 hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
                           int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
-                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, int64_t ld_dh,
+                          int mode, float slope, float gscale, float p, uint64_t seed, const uint64_t* seed_in,
+                          float* dh, int64_t ld_dh,
                           float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
                           const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
 hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, float* ds_dst, int64_t ld, float* partial,
@@ -93,9 +94,14 @@ hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st);
 hipError_t rep_merge(int phase, const int32_t* rowptr, int64_t n, int heads, int C, float eps, float* out, float* agg,
                      const float* bias, float* m, float* invl, float* mx, float* pack_a, float* pack_c,
                      hipStream_t st);
+// halo exchange rows (ppgat_dist.hip)
+hipError_t rows_gather(const float* src, int64_t lds, const int64_t* idx, int64_t n, int cols, float* dst,
+                       int64_t ldd, hipStream_t st);
+hipError_t rows_return_add(float* dst, int64_t ldd, const float* ret, int64_t ldr, const int32_t* ptr,
+                           const int32_t* pos, int64_t n, int cols, hipStream_t st);
 hipError_t adam_step(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
                      const int64_t* n, const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
-                     float eps, float wd, const float* tstep, double lr, hipStream_t st);
+                     float eps, float wd, const float* const* tstep, double lr, hipStream_t st);
 
 // I-I kNN neighbour selection (ppgat_knn.hip)
 int knn_max_k();

@@ -78,6 +78,14 @@ __device__ __forceinline__ uint64_t epoch_seed(uint64_t seed) {
   return seed + *(volatile const uint64_t*)&g_drop_epoch * kDropEpochMul;
 }
 
+// The seed the forward's masks use, stored for the backward (ppgat_fwd seed_used): the
+// backward then reads it instead of the epoch counter, so an epoch advance enqueued between
+// a forward and its backward (another captured step replayed in between, a recompute) does
+// not change the backward's mask.
+__global__ void k_seed_snap(uint64_t seed, uint64_t* __restrict__ out) {
+  if (threadIdx.x == 0) out[0] = epoch_seed(seed);
+}
+
 // Counter-based dropout mask on alpha (restated in oracle/gat_oracle.py:dropout_scale).
 __device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t eid, uint32_t head, float p,
                                             float inv_keep) {
@@ -449,9 +457,10 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
                                                  const float4* __restrict__ nstate,
                                                  const float* __restrict__ grad_out, int mode, float slope,
                                                  float gscale, float p, float inv_keep, uint64_t seed,
+    const uint64_t* __restrict__ seed_in,
                                                  float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
                                                  int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
-  if (p > 0.f) seed = epoch_seed(seed);
+  if (p > 0.f) seed = seed_in != nullptr ? *seed_in : epoch_seed(seed);
   using G = Geo<C>;
   constexpr int GRP = G::LPR / G::U;  // lanes sharing one reduced edge value
   // per wave, per chunk edge: {dst row, beta * gscale} and {c1, c0, CSR slot}, where
@@ -544,10 +553,11 @@ __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, 
                                                        const float4* __restrict__ nstate,
                                                        const float* __restrict__ grad_out, int mode, float slope,
                                                        float gscale, float p, float inv_keep, uint64_t seed,
+    const uint64_t* __restrict__ seed_in,
                                                        float* __restrict__ dh, int64_t ld_dh,
                                                        float* __restrict__ ds_src, int64_t ld_ds,
                                                        float* __restrict__ dz) {
-  if (p > 0.f) seed = epoch_seed(seed);
+  if (p > 0.f) seed = seed_in != nullptr ? *seed_in : epoch_seed(seed);
   constexpr int NV = C / 64;
   static_assert(NV >= 1, "k_bwd_src_short: C >= 64");
   __shared__ int2 rec[4][64];
@@ -672,9 +682,10 @@ __global__ void __launch_bounds__(256) k_bwd_src_mh(Items it, const int32_t* __r
                                                     const float4* __restrict__ nstate,
                                                     const float* __restrict__ grad_out, int mode, float slope,
                                                     float gscale, float p, float inv_keep, uint64_t seed,
+    const uint64_t* __restrict__ seed_in,
                                                     float* __restrict__ dh, int64_t ld_dh, float* __restrict__ ds_src,
                                                     int64_t ld_ds, float* __restrict__ dz, float* __restrict__ partial) {
-  if (p > 0.f) seed = epoch_seed(seed);
+  if (p > 0.f) seed = seed_in != nullptr ? *seed_in : epoch_seed(seed);
   using G = Geo<C>;
   static_assert(C >= 32, "k_bwd_src_mh: C >= 32");
   constexpr int U = G::U * H > 16 ? (16 / H > 0 ? 16 / H : 1) : G::U;  // <= 16 partial dots per lane
@@ -1007,10 +1018,11 @@ static int64_t short_begin(const ItemsArg& it, int heads, int C) {
 
 hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, int heads, int C,
                       const float* h, const float* ss, const float* sd, const float* bias, int mode, float slope,
-                      float eps, float p, uint64_t seed, float* out, float* m, float* invl, float* agg,
-                      float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                      float eps, float p, uint64_t seed, uint64_t* seed_out, float* out, float* m, float* invl,
+                      float* agg, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                       hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (seed_out != nullptr) hipLaunchKernelGGL(k_seed_snap, dim3(1), dim3(64), 0, st, seed, seed_out);
   const int64_t n_long = short_begin(it, heads, C);
   const Items its{it.row, it.beg, it.end, n_long, it.n_hub_items};
   if (n_long > 0) {
@@ -1044,7 +1056,8 @@ hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, c
 
 hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
                           int heads, int C, const float* h, const float* ss, const float* nstate, const float* go,
-                          int mode, float slope, float gscale, float p, uint64_t seed, float* dh, int64_t ld_dh,
+                          int mode, float slope, float gscale, float p, uint64_t seed, const uint64_t* seed_in,
+                          float* dh, int64_t ld_dh,
                           float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
                           const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -1055,7 +1068,7 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
     const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16);
     PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_bwd_src_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, row,
                                              csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go,
-                                             mode, slope, gscale, p, inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz));
+                                             mode, slope, gscale, p, inv_keep, seed, seed_in, dh, ld_dh, ds_src, ld_ds, dz));
   }
   if (n_long > 0) {
     const bool mh = heads > 1 && C >= 32 && (heads == 2 || heads == 4 || heads == 8);
@@ -1064,7 +1077,7 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
   PPGAT_DISPATCH_C(C, if constexpr (CC >= 32) {                                                             \
     hipLaunchKernelGGL((k_bwd_src_mh<CC, HH>), dim3(blocks_for(n_long * 64)), dim3(256), 0, st, its, row,      \
                        csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, \
-                       p, inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial);                             \
+                       p, inv_keep, seed, seed_in, dh, ld_dh, ds_src, ld_ds, dz, partial);                    \
   })
       if (heads == 2) { PPGAT_MH(2); } else if (heads == 4) { PPGAT_MH(4); } else { PPGAT_MH(8); }
 #undef PPGAT_MH
@@ -1072,7 +1085,7 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
       PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_src<CC>, dim3(blocks_for(n_long * 64)), dim3(256), 0, st, its,
                                              row, csc_eid, csc2csr, heads, h, ss,
                                              reinterpret_cast<const float4*>(nstate), go, mode, slope, gscale, p,
-                                             inv_keep, seed, dh, ld_dh, ds_src, ld_ds, dz, partial));
+                                             inv_keep, seed, seed_in, dh, ld_dh, ds_src, ld_ds, dz, partial));
     }
   }
   if (n_hubs > 0) {

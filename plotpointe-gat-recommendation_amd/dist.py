@@ -1,37 +1,43 @@
-"""Row-sharded multi-GPU GAT: one process per GPU, RCCL over xGMI.
+"""Multi-GPU GAT: one process per GPU, RCCL (torch "nccl") over xGMI.
 
-Partition.  The node ids are cut into segments (default: one, [0, N); the recommender
-uses two, users [0, n_users) and items [n_users, N)) and every segment into `world`
-contiguous ranges balanced by in-degree + out-degree + a per-node constant, so each rank
-holds a slice of every segment.  A rank's block is its segment slices, each padded to
-that segment's largest slice, R rows in all; per-node tensors are [R, ...] per rank and
-[world*R, ...] gathered ("padded space"; node n of segment s owned by rank r lives at row
-r*R + off_s + n - lo_s(r)).  The graph is static: the global
-CSR/CSC in padded space is built once on every rank (device radix sort) and each rank
-keeps slices of it:
-  forward : CSR rows of its own destinations (col indexes the gathered padded space)
-  backward: CSC rows of its own sources with their full out-edge lists (row indexes the
-            gathered padded space); each edge's logit gradient goes to its slot in a
-            [world, E_max] buffer laid out by destination owner and CSR slot.
+Two partitions of the node rows, both exact (every result equals the single-device layer):
 
-Per layer.
-  forward : local lin -> node scores -> all_gather(h, s_src) -> fused kernel on own rows
-  backward: prologue on own rows -> all_gather(grad_out, nstate) -> edge pass on own
-            sources (complete dh for them: no reverse exchange) -> reduce_scatter(dz)
-            (every slot is written by exactly one rank, so the sum is exact) -> epilogue
-            on own rows.
-Loss: with the (users, items) segments a rank evaluates the triples of its own users
-against an all_gather of the item rows only (n_items x C instead of N x C), and the
-item-row gradients return by reduce_scatter; with one segment, all_gather of Z and a
-contiguous share of the triples.  Dense parameters (lin, att, bias, item_proj) are
-replicated and all-reduced once per step; user-embedding rows are owner-held.
-On a locality-free graph the halo is ~all nodes, so all_gather is the natural collective
-here (a per-peer all-to-all index list would carry the same rows).
+Halo partition (``build_halo_graph`` / ``HaloPyGGAT``, any graph; configs 4 and 5).
+  Users and items are two segments, each cut into `world` contiguous ranges balanced by
+  degree, so every rank owns a slice of both: its "own" rows, users first then items.
+  Every edge_index column lives on the rank that owns its DESTINATION, so a rank holds the
+  complete in-edge list (CSR) of each own row.  The sources those edges read that belong to
+  other ranks are its halo rows; the local row space is [own rows | halo rows], the halo
+  grouped by owner rank in the owner's row order.  The graph is static, so the exchange
+  plan is built once (ExchangePlan: which own rows go to which peer, how many rows arrive
+  from each):
+    forward : per layer one RCCL all_to_all_single of the halo rows of the layer's
+              exchanged operand -- the pre-projection x when H*C > C_in (config 5: 1 KB per
+              row instead of 4 KB of h, the projection recomputed on the halo rows), else the
+              projected h (config 4: 512 B, nothing recomputed) -- then the fused kernels on
+              the local CSR (own destination rows, columns into [own | halo]).
+    backward: the edge pass by source over the local CSC writes gradients for own AND halo
+              source rows; one reverse all_to_all returns the halo rows' gradients to their
+              owners, which add them in peer order (ppgat_rows_return_add: deterministic).
+              Logit gradients of an edge stay on its destination's rank: no other exchange.
+  Loss: a rank takes the triples of its own users; the item rows they read come by one
+  all_to_all of exactly those rows (a plan per triple set), and go back the same way.
+  Dense parameters are replicated and all-reduced once per step; user-embedding rows are
+  owner-held.
+
+Replicated-item partition (``build_replicated_graph`` / ``ReplicatedPyGGAT``; the U-I
+graph of configs 2/3, default of ``bench.py --gpus N`` there): see its section below.
+
+Dropout masks are keyed by the original edge_index column and a per-layer seed every rank
+agrees on (``SharedSeeds``: a base drawn on rank 0 and broadcast once, then a counter), so
+a source-side backward and a destination-side forward regenerate the same mask whatever
+the ranks' own RNG states.
 """
 from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+from types import SimpleNamespace
 from typing import Callable, Optional
 
 import numpy as np
@@ -98,20 +104,143 @@ class Comm:
         dist.all_reduce(t, op=op, group=self.group)
         return t
 
+    def all_to_all_rows(self, t: torch.Tensor, send_counts, recv_counts, out: Optional[torch.Tensor] = None):
+        """all_to_all_single of row blocks: rows [sum(send_counts[:r]), +send_counts[r]) of t go
+        to rank r; the result holds recv_counts[s] rows from each rank s, in rank order.
+        ``out`` (optional): a contiguous [sum(recv_counts), ...] destination."""
+        t = t.contiguous()
+        n_out = int(sum(recv_counts))
+        shape = (n_out,) + tuple(t.shape[1:])
+        if out is None:
+            out = torch.empty(shape, dtype=t.dtype, device=t.device)
+        if not self.active:
+            if n_out:
+                out.copy_(t[:n_out])
+            return out
+        sc, rc = [int(c) for c in send_counts], [int(c) for c in recv_counts]
+        if self.backend == "gloo" and t.is_cuda:  # several ranks sharing one GPU in a test: stage through host
+            host = torch.empty(shape, dtype=t.dtype)
+            dist.all_to_all_single(host, t.cpu(), rc, sc, group=self.group)
+            out.copy_(host)
+            return out
+        dist.all_to_all_single(out, t, rc, sc, group=self.group)
+        return out
 
-class _AllGatherRows(torch.autograd.Function):
+    def broadcast_int(self, value: int, src: int = 0) -> int:
+        if not self.active:
+            return int(value)
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else "cpu"
+        t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+        dist.broadcast(t, src, group=self.group)
+        return int(t.item())
+
+    def all_to_all_counts(self, counts) -> list:
+        """Every rank sends counts[r] to rank r; returns what each rank sent here (host ints)."""
+        if not self.active:
+            return [int(c) for c in counts]
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else "cpu"
+        src = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+        dst = torch.empty_like(src)
+        dist.all_to_all_single(dst, src, group=self.group)
+        return [int(v) for v in dst.cpu().tolist()]
+
+
+# ---------------------------------------------------------------------------
+# dropout seeds every rank agrees on
+# ---------------------------------------------------------------------------
+def _dropout_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+def derive_seed(base: int, k: int) -> int:
+    """splitmix64(base + k * golden gamma): the k-th layer call's dropout seed."""
+    x = (int(base) + (int(k) + 1) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return (x ^ (x >> 31)) & ((1 << 62) - 1)
+
+
+class SharedSeeds:
+    """Per-layer-call dropout seeds identical on every rank: the base is drawn from torch's
+    CPU generator on rank 0 at the first draw and broadcast once (the only host sync), then
+    call k uses derive_seed(base, k).  Ranks call the model the same number of times, so
+    their counters agree; per-rank seeding of torch's RNG does not matter."""
+
+    def __init__(self, comm: "Comm"):
+        self.comm = comm
+        self.base = None
+        self.count = 0
+
+    def next(self) -> int:
+        if self.base is None:
+            self.base = self.comm.broadcast_int(_dropout_seed() if self.comm.rank == 0 else 0)
+        s = derive_seed(self.base, self.count)
+        self.count += 1
+        return s
+
+
+# ---------------------------------------------------------------------------
+# exchange plans: static all_to_all of rows (RCCL) and the ordered return of gradients
+# ---------------------------------------------------------------------------
+@dataclass
+class ExchangePlan:
+    """This rank sends its own rows ``send_idx`` (concatenated per peer, peers in rank
+    order, send_counts[r] rows to rank r) and receives recv_counts[s] rows from each peer
+    s, appended after its n_own own rows in peer order.  Backward: the peers return the
+    gradients of the rows they received; own row o adds its copies ret_pos[ret_ptr[o] :
+    ret_ptr[o+1]] (positions in the returned block) in that order -- peer order."""
+    n_own: int
+    send_idx: torch.Tensor      # int64 [n_send]
+    send_counts: list
+    recv_counts: list
+    ret_ptr: torch.Tensor       # int32 [n_own + 1]
+    ret_pos: torch.Tensor       # int32 [n_send]
+
+    @property
+    def n_send(self) -> int:
+        return int(sum(self.send_counts))
+
+    @property
+    def n_recv(self) -> int:
+        return int(sum(self.recv_counts))
+
+
+def make_plan(n_own: int, send_idx: np.ndarray, send_counts, recv_counts, device) -> ExchangePlan:
+    send_idx = np.asarray(send_idx, np.int64)
+    order = np.argsort(send_idx, kind="stable")           # by own row, peer order kept
+    ptr = np.zeros(n_own + 1, np.int64)
+    np.cumsum(np.bincount(send_idx, minlength=n_own), out=ptr[1:])
+    return ExchangePlan(int(n_own), torch.from_numpy(send_idx).to(device), [int(c) for c in send_counts],
+                        [int(c) for c in recv_counts], torch.from_numpy(ptr.astype(np.int32)).to(device),
+                        torch.from_numpy(order.astype(np.int32)).to(device))
+
+
+class _Exchange(torch.autograd.Function):
+    """[n_own, ...] own rows -> [n_own + n_recv, ...] = [own | rows received from the peers]."""
+
     @staticmethod
-    def forward(ctx, t, comm):
-        ctx.comm = comm
-        return comm.all_gather_rows(t)
+    def forward(ctx, t_own, plan: ExchangePlan, comm: "Comm", stages):
+        t_own = t_own.contiguous()
+        out = torch.empty((plan.n_own + plan.n_recv,) + tuple(t_own.shape[1:]), dtype=t_own.dtype,
+                          device=t_own.device)
+        out[:plan.n_own].copy_(t_own)
+        send = stages.gather_rows(t_own, plan.send_idx)
+        comm.all_to_all_rows(send, plan.send_counts, plan.recv_counts, out=out[plan.n_own:])
+        ctx.plan, ctx.comm, ctx.stages = plan, comm, stages
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        return ctx.comm.reduce_scatter_rows(g), None
+        plan, comm, st = ctx.plan, ctx.comm, ctx.stages
+        g = g.contiguous()
+        g_own = g[:plan.n_own].clone()
+        ret = comm.all_to_all_rows(g[plan.n_own:], plan.recv_counts, plan.send_counts)
+        st.return_add(g_own, ret, plan.ret_ptr, plan.ret_pos)
+        return g_own, None, None, None
 
 
-def all_gather_rows(t, comm):
-    return _AllGatherRows.apply(t, comm)
+def exchange(t_own, plan: ExchangePlan, comm: "Comm", stages):
+    return _Exchange.apply(t_own, plan, comm, stages)
 
 
 # ---------------------------------------------------------------------------
@@ -129,61 +258,19 @@ def partition_bounds(weights: np.ndarray, world: int) -> np.ndarray:
 
 @dataclass
 class LocalView:
-    """Slices of the padded-space CSR/CSC a rank runs the stages on."""
-    n_rows: int                 # R
-    rowptr: torch.Tensor        # [R+1] rebased, CSR of own destination rows
-    col: torch.Tensor           # [E_fwd] padded source ids
-    csr_eid: torch.Tensor       # [E_fwd] original column ids (dropout hash key)
+    """A rank's slice of a CSR (destination rows) / CSC (source rows) the stages run on."""
+    n_rows: int                 # rows this view's stage iterates / writes
+    rowptr: torch.Tensor        # CSR of destination rows (rebased)
+    col: torch.Tensor           # [E_fwd] source row ids (local row space)
+    csr_eid: torch.Tensor       # [E_fwd] original edge_index columns (dropout hash key)
     n_fwd_edges: int
-    colptr: torch.Tensor        # [R+1] rebased, CSC of own source rows
-    row: torch.Tensor           # [E_bwd] padded destination ids
+    colptr: torch.Tensor        # CSC of source rows (rebased)
+    row: torch.Tensor           # [E_bwd] destination row ids
     csc_eid: torch.Tensor       # [E_bwd]
-    dz_slot: torch.Tensor       # [E_bwd] position in the [world * E_max] dz buffer
+    dz_slot: torch.Tensor       # [E_bwd] CSR slot of each CSC edge (the logit-gradient buffer)
     n_bwd_edges: int
     fwd_sched: object = None
     bwd_sched: object = None
-
-
-@dataclass
-class DistGraph:
-    world: int
-    rank: int
-    n_nodes: int
-    n_edges: int
-    bounds: np.ndarray          # segment 0's range bounds (the only segment by default)
-    R: int
-    row_map: torch.Tensor       # [N] int32, node id -> padded row
-    e_max: int
-    view: LocalView
-    seg_bounds: list = None     # per segment: [world + 1] range bounds (node ids)
-    seg_R: list = None          # per segment: padded rows per rank
-    seg_off: list = None        # per segment: row offset inside a rank's block
-    loss_map: Optional[torch.Tensor] = None  # lazily built by sharded_bpr_loss
-
-    @property
-    def lo(self) -> int:
-        return int(self.bounds[self.rank])
-
-    @property
-    def hi(self) -> int:
-        return int(self.bounds[self.rank + 1])
-
-    @property
-    def P(self) -> int:
-        return self.world * self.R
-
-    def owned(self, rank: Optional[int] = None):
-        """[(lo, hi, row offset in the block, padded rows)] per segment of a rank."""
-        r = self.rank if rank is None else rank
-        return [(int(b[r]), int(b[r + 1]), off, Rs) for b, off, Rs in zip(self.seg_bounds, self.seg_off, self.seg_R)]
-
-    def owned_users(self, n_users: int, rank: Optional[int] = None):
-        """(u0, u1): the rank's users (one contiguous range at the top of its block)."""
-        rng = [(max(lo, 0), min(hi, n_users), off) for lo, hi, off, _ in self.owned(rank) if min(hi, n_users) > lo]
-        if not rng:
-            return 0, 0
-        assert len(rng) == 1 and rng[0][2] == 0, "users must be one range at the top of the block"
-        return rng[0][0], rng[0][1]
 
 
 def _hip_csr(ei, P):
@@ -196,83 +283,123 @@ def _hip_sched(ptr, E):
     return schedule_build(ptr, E)
 
 
-def build_dist_graph(edge_index: torch.Tensor, n_nodes: int, world: int, rank: int,
+@dataclass
+class HaloGraph:
+    world: int
+    rank: int
+    n_nodes: int
+    n_edges: int
+    n_users: int
+    seg_bounds: list            # [user bounds [world+1], item bounds [world+1]] (node ids)
+    n_own: int                  # own rows: users [u0, u1) then items [i0, i1)
+    n_halo: int
+    plan: ExchangePlan          # the layer halo exchange
+    fwd_view: LocalView         # CSR over the own destination rows (n_rows = n_own)
+    bwd_view: LocalView         # CSC over [own | halo] source rows (n_rows = n_own + n_halo)
+    local_of: np.ndarray        # [N] int64: node id -> own row, -1 elsewhere (host)
+    owner: np.ndarray           # [N] int32 node owner (host)
+    loss_plans: dict = None
+
+    @property
+    def R(self) -> int:
+        return self.n_own + self.n_halo
+
+    @property
+    def bounds(self) -> np.ndarray:
+        return self.seg_bounds[0]
+
+    def owned(self, rank: Optional[int] = None):
+        """((u0, u1), (i0, i1)): the node-id ranges of a rank's users and items."""
+        r = self.rank if rank is None else rank
+        ub, ib = self.seg_bounds
+        return (int(ub[r]), int(ub[r + 1])), (int(ib[r]), int(ib[r + 1]))
+
+    def owned_users(self, n_users: int, rank: Optional[int] = None):
+        return self.owned(rank)[0]
+
+
+def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,
                      csr_builder: Callable = _hip_csr, sched_builder: Optional[Callable] = _hip_sched,
-                     node_weight: float = 4.0, segments=None) -> DistGraph:
-    """Every rank calls this with the same global edge_index (LongTensor [2, E], original
-    node ids) and gets its own slices.  ``segments``: contiguous node-id ranges covering
-    [0, N) in order, each split over the ranks (default one segment).  Deterministic: all
-    ranks agree on every array."""
+                     node_weight: float = 4.0) -> HaloGraph:
+    """Every rank calls this with the same global edge_index (LongTensor [2, E], users
+    [0, n_users), items [n_users, N)) and gets its own slices; deterministic, so all ranks
+    agree on the plan without exchanging it."""
     dev = edge_index.device
-    N = int(n_nodes)
+    N, nu = int(n_nodes), int(n_users)
     E = int(edge_index.size(1))
-    segs = [(0, N)] if segments is None else [(int(a), int(b)) for a, b in segments]
-    assert segs[0][0] == 0 and segs[-1][1] == N and all(segs[k][1] == segs[k + 1][0] for k in range(len(segs) - 1))
-    deg = (torch.bincount(edge_index[1], minlength=N) + torch.bincount(edge_index[0], minlength=N)).cpu().numpy()
-    seg_bounds, seg_R, seg_off = [], [], []
-    off = 0
-    for a, b in segs:
-        bnd = a + partition_bounds(deg[a:b].astype(np.float64) + node_weight, world)
+    ei = edge_index.cpu().numpy()
+    src, dst = ei[0], ei[1]
+    deg = (np.bincount(dst, minlength=N) + np.bincount(src, minlength=N)).astype(np.float64) + node_weight
+    seg_bounds = []
+    owner = np.empty(N, np.int32)
+    for a, b in ((0, nu), (nu, N)):
+        bnd = a + partition_bounds(deg[a:b], world)
         seg_bounds.append(bnd)
-        Rs = max(int(np.max(np.diff(bnd))), 1 if len(segs) == 1 else 0)
-        seg_R.append(Rs)
-        seg_off.append(off)
-        off += Rs
-    R = max(off, 1)
-    row_map_np = np.empty(N, np.int64)
-    for (a, b), bnd, o in zip(segs, seg_bounds, seg_off):
-        owner = np.repeat(np.arange(world), np.diff(bnd))
-        row_map_np[a:b] = owner * R + o + (np.arange(a, b) - bnd[owner])
-    row_map = torch.from_numpy(row_map_np).to(dev)
-    ei_p = row_map[edge_index]                       # [2, E] padded ids
-    P = world * R
-    G = csr_builder(ei_p, P)
-    rowptr = G.rowptr.to(torch.int64)
-    colptr = G.colptr.to(torch.int64)
-    starts = rowptr[torch.arange(world, device=dev) * R].cpu().numpy()
-    ends = rowptr[torch.arange(1, world + 1, device=dev) * R].cpu().numpy()
-    e_max = max(int(np.max(ends - starts)), 1)
-    r0, r1 = rank * R, (rank + 1) * R
-    e0, e1 = int(starts[rank]), int(ends[rank])
-    c0, c1 = int(colptr[r0].item()), int(colptr[r1].item())
-    v_rowptr = (rowptr[r0:r1 + 1] - e0).to(torch.int32).contiguous()
-    v_colptr = (colptr[r0:r1 + 1] - c0).to(torch.int32).contiguous()
-    row = G.row[c0:c1].contiguous()
-    glob_slot = G.csc2csr[c0:c1].to(torch.int64)
-    dst_owner = row.to(torch.int64) // R
-    starts_t = torch.from_numpy(starts).to(dev)
-    dz_slot = (dst_owner * e_max + glob_slot - starts_t[dst_owner]).to(torch.int32).contiguous()
-    view = LocalView(R, v_rowptr, G.col[e0:e1].contiguous(), G.csr_eid[e0:e1].contiguous(), e1 - e0,
-                     v_colptr, row, G.csc_eid[c0:c1].contiguous(), dz_slot, c1 - c0)
+        owner[a:b] = np.repeat(np.arange(world, dtype=np.int32), np.diff(bnd))
+    u0, u1 = int(seg_bounds[0][rank]), int(seg_bounds[0][rank + 1])
+    i0, i1 = int(seg_bounds[1][rank]), int(seg_bounds[1][rank + 1])
+    n_own = (u1 - u0) + (i1 - i0)
+    local_of = np.full(N, -1, np.int64)
+    local_of[u0:u1] = np.arange(u1 - u0)
+    local_of[i0:i1] = (u1 - u0) + np.arange(i1 - i0)
+    od, osrc = owner[dst], owner[src]
+    loc = np.flatnonzero(od == rank)                       # edges homed here (destination owned)
+    lsrc = src[loc]
+    halo = np.unique(lsrc[osrc[loc] != rank])              # ascending ids ...
+    halo = halo[np.argsort(owner[halo], kind="stable")]    # ... grouped by owner: the owner's row order
+    recv_counts = np.bincount(owner[halo], minlength=world)
+    lidx = local_of.copy()
+    lidx[halo] = n_own + np.arange(len(halo))
+    # what this rank sends: its own sources of edges homed on other ranks, per peer, by id
+    out_e = np.flatnonzero((osrc == rank) & (od != rank))
+    key = np.unique(od[out_e].astype(np.int64) * N + src[out_e])
+    send_counts = np.bincount(key // N, minlength=world)
+    send_idx = local_of[key % N]
+    plan = make_plan(n_own, send_idx, send_counts, recv_counts, dev)
+    R = n_own + len(halo)
+    ei_l = torch.from_numpy(np.stack([lidx[lsrc], lidx[dst[loc]]])).to(dev)
+    El = len(loc)
+    G = csr_builder(ei_l, R)
+    gid = torch.from_numpy(loc.astype(np.int32)).to(dev)
+    orig = (lambda t: gid[t.long()].contiguous()) if El else (lambda t: t[:0].contiguous())
+    rowptr_own = G.rowptr[:n_own + 1].contiguous()
+    col, csr_eid = G.col[:El].contiguous(), orig(G.csr_eid[:El])
+    row, csc_eid, slot = G.row[:El].contiguous(), orig(G.csc_eid[:El]), G.csc2csr[:El].contiguous()
+    fwd_view = LocalView(n_own, rowptr_own, col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
+    bwd_view = LocalView(R, G.rowptr.contiguous(), col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
     if sched_builder is not None:
-        view.fwd_sched = sched_builder(v_rowptr, e1 - e0)
-        view.bwd_sched = sched_builder(v_colptr, c1 - c0)
-    return DistGraph(world, rank, N, E, seg_bounds[0], R, row_map.to(torch.int32), e_max, view,
-                     seg_bounds, seg_R, seg_off)
+        fwd_view.fwd_sched = sched_builder(rowptr_own, El)
+        bwd_view.bwd_sched = sched_builder(bwd_view.colptr, El)
+        bwd_view.fwd_sched = fwd_view.fwd_sched
+    return HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan, fwd_view, bwd_view, local_of, owner,
+                     {})
 
 
 # ---------------------------------------------------------------------------
-# the sharded layer
+# the layer on a rank's local rows
 # ---------------------------------------------------------------------------
-class _ShardedGAT(torch.autograd.Function):
+class _LocalGAT(torch.autograd.Function):
+    """h_loc [own + halo rows, H*C] -> out [own rows, C]: node scores, the fused forward over
+    the own destination rows; backward over the local CSC (own and halo source rows)."""
+
     @staticmethod
-    def forward(ctx, h, att_src, att_dst, bias, dg: DistGraph, comm: Comm, stages, heads: int, C: int, mode: int,
-                slope: float, p: float, seed: int):
+    def forward(ctx, h, att_src, att_dst, bias, hg: HaloGraph, stages, heads: int, C: int, mode: int, slope: float,
+                p: float, seed: int):
         h = h.contiguous()
         a_s = att_src.detach().reshape(heads, C).contiguous()
         a_d = att_dst.detach().reshape(heads, C).contiguous()
         b = bias.detach().contiguous() if bias is not None else None
         s_src, s_dst = stages.scores(h, a_s, a_d, heads, C)
-        h_full = comm.all_gather_rows(h)
-        s_src_full = comm.all_gather_rows(s_src)
+        s_dst = s_dst[:hg.n_own].contiguous()
         need = any(ctx.needs_input_grad[:4])
-        out, m, inv_l, agg = stages.fwd(dg.view, h_full, s_src_full, s_dst, b, heads, C, mode, slope, p, seed,
-                                        need and heads > 1)
+        seed_buf = stages.seed_buffer(p, h.device) if need else None
+        out, m, inv_l, agg = stages.fwd(hg.fwd_view, h, s_src, s_dst, b, heads, C, mode, slope, p, seed,
+                                        need and heads > 1, seed_buf=seed_buf)
         if need:
             empty = torch.empty(0, device=h.device)
             ctx.save_for_backward(h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg if agg is not None else empty,
                                   b if b is not None else empty)
-        ctx.dg, ctx.comm, ctx.stages = dg, comm, stages
+        ctx.hg, ctx.stages, ctx.seed_buf = hg, stages, seed_buf
         ctx.meta = (heads, C, mode, slope, p, seed, bias is not None, agg is not None)
         ctx.att_shapes = (att_src.shape, att_dst.shape)
         return out
@@ -281,76 +408,41 @@ class _ShardedGAT(torch.autograd.Function):
     def backward(ctx, g):
         h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg, b = ctx.saved_tensors
         heads, C, mode, slope, p, seed, has_bias, has_agg = ctx.meta
-        dg, comm, st = ctx.dg, ctx.comm, ctx.stages
+        hg, st = ctx.hg, ctx.stages
         g = g.contiguous()
         want_db = has_bias and ctx.needs_input_grad[3]
         nstate, dbias = st.bwd_prologue(g, out, agg if has_agg else None, b if has_bias else None, s_dst, m, inv_l,
                                         heads, C, mode, want_db)
-        g_full = comm.all_gather_rows(g)
-        nstate_full = comm.all_gather_rows(nstate)
-        dz = torch.zeros(dg.world * dg.e_max * heads, dtype=h.dtype, device=h.device)
-        grad_h, ds_src = st.bwd_edges(dg.view, h, s_src, nstate_full, g_full, dz, heads, C, mode, slope, p, seed)
-        dz_local = comm.reduce_scatter_rows(dz.view(dg.world, dg.e_max * heads)).reshape(-1)
-        datt_src, datt_dst = st.bwd_epilogue(dg.view, h, a_s, a_d, ds_src, dz_local, grad_h, heads, C)
+        dz = torch.zeros(max(hg.bwd_view.n_bwd_edges, 1) * heads, dtype=h.dtype, device=h.device)
+        grad_h, ds_src = st.bwd_edges(hg.bwd_view, h, s_src, nstate, g, dz, heads, C, mode, slope, p, seed,
+                                      seed_buf=ctx.seed_buf)
+        datt_src, datt_dst = st.bwd_epilogue(hg.bwd_view, h, a_s, a_d, ds_src, dz, grad_h, heads, C)
         return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
-def _dropout_seed() -> int:
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
-
-
-class ShardedPyGGAT(torch.nn.Module):
-    """PyGGAT (train_gat_pyg.py:68-88) with row-sharded nodes.  Built from a full model
-    constructed identically on every rank (same seed), so the sharded and single-GPU runs
+class _ShardedBase(torch.nn.Module):
+    """Shared parts of the sharded PyGGAT variants (train_gat_pyg.py:68-88): built from a
+    full model constructed identically on every rank, so the sharded and single-GPU runs
     start from the same parameters; ``full_state_dict`` reassembles the reference keys."""
 
-    def __init__(self, full, dg: DistGraph, comm: Comm, stages=None):
+    def __init__(self, full, dg, comm: "Comm", stages=None):
         super().__init__()
         from .hip_ops import HipStages
         self.dg, self.comm = dg, comm
         self.stages = stages if stages is not None else HipStages()
         self.n_users, self.n_items = full.n_users, full.n_items
-        nu = self.n_users
-        self.u0, self.u1 = dg.owned_users(nu)
+        self.u0, self.u1 = dg.owned_users(self.n_users)
         self.user_emb_local = torch.nn.Parameter(full.user_emb.weight.detach()[self.u0:self.u1].clone())
         self.item_proj = full.item_proj
         self.convs = full.convs
+        self.seeds = SharedSeeds(comm)
+
+    def layer_seed(self, conv) -> int:
+        return self.seeds.next() if (self.training and float(conv.dropout) > 0) else 0
 
     def dense_parameters(self):
         return [p for n, p in self.named_parameters() if n != "user_emb_local"]
-
-    def node_features(self, item_feats):
-        """The rank's block: per segment, its users (user_emb rows) then its items
-        (item_proj of the feature rows), padded to the segment's row count."""
-        nu = self.n_users
-        parts = []
-        for lo, hi, _, Rs in self.dg.owned():
-            n = 0
-            if min(hi, nu) > lo:
-                parts.append(self.user_emb_local[max(lo, 0) - self.u0:min(hi, nu) - self.u0])
-                n += min(hi, nu) - lo
-            a, b = max(lo, nu), hi
-            if b > a:
-                parts.append(self.stages.linear(item_feats[a - nu:b - nu].contiguous(), self.item_proj.weight,
-                                                self.item_proj.bias))
-                n += b - a
-            if Rs > n:
-                parts.append(torch.zeros(Rs - n, self.user_emb_local.size(1), dtype=self.user_emb_local.dtype,
-                                         device=self.user_emb_local.device))
-        if self.u1 == self.u0:  # no users here: keep user_emb_local in the graph (a defined, empty grad)
-            parts.insert(0, self.user_emb_local[:0])
-        return torch.cat(parts, 0)
-
-    def forward(self, item_feats):
-        x = self.node_features(item_feats)
-        for conv in self.convs:
-            h = self.stages.linear(x, conv.lin.weight, None)
-            p = float(conv.dropout) if self.training else 0.0
-            seed = _dropout_seed() if p > 0 else 0
-            x = _ShardedGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, self.dg, self.comm, self.stages,
-                                  conv.heads, conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p, seed)
-        return x  # own rows of Z, [R, C] (pad rows last)
 
     def allreduce_grads(self):
         """One flat all-reduce of every dense parameter gradient (replicated params)."""
@@ -369,67 +461,117 @@ class ShardedPyGGAT(torch.nn.Module):
             off += n
         torch._foreach_copy_([p.grad for p in ps], views)  # one multi-tensor launch, not one copy per tensor
 
+    def _user_rows_global(self, rows: torch.Tensor, pad: int) -> torch.Tensor:
+        """Own user rows of a [*, C] tensor -> every rank's, in user-id order (all_gather)."""
+        C = rows.size(1)
+        blk = rows.new_zeros(pad, C)
+        blk[:rows.size(0)] = rows
+        allb = self.comm.all_gather_rows(blk)
+        out = []
+        for r in range(self.comm.world):
+            a, b = self.dg.owned_users(self.n_users, r)
+            out.append(allb[r * pad: r * pad + (b - a)])
+        return torch.cat(out, 0)
+
     def full_state_dict(self):
         """Reference-keyed state_dict (user_emb gathered from the owners)."""
-        dev = self.user_emb_local.device
-        C = self.user_emb_local.size(1)
-        blk = torch.zeros(self.dg.R, C, dtype=torch.float32, device=dev)
-        blk[:self.u1 - self.u0] = self.user_emb_local.detach()
-        allb = self.comm.all_gather_rows(blk)
-        rows = []
-        for r in range(self.dg.world):
-            u0, u1 = self.dg.owned_users(self.n_users, r)
-            rows.append(allb[r * self.dg.R: r * self.dg.R + (u1 - u0)])
-        sd = {"user_emb.weight": torch.cat(rows, 0)}
+        pad = max(int(b - a) for a, b in (self.dg.owned_users(self.n_users, r) for r in range(self.comm.world)))
+        sd = {"user_emb.weight": self._user_rows_global(self.user_emb_local.detach(), max(pad, 1))}
         for k, v in self.state_dict().items():
             if k != "user_emb_local":
                 sd[k] = v
         return sd
 
 
-def _item_loss_map(dg: DistGraph, n_users: int) -> torch.Tensor:
-    """Node id -> row of [own block's user rows ; all_gather of every rank's item slice]:
-    own users -> their block row, other users -> -1 (triple skipped), items -> gathered row."""
-    if dg.loss_map is None:
-        (ub, ib), (RU, RI) = dg.seg_bounds, dg.seg_R
-        N = dg.n_nodes
-        m = np.full(N, -1, np.int64)
-        u0, u1 = int(ub[dg.rank]), int(ub[dg.rank + 1])
-        m[u0:u1] = np.arange(u1 - u0)
-        owner = np.repeat(np.arange(dg.world), np.diff(ib))
-        m[n_users:] = RU + owner * RI + (np.arange(n_users, N) - ib[owner])
-        dg.loss_map = torch.from_numpy(m).to(torch.int32).to(dg.row_map.device)
-    return dg.loss_map
+class HaloPyGGAT(_ShardedBase):
+    """PyGGAT with row-sharded users and items and halo all_to_all exchange (module doc).
+    ``forward`` returns the own rows [n_own, C]: own users, then own items."""
+
+    def node_features(self, item_feats):
+        (i0, i1) = self.dg.owned()[1]
+        nu = self.n_users
+        x_items = self.stages.linear(item_feats[i0 - nu:i1 - nu].contiguous(), self.item_proj.weight,
+                                     self.item_proj.bias)
+        return torch.cat([self.user_emb_local, x_items], 0)
+
+    @staticmethod
+    def exchanges_input(conv) -> bool:
+        """Exchange the pre-projection rows when they are narrower than h (H*C > C_in)."""
+        return conv.heads * conv.out_channels > conv.in_channels
+
+    def forward(self, item_feats):
+        hg = self.dg
+        x = self.node_features(item_feats)
+        for conv in self.convs:
+            if self.exchanges_input(conv):
+                h = self.stages.linear(exchange(x, hg.plan, self.comm, self.stages), conv.lin.weight, None)
+            else:
+                h = exchange(self.stages.linear(x, conv.lin.weight, None), hg.plan, self.comm, self.stages)
+            x = _LocalGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, hg, self.stages, conv.heads,
+                                conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope),
+                                float(conv.dropout) if self.training else 0.0, self.layer_seed(conv))
+        return x
 
 
-def sharded_bpr_loss(Z_local, dg: DistGraph, comm: Comm, u, i, j, n_users: int, n_items: int, loss: str = "bpr",
-                     stages=None):
-    """The BPR/BCE loss of train_gat_pyg.py:313-322 over row-sharded Z; the ranks' returned
-    values add up to the reference's mean loss.
+def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j):
+    """Exchange plan + row map for the triples of this rank's own users: the item rows they
+    read that other ranks own come by one all_to_all (requests exchanged once per triple set)."""
+    key = (u.data_ptr(), i.data_ptr(), j.data_ptr(), int(u.numel()), u._version, i._version, j._version)
+    hit = hg.loss_plans.get(key)
+    if hit is not None:
+        return hit
+    nu, N = hg.n_users, hg.n_nodes
+    (u0, u1), _ = hg.owned()
+    un, inn, jn = (t.detach().cpu().numpy().astype(np.int64) for t in (u, i, j))
+    mine = (un >= u0) & (un < u1)
+    items = np.unique(np.concatenate([inn[mine], jn[mine]])) + nu if mine.any() else np.zeros(0, np.int64)
+    items = items[(items >= nu) & (items < N)]
+    req = items[hg.owner[items] != hg.rank]                    # ascending ids, grouped by owner below
+    req = req[np.argsort(hg.owner[req], kind="stable")]
+    recv_counts = np.bincount(hg.owner[req], minlength=hg.world)
+    send_counts = comm.all_to_all_counts(recv_counts)          # what each peer asks of this rank
+    dev = u.device
+    ids_in = comm.all_to_all_rows(torch.from_numpy(req).to(dev if comm.backend == "nccl" else "cpu"),
+                                  recv_counts, send_counts).cpu().numpy()
+    plan = make_plan(hg.n_own, hg.local_of[ids_in], send_counts, recv_counts, dev)
+    rmap = np.full(N, -1, np.int64)
+    rmap[u0:u1] = hg.local_of[u0:u1]
+    own_items = items[hg.owner[items] == hg.rank]
+    rmap[own_items] = hg.local_of[own_items]
+    rmap[req] = hg.n_own + np.arange(len(req))
+    res = (plan, torch.from_numpy(rmap.astype(np.int32)).to(dev))
+    hg.loss_plans.clear()  # one live triple set at a time (an epoch's draw)
+    hg.loss_plans[key] = res
+    return res
 
-    (users, items) segments: every rank evaluates the triples of its own users against
-    the all-gathered item rows (n_items x C), item gradients return by reduce_scatter.
-    Otherwise: all_gather of Z and a contiguous share of the triples."""
+
+def halo_bpr_loss(Z_own, hg: HaloGraph, comm: "Comm", u, i, j, n_users: int, n_items: int, loss: str = "bpr",
+                  stages=None):
+    """The BPR/BCE loss of train_gat_pyg.py:313-322 over row-sharded Z: each rank takes the
+    triples of its own users; the ranks' returned values add up to the reference's mean."""
     if stages is None:
         from .hip_ops import HipStages
         stages = HipStages()
-    S = int(u.numel())
-    segs = dg.seg_bounds
-    if len(segs) == 2 and int(segs[0][0]) == 0 and int(segs[0][-1]) == n_users:
-        RU, RI = dg.seg_R
-        I_full = all_gather_rows(Z_local[RU:RU + RI], comm)
-        Zl = torch.cat([Z_local[:RU], I_full], 0)
-        return stages.bpr(Zl, n_users, n_items, _item_loss_map(dg, n_users), u, i, j, loss)
-    a, b = S * comm.rank // comm.world, S * (comm.rank + 1) // comm.world
-    Z_full = all_gather_rows(Z_local, comm)
-    part = stages.bpr(Z_full, n_users, n_items, dg.row_map, u[a:b], i[a:b], j[a:b], loss)
-    return part * ((b - a) / max(S, 1))
+    plan, rmap = _loss_plan(hg, comm, u, i, j)
+    Zl = exchange(Z_own, plan, comm, stages)
+    return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss)
 
 
-def gather_rows_to_global(Z_local, dg: DistGraph, comm: Comm) -> torch.Tensor:
-    """[R, C] own rows -> [N, C] in node-id order (every rank gets the full matrix)."""
-    Z_full = comm.all_gather_rows(Z_local.contiguous())
-    return Z_full.index_select(0, dg.row_map.to(torch.int64))
+def halo_rows_to_global(Z_own, hg: HaloGraph, comm: "Comm") -> torch.Tensor:
+    """[n_own, C] own rows -> [N, C] in node-id order on every rank (all_gather; export and
+    test helper, not on the training path)."""
+    pad = max(int(hg.seg_bounds[0][r + 1] - hg.seg_bounds[0][r] + hg.seg_bounds[1][r + 1] - hg.seg_bounds[1][r])
+              for r in range(hg.world))
+    blk = Z_own.new_zeros(max(pad, 1), Z_own.size(1))
+    blk[:hg.n_own] = Z_own
+    allb = comm.all_gather_rows(blk)
+    idx = np.empty(hg.n_nodes, np.int64)
+    ub, ib = hg.seg_bounds
+    for r in range(hg.world):
+        nur = int(ub[r + 1] - ub[r])
+        idx[ub[r]:ub[r + 1]] = r * pad + np.arange(nur)
+        idx[ib[r]:ib[r + 1]] = r * pad + nur + np.arange(int(ib[r + 1] - ib[r]))
+    return allb.index_select(0, torch.from_numpy(idx).to(allb.device))
 
 
 # ---------------------------------------------------------------------------
@@ -602,14 +744,16 @@ class _ReplicatedGAT(torch.autograd.Function):
         a_d = att_dst.detach().reshape(heads, C).contiguous()
         b = bias.detach().contiguous() if bias is not None else None
         s_src, s_dst = stages.scores(h, a_s, a_d, heads, C)
-        out, m, inv_l, agg = stages.fwd(rg.view, h, s_src, s_dst, b, heads, C, mode, slope, p, seed, heads > 1)
+        seed_buf = stages.seed_buffer(p, h.device)
+        out, m, inv_l, agg = stages.fwd(rg.view, h, s_src, s_dst, b, heads, C, mode, slope, p, seed, heads > 1,
+                                        seed_buf=seed_buf)
         if comm.active:
             _merge_item_rows(rg, comm, out, m, inv_l, agg, b, heads, C)
         if any(ctx.needs_input_grad[:4]):
             empty = torch.empty(0, device=h.device)
             ctx.save_for_backward(h, a_s, a_d, s_src, s_dst, out, m, inv_l, agg if agg is not None else empty,
                                   b if b is not None else empty)
-        ctx.rg, ctx.comm, ctx.stages = rg, comm, stages
+        ctx.rg, ctx.comm, ctx.stages, ctx.seed_buf = rg, comm, stages, seed_buf
         ctx.meta = (heads, C, mode, slope, p, seed, bias is not None, agg is not None)
         ctx.att_shapes = (att_src.shape, att_dst.shape)
         return out
@@ -629,7 +773,8 @@ class _ReplicatedGAT(torch.autograd.Function):
         nstate, _ = st.bwd_prologue(g, out, agg if has_agg else None, b if has_bias else None, s_dst, m, inv_l,
                                     heads, C, mode, False)
         dz = torch.zeros(max(rg.view.n_bwd_edges, 1) * heads, dtype=h.dtype, device=h.device)
-        grad_h, ds_src = st.bwd_edges(rg.view, h, s_src, nstate, g, dz, heads, C, mode, slope, p, seed)
+        grad_h, ds_src = st.bwd_edges(rg.view, h, s_src, nstate, g, dz, heads, C, mode, slope, p, seed,
+                                      seed_buf=ctx.seed_buf)
         datt_src, datt_dst = st.bwd_epilogue(rg.view, h, a_s, a_d, ds_src, dz, grad_h, heads, C)
         dbias = None
         if has_bias and ctx.needs_input_grad[3]:
@@ -640,7 +785,7 @@ class _ReplicatedGAT(torch.autograd.Function):
                 None, None, None, None, None, None, None, None, None)
 
 
-class ReplicatedPyGGAT(ShardedPyGGAT):
+class ReplicatedPyGGAT(_ShardedBase):
     """PyGGAT with the users sharded and the item rows replicated (see above).  Local rows:
     [own users | every item]; ``forward`` returns them (Z's item rows are the same on every
     rank).  With the HIP stages (default) each layer is the fused hip_ops.GATLayer on the
@@ -663,7 +808,7 @@ class ReplicatedPyGGAT(ShardedPyGGAT):
             x = self.user_emb_local
             for li, conv in enumerate(self.convs):
                 p = float(conv.dropout) if self.training else 0.0
-                seed = _dropout_seed() if p > 0 else 0
+                seed = self.layer_seed(conv)
                 x = gat_layer(x, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, self.dg.graph, conv.heads,
                               conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p, seed,
                               x_items=x_items if li == 0 else None, rep=self.hooks)
@@ -672,30 +817,11 @@ class ReplicatedPyGGAT(ShardedPyGGAT):
         for conv in self.convs:
             h = self.stages.linear(x, conv.lin.weight, None)
             p = float(conv.dropout) if self.training else 0.0
-            seed = _dropout_seed() if p > 0 else 0
+            seed = self.layer_seed(conv)
             x = _ReplicatedGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, self.dg, self.comm, self.stages,
                                      conv.heads, conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p,
                                      seed)
         return x
-
-
-def _replicated_full_state_dict(self):
-    """Reference-keyed state_dict (user_emb gathered from the owners)."""
-    rg = self.dg
-    C = self.user_emb_local.size(1)
-    blk = torch.zeros(rg.RU_max, C, dtype=torch.float32, device=self.user_emb_local.device)
-    blk[:rg.RU] = self.user_emb_local.detach()
-    allb = self.comm.all_gather_rows(blk)
-    ub = rg.user_bounds
-    sd = {"user_emb.weight": torch.cat([allb[r * rg.RU_max: r * rg.RU_max + int(ub[r + 1] - ub[r])]
-                                        for r in range(rg.world)], 0)}
-    for k, v in self.state_dict().items():
-        if k != "user_emb_local":
-            sd[k] = v
-    return sd
-
-
-ReplicatedPyGGAT.full_state_dict = _replicated_full_state_dict
 
 
 def replicated_bpr_loss(Z_local, rg: RepGraph, comm: Comm, u, i, j, n_users: int, n_items: int,

@@ -195,8 +195,14 @@ def node_scores(h: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, h
     return s_src, s_dst
 
 
+def seed_buffer(dropout_p: float, device) -> Optional[torch.Tensor]:
+    """Device slot for the effective mask seed a forward used (include/ppgat.h ppgat_fwd
+    seed_used), handed to its backward; None without dropout."""
+    return torch.empty(1, dtype=torch.int64, device=device) if dropout_p > 0 else None
+
+
 def gat_fwd(g: CSRGraph, h, s_src, s_dst, bias, heads: int, channels: int, mode: int, slope: float,
-            dropout_p: float, seed: int, want_agg: bool):
+            dropout_p: float, seed: int, want_agg: bool, seed_buf: Optional[torch.Tensor] = None):
     lib = _lib.load()
     N = g.n_nodes
     dev = h.device
@@ -214,14 +220,15 @@ def gat_fwd(g: CSRGraph, h, s_src, s_dst, bias, heads: int, channels: int, mode:
     _lib.check(lib.ppgat_fwd(ctypes.byref(cs), _lib.ptr(g.col) if g.n_edges else None,
                              _lib.ptr(g.csr_eid) if g.n_edges else None, N, g.n_edges, heads, channels,
                              h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), _lib.ptr(bias), mode, float(slope),
-                             float(dropout_p), int(seed) & (2**64 - 1), out.data_ptr(), m.data_ptr(),
-                             inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
+                             float(dropout_p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf), out.data_ptr(),
+                             m.data_ptr(), inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
                              _lib.stream_handle(dev)), "gat_fwd")
     return out, m, inv_l, agg
 
 
 def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, inv_l, grad_out, heads: int,
-            channels: int, mode: int, slope: float, dropout_p: float, seed: int, want_bias_grad: bool = False):
+            channels: int, mode: int, slope: float, dropout_p: float, seed: int, want_bias_grad: bool = False,
+            seed_buf: Optional[torch.Tensor] = None):
     lib = _lib.load()
     N = g.n_nodes
     dev = h.device
@@ -242,7 +249,8 @@ def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, i
                              channels, h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), att_src.data_ptr(),
                              att_dst.data_ptr(), _lib.ptr(bias), out.data_ptr(), _lib.ptr(agg), m.data_ptr(),
                              inv_l.data_ptr(), grad_out.data_ptr(), mode, float(slope), float(dropout_p),
-                             int(seed) & (2**64 - 1), grad_h.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(),
+                             int(seed) & (2**64 - 1), _lib.ptr(seed_buf), grad_h.data_ptr(), datt_src.data_ptr(),
+                             datt_dst.data_ptr(),
                              _lib.ptr(dbias), ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "gat_bwd")
     return grad_h, datt_src, datt_dst, dbias
 
@@ -260,8 +268,9 @@ class GATAggregate(torch.autograd.Function):
         bias_c = bias.detach().contiguous() if bias is not None else None
         s_src, s_dst = node_scores(h, att_src_c, att_dst_c, heads, channels)
         need_grad = any(ctx.needs_input_grad[:4])
+        ctx.seed_buf = seed_buffer(dropout_p, h.device) if need_grad else None
         out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, bias_c, heads, channels, mode, slope, dropout_p, seed,
-                                     want_agg=need_grad and heads > 1)
+                                     want_agg=need_grad and heads > 1, seed_buf=ctx.seed_buf)
         if need_grad:
             ctx.save_for_backward(h, att_src_c, att_dst_c, s_src, s_dst, out, m, inv_l,
                                   agg if agg is not None else torch.empty(0, device=h.device),
@@ -280,7 +289,7 @@ class GATAggregate(torch.autograd.Function):
         grad_h, datt_src, datt_dst, dbias = gat_bwd(ctx.graph, h, s_src, s_dst, att_src, att_dst,
                                                     bias if has_bias else None, out, agg if has_agg else None, m,
                                                     inv_l, grad_out, heads, channels, mode, slope, p, seed,
-                                                    want_bias_grad=want_db)
+                                                    want_bias_grad=want_db, seed_buf=ctx.seed_buf)
         return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
                 None, None, None, None, None, None, None)
 
@@ -289,7 +298,8 @@ def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope
     return GATAggregate.apply(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
 
 
-def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channels, mode, slope, p, seed):
+def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channels, mode, slope, p, seed,
+                   seed_buf=None):
     """Pass B into D [N, HC] (dh_msg) and S[:, :H] (ds_src); the destination sum into
     S[:, H:2H] (ds_dst).  S [N, 2H] is compact (its scattered per-node writes stay in L2)
     and D keeps whole 512-B rows for the GEMMs that read it."""
@@ -307,7 +317,8 @@ def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channel
     _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(g.row) if E else None,
                                    _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, E, heads,
                                    channels, h.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), grad_out.data_ptr(),
-                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), D.data_ptr(), HC,
+                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                   D.data_ptr(), HC,
                                    S.data_ptr(), 2 * heads, dz.data_ptr(), ws.data_ptr(), nbytes.value, st),
                "bwd_edges")
     fs = g.fwd_sched.cstruct()
@@ -466,8 +477,9 @@ class GATLayer(torch.autograd.Function):
             h = torch.nn.functional.linear(x, W)
             s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
         need = any(ctx.needs_input_grad[:5]) or (had_items and ctx.needs_input_grad[12])
+        ctx.seed_buf = seed_buffer(dropout_p, x.device) if need else None
         out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed,
-                                     want_agg=(need or rep is not None) and heads > 1)
+                                     want_agg=(need or rep is not None) and heads > 1, seed_buf=ctx.seed_buf)
         if rep is not None:  # replicated item rows (dist.py): merge their softmax over the ranks
             rep.merge_fwd(out, m, inv_l, agg, b, heads, channels)
         if need:
@@ -523,7 +535,7 @@ class GATLayer(torch.autograd.Function):
                 dbias = dbias + db_i
         D = torch.empty(N, HC, dtype=torch.float32, device=dev)
         S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
-        _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed)
+        _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed, ctx.seed_buf)
         need_dx = ctx.needs_input_grad[0] or (had_items and ctx.needs_input_grad[12])
         dx = None
         if need_dx:
@@ -761,13 +773,37 @@ class HipStages:
     def linear(self, x, weight, bias):
         return linear(x, weight, bias)
 
+    def seed_buffer(self, p, device):
+        return seed_buffer(p, device)
+
+    def gather_rows(self, t, idx):
+        """t[idx] (the all_to_all send buffer) through ppgat_rows_gather."""
+        lib = _lib.load()
+        _check_dev("rows", t, torch.float32)
+        _check_dev("idx", idx, torch.int64, t.device)
+        out = torch.empty((idx.numel(),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        cols = t[0].numel() if t.size(0) else (out[0].numel() if idx.numel() else 0)
+        _lib.check(lib.ppgat_rows_gather(t.data_ptr(), cols, idx.data_ptr(), idx.numel(), cols, out.data_ptr(), cols,
+                                         _lib.stream_handle(t.device)), "rows_gather")
+        return out
+
+    def return_add(self, dst, ret, ptr, pos):
+        """dst[o] += ret[pos[ptr[o]:ptr[o+1]]] in order (ppgat_rows_return_add), in place."""
+        lib = _lib.load()
+        _check_dev("dst", dst, torch.float32)
+        cols = dst[0].numel() if dst.size(0) else 0
+        _lib.check(lib.ppgat_rows_return_add(dst.data_ptr(), cols, ret.data_ptr() if ret.numel() else None, cols,
+                                             ptr.data_ptr(), pos.data_ptr() if pos.numel() else None, dst.size(0),
+                                             cols, _lib.stream_handle(dst.device)), "rows_return_add")
+        return dst
+
     def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss):
         return bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, loss)
 
     def scores(self, h, att_src, att_dst, heads, channels):
         return node_scores(h, att_src, att_dst, heads, channels)
 
-    def fwd(self, v, h_full, s_src_full, s_dst, bias, heads, channels, mode, slope, p, seed, want_agg):
+    def fwd(self, v, h_full, s_src_full, s_dst, bias, heads, channels, mode, slope, p, seed, want_agg, seed_buf=None):
         lib = _lib.load()
         dev = h_full.device
         R = v.n_rows
@@ -783,8 +819,8 @@ class HipStages:
         _lib.check(lib.ppgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if v.n_fwd_edges else None,
                                  _lib.ptr(v.csr_eid) if v.n_fwd_edges else None, R, v.n_fwd_edges, heads, channels,
                                  h_full.data_ptr(), s_src_full.data_ptr(), s_dst.data_ptr(), _lib.ptr(bias), mode,
-                                 float(slope), float(p), int(seed) & (2**64 - 1), out.data_ptr(), m.data_ptr(),
-                                 inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
+                                 float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf), out.data_ptr(),
+                                 m.data_ptr(), inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
                                  _lib.stream_handle(dev)), "gat_fwd")
         return out, m, inv_l, agg
 
@@ -802,7 +838,8 @@ class HipStages:
                                           _lib.stream_handle(dev)), "bwd_prologue")
         return nstate, dbias
 
-    def bwd_edges(self, v, h, s_src, nstate_full, grad_out_full, dz, heads, channels, mode, slope, p, seed):
+    def bwd_edges(self, v, h, s_src, nstate_full, grad_out_full, dz, heads, channels, mode, slope, p, seed,
+                  seed_buf=None):
         lib = _lib.load()
         dev = h.device
         R = v.n_rows
@@ -818,7 +855,8 @@ class HipStages:
                                        _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None, E,
                                        heads, channels, h.data_ptr(), s_src.data_ptr(), nstate_full.data_ptr(),
                                        grad_out_full.data_ptr(), mode, float(slope), float(p),
-                                       int(seed) & (2**64 - 1), grad_h.data_ptr(), heads * channels,
+                                       int(seed) & (2**64 - 1), _lib.ptr(seed_buf), grad_h.data_ptr(),
+                                       heads * channels,
                                        ds_src.data_ptr(), heads, dz.data_ptr(), ws.data_ptr(), nbytes.value,
                                        _lib.stream_handle(dev)), "bwd_edges")
         return grad_h, ds_src

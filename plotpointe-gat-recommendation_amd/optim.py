@@ -7,12 +7,11 @@ hyper-parameters, the same per-parameter state keys (``step``, ``exp_avg``,
 corrections, eps after the square root), so optimizer state_dicts move between the two.
 Supported: fp32 dense tensors on one ROCm device, amsgrad=False, maximize=False.
 
-``capturable=True`` (torch.optim.Adam's flag of the same name): the step count lives on
-the device (one float per param group, shared by its parameters' ``state["step"]``) and is
-incremented and turned into the bias corrections on the stream
-(``ppgat_adam_step_device``), so ``step()`` can be captured in a hipGraph and replayed.
-All parameters of a group are assumed to step together (a parameter with no gradient is
-skipped, but the group's count still advances).
+``capturable=True`` (torch.optim.Adam's flag of the same name): every parameter's step
+count ``state["step"]`` is a device float (as in torch's capturable Adam), incremented with
+one multi-tensor launch and turned into the bias corrections on the stream
+(``ppgat_adam_step_device``), so ``step()`` can be captured in a hipGraph and replayed; a
+parameter without a gradient keeps its count, and saved state has one count per parameter.
 """
 from __future__ import annotations
 
@@ -80,12 +79,6 @@ class Adam(torch.optim.Optimizer):
         ps = [p for p in group["params"] if p.grad is not None]
         if not ps:
             return
-        tstep = None
-        for p in group["params"]:
-            st = self.state[p]
-            if "step" in st:
-                tstep = st["step"]
-                break
         for p in ps:
             g = p.grad
             if g.is_sparse or not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous()
@@ -93,12 +86,14 @@ class Adam(torch.optim.Optimizer):
                 raise RuntimeError("ppgat Adam: fp32 contiguous dense ROCm parameters and gradients only")
             st = self.state[p]
             if len(st) == 0:
-                if tstep is None:
-                    tstep = torch.zeros((), dtype=torch.float32, device=p.device)
-                st["step"] = tstep
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-        tstep.add_(1.0)  # on the stream: graph replays advance it
+            elif not (st["step"].is_cuda and st["step"].device == p.device and st["step"].dtype == torch.float32):
+                # a state_dict loaded from a host-step run: the count moves to the device once
+                st["step"] = st["step"].to(device=p.device, dtype=torch.float32).reshape(())
+        steps = [self.state[p]["step"] for p in ps]
+        torch._foreach_add_(steps, 1.0)  # one launch, on the stream: graph replays advance every count
         for k in range(0, len(ps), cap):
             chunk = ps[k:k + cap]
             n = len(chunk)
@@ -108,8 +103,9 @@ class Adam(torch.optim.Optimizer):
             M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in chunk])
             V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in chunk])
             NE = (ctypes.c_int64 * n)(*[p.numel() for p in chunk])
-            _lib.check(lib.ppgat_adam_step_device(n, P, G, M, V, NE, tstep.data_ptr(), float(group["lr"]), float(b1),
-                                                  float(b2), float(group["eps"]), float(group["weight_decay"]),
+            T = (ctypes.c_void_p * n)(*[self.state[p]["step"].data_ptr() for p in chunk])
+            _lib.check(lib.ppgat_adam_step_device(n, P, G, M, V, NE, T, float(group["lr"]), float(b1), float(b2),
+                                                  float(group["eps"]), float(group["weight_decay"]),
                                                   _lib.stream_handle(dev)), "adam_step_device")
 
     @staticmethod

@@ -45,6 +45,20 @@ class CpuStages:
     def linear(self, x, W, b):
         return torch.nn.functional.linear(x, W, b)
 
+    def seed_buffer(self, p, device):
+        return None
+
+    def gather_rows(self, t, idx):
+        return t.index_select(0, idx.long())
+
+    def return_add(self, dst, ret, ptr, pos):
+        """ppgat_rows_return_add restated: each row adds its returned copies in peer order."""
+        ptr, pos = ptr.long(), pos.long()
+        for o in torch.nonzero(ptr[1:] > ptr[:-1]).squeeze(1).tolist():
+            for k in range(int(ptr[o]), int(ptr[o + 1])):
+                dst[o] += ret[pos[k]]
+        return dst
+
     def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss):
         """Triples whose user maps to -1 are not held by this rank: they contribute 0 and
         the mean stays over all S triples (include/ppgat.h ppgat_bpr_fwd)."""
@@ -61,7 +75,7 @@ class CpuStages:
         hv = h.view(-1, H, C)
         return (hv * a_s).sum(-1), (hv * a_d).sum(-1)
 
-    def fwd(self, v, h_full, s_src_full, s_dst, bias, H, C, mode, slope, p, seed, want_agg):
+    def fwd(self, v, h_full, s_src_full, s_dst, bias, H, C, mode, slope, p, seed, want_agg, seed_buf=None):
         R = v.n_rows
         rowptr = v.rowptr.long()
         col = v.col.long()
@@ -93,7 +107,7 @@ class CpuStages:
         nstate = torch.stack([s_dst, m, inv_l, D], -1)
         return nstate, (g.sum(0) if want_db else None)
 
-    def bwd_edges(self, v, h, s_src, nstate_full, g_full, dz, H, C, mode, slope, p, seed):
+    def bwd_edges(self, v, h, s_src, nstate_full, g_full, dz, H, C, mode, slope, p, seed, seed_buf=None):
         R = v.n_rows
         colptr = v.colptr.long()
         src = torch.repeat_interleave(torch.arange(R), colptr[1:] - colptr[:-1])

@@ -24,7 +24,7 @@ def test_all_header_symbols_exported(pkg):
 
 def test_version_and_channels(pkg):
     lib = pkg._lib.load()
-    assert lib.ppgat_version() == 2
+    assert lib.ppgat_version() == 3
     assert [c for c in range(1, 300) if lib.ppgat_supported_channels(c)] == [4, 8, 16, 32, 64, 128, 256]
 
 
@@ -32,24 +32,24 @@ def test_invalid_arguments_return_codes(pkg):
     lib = pkg._lib.load()
     # unsupported channel count -> PPGAT_ERR_UNSUPPORTED before any device work
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 96, None, None, None, None, 0, 0.2, 0.0, 0,
-                       None, None, None, None, None, 0, None)
+                       None, None, None, None, None, None, 0, None)
     assert rc == 2 and b"channels" in lib.ppgat_last_error()
     # custom mode with a bias -> invalid
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, ctypes.c_void_p(16), 1, 0.2, 0.0, 0,
-                       None, None, None, None, None, 0, None)
+                       None, None, None, None, None, None, 0, None)
     assert rc == 1 and b"custom" in lib.ppgat_last_error()
     # dropout out of range
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 1.0, 0,
-                       None, None, None, None, None, 0, None)
+                       None, None, None, None, None, None, 0, None)
     assert rc == 1
     # missing schedule
     rc = lib.ppgat_fwd(None, None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 0.0, 0,
-                       None, None, None, None, None, 0, None)
+                       None, None, None, None, None, None, 0, None)
     assert rc == 1 and b"schedule" in lib.ppgat_last_error()
     # inconsistent schedule counts
     bad = pkg._lib.Schedule(None, None, None, 3, 5, None, None, 0)
     rc = lib.ppgat_fwd(ctypes.byref(bad), None, None, 10, 0, 1, 128, None, None, None, None, 0, 0.2, 0.0, 0,
-                       None, None, None, None, None, 0, None)
+                       None, None, None, None, None, None, 0, None)
     assert rc == 1 and b"inconsistent" in lib.ppgat_last_error()
     assert lib.ppgat_schedule_capacity(100, 1000, 256) == 100 + 4 + 1
     with pytest.raises(NotImplementedError):

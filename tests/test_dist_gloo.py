@@ -45,7 +45,7 @@ def _setup(n_users=300, n_items=120, n_int=3000, heads=1, C=32, ii=False):
     return pkg, g, ei, feats, full, [torch.from_numpy(a) for a in (u, i, j)]
 
 
-def _worker(rank, world, port, out_dir, heads, segmented):
+def _worker(rank, world, port, out_dir, heads, ii):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -53,42 +53,39 @@ def _worker(rank, world, port, out_dir, heads, segmented):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     from _cpu_stages import CpuStages, csr_builder
-    pkg, g, ei, feats, full, (u, i, j) = _setup(heads=heads)
+    pkg, g, ei, feats, full, (u, i, j) = _setup(heads=heads, ii=ii)
     dmod = pkg.dist
     comm = dmod.Comm()
-    segs = [(0, g.n_users), (g.n_users, g.n_nodes)] if segmented else None
-    dg = dmod.build_dist_graph(ei, g.n_nodes, world, rank, csr_builder=csr_builder, sched_builder=None,
-                               segments=segs)
+    hg = dmod.build_halo_graph(ei, g.n_nodes, g.n_users, world, rank, csr_builder=csr_builder, sched_builder=None)
     st = CpuStages()
-    model = dmod.ShardedPyGGAT(full, dg, comm, stages=st).train()
-    torch.manual_seed(123)
+    model = dmod.HaloPyGGAT(full, hg, comm, stages=st).train()
+    torch.manual_seed(123 + 1000 * rank)  # ranks seeded differently: the dropout seeds are shared anyway
     Z = model(feats)
-    loss = dmod.sharded_bpr_loss(Z, dg, comm, u, i, j, g.n_users, g.n_items, stages=st)
+    loss = dmod.halo_bpr_loss(Z, hg, comm, u, i, j, g.n_users, g.n_items, stages=st)
     loss.backward()
     model.allreduce_grads()
     tot = loss.detach().clone()
     comm.all_reduce_(tot)
-    Zg = dmod.gather_rows_to_global(Z.detach(), dg, comm)
+    Zg = dmod.halo_rows_to_global(Z.detach(), hg, comm)
     sd = model.full_state_dict()
     grads = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
-    ublk = torch.zeros(dg.R, model.user_emb_local.size(1), dtype=torch.float64)
-    ublk[:model.u1 - model.u0] = model.user_emb_local.grad
-    ug = comm.all_gather_rows(ublk)
-    urows = [ug[r * dg.R: r * dg.R + (min(int(dg.bounds[r + 1]), g.n_users) - min(int(dg.bounds[r]), g.n_users))]
-             for r in range(world)]
+    ug = model._user_rows_global(model.user_emb_local.grad, g.n_users)
     if rank == 0:
-        torch.save({"Z": Zg, "loss": tot, "grads": grads, "user_grad": torch.cat(urows), "sd": sd,
-                    "bounds": dg.bounds}, os.path.join(out_dir, "res.pt"))
+        torch.save({"Z": Zg, "loss": tot, "grads": grads, "user_grad": ug, "sd": sd, "bounds": hg.bounds,
+                    "n_halo": hg.n_halo, "n_send": hg.plan.n_send}, os.path.join(out_dir, "res.pt"))
     dist.destroy_process_group()
 
 
 def _reference(heads, ii=False):
+    """The unsharded fp64 oracle with the layer seeds the sharded run derives (rank 0's first
+    draw after torch.manual_seed(123), dist.SharedSeeds)."""
     sys.path.insert(0, str(ROOT))
     from oracle import gat_oracle as O
     pkg, g, ei, feats, full, (u, i, j) = _setup(heads=heads, ii=ii)
     P = {k: v.detach().clone().requires_grad_(True) for k, v in full.named_parameters()}
     torch.manual_seed(123)
-    seeds = [pkg.dist._dropout_seed() for _ in range(2)]
+    base = pkg.dist._dropout_seed()
+    seeds = [pkg.dist.derive_seed(base, k) for k in range(2)]
     x = torch.cat([P["user_emb.weight"], feats @ P["item_proj.weight"].t() + P["item_proj.bias"]], 0)
     for l in range(2):
         x = O.pyg_gat_conv(x, ei, P[f"convs.{l}.lin.weight"], P[f"convs.{l}.att_src"], P[f"convs.{l}.att_dst"],
@@ -102,16 +99,21 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("world,heads,segmented", [(2, 1, False), (3, 2, False), (2, 1, True), (3, 2, True)])
-def test_sharded_matches_unsharded(tmp_path, world, heads, segmented):
-    """segmented: users and items partitioned separately (every rank holds both), the loss
-    over the rank's own users with only the item rows gathered."""
+@pytest.mark.parametrize("world,heads,ii", [(2, 1, False), (3, 2, False), (2, 1, True), (3, 4, True),
+                                           (1, 1, False)])
+def test_halo_matches_unsharded_oracle(tmp_path, world, heads, ii):
+    """Halo partition (dist.build_halo_graph): users and items row-sharded, one all_to_all of
+    the halo rows per layer (h when H*C <= C_in, pre-lin x otherwise: heads 2/4 here), the
+    reverse all_to_all of their gradients, the item rows of the loss by all_to_all; forward,
+    loss, every gradient == the unsharded fp64 oracle, with attention dropout."""
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path), heads, segmented), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), heads, ii), nprocs=world, join=True,
                        start_method="spawn")
     res = torch.load(tmp_path / "res.pt", weights_only=False)
-    Zr, lr, gr, full = _reference(heads)
+    Zr, lr, gr, full = _reference(heads, ii)
     assert len(res["bounds"]) == world + 1
+    if world > 1:
+        assert res["n_halo"] > 0 and res["n_send"] > 0
     assert _rel(res["Z"], Zr) <= 1e-10
     assert abs(float(res["loss"]) - float(lr)) <= 1e-12
     assert _rel(res["user_grad"], gr["user_emb.weight"]) <= 1e-10
@@ -139,7 +141,7 @@ def _rep_worker(rank, world, port, out_dir, heads, ii):
                                      sched_builder=None)
     st = CpuStages()
     model = dmod.ReplicatedPyGGAT(full, rg, comm, stages=st).train()
-    torch.manual_seed(123)
+    torch.manual_seed(123 + 1000 * rank)
     Z = model(feats)
     loss = dmod.replicated_bpr_loss(Z, rg, comm, u, i, j, g.n_users, g.n_items, stages=st)
     loss.backward()
@@ -150,13 +152,9 @@ def _rep_worker(rank, world, port, out_dir, heads, ii):
     items = comm.all_gather_rows(Z.detach()[rg.RU:].contiguous())   # replicas must agree bitwise
     sd = model.full_state_dict()
     grads = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
-    ublk = torch.zeros(rg.RU_max, model.user_emb_local.size(1), dtype=torch.float64)
-    ublk[:model.u1 - model.u0] = model.user_emb_local.grad
-    ug = comm.all_gather_rows(ublk)
-    ub = rg.user_bounds
-    urows = [ug[r * rg.RU_max: r * rg.RU_max + int(ub[r + 1] - ub[r])] for r in range(world)]
+    ug = model._user_rows_global(model.user_emb_local.grad, rg.RU_max)
     if rank == 0:
-        torch.save({"Z": Zg, "loss": tot, "grads": grads, "user_grad": torch.cat(urows), "sd": sd,
+        torch.save({"Z": Zg, "loss": tot, "grads": grads, "user_grad": ug, "sd": sd,
                     "items": items.view(world, g.n_items, -1), "n_local_edges": rg.view.n_fwd_edges},
                    os.path.join(out_dir, "res.pt"))
     dist.destroy_process_group()

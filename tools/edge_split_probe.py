@@ -78,13 +78,13 @@ def main():
             if name == "fwd":
                 fn = lambda cs=cs, Ns=Ns: _lib.check(lib.ppgat_fwd(ctypes.byref(cs), G.col.data_ptr(), G.csr_eid.data_ptr(), Ns,
                                                             E, 1, C, h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
-                                                            None, 0, 0.2, 0.1, 7, out.data_ptr(), m.data_ptr(),
+                                                            None, 0, 0.2, 0.1, 7, None, out.data_ptr(), m.data_ptr(),
                                                             invl.data_ptr(), None, ws.data_ptr(), nb.value, st), "fwd")
             else:
                 fn = lambda cs=cs, Ns=Ns: _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), G.row.data_ptr(),
                                                                   G.csc_eid.data_ptr(), G.csc2csr.data_ptr(), E, 1, C,
                                                                   h.data_ptr(), s_src.data_ptr(), nstate.data_ptr(),
-                                                                  go.data_ptr(), 0, 0.2, 0.1, 7, D.data_ptr(), C,
+                                                                  go.data_ptr(), 0, 0.2, 0.1, 7, None, D.data_ptr(), C,
                                                                   S.data_ptr(), 2, dz.data_ptr(), ws.data_ptr(),
                                                                   nb.value, st), "bwd")
             res[f"{name}_{part}"] = {"us": timeit(fn), "items": hi - lo, "edges": int(deg[lo:hi].sum())}

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One rank's share of an N-GPU config-2 step, on one GPU, collectives stubbed out.
 
-    python tools/scale_probe.py --world 8 --rank 0 [--partition replicated|rows]
+    python tools/scale_probe.py --world 8 --rank 0 [--partition replicated|halo]
 
 Builds the same per-rank graph and model as `bench.py --gpus N` and times the step with
 every collective replaced by a no-op (results are NOT the job's; only the compute and the
@@ -39,12 +39,25 @@ class NullComm:
     def all_reduce_(self, t, op=None):
         return t
 
+    def all_to_all_rows(self, t, send_counts, recv_counts, out=None):
+        # stub: the received rows are left as they are (uninitialised); timing only
+        n = int(sum(recv_counts))
+        if out is None:
+            out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        return out
+
+    def all_to_all_counts(self, counts):
+        return [int(c) for c in counts]
+
+    def broadcast_int(self, value, src=0):
+        return int(value)
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
-    ap.add_argument("--partition", choices=["replicated", "rows"], default="replicated")
+    ap.add_argument("--partition", choices=["replicated", "halo"], default="replicated")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph (as bench.py for N>1)")
@@ -66,10 +79,10 @@ def main():
         loss_fn = D.replicated_bpr_loss
         n_edges = dg.view.n_fwd_edges
     else:
-        dg = D.build_dist_graph(ei, g.n_nodes, args.world, args.rank, segments=[(0, g.n_users), (g.n_users, g.n_nodes)])
-        model = D.ShardedPyGGAT(full, dg, comm)
-        loss_fn = D.sharded_bpr_loss
-        n_edges = dg.view.n_fwd_edges
+        dg = D.build_halo_graph(ei, g.n_nodes, g.n_users, args.world, args.rank)
+        model = D.HaloPyGGAT(full, dg, comm)
+        loss_fn = D.halo_bpr_loss
+        n_edges = dg.fwd_view.n_fwd_edges
     opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=args.graph)
 
     def step():
