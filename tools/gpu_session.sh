@@ -21,7 +21,10 @@ run() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
+    tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v -rf --durations=15 --timeout 170 --timeout-method thread ;;
+    fast) run pytest_gpu_fast 900 python -u -m pytest tests -m gpu -q -rf --durations=10 --timeout 120 --timeout-method thread --deselect tests/test_gpu_fullsize.py ;;
+    fullsize) run pytest_fullsize 900 python -u -m pytest tests/test_gpu_fullsize.py -m gpu -v -s -rf --durations=0 --timeout 170 --timeout-method thread ;;
+    dist) run pytest_dist 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_graph.py -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     gemm) run pytest_gemm 300 python -u -m pytest tests/test_gpu_gemm.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     sampler) run pytest_sampler 300 python -u -m pytest tests/test_sampler.py "tests/test_gpu_eval.py::test_trainer_device_sampler" -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     bsampler) run bench_sampler 300 python tools/bench_sampler.py ;;
