@@ -384,6 +384,72 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
                      const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
                      void* stream);
 
+/* ---- fp32 matrix-core GEMMs (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains) ---------------
+ * Replaces: the hipBLAS/cuBLAS GEMMs of torch.nn.Linear in GATConv.lin at shapes past the fused
+ *           128-column projection (config 5: lin 256 -> 1024, train_gat_pyg.py:77) and of
+ *           PyGGAT.item_proj (train_gat_pyg.py:74,81), and their weight gradients.
+ * ppgat_gemm_nn:  y[m, n] = alpha x[m, k] B + bias  with B[k][j] = b[k * ldb + j] (b_layout 0)
+ *                 or b[j * ldb + k] (b_layout 1: x W^T with W = b [n, k]); k % 32 == 0,
+ *                 n % 128 == 0; bias nullable.
+ * ppgat_gemm_tn_big: out[ma, nb] = a[m, ma]^T b[m, nb] over m rows, ma and nb multiples of 128;
+ *                 row splits summed in split order (deterministic); workspace queried first.
+ * ppgat_colsum:   out[c] = sum_i y[i, c] (c in {128, 256}), fixed order. */
+int ppgat_gemm_nn_supported(int64_t m, int k, int n, int b_layout);
+int ppgat_gemm_nn(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
+                  float alpha, const float* bias, float* y, int64_t ldy, void* stream);
+int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes);
+int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb, float* out,
+                      void* workspace, size_t workspace_bytes, void* stream);
+int ppgat_colsum_workspace_bytes(int64_t n, int c, size_t* bytes);
+int ppgat_colsum(const float* y, int64_t ldy, int64_t n, int c, float* out, void* workspace, size_t workspace_bytes,
+                 void* stream);
+
+/* ---- multi-head layer, aggregate-then-transform ----------------------------------------------
+ * Replaces: GATConv(C_in, C, heads=H, concat=False) forward and backward (train_gat_pyg.py:77,
+ *           SURVEY.md Appendix A) when H*C > C_in -- config 5 (C_in = C = 256, H = 4).  The
+ *           message is linear in x_j, so the edge pass gathers x_j (C_in floats) once per edge
+ *           for all heads instead of h_j (H*C floats):
+ *   att_proj [2, H, C_in]: A_v[h] = W_h^T att_v[h]                      (ppgat_xgat_weights)
+ *   w_xform [H*C_in, C]: w_xform[h*C_in + k][c] = W[h*C + c][k];  w_grad [C, H*C_in] = w_xform^T / H
+ *   s_src[n][h] = x_n . A_src[h] (n < n_rows), s_dst likewise (n < n_dst)   (ppgat_xgat_scores)
+ *   agg[i][h] = sum_{j->i} alpha_ij^h x_j, m, inv_l [n_dst, H]  (ppgat_xgat_fwd; CSR over the
+ *     destination rows; x rows indexed by col may extend past n_dst: the halo rows of dist.py)
+ *   out = agg w_xform / H + bias                                          (ppgat_gemm_nn)
+ * Backward with g = dL/dout: gt = g w_grad [n_dst, H*C_in] (ppgat_gemm_nn); nstate[i][h] =
+ * {s_dst, m, inv_l, gt_i^h . agg_i^h} (prologue); one pass by source over the CSC
+ * (ppgat_xgat_bwd_edges): dx_j = sum_k sum_h beta gt_i^h + sum_h ds_src_j^h A_src[h],
+ * S[j][h] = ds_src, dz at each edge's CSR slot; S[i][H + h] = ds_dst by ppgat_bwd_dst_sum;
+ * dx_i += sum_h ds_dst_i^h A_dst[h] (epilogue); GV = S^T x [2H, C_in] (ppgat_gemm_tn),
+ * G = g^T agg [C, H*C_in] (ppgat_gemm_tn_big); dW, datt (ppgat_xgat_weight_grads):
+ *   dW[h*C + c][k] = G[c][h*C_in + k] / H + att_src[h][c] GV[h][k] + att_dst[h][c] GV[H+h][k],
+ *   datt_v[h][c] = sum_k W[h*C + c][k] GV[v*H + h][k].
+ * Supported: C_in = 256, H in {2, 4}, C % 128 == 0 (ppgat_xgat_supported).  Dropout as ppgat_fwd
+ * (seed_used required when dropout_p > 0: the forward writes it, the backward reads it). */
+int ppgat_xgat_supported(int in_channels, int heads, int channels);
+int ppgat_xgat_weights(const float* w, const float* att_src, const float* att_dst, int heads, int channels,
+                       int in_channels, float* att_proj, float* w_xform, float* w_grad, void* stream);
+int ppgat_xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_dst, int in_channels, int heads,
+                      const float* att_proj, float* s_src, float* s_dst, void* stream);
+int ppgat_xgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int in_channels, size_t* bytes);
+int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
+                   int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
+                   const float* s_dst, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
+                   float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream);
+int ppgat_xgat_bwd_prologue(const float* gt, const float* agg, const float* s_dst, const float* m, const float* inv_l,
+                            int64_t n_dst, int in_channels, int heads, float* nstate, void* stream);
+int ppgat_xgat_bwd_workspace_bytes(int64_t n_hub_items, int in_channels, size_t* bytes);
+int ppgat_xgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                         const int32_t* dz_slot, int64_t n_edges, int in_channels, int heads, const float* x,
+                         int64_t ldx, const float* s_src, const float* nstate, const float* gt, const float* att_proj,
+                         float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used, float* dx,
+                         int64_t lddx, float* S, int64_t lds, float* dz, void* workspace, size_t workspace_bytes,
+                         void* stream);
+int ppgat_xgat_bwd_epilogue(const float* S, int64_t lds, const float* att_proj, int64_t n_dst, int in_channels,
+                            int heads, float* dx, int64_t lddx, void* stream);
+int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src,
+                            const float* att_dst, int heads, int channels, int in_channels, float* dW, float* datt_src,
+                            float* datt_dst, void* stream);
+
 /* ---- in-process kernel timing (HIP events on the launch stream) --------- */
 #define PPGAT_K_CSR 0
 #define PPGAT_K_SCORES 1

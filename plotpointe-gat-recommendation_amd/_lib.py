@@ -89,6 +89,24 @@ SIGNATURES = {
     "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),
+    "ppgat_gemm_nn_supported": (c_int, [c_i64, c_int, c_int, c_int]),
+    "ppgat_gemm_nn": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_int, c_f, c_vp, c_vp, c_i64, c_vp]),
+    "ppgat_gemm_tn_big_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_gemm_tn_big": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_colsum_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_colsum": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_supported": (c_int, [c_int, c_int, c_int]),
+    "ppgat_xgat_weights": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_xgat_scores": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_xgat_fwd_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_xgat_fwd": (c_int, [SP, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_f, c_f, c_u64,
+                               c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_bwd_prologue": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp]),
+    "ppgat_xgat_bwd_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_xgat_bwd_edges": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                     c_f, c_f, c_u64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_bwd_epilogue": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp]),
+    "ppgat_xgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_profile_enable": (c_int, [c_int]),
     "ppgat_profile_reset": (c_int, []),
     "ppgat_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),

@@ -715,6 +715,207 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
   return PPGAT_OK;
 }
 
+// ---- fp32 matrix-core GEMMs and the aggregate-then-transform multi-head layer ----------
+int ppgat_gemm_nn_supported(int64_t m, int k, int n, int b_layout) {
+  return ppgat::gemm_nn_shape_ok(m, k, n, b_layout) ? 1 : 0;
+}
+
+int ppgat_gemm_nn(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
+                  float alpha, const float* bias, float* y, int64_t ldy, void* stream) {
+  if (!ppgat::gemm_nn_shape_ok(m, k, n, b_layout))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn: needs k % 32 == 0, n % 128 == 0, b_layout 0 or 1");
+  if (ldx < k || (ldx % 4) || ldy < n || (b_layout == 0 ? ldb < n : ldb < k) || (ldb % 4))
+    return fail(PPGAT_ERR_INVALID, "gemm_nn: bad leading dimension (>= width, multiple of 4)");
+  if (m > 0 && (!x || !b || !y)) return fail(PPGAT_ERR_INVALID, "gemm_nn: null pointer");
+  if (!al16(x) || !al16(b)) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn: 16-byte aligned rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ, st);
+  hipError_t e = ppgat::gemm_nn(x, ldx, m, k, b, ldb, b_layout, n, alpha, bias, y, ldy, st);
+  if (e != hipSuccess) return hip_fail(e, "gemm_nn");
+  return PPGAT_OK;
+}
+
+int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes) {
+  if (!bytes || m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big: needs ma, nb multiples of 128");
+  *bytes = ppgat::gemm_tn_big_workspace_bytes(m, ma, nb);
+  return PPGAT_OK;
+}
+
+int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb, float* out,
+                      void* workspace, size_t workspace_bytes, void* stream) {
+  if (m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big: needs ma, nb multiples of 128");
+  if (lda < ma || ldb < nb || (lda % 4) || (ldb % 4)) return fail(PPGAT_ERR_INVALID, "gemm_tn_big: bad leading dimension");
+  if (!out || (m > 0 && (!a || !b))) return fail(PPGAT_ERR_INVALID, "gemm_tn_big: null pointer");
+  if (!al16(a) || !al16(b)) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big: 16-byte aligned rows");
+  if (!workspace || workspace_bytes < ppgat::gemm_tn_big_workspace_bytes(m, ma, nb))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn_big: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = ppgat::gemm_tn_big(a, lda, b, ldb, m, ma, nb, out, workspace, st);
+  if (e != hipSuccess) return hip_fail(e, "gemm_tn_big");
+  return PPGAT_OK;
+}
+
+int ppgat_colsum_workspace_bytes(int64_t n, int c, size_t* bytes) {
+  if (!bytes || n < 0 || (c != 128 && c != 256)) return fail(PPGAT_ERR_UNSUPPORTED, "colsum: c must be 128 or 256");
+  *bytes = align_up((size_t)ppgat::colsum_blocks(n) * c * 4);
+  return PPGAT_OK;
+}
+
+int ppgat_colsum(const float* y, int64_t ldy, int64_t n, int c, float* out, void* workspace, size_t workspace_bytes,
+                 void* stream) {
+  if (n < 0 || (c != 128 && c != 256) || ldy < c || (ldy % 4)) return fail(PPGAT_ERR_INVALID, "colsum: bad sizes");
+  if (!out || (n > 0 && !y)) return fail(PPGAT_ERR_INVALID, "colsum: null pointer");
+  if (!workspace || workspace_bytes < (size_t)ppgat::colsum_blocks(n) * c * 4)
+    return fail(PPGAT_ERR_INVALID, "colsum: workspace too small");
+  hipError_t e = ppgat::colsum(y, ldy, n, c, out, static_cast<float*>(workspace), static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "colsum");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_supported(int in_channels, int heads, int channels) {
+  return ppgat::xgat_shape_ok(in_channels, heads, channels) ? 1 : 0;
+}
+
+int ppgat_xgat_weights(const float* w, const float* att_src, const float* att_dst, int heads, int channels,
+                       int in_channels, float* att_proj, float* w_xform, float* w_grad, void* stream) {
+  if (!ppgat::xgat_shape_ok(in_channels, heads, channels)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat: shape");
+  if (!w || (att_proj && (!att_src || !att_dst))) return fail(PPGAT_ERR_INVALID, "xgat_weights: null pointer");
+  hipError_t e = ppgat::xgat_weights(w, att_src, att_dst, heads, channels, in_channels, att_proj, w_xform, w_grad,
+                                     static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "xgat_weights");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_dst, int in_channels, int heads,
+                      const float* att_proj, float* s_src, float* s_dst, void* stream) {
+  if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_scores: shape");
+  if (n_rows < 0 || n_dst < 0 || n_dst > n_rows || ldx < in_channels || (ldx % 4))
+    return fail(PPGAT_ERR_INVALID, "xgat_scores: bad sizes");
+  if (n_rows > 0 && (!x || !att_proj || !s_src || (n_dst > 0 && !s_dst)))
+    return fail(PPGAT_ERR_INVALID, "xgat_scores: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_SCORES, st);
+  hipError_t e = ppgat::xgat_scores(x, ldx, n_rows, n_dst, in_channels, heads, att_proj, s_src, s_dst, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_scores");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int in_channels, size_t* bytes) {
+  if (!bytes || n_hub_items < 0 || heads < 1 || in_channels < 1) return fail(PPGAT_ERR_INVALID, "xgat_fwd_ws: bad args");
+  *bytes = partial_bytes(n_hub_items, heads, in_channels);
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
+                   int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
+                   const float* s_dst, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
+                   float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream) {
+  if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_fwd: shape");
+  if (n_dst < 0 || n_edges < 0 || ldx < in_channels || (ldx % 4)) return fail(PPGAT_ERR_INVALID, "xgat_fwd: bad sizes");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
+  if (int rc = check_sched(dst_sched, n_dst, "xgat_fwd")) return rc;
+  if (n_dst > 0 && (!x || !s_src || !s_dst || !agg || !m || !inv_l)) return fail(PPGAT_ERR_INVALID, "xgat_fwd: null pointer");
+  if (n_edges > 0 && !col) return fail(PPGAT_ERR_INVALID, "xgat_fwd: null col");
+  if (dropout_p > 0.f && (!seed_used || (n_edges > 0 && !csr_eid)))
+    return fail(PPGAT_ERR_INVALID, "xgat_fwd: dropout needs seed_used and csr_eid");
+  if (dst_sched->n_hub_items > 0 &&
+      (!workspace || workspace_bytes < partial_bytes(dst_sched->n_hub_items, heads, in_channels)))
+    return fail(PPGAT_ERR_INVALID, "xgat_fwd: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{dst_sched->item_row, dst_sched->item_beg, dst_sched->item_end, dst_sched->n_items,
+                           dst_sched->n_hub_items, dst_sched->n_long_items};
+  Timed t(PPGAT_K_FWD, st);
+  hipError_t e = hipSuccess;
+  if (dropout_p > 0.f) e = ppgat::seed_snapshot(seed, seed_used, st);
+  if (e == hipSuccess)
+    e = ppgat::xgat_fwd(it, col, csr_eid, x, ldx, in_channels, heads, s_src, s_dst, negative_slope, dropout_p, seed,
+                        seed_used, agg, m, inv_l, static_cast<float*>(workspace), dst_sched->hub_row,
+                        dst_sched->hub_ptr, dst_sched->n_hubs, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_fwd");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_prologue(const float* gt, const float* agg, const float* s_dst, const float* m, const float* inv_l,
+                            int64_t n_dst, int in_channels, int heads, float* nstate, void* stream) {
+  if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_prologue: shape");
+  if (n_dst < 0) return fail(PPGAT_ERR_INVALID, "xgat_bwd_prologue: bad sizes");
+  if (n_dst > 0 && (!gt || !agg || !s_dst || !m || !inv_l || !nstate))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_prologue: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_BWD_PRO, st);
+  hipError_t e = ppgat::xgat_bwd_pro(gt, agg, s_dst, m, inv_l, n_dst, in_channels, heads, nstate, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_prologue");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_workspace_bytes(int64_t n_hub_items, int in_channels, size_t* bytes) {
+  if (!bytes || n_hub_items < 0 || in_channels < 1) return fail(PPGAT_ERR_INVALID, "xgat_bwd_ws: bad args");
+  *bytes = partial_bytes(n_hub_items, 1, in_channels);
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                         const int32_t* dz_slot, int64_t n_edges, int in_channels, int heads, const float* x,
+                         int64_t ldx, const float* s_src, const float* nstate, const float* gt, const float* att_proj,
+                         float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used, float* dx,
+                         int64_t lddx, float* S, int64_t lds, float* dz, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_edges: shape");
+  if (n_edges < 0 || ldx < in_channels || (ldx % 4) || lddx < in_channels || (lddx % 4) || lds < 2 * heads)
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: bad sizes / leading dimensions");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
+  if (int rc = check_sched(src_sched, 0, "xgat_bwd_edges")) return rc;
+  if (src_sched->n_items > 0 && (!x || !s_src || !att_proj || !dx || !S))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: null pointer");
+  if (n_edges > 0 && (!row || !dz_slot || !nstate || !gt || !dz))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: null edge pointer");
+  if (dropout_p > 0.f && (!seed_used || (n_edges > 0 && !csc_eid)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: dropout needs seed_used and csc_eid");
+  if (src_sched->n_hub_items > 0 &&
+      (!workspace || workspace_bytes < partial_bytes(src_sched->n_hub_items, 1, in_channels)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{src_sched->item_row, src_sched->item_beg, src_sched->item_end, src_sched->n_items,
+                           src_sched->n_hub_items, src_sched->n_long_items};
+  Timed t(PPGAT_K_BWD_SRC, st);
+  hipError_t e = ppgat::xgat_bwd_edges(it, row, csc_eid, dz_slot, x, ldx, in_channels, heads, s_src, nstate, gt,
+                                       att_proj, negative_slope, dropout_p, seed, seed_used, dx, lddx, S, lds, dz,
+                                       static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
+                                       src_sched->n_hubs, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_edges");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_epilogue(const float* S, int64_t lds, const float* att_proj, int64_t n_dst, int in_channels,
+                            int heads, float* dx, int64_t lddx, void* stream) {
+  if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_epilogue: shape");
+  if (n_dst < 0 || lds < 2 * heads || lddx < in_channels || (lddx % 4))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_epilogue: bad sizes");
+  if (n_dst > 0 && (!S || !att_proj || !dx)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_epilogue: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_BWD_EPI, st);
+  hipError_t e = ppgat::xgat_bwd_epi(S, lds, att_proj + (size_t)heads * in_channels, n_dst, in_channels, heads, dx,
+                                     lddx, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_epilogue");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src,
+                            const float* att_dst, int heads, int channels, int in_channels, float* dW, float* datt_src,
+                            float* datt_dst, void* stream) {
+  if (heads < 1 || channels < 1 || in_channels < 1) return fail(PPGAT_ERR_INVALID, "xgat_weight_grads: bad sizes");
+  if (!G || !GV || !w || !att_src || !att_dst || !dW || !datt_src || !datt_dst)
+    return fail(PPGAT_ERR_INVALID, "xgat_weight_grads: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = ppgat::xgat_wgrad(G, GV, w, att_src, att_dst, heads, channels, in_channels, dW, datt_src, datt_dst, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_weight_grads");
+  return PPGAT_OK;
+}
+
 int ppgat_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
   g_prof.on = on != 0;

@@ -49,6 +49,8 @@ hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, co
                           int64_t blocks, hipStream_t st);
 hipError_t launch_col_reduce(const float* partial, int64_t rows, int cols, int split, float* out_a, float* out_b,
                              hipStream_t st);
+hipError_t launch_fwd_merge(int C, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, int heads,
+                            const float* partial, float eps, float* m, float* invl, float* agg, hipStream_t st);
 
 // graph preprocessing (ppgat_graph.hip)
 size_t csr_workspace_bytes(int64_t n_nodes, int64_t n_edges);
@@ -127,5 +129,38 @@ bool fusion_shape_ok(int Dt, int Di, int h1, int d_out);
 hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
                       int normalize, float* out, float* z1_out, hipStream_t st);
+
+// aggregate-then-transform multi-head layer and fp32 MFMA GEMMs (ppgat_xform.hip)
+hipError_t seed_snapshot(uint64_t seed, uint64_t* out, hipStream_t st);
+bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode);
+hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
+                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st);
+bool gemm_tn_big_shape_ok(int Ma, int Nb);
+size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
+hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
+                       void* ws, hipStream_t st);
+bool xgat_shape_ok(int K, int H, int C);
+hipError_t xgat_weights(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
+                        float* Wt, float* Wg, hipStream_t st);
+hipError_t xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_dst, int K, int H, const float* A,
+                       float* s_src, float* s_dst, hipStream_t st);
+hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, const float* x, int64_t ldx, int K,
+                    int H, const float* s_src, const float* s_dst, float slope, float p, uint64_t seed,
+                    const uint64_t* seed_in, float* agg, float* m, float* invl, float* partial,
+                    const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
+hipError_t xgat_bwd_pro(const float* gt, const float* agg, const float* s_dst, const float* m, const float* invl,
+                        int64_t n, int K, int H, float* nstate, hipStream_t st);
+hipError_t xgat_bwd_edges(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                          const float* x, int64_t ldx, int K, int H, const float* s_src, const float* nstate,
+                          const float* gt, const float* A_src, float slope, float p, uint64_t seed,
+                          const uint64_t* seed_in, float* dx, int64_t lddx, float* S, int64_t lds, float* dz,
+                          float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                          hipStream_t st);
+hipError_t xgat_bwd_epi(const float* S, int64_t lds, const float* A_dst, int64_t n, int K, int H, float* dx,
+                        int64_t lddx, hipStream_t st);
+hipError_t xgat_wgrad(const float* G, const float* GV, const float* W, const float* att_src, const float* att_dst,
+                      int H, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st);
+int64_t colsum_blocks(int64_t n);
+hipError_t colsum(const float* Y, int64_t ldy, int64_t n, int C, float* out, float* part, hipStream_t st);
 
 }  // namespace ppgat

@@ -379,6 +379,7 @@ __global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ h
       invl_out[i * heads + hd] = invl;
     }
   }
+  if (out == nullptr) return;  // aggregate-then-transform: the per-head aggregates only
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
   if (sg == 0) st4(out + i * C + sl * 4, osum);
@@ -1044,6 +1045,16 @@ hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid
   return hipGetLastError();
 }
 
+// hub merge of per-head aggregates only (aggregate-then-transform forward, ppgat_xform.hip)
+hipError_t launch_fwd_merge(int C, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, int heads,
+                            const float* partial, float eps, float* m, float* invl, float* agg, hipStream_t st) {
+  if (n_hubs <= 0) return hipSuccess;
+  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st, hub_row,
+                                         hub_ptr, n_hubs, heads, partial, nullptr, kModePyg, eps, nullptr, m, invl,
+                                         agg));
+  return hipGetLastError();
+}
+
 hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
                           const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
                           float* nstate, float* bias_part, int64_t blocks, hipStream_t st) {
@@ -1137,6 +1148,11 @@ __global__ void k_drop_epoch(int set, uint64_t value) {
   if (threadIdx.x == 0) g_drop_epoch = set ? value : g_drop_epoch + 1;
 }
 }  // namespace
+
+hipError_t seed_snapshot(uint64_t seed, uint64_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_seed_snap, dim3(1), dim3(64), 0, st, seed, out);
+  return hipGetLastError();
+}
 
 hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st) {
   hipLaunchKernelGGL(k_drop_epoch, dim3(1), dim3(64), 0, st, set, value);

@@ -1,0 +1,918 @@
+// ppgat_xform.hip -- the multi-head GAT layer in the aggregate-then-transform formulation,
+// and the fp32 matrix-core GEMMs it (and the row-sharded config-5 path) runs on (gfx950).
+//
+// GATConv(C_in, C, heads=H, concat=False) (scripts/train_gat_pyg.py:77)
+// computes out_i = 1/H sum_h sum_{j->i} alpha_ij^h W_h x_j + bias with W_h = lin.weight rows
+// [h C, (h+1) C).  The message is linear in x_j, so
+//     out_i = 1/H sum_h W_h ax_i^h + bias,   ax_i^h = sum_{j->i} alpha_ij^h x_j   [H, C_in]
+// and the attention logits only need s_src_j^h = x_j . A_src^h with A_src^h = W_h^T att_src^h
+// (likewise s_dst).  With H*C > C_in (config 5: 4*256 = 1024 against 256) the edge pass
+// gathers x_j (C_in floats) instead of h_j (H*C floats), h is never materialised, and a
+// row-sharded rank exchanges x for its halo rows (dist.py).  Backward, with g = dOut:
+//     gt_i^h = W_h^T g_i / H                  (GEMM [n, C] x [C, H C_in])
+//     D_i^h  = gt_i^h . ax_i^h                (= sum_k beta dalpha, Appendix B)
+//     per edge k = (j -> i): dz = alpha (d gt_i^h . x_j - D_i^h) lrelu'
+//     dx_j   = sum_k sum_h beta_k^h gt_i^h + sum_h ds_src_j^h A_src^h + sum_h ds_dst_j^h A_dst^h
+//     dW_h   = g^T ax^h / H + att_src^h (x) (ds_src^h)^T x + att_dst^h (x) (ds_dst^h)^T x
+//     datt_src^h = W_h (ds_src^h)^T x, datt_dst^h likewise,  dbias = sum_i g_i.
+// One edge pass by source (CSC) produces dx_msg, ds_src and the per-edge dz (at its CSR
+// slot, summed per destination by k_dst_sum); no atomics anywhere, fixed summation orders.
+//
+// GEMMs (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains; 157 TF peak):
+//  * k_gemm_nn: Y = alpha X B (+ bias), X [M, K] row-major streamed from HBM straight into
+//    the A-operand layout (float4 per lane = 4 MFMA steps, reduction index permuted),
+//    B [K, N] (row-major) or [N, K] (X W^T) staged per 32-deep k chunk in LDS; each wave owns
+//    32 rows x BN columns (NT 32x32 accumulator tiles), workgroups mapped XCD-aware so the
+//    column blocks of one row block share an L2.
+//  * k_gemm_tn: G = A^T B over M rows (weight gradients): 128 x 256 output tile per
+//    workgroup, 32-row chunks staged in LDS, row splits summed in split order (deterministic);
+//    the tiles of one row split run on one XCD, so the rows leave HBM once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "ppgat_internal.h"
+#include "ppgat_lanes.h"
+
+namespace ppgat {
+namespace {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 fma4(float s, float4 v, float4 a) {
+  return make_float4(fmaf(s, v.x, a.x), fmaf(s, v.y, a.y), fmaf(s, v.z, a.z), fmaf(s, v.w, a.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 mul4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+__device__ __forceinline__ float comp(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// logit / dropout rules shared with ppgat_kernels.hip (PyG mode only here)
+__device__ __forceinline__ float lrelu(float z, float slope) { return z > 0.f ? z : z * slope; }
+__device__ __forceinline__ float dlrelu(float z, float slope) { return z > 0.f ? 1.f : slope; }
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t eid, uint32_t head, float p, float inv_keep) {
+  uint64_t x = seed ^ ((uint64_t)eid * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)head * 0xC2B2AE3D27D4EB4Full);
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+  return u >= p ? inv_keep : 0.f;
+}
+
+// ===========================================================================
+// NN GEMM: Y[M, N] = alpha X[M, K] B + bias
+// ===========================================================================
+constexpr int kGBM = 128;  // rows per workgroup (4 waves x 32)
+constexpr int kGBK = 32;   // reduction chunk
+constexpr int kNkLd = kGBK + 4;  // LDS row stride of the [n][k] image (NK mode): conflict-free b128 reads
+
+struct NnArg {
+  const float* X;
+  int64_t ldx;
+  int64_t M;
+  int K;
+  const float* B;
+  int64_t ldb;
+  int N;
+  float alpha;
+  const float* bias;
+  float* Y;
+  int64_t ldy;
+  int n_blocks;
+  int64_t row_blocks;
+};
+
+// BMODE 0: B[k][n] = B[k * ldb + n] (image [k][n], b32 reads); 1: B[k][n] = B[n * ldb + k] (X W^T,
+// image [n][k], b128 reads).  MFMA 32x32x2 lane maps (r = lane & 31, hf = lane >> 5): A operand
+// X[row r][k], B operand B[k][col r], accumulator q at row (q & 3) + 8 (q >> 2) + 4 hf, col r;
+// within a group of 8 k, lane half hf supplies k = 8g + 4 hf + s at MFMA step s.
+template <int NT, int BMODE>
+__global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
+  constexpr int BN = 32 * NT;
+  constexpr int IMG = BMODE == 0 ? kGBK * BN : BN * kNkLd;
+  __shared__ float sB[IMG];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, hf = lane >> 5;
+  // XCD-aware order: blocks b, b + 8, b + 16, ... land on one XCD; the n blocks of a row block
+  // are consecutive there, so its X rows are fetched from HBM once
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int64_t rb = (idx / a.n_blocks) * 8 + (b & 7);
+  if (rb >= a.row_blocks) return;
+  const int n0 = (int)(idx % a.n_blocks) * BN;
+  const int64_t M = a.M;
+  const int K = a.K;
+  const int64_t m = rb * kGBM + wv * 32 + r;
+  const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
+
+  float4 bst[NT];
+  auto load_b = [&](int kc) {
+#pragma unroll
+    for (int s = 0; s < NT; ++s) {
+      const int e = tid + 256 * s;
+      if (BMODE == 0) {
+        const int k = e / (BN / 4), n4 = (e % (BN / 4)) * 4;
+        bst[s] = ld4(a.B + (int64_t)(kc + k) * a.ldb + n0 + n4);
+      } else {
+        const int n = e >> 3, k4 = (e & 7) * 4;
+        bst[s] = ld4(a.B + (int64_t)(n0 + n) * a.ldb + kc + k4);
+      }
+    }
+  };
+  auto store_b = [&]() {
+#pragma unroll
+    for (int s = 0; s < NT; ++s) {
+      const int e = tid + 256 * s;
+      if (BMODE == 0) {
+        const int k = e / (BN / 4), n4 = (e % (BN / 4)) * 4;
+        st4(&sB[k * BN + n4], bst[s]);
+      } else {
+        const int n = e >> 3, k4 = (e & 7) * 4;
+        st4(&sB[n * kNkLd + k4], bst[s]);
+      }
+    }
+  };
+  float4 xa[4], xn[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) xa[g] = ld4(xrow + 8 * g);
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+  load_b(0);
+  store_b();
+  __syncthreads();
+  for (int kc = 0; kc < K; kc += kGBK) {
+    const bool more = kc + kGBK < K;
+    if (more) {
+      load_b(kc + kGBK);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xn[g] = ld4(xrow + kc + kGBK + 8 * g);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (BMODE == 1) {
+        float4 bv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bv[t] = ld4(&sB[(32 * t + r) * kNkLd + 8 * g + 4 * hf]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma32(comp(xa[g], s), comp(bv[t], s), acc[t]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float* brow = &sB[(8 * g + 4 * hf + s) * BN + r];
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma32(comp(xa[g], s), brow[32 * t], acc[t]);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_b();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xa[g] = xn[g];
+    }
+    __syncthreads();
+  }
+  const int64_t row0 = rb * kGBM + wv * 32;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 32 * t + r;
+    const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      if (row < M) a.Y[row * a.ldy + col] = fmaf(a.alpha, acc[t][q], bv);
+    }
+  }
+}
+
+// ===========================================================================
+// TN GEMM: part[split] = A[rows of split]^T B[rows of split], A [M, Ma], B [M, Nb]
+// ===========================================================================
+constexpr int kTA = 128;  // a-tile (output rows)
+constexpr int kTR = 32;   // rows per LDS chunk
+
+struct TnArg {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  int64_t M;
+  int Ma, Nb;
+  int tiles_a, tiles_b, splits;
+  int64_t rows_per_split;  // multiple of kTR
+  float* part;             // [splits, Ma, Nb]
+};
+
+// BT: b-tile width (256 or 128).  Waves 2 x 2: wave (wa, wb) owns a-columns [64 wa, +64) (2 MFMA
+// tiles) x b-columns [BT/2 wb, +BT/2) (BT/64 tiles).  MFMA: i = a column, j = b column, kk = row.
+template <int BT>
+__global__ void __launch_bounds__(256, 2) k_gemm_tn(TnArg a) {
+  constexpr int NB = BT / 64;  // b tiles per wave
+  constexpr int LA = kTA + 4, LB = BT + 4;
+  __shared__ float sA[kTR * LA];
+  __shared__ float sB[kTR * LB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, hf = lane >> 5;
+  const int wa = wv & 1, wb = wv >> 1;
+  const int T = a.tiles_a * a.tiles_b;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int tile = (int)(idx % T);
+  const int64_t split = (b & 7) + 8 * (idx / T);  // one split's tiles share an XCD (and its L2)
+  if (split >= a.splits) return;
+  const int ta = tile % a.tiles_a, tb = tile / a.tiles_a;
+  const int64_t r0 = split * a.rows_per_split;
+  const int64_t r1 = min(a.M, r0 + a.rows_per_split);
+  constexpr int A4 = kTR * kTA / 4 / 256;  // float4 per thread per chunk (4)
+  constexpr int B4 = kTR * BT / 4 / 256;   // (8 or 4)
+  float4 ar[A4], br[B4];
+  auto load = [&](int64_t c0) {
+#pragma unroll
+    for (int s = 0; s < A4; ++s) {
+      const int e = tid + 256 * s;
+      const int rr = e / (kTA / 4), c4 = (e % (kTA / 4)) * 4;
+      const int64_t row = c0 + rr;
+      ar[s] = row < r1 ? ld4(a.A + row * a.lda + ta * kTA + c4) : f4(0.f);
+    }
+#pragma unroll
+    for (int s = 0; s < B4; ++s) {
+      const int e = tid + 256 * s;
+      const int rr = e / (BT / 4), c4 = (e % (BT / 4)) * 4;
+      const int64_t row = c0 + rr;
+      br[s] = row < r1 ? ld4(a.B + row * a.ldb + tb * BT + c4) : f4(0.f);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int s = 0; s < A4; ++s) {
+      const int e = tid + 256 * s;
+      st4(&sA[(e / (kTA / 4)) * LA + (e % (kTA / 4)) * 4], ar[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < B4; ++s) {
+      const int e = tid + 256 * s;
+      st4(&sB[(e / (BT / 4)) * LB + (e % (BT / 4)) * 4], br[s]);
+    }
+  };
+  f32x16 acc[2][NB];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < NB; ++t) acc[u][t] = f32x16{};
+  if (r0 < r1) {
+    load(r0);
+    store();
+  }
+  __syncthreads();
+  for (int64_t c0 = r0; c0 < r1; c0 += kTR) {
+    const bool more = c0 + kTR < r1;
+    if (more) load(c0 + kTR);
+#pragma unroll 4
+    for (int s = 0; s < kTR / 2; ++s) {
+      const int row = 2 * s + hf;
+      float av[2], bv[NB];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) av[u] = sA[row * LA + 64 * wa + 32 * u + r];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) bv[t] = sB[row * LB + (BT / 2) * wb + 32 * t + r];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) acc[u][t] = mfma32(av[u], bv[t], acc[u][t]);
+    }
+    __syncthreads();
+    if (more) store();
+    __syncthreads();
+  }
+  float* P = a.part + (size_t)split * a.Ma * a.Nb;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const int col = tb * BT + (BT / 2) * wb + 32 * t + r;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int arow = ta * kTA + 64 * wa + 32 * u + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        P[(size_t)arow * a.Nb + col] = acc[u][t][q];
+      }
+    }
+}
+
+// out[e] = scale * sum_s part[s][e] (split order) -- float4 per thread
+__global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ part, int64_t n4, int splits,
+                                                   float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n4) return;
+  float4 s = ld4(part + e * 4);
+  for (int k = 1; k < splits; ++k) s = add4(s, ld4(part + ((size_t)k * n4 + e) * 4));
+  st4(out + e * 4, s);
+}
+
+// ===========================================================================
+// aggregate-then-transform layer pieces
+// ===========================================================================
+// A[v][h][k] = sum_c att_v[h][c] W[h C + c][k]  (v = 0: src, 1: dst) -> [2, H, K]
+__global__ void __launch_bounds__(256) k_att_proj(const float* __restrict__ W, const float* __restrict__ att_src,
+                                                  const float* __restrict__ att_dst, int H, int C, int K,
+                                                  float* __restrict__ A) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)2 * H * K) return;
+  const int v = (int)(t / ((int64_t)H * K));
+  const int h = (int)((t / K) % H), k = (int)(t % K);
+  const float* att = (v == 0 ? att_src : att_dst) + h * C;
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s = fmaf(att[c], W[(int64_t)(h * C + c) * K + k], s);
+  A[t] = s;
+}
+
+// Wt[h K + k][c] = W[h C + c][k]  (the transform, [H K, C]) and Wg[c][h K + k] = W[h C + c][k] / H
+__global__ void __launch_bounds__(256) k_wperm(const float* __restrict__ W, int H, int C, int K,
+                                               float* __restrict__ Wt, float* __restrict__ Wg) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)H * C * K) return;
+  const int hc = (int)(t / K), k = (int)(t % K);
+  const int h = hc / C, c = hc % C;
+  const float w = W[t];
+  if (Wt) Wt[((int64_t)h * K + k) * C + c] = w;
+  if (Wg) Wg[(int64_t)c * H * K + (int64_t)h * K + k] = w * (1.f / (float)H);
+}
+
+// s_src[n][h] = x_n . A_src[h] (n < n_rows), s_dst[n][h] = x_n . A_dst[h] (n < n_dst).
+// LPR = K/4 lanes per row, 64/LPR rows per wave, grid-stride.
+template <int K, int H>
+__global__ void __launch_bounds__(256) k_xscores(const float* __restrict__ x, int64_t ldx, int64_t n_rows,
+                                                 int64_t n_dst, const float* __restrict__ A, float* __restrict__ s_src,
+                                                 float* __restrict__ s_dst) {
+  constexpr int LPR = K / 4, RPW = 64 / LPR, V = 2 * H;
+  const int lane = threadIdx.x & 63;
+  const int sl = lane % LPR, sr = lane / LPR;
+  float4 av[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) av[v] = ld4(A + v * K + sl * 4);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW; base < n_rows; base += nw * RPW) {
+    const int64_t n = base + sr;
+    const float4 xv = ld4(x + (n < n_rows ? n : n_rows - 1) * ldx + sl * 4);
+    float res[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) res[v] = group_reduce<Op::Sum, 1, LPR / 2>(dot4(xv, av[v]));
+    if (n < n_rows && sl == 0) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) s_src[n * H + h] = res[h];
+      if (n < n_dst) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) s_dst[n * H + h] = res[H + h];
+      }
+    }
+  }
+}
+
+struct XItems {
+  const int32_t* row;
+  const int32_t* beg;
+  const int32_t* end;
+  int64_t n_items;
+  int64_t n_hub_items;
+};
+
+// ---------------------------------------------------------------------------
+// forward edge pass: one wave per destination item (CSR), the neighbour row x_j (K floats)
+// gathered ONCE per edge for all H heads: ax^h += p^h x_j with the online softmax per head.
+// K = 256: one float4 per lane, one edge at a time across the wave, 8 rows in flight.
+// Hub pieces leave [ax^h (K) | m | l | - -] per (item, head) for k_fwd_merge.
+// ---------------------------------------------------------------------------
+template <int K, int H>
+__global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restrict__ col,
+                                               const int32_t* __restrict__ eid, const float* __restrict__ x,
+                                               int64_t ldx, const float* __restrict__ s_src,
+                                               const float* __restrict__ s_dst, float slope, float p, float inv_keep,
+                                               uint64_t seed, const uint64_t* __restrict__ seed_in,
+                                               float* __restrict__ agg, float* __restrict__ m_out,
+                                               float* __restrict__ invl_out, float* __restrict__ partial) {
+  static_assert(K == 256, "k_fwd_x: K == 256 (one float4 per lane)");
+  constexpr int U = 8;
+  if (p > 0.f) seed = *seed_in;
+  __shared__ int recj[4][64];
+  __shared__ float recw[4][H][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+  if (w >= it.n_items) return;
+  const int64_t i = it.row[w];
+  const int rs = it.beg[w], re = it.end[w];
+  const bool hub = w < it.n_hub_items;
+  float sd[H], mh[H], lh[H];
+  float4 acc[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    sd[h] = s_dst[i * H + h];
+    mh[h] = -INFINITY;
+    lh[h] = 0.f;
+    acc[h] = f4(0.f);
+  }
+  for (int base = rs; base < re; base += 64) {
+    const int k = base + lane;
+    const bool valid = k < re;
+    const int j = valid ? col[k] : 0;
+    const uint32_t e_id = (valid && p > 0.f) ? (uint32_t)eid[k] : 0u;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float e = valid ? lrelu(s_src[(int64_t)j * H + h] + sd[h], slope) : -INFINITY;
+      const float mn = fmaxf(mh[h], wave_max(e));
+      const float sc = expf(mh[h] - mn);
+      const float pe = valid ? expf(e - mn) : 0.f;
+      lh[h] = fmaf(lh[h], sc, wave_sum(pe));
+      acc[h] = mul4(acc[h], sc);
+      mh[h] = mn;
+      float pw = pe;
+      if (p > 0.f && valid) pw *= drop_scale(seed, e_id, (uint32_t)h, p, inv_keep);
+      recw[wv][h][lane] = pw;
+    }
+    recj[wv][lane] = j;
+    wave_sync();
+    const int n = min(64, re - base);
+    for (int q0 = 0; q0 < n; q0 += U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u;
+        v[u] = q < n ? ld4(x + (int64_t)recj[wv][q] * ldx + lane * 4) : f4(0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = min(q0 + u, 63);
+#pragma unroll
+        for (int h = 0; h < H; ++h) acc[h] = fma4(q0 + u < n ? recw[wv][h][q] : 0.f, v[u], acc[h]);
+      }
+    }
+    wave_sync();
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    if (hub) {
+      float* slot = partial + (w * H + h) * (K + 4);
+      st4(slot + lane * 4, acc[h]);
+      if (lane == 0) st4(slot + K, make_float4(mh[h], lh[h], 0.f, 0.f));
+      continue;
+    }
+    const float invl = 1.f / (lh[h] + 1e-16f);
+    st4(agg + (i * H + h) * K + lane * 4, mul4(acc[h], invl));
+    if (lane == 0) {
+      m_out[i * H + h] = re > rs ? mh[h] : 0.f;
+      invl_out[i * H + h] = invl;
+    }
+  }
+}
+
+// backward prologue: nstate[i][h] = {s_dst, m, inv_l, D = gt_i^h . ax_i^h}; one wave per row
+template <int K, int H>
+__global__ void __launch_bounds__(256) k_bwd_x_pro(const float* __restrict__ gt, const float* __restrict__ agg,
+                                                   const float* __restrict__ s_dst, const float* __restrict__ m,
+                                                   const float* __restrict__ invl, int64_t n,
+                                                   float4* __restrict__ nstate) {
+  static_assert(K == 256, "k_bwd_x_pro: K == 256");
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    float d[16];
+#pragma unroll
+    for (int h = 0; h < 16; ++h) d[h] = 0.f;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      d[h] = dot4(ld4(gt + (i * H + h) * K + lane * 4), ld4(agg + (i * H + h) * K + lane * 4));
+#pragma unroll
+    for (int h = 0; h < H; ++h) d[h] = wave_sum(d[h]);
+    if (lane < H) {
+      float dv = d[0];
+#pragma unroll
+      for (int h = 1; h < H; ++h) dv = lane == h ? d[h] : dv;
+      const int64_t pr = i * H + lane;
+      nstate[pr] = make_float4(s_dst[pr], m[pr], invl[pr], dv);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward edge pass by SOURCE (CSC): one wave per source item; x_j in registers (float4
+// per lane), per out-edge the destination's gt_i (H x K floats) and packed state gathered
+// once.  Per group of 4 edges the 16 partial dots <gt_i^h, x_j> are summed over the wave
+// with a transposing butterfly.  Writes dx_j = sum beta gt + sum_h ds_src^h A_src^h (hub
+// pieces: [msg (K) | ds_h (H <= 4)] partials), ds_src[j][h], and dz at each edge's CSR slot.
+// ---------------------------------------------------------------------------
+template <int OFF, int N>
+__device__ __forceinline__ int tr_reduce(float (&v)[16], int sl, int& base) {
+  if constexpr (OFF >= 8 && N > 1) {
+    constexpr int Hh = N / 2;
+    const bool bit = (sl & OFF) != 0;
+#pragma unroll
+    for (int t = 0; t < Hh; ++t) {
+      if constexpr (OFF >= 16) {
+        float r0, r1;
+        row_swap<OFF>(v[t], v[Hh + t], r0, r1);
+        v[t] = r0 + r1;
+      } else {
+        const float send = bit ? v[t] : v[Hh + t];
+        const float keep = bit ? v[Hh + t] : v[t];
+        v[t] = keep + dpp<0x128>(send);
+      }
+    }
+    if (bit) base += Hh;
+    return tr_reduce<OFF / 2, Hh>(v, sl, base);
+  } else {
+#pragma unroll
+    for (int t = 0; t < N; ++t) v[t] = group_reduce<Op::Sum, 1, 4>(v[t]);
+    return N;
+  }
+}
+
+template <int K, int H>
+__global__ void __launch_bounds__(256) k_bwd_x(XItems it, const int32_t* __restrict__ row,
+                                               const int32_t* __restrict__ csc_eid,
+                                               const int32_t* __restrict__ csc2csr, const float* __restrict__ x,
+                                               int64_t ldx, const float* __restrict__ s_src,
+                                               const float4* __restrict__ nstate, const float* __restrict__ gt,
+                                               const float* __restrict__ A_src, float slope, float p, float inv_keep,
+                                               uint64_t seed, const uint64_t* __restrict__ seed_in,
+                                               float* __restrict__ dx, int64_t lddx, float* __restrict__ S,
+                                               int64_t lds, float* __restrict__ dz, float* __restrict__ partial) {
+  static_assert(K == 256 && H <= 4, "k_bwd_x: K == 256, H <= 4");
+  constexpr int U = 16 / H;  // edges per reduction group (16 partial dots per lane)
+  if (p > 0.f) seed = *seed_in;
+  __shared__ int2 recA[4][64];          // {dst row, CSR slot}
+  __shared__ float4 recH[4][H][64];     // per head {beta, c1, c0, -}
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+  if (w >= it.n_items) return;
+  const int64_t j = it.row[w];
+  const int cs = it.beg[w], ce = it.end[w];
+  const bool hub = w < it.n_hub_items;
+  const float4 xv = ld4(x + j * ldx + lane * 4);
+  float ss[H], dsa[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    ss[h] = s_src[j * H + h];
+    dsa[h] = 0.f;
+  }
+  float4 acc = f4(0.f);
+  for (int base = cs; base < ce; base += 64) {
+    const int k = base + lane;
+    const bool valid = k < ce;
+    const int i = valid ? row[k] : 0;
+    const int slot = valid ? csc2csr[k] : 0;
+    const uint32_t e_id = (valid && p > 0.f) ? (uint32_t)csc_eid[k] : 0u;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float bg = 0.f, c1 = 0.f, c0 = 0.f;
+      if (valid) {
+        const float4 st = nstate[(int64_t)i * H + h];  // {s_dst, m, inv_l, D}
+        const float z = ss[h] + st.x;
+        const float af = expf(lrelu(z, slope) - st.y) * st.z;
+        const float dm = p > 0.f ? drop_scale(seed, e_id, (uint32_t)h, p, inv_keep) : 1.f;
+        bg = af * dm;
+        const float a1 = af * dlrelu(z, slope);
+        c1 = a1 * dm;
+        c0 = a1 * st.w;
+      }
+      recH[wv][h][lane] = make_float4(bg, c1, c0, 0.f);
+    }
+    recA[wv][lane] = make_int2(i, slot);
+    wave_sync();
+    const int n = min(64, ce - base);
+    for (int q0 = 0; q0 < n; q0 += U) {
+      float4 g[U][H];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u;
+        const int64_t ii = recA[wv][min(q, 63)].x;
+#pragma unroll
+        for (int h = 0; h < H; ++h) g[u][h] = q < n ? ld4(gt + (ii * H + h) * K + lane * 4) : f4(0.f);
+      }
+      float part[16];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = min(q0 + u, 63);
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const float bq = q0 + u < n ? recH[wv][h][q].x : 0.f;
+          acc = fma4(bq, g[u][h], acc);
+          part[u * H + h] = dot4(g[u][h], xv);
+        }
+      }
+      int vbase = 0;
+      const int R = tr_reduce<32, 16>(part, lane, vbase);
+      const int t = lane & 7;
+      if (t < R) {
+        float dot = part[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c)
+          if (c == t) dot = part[c];
+        const int vi = vbase + t;
+        const int u = vi / H, h = vi % H;
+        const int q = q0 + u;
+        if (q < n) {
+          const float4 rb = recH[wv][h][q];
+          const float dzv = fmaf(rb.y, dot, -rb.z);
+#pragma unroll
+          for (int c = 0; c < H; ++c)
+            if (c == h) dsa[c] += dzv;
+          dz[(int64_t)recA[wv][q].y * H + h] = dzv;
+        }
+      }
+    }
+    wave_sync();
+  }
+  float ds[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ds[h] = wave_sum(dsa[h]);
+  if (hub) {
+    float* sp = partial + w * (K + 4);
+    st4(sp + lane * 4, acc);
+    if (lane == 0) {
+      float4 d = f4(0.f);
+      d.x = ds[0];
+      if (H > 1) d.y = ds[1];
+      if (H > 2) d.z = ds[2];
+      if (H > 3) d.w = ds[3];
+      st4(sp + K, d);
+    }
+    return;
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) acc = fma4(ds[h], ld4(A_src + h * K + lane * 4), acc);
+  st4(dx + j * lddx + lane * 4, acc);
+  if (lane < H) {
+    float v = ds[0];
+#pragma unroll
+    for (int h = 1; h < H; ++h) v = lane == h ? ds[h] : v;
+    S[j * lds + lane] = v;
+  }
+}
+
+// hub sources: sum the pieces in order, add the attention term
+template <int K, int H>
+__global__ void __launch_bounds__(256) k_bwd_x_merge(const int32_t* __restrict__ hub_row,
+                                                     const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
+                                                     const float* __restrict__ partial, const float* __restrict__ A_src,
+                                                     float* __restrict__ dx, int64_t lddx, float* __restrict__ S,
+                                                     int64_t lds) {
+  const int lane = threadIdx.x & 63;
+  const int64_t hb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;
+  const int64_t j = hub_row[hb];
+  float4 acc = f4(0.f), d = f4(0.f);
+  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) {
+    acc = add4(acc, ld4(partial + (int64_t)q * (K + 4) + lane * 4));
+    d = add4(d, ld4(partial + (int64_t)q * (K + 4) + K));
+  }
+  const float ds[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+  for (int h = 0; h < H; ++h) acc = fma4(ds[h], ld4(A_src + h * K + lane * 4), acc);
+  st4(dx + j * lddx + lane * 4, acc);
+  if (lane < H) S[j * lds + lane] = ds[lane];
+}
+
+// dx_i += sum_h ds_dst_i^h A_dst[h] over the destination rows (S[i][H + h] = ds_dst)
+template <int K, int H>
+__global__ void __launch_bounds__(256) k_bwd_x_epi(const float* __restrict__ S, int64_t lds,
+                                                   const float* __restrict__ A_dst, int64_t n, float* __restrict__ dx,
+                                                   int64_t lddx) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = t / (K / 4);
+  if (i >= n) return;
+  const int c4 = (int)(t % (K / 4)) * 4;
+  float4 v = ld4(dx + i * lddx + c4);
+#pragma unroll
+  for (int h = 0; h < H; ++h) v = fma4(S[i * lds + H + h], ld4(A_dst + h * K + c4), v);
+  st4(dx + i * lddx + c4, v);
+}
+
+// dW[h C + c][k] = G[c][h K + k] * gs + att_src[h][c] GV[h][k] + att_dst[h][c] GV[H + h][k];
+// datt_v[h][c] = sum_k W[h C + c][k] GV[v H + h][k].  One wave per (h, c) row of W.
+__global__ void __launch_bounds__(256) k_wgrad_x(const float* __restrict__ G, const float* __restrict__ GV,
+                                                 const float* __restrict__ W, const float* __restrict__ att_src,
+                                                 const float* __restrict__ att_dst, int H, int C, int K, float gs,
+                                                 float* __restrict__ dW, float* __restrict__ datt_src,
+                                                 float* __restrict__ datt_dst) {
+  const int lane = threadIdx.x & 63;
+  const int64_t hc = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hc >= (int64_t)H * C) return;
+  const int h = (int)(hc / C), c = (int)(hc % C);
+  const float as = att_src[hc], ad = att_dst[hc];
+  float ps = 0.f, pd = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float gs_ = GV[(int64_t)h * K + k], gd = GV[(int64_t)(H + h) * K + k];
+    const float w = W[hc * K + k];
+    dW[hc * K + k] = fmaf(G[(int64_t)c * H * K + (int64_t)h * K + k], gs, fmaf(as, gs_, ad * gd));
+    ps = fmaf(w, gs_, ps);
+    pd = fmaf(w, gd, pd);
+  }
+  ps = wave_sum(ps);
+  pd = wave_sum(pd);
+  if (lane == 0) {
+    datt_src[hc] = ps;
+    datt_dst[hc] = pd;
+  }
+}
+
+// block partial column sums of Y [n, C] (dbias); reduced by k_col_reduce in block order
+template <int C>
+__global__ void __launch_bounds__(256) k_colsum_part(const float* __restrict__ Y, int64_t ldy, int64_t n,
+                                                     float* __restrict__ part) {
+  constexpr int LPR = C / 4, SPB = 256 / LPR;
+  __shared__ float4 red[SPB][LPR];
+  const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
+  float4 s = f4(0.f);
+  for (int64_t i = (int64_t)blockIdx.x * SPB + sg; i < n; i += (int64_t)gridDim.x * SPB)
+    s = add4(s, ld4(Y + i * ldy + sl * 4));
+  red[sg][sl] = s;
+  __syncthreads();
+  if (threadIdx.x < LPR) {
+    float4 t = red[0][threadIdx.x];
+    for (int q = 1; q < SPB; ++q) t = add4(t, red[q][threadIdx.x]);
+    st4(part + ((int64_t)blockIdx.x * LPR + threadIdx.x) * 4, t);
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// host launchers
+// ===========================================================================
+bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode) {
+  return M >= 0 && K >= kGBK && K % kGBK == 0 && N >= 128 && N % 128 == 0 && (bmode == 0 || bmode == 1);
+}
+
+hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
+                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  NnArg a{};
+  a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.B = B; a.ldb = ldb; a.N = N; a.alpha = alpha; a.bias = bias;
+  a.Y = Y; a.ldy = ldy;
+  a.row_blocks = (M + kGBM - 1) / kGBM;
+  const int64_t padded = (a.row_blocks + 7) / 8 * 8;
+  const bool wide = N % 256 == 0;
+  a.n_blocks = N / (wide ? 256 : 128);
+  const unsigned grid = (unsigned)(padded * a.n_blocks);
+#define PPGAT_NN(NT_, BM_) hipLaunchKernelGGL((k_gemm_nn<NT_, BM_>), dim3(grid), dim3(256), 0, st, a)
+  if (wide) {
+    if (bmode == 0) PPGAT_NN(8, 0); else PPGAT_NN(8, 1);
+  } else {
+    if (bmode == 0) PPGAT_NN(4, 0); else PPGAT_NN(4, 1);
+  }
+#undef PPGAT_NN
+  return hipGetLastError();
+}
+
+static int tn_splits(int64_t M, int T) {
+  int s = 8;
+  while (s < 512 && (int64_t)s * T < 512 && M / (2 * s) >= 4 * kTR) s *= 2;
+  return s;
+}
+
+bool gemm_tn_big_shape_ok(int Ma, int Nb) { return Ma >= 128 && Ma % 128 == 0 && Nb >= 128 && Nb % 128 == 0; }
+
+size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb) {
+  const int T = (Ma / kTA) * (Nb / (Nb % 256 == 0 ? 256 : 128));
+  return align_up((size_t)tn_splits(M, T) * Ma * Nb * 4);
+}
+
+hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
+                       void* ws, hipStream_t st) {
+  const bool wide = Nb % 256 == 0;
+  TnArg a{};
+  a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.M = M; a.Ma = Ma; a.Nb = Nb;
+  a.tiles_a = Ma / kTA;
+  a.tiles_b = Nb / (wide ? 256 : 128);
+  const int T = a.tiles_a * a.tiles_b;
+  a.splits = tn_splits(M, T);
+  a.rows_per_split = ((M + a.splits - 1) / a.splits + kTR - 1) / kTR * kTR;
+  a.part = static_cast<float*>(ws);
+  const unsigned grid = (unsigned)(8 * T * ((a.splits + 7) / 8));
+  if (wide) hipLaunchKernelGGL((k_gemm_tn<256>), dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_tn<128>), dim3(grid), dim3(256), 0, st, a);
+  const int64_t n4 = (int64_t)Ma * Nb / 4;
+  hipLaunchKernelGGL(k_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, n4, a.splits, out);
+  return hipGetLastError();
+}
+
+bool xgat_shape_ok(int K, int H, int C) { return K == 256 && (H == 2 || H == 4) && C >= 128 && C % 128 == 0; }
+
+#define PPGAT_XH(H_, ...)                                   \
+  do {                                                      \
+    if ((H_) == 2) { constexpr int HH = 2; __VA_ARGS__; }   \
+    else { constexpr int HH = 4; __VA_ARGS__; }             \
+  } while (0)
+
+hipError_t xgat_weights(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
+                        float* Wt, float* Wg, hipStream_t st) {
+  const int64_t na = (int64_t)2 * H * K;
+  if (A) hipLaunchKernelGGL(k_att_proj, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, st, W, att_src, att_dst, H, C,
+                            K, A);
+  const int64_t nw = (int64_t)H * C * K;
+  if (Wt || Wg) hipLaunchKernelGGL(k_wperm, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, W, H, C, K, Wt, Wg);
+  return hipGetLastError();
+}
+
+hipError_t xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_dst, int K, int H, const float* A,
+                       float* s_src, float* s_dst, hipStream_t st) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows + 3) / 4;  // one row per wave (K = 256), grid-stride
+  if (blocks > 4096) blocks = 4096;
+  PPGAT_XH(H, hipLaunchKernelGGL((k_xscores<256, HH>), dim3((unsigned)blocks), dim3(256), 0, st, x, ldx, n_rows, n_dst,
+                                 A, s_src, s_dst));
+  (void)K;
+  return hipGetLastError();
+}
+
+hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, const float* x, int64_t ldx, int K,
+                    int H, const float* s_src, const float* s_dst, float slope, float p, uint64_t seed,
+                    const uint64_t* seed_in, float* agg, float* m, float* invl, float* partial,
+                    const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  if (it.n_items > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_fwd_x<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
+                                   col, eid, x, ldx, s_src, s_dst, slope, p, inv_keep, seed, seed_in, agg, m, invl,
+                                   partial));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  (void)K;
+  return launch_fwd_merge(256, hub_row, hub_ptr, n_hubs, H, partial, 1e-16f, m, invl, agg, st);
+}
+
+hipError_t xgat_bwd_pro(const float* gt, const float* agg, const float* s_dst, const float* m, const float* invl,
+                        int64_t n, int K, int H, float* nstate, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_x_pro<256, HH>), dim3((unsigned)blocks), dim3(256), 0, st, gt, agg, s_dst, m,
+                                 invl, n, reinterpret_cast<float4*>(nstate)));
+  (void)K;
+  return hipGetLastError();
+}
+
+hipError_t xgat_bwd_edges(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                          const float* x, int64_t ldx, int K, int H, const float* s_src, const float* nstate,
+                          const float* gt, const float* A_src, float slope, float p, uint64_t seed,
+                          const uint64_t* seed_in, float* dx, int64_t lddx, float* S, int64_t lds, float* dz,
+                          float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                          hipStream_t st) {
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  if (it.n_items > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_x<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
+                                   row, csc_eid, csc2csr, x, ldx, s_src, reinterpret_cast<const float4*>(nstate), gt,
+                                   A_src, slope, p, inv_keep, seed, seed_in, dx, lddx, S, lds, dz, partial));
+  if (n_hubs > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_x_merge<256, HH>), dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st,
+                                   hub_row, hub_ptr, n_hubs, partial, A_src, dx, lddx, S, lds));
+  (void)K;
+  return hipGetLastError();
+}
+
+hipError_t xgat_bwd_epi(const float* S, int64_t lds, const float* A_dst, int64_t n, int K, int H, float* dx,
+                        int64_t lddx, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t th = n * (K / 4);
+  PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_x_epi<256, HH>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, S, lds,
+                                 A_dst, n, dx, lddx));
+  return hipGetLastError();
+}
+
+hipError_t xgat_wgrad(const float* G, const float* GV, const float* W, const float* att_src, const float* att_dst,
+                      int H, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st) {
+  const int64_t rows = (int64_t)H * C;
+  hipLaunchKernelGGL(k_wgrad_x, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, G, GV, W, att_src, att_dst, H, C,
+                     K, 1.f / (float)H, dW, datt_src, datt_dst);
+  return hipGetLastError();
+}
+
+int64_t colsum_blocks(int64_t n) {
+  int64_t b = (n + 63) / 64;
+  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+}
+
+hipError_t colsum(const float* Y, int64_t ldy, int64_t n, int C, float* out, float* part, hipStream_t st) {
+  const int64_t blocks = colsum_blocks(n);
+  if (C == 256) hipLaunchKernelGGL((k_colsum_part<256>), dim3((unsigned)blocks), dim3(256), 0, st, Y, ldy, n, part);
+  else if (C == 128) hipLaunchKernelGGL((k_colsum_part<128>), dim3((unsigned)blocks), dim3(256), 0, st, Y, ldy, n, part);
+  else return hipErrorInvalidValue;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_col_reduce(part, blocks, C, C, out, nullptr, st);
+}
+
+}  // namespace ppgat

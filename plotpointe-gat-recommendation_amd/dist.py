@@ -317,6 +317,14 @@ class HaloGraph:
     def owned_users(self, n_users: int, rank: Optional[int] = None):
         return self.owned(rank)[0]
 
+    def xviews(self):
+        """The local edge lists as hip_ops.XViews (aggregate-then-transform layer): CSR over the
+        own destination rows, CSC over [own | halo] sources."""
+        from .hip_ops import XViews
+        f, b = self.fwd_view, self.bwd_view
+        return XViews(self.n_own, self.R, f.n_fwd_edges, f.col, f.csr_eid, f.fwd_sched, b.row, b.csc_eid, b.dz_slot,
+                      b.bwd_sched)
+
 
 def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,
                      csr_builder: Callable = _hip_csr, sched_builder: Optional[Callable] = _hip_sched,
@@ -503,13 +511,20 @@ class HaloPyGGAT(_ShardedBase):
         hg = self.dg
         x = self.node_features(item_feats)
         for conv in self.convs:
+            p = float(conv.dropout) if self.training else 0.0
+            seed = self.layer_seed(conv)
             if self.exchanges_input(conv):
-                h = self.stages.linear(exchange(x, hg.plan, self.comm, self.stages), conv.lin.weight, None)
+                x_loc = exchange(x, hg.plan, self.comm, self.stages)
+                gat_x = getattr(self.stages, "gat_x", None)
+                out = gat_x(x_loc, conv, hg.xviews(), p, seed) if gat_x is not None else None
+                if out is not None:  # aggregate-then-transform on the local rows (no halo projection)
+                    x = out
+                    continue
+                h = self.stages.linear(x_loc, conv.lin.weight, None)
             else:
                 h = exchange(self.stages.linear(x, conv.lin.weight, None), hg.plan, self.comm, self.stages)
             x = _LocalGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, hg, self.stages, conv.heads,
-                                conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope),
-                                float(conv.dropout) if self.training else 0.0, self.layer_seed(conv))
+                                conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p, seed)
         return x
 
 

@@ -574,6 +574,12 @@ def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, s
     if x_items is not None:
         _require(x_items.is_cuda and x_items.dtype == torch.float32 and x_items.dim() == 2
                  and x_items.size(1) == x.size(1), "gat_layer: x_items must match x in dtype/device/width")
+    if (mode == _lib.MODE_PYG and heads > 1 and heads * channels > x.size(1) and rep is None
+            and xgat_supported(x.size(1), heads, channels)):
+        # multi-head layers wider than their input: aggregate x, then transform (config 5)
+        xx = torch.cat([x, x_items], 0) if x_items is not None else x
+        return gat_layer_x(xx, weight, att_src, att_dst, bias, XViews.of_graph(graph), heads, channels, slope,
+                           dropout_p, seed)
     return GATLayer.apply(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed,
                           x_items, rep)
 
@@ -596,12 +602,12 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     _require(A.size(0) == nb, "gemm_tn: A [N,M], B [N,K]")
     N, M, K = A.size(0), A.size(1), B.size(1)
     nv = 0 if V is None else V.size(1)
-    if B_items is None and M * K > 128 * 128 and N >= 65536:
-        # beyond one 128 x 128 tile (config 5: 1024 x 256 over 1.9M rows) the library GEMM
-        # (hipBLASLt, ~130 TF at these shapes) beats the split-N kernel; still one pass each
-        out = torch.mm(A.t(), B)
-        cs = A.sum(0) if want_colsum else None
-        vout = torch.mm(V.t(), B) if nv else None
+    if B_items is None and M * K > 128 * 128 and gemm_tn_big_supported(M, K):
+        # beyond one 128 x 128 tile (config 5: 1024 x 256 over 1.9M rows): the matrix-core TN
+        # kernel (ppgat_gemm_tn_big); column sums and V^T B through the small kernels
+        out = gemm_tn_big(A, B)
+        cs = colsum(A) if want_colsum else None
+        vout = gemm_tn(V, B)[0] if nv else None
         return out, cs, vout
     if V is not None:
         _require(V.is_cuda and V.dtype == torch.float32 and V.dim() == 2 and V.stride(1) == 1 and V.size(0) == N,
@@ -629,23 +635,35 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
 
 
 class _Linear(torch.autograd.Function):
-    """y = x W^T + b.  Forward and dx through the BLAS library GEMM (square, well-shaped);
-    dW (and db) through ppgat_gemm_tn (N = 10^5..10^7 rows split over the chip)."""
+    """y = x W^T + b on the fp32 matrix cores: the fused 128-column projection
+    (ppgat_project) or the general GEMM (ppgat_gemm_nn, config 5's 256-wide layers); dx by
+    ppgat_gemm_nn, dW (and db) through ppgat_gemm_tn (N = 10^5..10^7 rows split over the
+    chip).  Shapes outside both kernels (tests' odd widths) use torch's GEMM."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        if project_supported(x.size(1), weight.size(0)) and weight.is_contiguous():
-            return project(x, weight.detach(), bias.detach().contiguous() if bias is not None else None)
+        W = weight.detach().contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        if project_supported(x.size(1), weight.size(0)):
+            return project(x, W, b)
+        if gemm_nn_supported(x.size(0), x.size(1), weight.size(0), 1):
+            return gemm_nn(x, W, 1, weight.size(0), bias=b)
         return torch.nn.functional.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, g):
         x, weight = ctx.saved_tensors
         g = g.contiguous()
-        dx = g @ weight if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            W = weight.detach().contiguous()
+            if gemm_nn_supported(g.size(0), g.size(1), W.size(1), 0):
+                dx = gemm_nn(g, W, 0, W.size(1))
+            else:
+                dx = g @ weight
         dW = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dW, db, _ = gemm_tn(g, x, want_colsum=ctx.has_bias)
@@ -657,6 +675,201 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     if x.dtype != torch.float32 or x.dim() != 2:
         raise NotImplementedError("ppgat linear: fp32 2-D input only")
     return _Linear.apply(x, weight, bias)
+
+
+# ---------------------------------------------------------------------------
+# general fp32 matrix-core GEMMs (include/ppgat.h ppgat_gemm_nn / ppgat_gemm_tn_big)
+# ---------------------------------------------------------------------------
+def gemm_nn_supported(m: int, k: int, n: int, b_layout: int) -> bool:
+    return bool(_lib.load().ppgat_gemm_nn_supported(int(m), int(k), int(n), int(b_layout)))
+
+
+def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: float = 1.0,
+            bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """alpha x B (+ bias): B [K, n] row-major (b_layout 0) or [n, K] (b_layout 1: x B^T)."""
+    lib = _lib.load()
+    _check_dev("x", x, torch.float32)
+    _check_dev("B", B, torch.float32, x.device)
+    M, K = x.shape
+    y = out if out is not None else torch.empty(M, n, dtype=torch.float32, device=x.device)
+    ldb = B.stride(0)
+    _lib.check(lib.ppgat_gemm_nn(x.data_ptr(), x.stride(0) if M > 1 else K, M, K, B.data_ptr(), ldb, b_layout, n,
+                                 float(alpha), _lib.ptr(bias), y.data_ptr(), y.stride(0) if M > 1 else n,
+                                 _lib.stream_handle(x.device)), "gemm_nn")
+    return y
+
+
+def gemm_tn_big_supported(ma: int, nb: int) -> bool:
+    return ma % 128 == 0 and nb % 128 == 0 and ma >= 128 and nb >= 128
+
+
+def gemm_tn_big(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """A [M, ma]^T B [M, nb] on the matrix cores (ppgat_gemm_tn_big), deterministic."""
+    lib = _lib.load()
+    _check_dev("A", A, torch.float32)
+    _check_dev("B", B, torch.float32, A.device)
+    M, ma = A.shape
+    nb = B.size(1)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_gemm_tn_big_workspace_bytes(M, ma, nb, ctypes.byref(nbytes)), "gemm_tn_big_workspace")
+    ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=A.device)
+    out = torch.empty(ma, nb, dtype=torch.float32, device=A.device)
+    _lib.check(lib.ppgat_gemm_tn_big(A.data_ptr(), A.stride(0) if M > 1 else ma, B.data_ptr(),
+                                     B.stride(0) if M > 1 else nb, M, ma, nb, out.data_ptr(), ws.data_ptr(),
+                                     nbytes.value, _lib.stream_handle(A.device)), "gemm_tn_big")
+    return out
+
+
+def colsum(Y: torch.Tensor) -> torch.Tensor:
+    """Column sums of Y [n, c] (ppgat_colsum, c in {128, 256}; torch otherwise)."""
+    lib = _lib.load()
+    _check_dev("Y", Y, torch.float32)
+    n, c = Y.shape
+    if c not in (128, 256):
+        return Y.sum(0)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_colsum_workspace_bytes(n, c, ctypes.byref(nbytes)), "colsum_workspace")
+    ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=Y.device)
+    out = torch.empty(c, dtype=torch.float32, device=Y.device)
+    _lib.check(lib.ppgat_colsum(Y.data_ptr(), Y.stride(0) if n > 1 else c, n, c, out.data_ptr(), ws.data_ptr(),
+                                nbytes.value, _lib.stream_handle(Y.device)), "colsum")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# multi-head layer, aggregate-then-transform (include/ppgat.h ppgat_xgat_*)
+# ---------------------------------------------------------------------------
+@dataclass
+class XViews:
+    """The edge lists the aggregate-then-transform layer runs on: CSR over the n_dst
+    destination rows (forward, destination sums) and CSC over the n_src source rows
+    (backward edge pass); source ids index x rows [0, n_src)."""
+    n_dst: int
+    n_src: int
+    n_edges: int
+    col: torch.Tensor
+    csr_eid: torch.Tensor
+    fwd_sched: Schedule
+    row: torch.Tensor
+    csc_eid: torch.Tensor
+    dz_slot: torch.Tensor
+    bwd_sched: Schedule
+
+    @staticmethod
+    def of_graph(g: "CSRGraph") -> "XViews":
+        return XViews(g.n_nodes, g.n_nodes, g.n_edges, g.col, g.csr_eid, g.fwd_sched, g.row, g.csc_eid, g.csc2csr,
+                      g.bwd_sched)
+
+
+def xgat_supported(in_channels: int, heads: int, channels: int) -> bool:
+    return bool(_lib.load().ppgat_xgat_supported(int(in_channels), int(heads), int(channels)))
+
+
+class GATLayerX(torch.autograd.Function):
+    """x [n_src, C_in] -> out [n_dst, C]: GATConv with H heads in the aggregate-then-transform
+    form (include/ppgat.h ppgat_xgat_*): the edge pass gathers x_j once per edge for all heads,
+    the per-head aggregates are transformed by one matrix-core GEMM; backward gt = g W / H
+    (GEMM), one edge pass by source, dW = g^T agg (TN GEMM) + attention terms."""
+
+    @staticmethod
+    def forward(ctx, x, weight, att_src, att_dst, bias, v: XViews, heads: int, C: int, slope: float, p: float,
+                seed: int):
+        lib = _lib.load()
+        x = x.contiguous()
+        dev = x.device
+        K = x.size(1)
+        H = heads
+        _require(x.size(0) == v.n_src, f"x has {x.size(0)} rows, the edge lists {v.n_src} sources")
+        W = weight.detach().contiguous()
+        a_s = att_src.detach().reshape(H, C).contiguous()
+        a_d = att_dst.detach().reshape(H, C).contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        st = _lib.stream_handle(dev)
+        A = torch.empty(2, H, K, dtype=torch.float32, device=dev)
+        Wt = torch.empty(H * K, C, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), H, C, K, A.data_ptr(),
+                                          Wt.data_ptr(), None, st), "xgat_weights")
+        s_src = torch.empty(v.n_src, H, dtype=torch.float32, device=dev)
+        s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_src, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
+                                         s_dst.data_ptr(), st), "xgat_scores")
+        agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
+        m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
+        inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
+        seed_buf = seed_buffer(p, dev)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_fwd_workspace_bytes(v.fwd_sched.n_hub_items, H, K, ctypes.byref(nbytes)), "xgat_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = v.fwd_sched.cstruct()
+        E = v.n_edges
+        _lib.check(lib.ppgat_xgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
+                                      _lib.ptr(v.csr_eid) if E else None, v.n_dst, E, K, H, x.data_ptr(), K,
+                                      s_src.data_ptr(), s_dst.data_ptr(), float(slope), float(p),
+                                      int(seed) & (2**64 - 1), _lib.ptr(seed_buf), agg.data_ptr(), m.data_ptr(),
+                                      inv_l.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_fwd")
+        out = gemm_nn(agg.view(v.n_dst, H * K), Wt, 0, C, alpha=1.0 / H, bias=b)
+        ctx.save_for_backward(x, W, a_s, a_d, A, s_src, s_dst, agg, m, inv_l)
+        ctx.v, ctx.seed_buf = v, seed_buf
+        ctx.meta = (H, C, K, slope, p, seed, bias is not None)
+        ctx.att_shapes = (att_src.shape, att_dst.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        x, W, a_s, a_d, A, s_src, s_dst, agg, m, inv_l = ctx.saved_tensors
+        H, C, K, slope, p, seed, has_bias = ctx.meta
+        v = ctx.v
+        dev = x.device
+        st = _lib.stream_handle(dev)
+        g = g.contiguous()
+        Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
+                   "xgat_weights")
+        gt = gemm_nn(g, Wg, 0, H * K)
+        nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_xgat_bwd_prologue(gt.data_ptr(), agg.data_ptr(), s_dst.data_ptr(), m.data_ptr(),
+                                               inv_l.data_ptr(), v.n_dst, K, H, nstate.data_ptr(), st),
+                   "xgat_bwd_prologue")
+        E = v.n_edges
+        S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
+        dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+        dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_bwd_workspace_bytes(v.bwd_sched.n_hub_items, K, ctypes.byref(nbytes)), "xgat_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = v.bwd_sched.cstruct()
+        _lib.check(lib.ppgat_xgat_bwd_edges(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                            _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None,
+                                            E, K, H, x.data_ptr(), K, s_src.data_ptr(), nstate.data_ptr(),
+                                            gt.data_ptr(), A.data_ptr(), float(slope), float(p),
+                                            int(seed) & (2**64 - 1), _lib.ptr(ctx.seed_buf), dx.data_ptr(), K,
+                                            S.data_ptr(), 2 * H, dz.data_ptr(), ws.data_ptr(), nbytes.value, st),
+                   "xgat_bwd_edges")
+        fs = v.fwd_sched.cstruct()
+        dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
+                                         dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
+        _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
+                   "xgat_bwd_epilogue")
+        GV = gemm_tn(S, x)[0]
+        G = gemm_tn_big(g, agg.view(v.n_dst, H * K))
+        dW = torch.empty_like(W)
+        datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)
+        datt_dst = torch.empty(H, C, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_xgat_weight_grads(G.data_ptr(), GV.data_ptr(), W.data_ptr(), a_s.data_ptr(),
+                                               a_d.data_ptr(), H, C, K, dW.data_ptr(), datt_src.data_ptr(),
+                                               datt_dst.data_ptr(), st), "xgat_weight_grads")
+        dbias = colsum(g) if (has_bias and ctx.needs_input_grad[4]) else None
+        return (dx, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None)
+
+
+def gat_layer_x(x, weight, att_src, att_dst, bias, views: XViews, heads: int, channels: int, slope: float,
+                dropout_p: float = 0.0, seed: int = 0):
+    _require(x.is_cuda, "gat_layer_x: ppgat runs on ROCm devices only; there is no CPU path")
+    return GATLayerX.apply(x, weight, att_src, att_dst, bias, views, heads, channels, float(slope), float(dropout_p),
+                           int(seed))
 
 
 LOSS_KINDS = {"bpr": 0, "bce": 1}
@@ -775,6 +988,14 @@ class HipStages:
 
     def seed_buffer(self, p, device):
         return seed_buffer(p, device)
+
+    def gat_x(self, x_loc, conv, views, p, seed):
+        """The aggregate-then-transform layer over a rank's local edge lists, or None when the
+        shape is not supported (the caller then projects and runs the staged layer)."""
+        if not (conv.heads > 1 and xgat_supported(conv.in_channels, conv.heads, conv.out_channels)):
+            return None
+        return gat_layer_x(x_loc, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, views, conv.heads,
+                           conv.out_channels, float(conv.negative_slope), p, seed)
 
     def gather_rows(self, t, idx):
         """t[idx] (the all_to_all send buffer) through ppgat_rows_gather."""

@@ -35,12 +35,16 @@ def _free_port():
 
 
 def _setup(dev, heads=1):
+    """heads 1, 2: hidden 128; heads 4: hidden 256 (config 5's layer shape: the halo path
+    exchanges x and runs the aggregate-then-transform kernels)."""
     pkg = importlib.import_module("plotpointe-gat-recommendation_amd")
     g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
     ei = torch.from_numpy(g.edge_index_numpy()).to(dev)
     feats = torch.from_numpy(pkg.data.synthetic_item_features(g.n_items, 64, seed=5)).to(dev)
     torch.manual_seed(0)
-    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=64, hidden=128, layers=2, heads=heads, attn_dropout=0.2)
+    hidden = 256 if heads == 4 else 128
+    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=64, hidden=hidden, layers=2, heads=heads,
+                      attn_dropout=0.2)
     with torch.no_grad():
         for conv in full.convs:
             conv.bias.uniform_(-0.1, 0.1)
@@ -121,7 +125,7 @@ def _check(res, ref):
         assert _rel(v, grads[k]) <= tol, (k, _rel(v, grads[k]))
 
 
-@pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (1, "replicated"), (2, "replicated"),
+@pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (4, "halo"), (1, "replicated"), (2, "replicated"),
                                         (1, "replicated-staged")])
 def test_sharded_world1_rccl(cuda, tmp_path, monkeypatch, heads, part):
     monkeypatch.setenv("PPGAT_COMM_ALWAYS", "1")  # run every collective through RCCL at world 1
@@ -135,7 +139,7 @@ def test_sharded_world1_rccl(cuda, tmp_path, monkeypatch, heads, part):
     _check(torch.load(tmp_path / "sharded_1.pt", weights_only=False), _oracle(heads))
 
 
-@pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (1, "replicated"), (2, "replicated"),
+@pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (4, "halo"), (1, "replicated"), (2, "replicated"),
                                         (1, "replicated-staged")])
 def test_sharded_world2_shared_gpu(cuda, tmp_path, heads, part):
     mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), heads, part), nprocs=2, join=True,

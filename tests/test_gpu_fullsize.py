@@ -81,7 +81,18 @@ def _train_step_check(pkg, oracle, cuda, g, ei_np, feats_np, triples):
     assert abs(loss.item() - lr.item()) <= 1e-5 * abs(lr.item())
     for k, v in m.named_parameters():
         tol = 1e-5 if v.dim() == 2 else 1e-4
-        assert rel(v.grad, P[k].grad) <= tol, (k, rel(v.grad, P[k].grad))
+        ref = P[k].grad
+        if k.endswith("att_dst"):
+            # datt_src and datt_dst are sums of the same per-edge logit gradients dz (over a
+            # source's out-edges / a destination's in-edges).  Where every in-edge of a
+            # destination sits on one side of the LeakyReLU, its dz sum cancels exactly, and
+            # datt_dst is rounding only (1.4e-18 in the fp64 oracle at config 3, layer 2):
+            # its error is judged on the scale of the pair
+            scale = max(float(ref.abs().max()), float(P[k.replace("att_dst", "att_src")].grad.abs().max()))
+            err = float((v.grad.detach().double().cpu() - ref).abs().max())
+            assert err <= tol * scale, (k, err, scale)
+            continue
+        assert rel(v.grad, ref) <= tol, (k, rel(v.grad, ref))
 
 
 def test_cfg2_full_eval_embeddings_and_top20(pkg, oracle, cuda, cfg2):
