@@ -72,8 +72,21 @@ def parse():
 # ---------------------------------------------------------------------------
 # algorithmic bytes per launch (DESIGN.md "Kernels and their rooflines")
 # ---------------------------------------------------------------------------
-def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool) -> float:
+def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool, xform_k: int = 0) -> float:
+    """Algorithmic bytes per launch.  xform_k > 0: the aggregate-then-
+    transform kernels (heads > 1, x rows of xform_k floats gathered instead of h rows)."""
     d = 4 if dropout else 0
+    if xform_k:
+        K = xform_k
+        if kernel == "fwd":    # k_fwd_x: col, s_src[H], x_j | sched, s_dst[H], agg[H, K], m, inv_l
+            return E * (4 + 4 * H + 4 * K + d) + N * (12 + 4 * H + 4 * H * K + 8 * H)
+        if kernel == "bwd_src":  # k_bwd_x: row, slot, nstate[H], gt_i[H, K], dz[H] | sched, x, s_src, dx, S
+            return E * (8 + 16 * H + 4 * H * K + 4 * H + d) + N * (12 + 4 * K + 4 * H + 4 * K + 4 * H)
+        if kernel == "bwd_pro":  # gt, agg in; s_dst, m, inv_l in; nstate out
+            return N * (8 * H * K + 12 * H + 16 * H)
+        if kernel == "scores":
+            return N * (4 * K + 8 * H)
+        return 0.0
     if kernel == "fwd":
         per_e = 4 + 4 * H + 4 * H * C + d * H / max(H, 1)
         per_n = 8 + 4 * H + 4 * C + 8 * H
@@ -312,6 +325,8 @@ def main():
         el = float(tt.item())
     K = args.steps
     H, C = args.heads, args.hidden
+    # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
+    xform_k = C if (H > 1 and H * C > C and pkg.hip_ops.xgat_supported(C, H, C)) else 0
     kern = {k: _lib.profile_read(k) for k in ("scores", "fwd", "bwd_pro", "bwd_src", "bwd_epi", "bwd_red",
                                                "proj", "gemm_tn", "adam")}
     fused_ms = sum(ms for k, (ms, _) in kern.items() if k not in ("proj", "gemm_tn", "adam"))
@@ -326,9 +341,9 @@ def main():
         else:
             v = dg.fwd_view if dom == "fwd" else dg.bwd_view
         ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
-                        args.attn_dropout > 0)
+                        args.attn_dropout > 0, xform_k)
     else:
-        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0)
+        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k)
     achieved = ab / avg_s / 1e9
     traffic = None
     try:
@@ -374,6 +389,8 @@ def main():
                                    if part == "replicated" else
                                    f"row-sharded x{world}, RCCL all_to_all halo + grad all_reduce")},
         "hip_graph": graph is not None,
+        "formulation": ("aggregate-then-transform (x_j gathered once per edge for all heads)" if xform_k else
+                        "transform-then-aggregate (h_j gathered per edge)"),
         "kernel_timing": kern_src,
         "fused_kernel_edges_per_sec": E * args.layers * K / (fused_ms / 1e3) if fused_ms else None,
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},

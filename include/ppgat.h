@@ -359,6 +359,18 @@ int ppgat_bpr_sample(const int64_t* user_ptr, const int32_t* items_sorted, const
                      const int64_t* n_eligible, int64_t n_items, int64_t n_triples, uint64_t seed, int64_t t0,
                      int64_t* u, int64_t* i, int64_t* j, int32_t* bad, void* stream);
 
+/* ---- sampled-evaluation candidates ---------------------------------------------------
+ * Replaces: the candidate draw of eval_sampled, scripts/train_gat_pyg.py:157-167 (a Python
+ *   loop over ~192k users: np.random.randint(0, n_items) redrawn while the item is in the
+ *   user's train set or is the held-out positive, eval_neg_k times per user).
+ * cands [n_eval, n_neg + 1] int64: column 0 = pos[b], column 1 + k = the first draw d of the
+ * counter-based stream (seed, t = b * n_neg + k, d) outside u's train items (items_sorted /
+ * user_ptr of ppgat_bpr_sampler_prepare) and != pos[b] (oracle/sampler_oracle.py restates it);
+ * *bad = 2 if some negative was not found in 1024 draws. */
+int ppgat_eval_sample(const int64_t* user_ptr, const int32_t* items_sorted, const int64_t* users, const int64_t* pos,
+                      int64_t n_eval, int64_t n_neg, int64_t n_items, uint64_t seed, int64_t* cands, int32_t* bad,
+                      void* stream);
+
 /* ---- sampled ranking (evaluation) ------------------------------------------------
  * Replaces: the per-user loop of eval_sampled, scripts/train_gat_pyg.py:160-175:
  *   scores = I[cands[b]] @ U[users[b]];  rank[b] = #(scores[1:] > scores[0]) + 1

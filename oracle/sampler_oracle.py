@@ -87,3 +87,37 @@ def bpr_sample(user_ptr: np.ndarray, user_items: np.ndarray, n_items: int, S: in
         j[open_] = 0
         bad = 2
     return u, i.astype(np.int64), j, bad
+
+
+def eval_sample(user_ptr: np.ndarray, user_items: np.ndarray, users: np.ndarray, pos: np.ndarray, n_items: int,
+                n_neg: int, seed: int):
+    """ppgat_eval_sample restated (csrc/ppgat_sample.hip k_eval_sample) -> (cands [B, n_neg+1], bad).
+    Rule of eval_sampled (scripts/train_gat_pyg.py:157-167): negatives uniform over the items
+    outside the user's train list and != the held-out positive, drawn independently."""
+    user_ptr = np.asarray(user_ptr, dtype=np.int64)
+    items_sorted, _ = prepare(user_ptr, user_items)
+    users = np.asarray(users, np.int64)
+    pos = np.asarray(pos, np.int64)
+    B = len(users)
+    owner = np.repeat(np.arange(len(user_ptr) - 1, dtype=np.int64), np.diff(user_ptr))
+    keys = owner * np.int64(n_items) + items_sorted
+    t = (np.arange(B, dtype=np.int64)[:, None] * n_neg + np.arange(n_neg, dtype=np.int64)[None, :]).reshape(-1)
+    ub = np.repeat(users, n_neg)
+    pb = np.repeat(pos, n_neg)
+    neg = np.full(B * n_neg, -1, np.int64)
+    open_ = np.arange(B * n_neg)
+    for d in range(MAX_NEG_DRAWS):
+        if open_.size == 0:
+            break
+        c = below(draw64(seed, t[open_].astype(np.uint64), d), n_items)
+        q = ub[open_] * np.int64(n_items) + c
+        ix = np.minimum(np.searchsorted(keys, q), max(len(keys) - 1, 0))
+        hit = (keys[ix] == q) if len(keys) else np.zeros(len(q), dtype=bool)
+        hit |= c == pb[open_]
+        neg[open_[~hit]] = c[~hit]
+        open_ = open_[hit]
+    bad = 0
+    if open_.size:
+        neg[open_] = 0
+        bad = 2
+    return np.concatenate([pos[:, None], neg.reshape(B, n_neg)], 1), bad

@@ -681,6 +681,18 @@ int ppgat_bpr_sample(const int64_t* user_ptr, const int32_t* items_sorted, const
   return PPGAT_OK;
 }
 
+int ppgat_eval_sample(const int64_t* user_ptr, const int32_t* items_sorted, const int64_t* users, const int64_t* pos,
+                      int64_t n_eval, int64_t n_neg, int64_t n_items, uint64_t seed, int64_t* cands, int32_t* bad,
+                      void* stream) {
+  if (n_eval < 0 || n_neg < 0 || n_items < 1 || n_items > INT32_MAX) return fail(PPGAT_ERR_INVALID, "eval_sample: sizes");
+  if (!bad || (n_eval > 0 && (!user_ptr || !users || !pos || !cands))) return fail(PPGAT_ERR_INVALID, "eval_sample: null");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_SAMPLE, st);
+  hipError_t e = ppgat::eval_sample(user_ptr, items_sorted, users, pos, n_eval, n_neg, n_items, seed, cands, bad, st);
+  if (e != hipSuccess) return hip_fail(e, "eval_sample");
+  return PPGAT_OK;
+}
+
 int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
                        int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
                        int32_t* rank, void* stream) {

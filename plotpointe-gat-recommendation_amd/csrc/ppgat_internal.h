@@ -119,6 +119,10 @@ hipError_t bpr_sample(const int64_t* ptr, const int32_t* items_sorted, const int
                       const int64_t* n_eligible, int64_t n_items, int64_t S, uint64_t seed, int64_t t0, int64_t* u,
                       int64_t* i, int64_t* j, int32_t* bad, hipStream_t st);
 
+hipError_t eval_sample(const int64_t* ptr, const int32_t* items_sorted, const int64_t* users, const int64_t* pos,
+                       int64_t n_eval, int64_t n_neg, int64_t n_items, uint64_t seed, int64_t* cands, int32_t* bad,
+                       hipStream_t st);
+
 // evaluation (ppgat_eval.hip)
 hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                         const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,

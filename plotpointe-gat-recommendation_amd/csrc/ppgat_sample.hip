@@ -83,6 +83,37 @@ __global__ void __launch_bounds__(256) k_bpr_sample(const int64_t* __restrict__ 
   u[s] = uu; i[s] = ii; j[s] = jj;
 }
 
+// Sampled-evaluation candidates (eval_sampled, scripts/train_gat_pyg.py:157-167): row b holds
+// the held-out positive, then n_neg negatives; negative k is the first draw d = 0, 1, ... of
+// the stream (seed, t = b * n_neg + k, d) that is neither one of the user's train items nor
+// the positive -- the reference's rule (np.random.randint(0, n_items) redrawn while in
+// train_pos | {pos}), drawn independently per negative.  One thread per negative.
+__global__ void __launch_bounds__(256) k_eval_sample(const int64_t* __restrict__ ptr,
+                                                     const int32_t* __restrict__ items,
+                                                     const int64_t* __restrict__ users,
+                                                     const int64_t* __restrict__ pos, int64_t n_eval, int64_t n_neg,
+                                                     int64_t n_items, uint64_t seed, int64_t* __restrict__ cands,
+                                                     int32_t* __restrict__ bad) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_eval * (n_neg + 1)) return;
+  const int64_t b = t / (n_neg + 1), k = t % (n_neg + 1);
+  const int64_t p = pos[b];
+  if (k == 0) {
+    cands[t] = p;
+    return;
+  }
+  const int64_t u = users[b];
+  const int64_t lo = ptr[u], hi = ptr[u + 1];
+  const uint64_t tt = (uint64_t)(b * n_neg + k - 1);
+  int64_t c = -1;
+  for (int d = 0; d < kMaxNegDraws; ++d) {
+    const int32_t x = (int32_t)below(draw64(seed, tt, d), n_items);
+    if (x != p && !member(items, lo, hi, x)) { c = x; break; }
+  }
+  if (c < 0) { c = 0; atomicOr(bad, 2); }
+  cands[t] = c;
+}
+
 size_t sort_bytes(int64_t n_users, int64_t nnz) {
   size_t b = 0;
   (void)rocprim::segmented_radix_sort_keys(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr,
@@ -132,6 +163,17 @@ hipError_t bpr_sample(const int64_t* ptr, const int32_t* items_sorted, const int
   if (err != hipSuccess || S <= 0) return err;
   hipLaunchKernelGGL(k_bpr_sample, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, ptr, items_sorted, eligible,
                      n_eligible, n_items, S, seed, t0, u, i, j, bad);
+  return hipGetLastError();
+}
+
+hipError_t eval_sample(const int64_t* ptr, const int32_t* items_sorted, const int64_t* users, const int64_t* pos,
+                       int64_t n_eval, int64_t n_neg, int64_t n_items, uint64_t seed, int64_t* cands, int32_t* bad,
+                       hipStream_t st) {
+  hipError_t err = hipMemsetAsync(bad, 0, sizeof(int32_t), st);
+  const int64_t th = n_eval * (n_neg + 1);
+  if (err != hipSuccess || th <= 0) return err;
+  hipLaunchKernelGGL(k_eval_sample, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, ptr, items_sorted, users, pos,
+                     n_eval, n_neg, n_items, seed, cands, bad);
   return hipGetLastError();
 }
 

@@ -6,7 +6,10 @@
   are drawn with the reference's exact ``np.random`` call sequence (so a seeded run
   evaluates the same candidates); the scoring of all users is ONE device pass
   (``ppgat_sampled_rank``) instead of a GEMV + device->host sync per user.
-  ``fast=True`` draws the same distribution with vectorised numpy (different stream).
+  ``sampler=`` (a sampler.BPRSampler over the train lists) draws the candidates on the
+  device too (``ppgat_eval_sample``: same rule, counter-based stream), so the whole
+  evaluation is two kernels and one copy of the ranks; ``fast=True`` draws the same
+  distribution with vectorised numpy (different stream).
 * ``export_item_embeddings`` -- tools/export_item_embeddings.py:139-145.
 * ``top_k_for_user_items``   -- serving/runtime.py:56-76 on the device (torch.topk);
   same rule: user vector = mean of history rows, history masked to -1e9.
@@ -70,7 +73,7 @@ def sampled_rank(Z: torch.Tensor, n_users: int, users: np.ndarray, cands: np.nda
     dev = Z.device
     n_rows, C = Z.shape
     n_items = (n_rows - n_users) if row_map is None else int(row_map.numel()) - n_users
-    u = torch.as_tensor(users, dtype=torch.int64).to(dev)
+    u = torch.as_tensor(users, dtype=torch.int64).to(dev).contiguous()
     c = torch.as_tensor(cands, dtype=torch.int64).to(dev).contiguous()
     rank = torch.empty(len(u), dtype=torch.int32, device=dev)
     _lib.check(lib.ppgat_sampled_rank(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(row_map), C, u.data_ptr(),
@@ -92,10 +95,18 @@ def metrics_from_ranks(ranks: np.ndarray, Ks: Sequence[int] = (10, 20)) -> Dict[
 
 
 def eval_sampled(model, cfg, item_feats: torch.Tensor, edge_index: torch.Tensor,
-                 train_pos_idx: Dict[int, np.ndarray], eval_pos: Dict[int, int], Ks=(10, 20), fast: bool = False):
+                 train_pos_idx: Dict[int, np.ndarray], eval_pos: Dict[int, int], Ks=(10, 20), fast: bool = False,
+                 sampler=None, seed: int = 0):
     """Mirror of eval_sampled (train_gat_pyg.py:150-176); ``cfg.eval_neg_k`` negatives."""
     with torch.no_grad():
         Z = model(item_feats, edge_index)
+    if sampler is not None:
+        if not eval_pos:
+            return metrics_from_ranks(np.zeros(0, np.int64), Ks)
+        users = np.fromiter(eval_pos.keys(), np.int64, len(eval_pos))
+        pos = np.fromiter(eval_pos.values(), np.int64, len(eval_pos))
+        cands = sampler.eval_candidates(users, pos, cfg.eval_neg_k, seed)
+        return metrics_from_ranks(sampled_rank(Z, model.n_users, users, cands), Ks)
     if fast:
         users, cands = sample_eval_candidates_fast(train_pos_idx, eval_pos, model.n_items, cfg.eval_neg_k)
     else:

@@ -68,3 +68,21 @@ class BPRSampler:
             if bad & 2:
                 raise ValueError("BPRSampler: a user holds (almost) every item; no negative found")
         return out[0], out[1], out[2]
+
+    def eval_candidates(self, users, pos, n_neg: int, seed: int = 0, check: bool = True) -> torch.Tensor:
+        """eval_sampled's candidates (train_gat_pyg.py:157-167) on the device: [B, n_neg + 1]
+        int64, column 0 the held-out positive, then n_neg negatives drawn uniformly from the
+        items outside the user's train list and != the positive (ppgat_eval_sample)."""
+        lib = _lib.load()
+        u = torch.as_tensor(users).to(self.device, torch.int64).contiguous()
+        p = torch.as_tensor(pos).to(self.device, torch.int64).contiguous()
+        if u.numel() != p.numel():
+            raise ValueError("eval_candidates: users and pos must have the same length")
+        cands = torch.empty(u.numel(), int(n_neg) + 1, dtype=torch.int64, device=self.device)
+        _lib.check(lib.ppgat_eval_sample(self.ptr.data_ptr(), self.items.data_ptr(), u.data_ptr(), p.data_ptr(),
+                                         u.numel(), int(n_neg), self.n_items, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                         cands.data_ptr(), self._bad.data_ptr(), _lib.stream_handle(self.device)),
+                   "eval_sample")
+        if check and u.numel() > 0 and int(self._bad.item()) & 2:
+            raise ValueError("eval_candidates: a user holds (almost) every item; no negative found")
+        return cands

@@ -160,6 +160,8 @@ def main(argv=None):
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--structured-logs", action="store_true")
     ap.add_argument("--fast-eval", action="store_true", help="vectorised negative sampling (same distribution)")
+    ap.add_argument("--device-eval", action="store_true",
+                    help="eval candidates drawn on the GPU (ppgat_eval_sample: same rule, counter-based stream)")
     ap.add_argument("--fast-sampler", action="store_true",
                     help="BPR triples drawn on the GPU (ppgat_bpr_sample: same rule, counter-based stream)")
     ap.add_argument("--synthetic", choices=["cfg1", "cfg2"], default=None)
@@ -195,7 +197,7 @@ def main(argv=None):
     best = -1.0
     val_metrics: Dict[str, float] = {}
     dev_sampler = None
-    if args.fast_sampler:
+    if args.fast_sampler or args.device_eval:
         lens = np.array([len(tr.get(uu, ())) for uu in range(n_users)], dtype=np.int64)
         ptr = np.concatenate([[0], np.cumsum(lens)])
         flat = np.concatenate([np.asarray(tr[uu], dtype=np.int64) for uu in range(n_users) if lens[uu]] or
@@ -203,7 +205,7 @@ def main(argv=None):
         dev_sampler = sampler_mod.BPRSampler(ptr, flat, n_items, device=device)
     for epoch in range(1, cfg.epochs + 1):
         model.train()
-        if dev_sampler is not None:
+        if args.fast_sampler:
             u, i, j = dev_sampler.sample(cfg.samples_per_epoch, seed=cfg.seed,
                                          offset=(epoch - 1) * cfg.samples_per_epoch)
         else:
@@ -218,7 +220,9 @@ def main(argv=None):
         opt.step()
         print(f"[{tag}][Epoch {epoch}] loss={loss.item():.4f} ({cfg.loss})")
         model.eval()
-        val_metrics = evaluation.eval_sampled(model, cfg, item_feats, edge_index, tr, va, fast=args.fast_eval)
+        val_metrics = evaluation.eval_sampled(model, cfg, item_feats, edge_index, tr, va, fast=args.fast_eval,
+                                              sampler=dev_sampler if args.device_eval else None,
+                                              seed=cfg.seed + epoch)
         print(f"[{tag}][Epoch {epoch}] val: {val_metrics}")
         if args.structured_logs:
             log_event("epoch_end", run_id=run_id, epoch=epoch, loss=float(loss.item()), val=val_metrics)
@@ -229,7 +233,8 @@ def main(argv=None):
     ckpt = torch.load(best_path, map_location=device, weights_only=True)
     model.load_state_dict(ckpt["state_dict"])
     model.eval()
-    test_metrics = evaluation.eval_sampled(model, cfg, item_feats, edge_index, tr, te, fast=args.fast_eval)
+    test_metrics = evaluation.eval_sampled(model, cfg, item_feats, edge_index, tr, te, fast=args.fast_eval,
+                                           sampler=dev_sampler if args.device_eval else None, seed=cfg.seed)
     print(f"[{tag}] test: {test_metrics}")
     out = {"best_val_ndcg@20": float(best), "val": val_metrics, "test": test_metrics, "config": cfg.__dict__,
            "notes": f"One-backward-per-epoch with S sampled BPR triples; features={cfg.item_features}; "

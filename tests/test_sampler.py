@@ -164,3 +164,56 @@ def test_gpu_flags_raise(pkg, cuda):
     with pytest.raises(ValueError, match="every item"):
         smp.sample(100, seed=1)
     assert smp.sample(0)[0].numel() == 0
+
+
+# ---------------------------------------------------------------------------
+# eval_sampled candidates (scripts/train_gat_pyg.py:157-167; ppgat_eval_sample)
+# ---------------------------------------------------------------------------
+def _eval_rule_probs(lists, users, pos, n_items):
+    """P(negative = c | row b): uniform over items outside train(u) and != pos."""
+    out = []
+    for u, p in zip(users, pos):
+        allowed = [c for c in range(n_items) if c not in set(lists[u]) and c != p]
+        out.append({c: 1 / len(allowed) for c in allowed})
+    return out
+
+
+def test_eval_candidates_oracle_and_reference_stream_follow_the_rule(pkg):
+    """The oracle's eval negatives and the reference's own np.random draw
+    (evaluation.sample_eval_candidates, the reference's call sequence) both follow the rule."""
+    ev = pkg.evaluation
+    lists = [[0, 5, 7], [], [3, 3, 9], [11], [2, 4, 6, 8, 10]]
+    users = np.array([0, 1, 2, 3, 4])
+    pos = np.array([1, 2, 4, 0, 3])
+    n_neg = 20_000
+    probs = _eval_rule_probs(lists, users, pos, N_ITEMS)
+    ptr, items = _csr(lists)
+    cands, bad = so.eval_sample(ptr, items, users, pos, N_ITEMS, n_neg, seed=11)
+    assert bad == 0 and cands.shape == (5, n_neg + 1)
+    assert np.array_equal(cands[:, 0], pos)
+    np.random.seed(0)
+    tr = {uu: np.array(x) for uu, x in enumerate(lists) if x}
+    _, ref = ev.sample_eval_candidates(tr, dict(zip(users.tolist(), pos.tolist())), N_ITEMS, n_neg)
+    for b in range(5):
+        for arr in (cands[b, 1:], ref[b, 1:]):
+            f = Counter(arr.tolist())
+            assert set(f) <= set(probs[b])  # never a train item nor the positive
+            assert max(abs(f.get(c, 0) / n_neg - p) for c, p in probs[b].items()) < 0.012
+
+
+@pytest.mark.gpu
+def test_eval_candidates_gpu_bit_exact(pkg, cuda):
+    import torch
+    rng = np.random.default_rng(4)
+    n_users, n_items = 3000, 900
+    lens = rng.integers(0, 30, n_users)
+    lens[7] = 0
+    lists = [rng.choice(n_items, int(k), replace=True).tolist() for k in lens]
+    ptr, items = _csr(lists)
+    users = rng.permutation(n_users)[:2000]
+    pos = rng.integers(0, n_items, 2000)
+    s = pkg.sampler.BPRSampler(ptr, items, n_items, device=cuda)
+    got = s.eval_candidates(torch.from_numpy(users), torch.from_numpy(pos), 100, seed=77).cpu().numpy()
+    ref, bad = so.eval_sample(ptr, items, users, pos, n_items, 100, seed=77)
+    assert bad == 0
+    assert np.array_equal(got, ref)
