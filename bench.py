@@ -265,7 +265,9 @@ def main():
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                loss_static = step()
+                # keep only the value: the captured autograd graph (and its AccumulateGrad
+                # nodes, tied to the capture stream) must not outlive the capture
+                loss_static = step().detach()
         except Exception as exc:  # capture refused (driver / RCCL): time the same step eagerly instead
             print(f"bench: hipGraph capture failed ({type(exc).__name__}: {exc})", file=sys.stderr, flush=True)
             graph, ok = None, 0

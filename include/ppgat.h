@@ -381,6 +381,19 @@ int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t 
                        int channels, const int64_t* users, const int64_t* cands, int64_t n_eval, int64_t n_cand,
                        int32_t* rank, void* stream);
 
+/* ---- serving top-K ------------------------------------------------------------------
+ * Replaces: RecommenderRuntime.top_k_for_user_items, serving/runtime.py:56-76 (numpy):
+ *   user_vec = mean(item_vecs[history]); scores = item_vecs @ user_vec; scores[history] = -1e9;
+ *   the k best, descending.
+ * Batched over n_users (<= 256) histories given as CSR (hist_ptr [n_users + 1] int64 into
+ * hist_items; max_hist = the longest history).  The mean adds the history rows in order and
+ * divides by the count (numpy's float32 mean over axis 0); ties between equal scores go to
+ * the smaller item index (a total order).  out_idx/out_score [n_users, k]. */
+int ppgat_serve_topk_workspace_bytes(int64_t n_items, int channels, int n_users, size_t* bytes);
+int ppgat_serve_topk(const float* item_vecs, int64_t n_items, int channels, const int64_t* hist_ptr,
+                     const int64_t* hist_items, int64_t max_hist, int n_users, int k, int32_t* out_idx,
+                     float* out_score, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- fusion MLP inference on the matrix cores (north star's MFMA target) ----------
  * Replaces: FusionMLP.forward + the normalisation and the per-row image copy loop of the
  *           inference pass, embeddings/fuse_modal.py:18-36,227-241:

@@ -88,6 +88,8 @@ SIGNATURES = {
     "ppgat_bpr_sample": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_u64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_eval_sample": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_u64, c_vp, c_vp, c_vp]),
     "ppgat_sampled_rank": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "ppgat_serve_topk_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_serve_topk": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),
     "ppgat_gemm_nn_supported": (c_int, [c_i64, c_int, c_int, c_int]),

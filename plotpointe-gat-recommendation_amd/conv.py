@@ -11,9 +11,11 @@
                       order (so a seeded construction yields the reference's weights)
                       and keys (``lin.weight``, ``a_src``, ``a_dst``).
 
-Both run the layer as ``hip_ops.gat_layer``: ``h = lin(x)`` through the BLAS library,
-everything on the edges through ``libppgat.so``, and a backward that folds the attention
-terms into the projection GEMMs (no epilogue pass).  Dropout on alpha is the counter-hash mask of
+Both run the layer as ``hip_ops.gat_layer``, entirely in ``libppgat.so``: ``h = lin(x)``
+on the fp32 matrix cores with the node attention terms in the GEMM epilogue, the fused
+edge kernels, and a backward that folds the attention terms into the projection GEMMs;
+multi-head layers wider than their input (config 5) run aggregate-then-transform
+(``hip_ops.GATLayerX``: x_j gathered once per edge, one transform GEMM).  Dropout on alpha is the counter-hash mask of
 include/ppgat.h, drawn fresh per training forward from torch's CPU generator.
 """
 from __future__ import annotations

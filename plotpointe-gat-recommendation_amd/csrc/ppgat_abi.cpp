@@ -707,6 +707,33 @@ int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t 
   return PPGAT_OK;
 }
 
+int ppgat_serve_topk_workspace_bytes(int64_t n_items, int channels, int n_users, size_t* bytes) {
+  if (!bytes || n_items < 1 || n_users < 0) return fail(PPGAT_ERR_INVALID, "serve_topk_workspace_bytes: bad sizes");
+  if (channels != 64 && channels != 128 && channels != 256) return fail(PPGAT_ERR_UNSUPPORTED, "serve_topk: channels");
+  *bytes = align_up((size_t)n_users * channels * 4) + align_up((size_t)n_users * n_items * 4);
+  return PPGAT_OK;
+}
+
+int ppgat_serve_topk(const float* item_vecs, int64_t n_items, int channels, const int64_t* hist_ptr,
+                     const int64_t* hist_items, int64_t max_hist, int n_users, int k, int32_t* out_idx,
+                     float* out_score, void* workspace, size_t workspace_bytes, void* stream) {
+  if (channels != 64 && channels != 128 && channels != 256) return fail(PPGAT_ERR_UNSUPPORTED, "serve_topk: channels");
+  if (k < 1 || k > ppgat::knn_max_k() || k > n_items) return fail(PPGAT_ERR_UNSUPPORTED, "serve_topk: 1 <= k <= 64");
+  if (n_items < 1 || n_items > INT32_MAX || n_users < 0 || n_users > 256 || max_hist < 0)
+    return fail(PPGAT_ERR_INVALID, "serve_topk: bad sizes (n_users <= 256 per call)");
+  if (n_users > 0 && (!item_vecs || !hist_ptr || !out_idx || !out_score || (max_hist > 0 && !hist_items)))
+    return fail(PPGAT_ERR_INVALID, "serve_topk: null pointer");
+  size_t need = 0;
+  ppgat_serve_topk_workspace_bytes(n_items, channels, n_users, &need);
+  if (!workspace || workspace_bytes < need) return fail(PPGAT_ERR_INVALID, "serve_topk: workspace too small");
+  float* U = static_cast<float*>(workspace);
+  float* scores = reinterpret_cast<float*>(static_cast<char*>(workspace) + align_up((size_t)n_users * channels * 4));
+  hipError_t e = ppgat::serve_topk(item_vecs, n_items, channels, hist_ptr, hist_items, max_hist, n_users, k, U, scores,
+                                   out_idx, out_score, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "serve_topk");
+  return PPGAT_OK;
+}
+
 int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
                      int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
                      const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,

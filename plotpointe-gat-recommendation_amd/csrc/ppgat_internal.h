@@ -124,6 +124,9 @@ hipError_t eval_sample(const int64_t* ptr, const int32_t* items_sorted, const in
                        hipStream_t st);
 
 // evaluation (ppgat_eval.hip)
+hipError_t serve_topk(const float* iv, int64_t n_items, int C, const int64_t* hptr, const int64_t* hist,
+                      int64_t max_hist, int B, int k, float* U, float* scores, int32_t* out_idx, float* out_score,
+                      hipStream_t st);
 hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                         const int64_t* users, const int64_t* cands, int64_t B, int64_t K1, int32_t* rank,
                         hipStream_t st);

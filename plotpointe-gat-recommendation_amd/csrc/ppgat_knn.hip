@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) k_knn_topk(const float* __restrict__ S, i
     }
     cnt += bv >= min_sim ? 1 : 0;  // sorted descending: the kept entries are a prefix
   }
-  if (lane == 0) out_cnt[r] = cnt;
+  if (lane == 0 && out_cnt != nullptr) out_cnt[r] = cnt;
 }
 
 }  // namespace

@@ -103,6 +103,47 @@ def node_maps_from_interactions(interactions) -> dict:
     }
 
 
+def build_ui_edges(interactions):
+    """graphs/build_ui_edges.py:50-85 without the GCS I/O: first-appearance node ids
+    (``node_maps_from_interactions``) and the user x item COO matrix of rating weights
+    (r - 1) / 4 (1.0 where there is no rating column), float32, one entry per interaction in
+    row order.  Returns (scipy.sparse.coo_matrix, node_maps)."""
+    from scipy.sparse import coo_matrix
+    maps = node_maps_from_interactions(interactions)
+    u2i = {k: v for k, v in maps["user_to_idx"].items()}
+    i2i = {k: v for k, v in maps["item_to_idx"].items()}
+    users = interactions["user_id"].astype(str).map(u2i).to_numpy()
+    items = interactions["asin"].astype(str).map(i2i).to_numpy()
+    if "rating" in interactions.columns:
+        values = (interactions["rating"].to_numpy() - 1.0) / 4.0
+    else:
+        values = np.ones(len(interactions), dtype=np.float32)
+    ui = coo_matrix((values.astype(np.float32), (users, items)), shape=(maps["n_users"], maps["n_items"]),
+                    dtype=np.float32)
+    return ui, maps
+
+
+def save_ui_edges(path, ui) -> None:
+    """Write ``ui_edges.npz`` exactly as graphs/build_ui_edges.py:84-85 (scipy.sparse.save_npz
+    of the COO matrix)."""
+    from scipy.sparse import save_npz
+    save_npz(str(path), ui)
+
+
+def load_ui_edges(path):
+    """Read a ``ui_edges.npz`` (scipy.sparse npz, no pickles): -> (users int64, items int64,
+    weights float32, (n_users, n_items)) in stored entry order."""
+    from scipy.sparse import load_npz
+    m = load_npz(str(path)).tocoo()
+    return (m.row.astype(np.int64), m.col.astype(np.int64), m.data.astype(np.float32), tuple(int(v) for v in m.shape))
+
+
+def edge_index_from_ui_edges(users: np.ndarray, items: np.ndarray, n_users: int) -> np.ndarray:
+    """The homogeneous message edge_index of a U-I COO (u -> n_users + i, n_users + i -> u per
+    entry, the column order of train_gat_pyg.py:141-146 for entries in user order)."""
+    return edge_index_numpy(n_users, users, items)
+
+
 def map_splits_to_index(train_pos_raw, val_pos_raw, test_pos_raw, user_to_idx, item_to_idx):
     """Raw-id -> index mapping exactly as scripts/train_gat_pyg.py:272-288."""
     train_pos_idx: Dict[int, np.ndarray] = {}

@@ -11,8 +11,9 @@
   evaluation is two kernels and one copy of the ranks; ``fast=True`` draws the same
   distribution with vectorised numpy (different stream).
 * ``export_item_embeddings`` -- tools/export_item_embeddings.py:139-145.
-* ``top_k_for_user_items``   -- serving/runtime.py:56-76 on the device (torch.topk);
-  same rule: user vector = mean of history rows, history masked to -1e9.
+* ``top_k_for_user_items`` / ``top_k_batch`` -- serving/runtime.py:56-76 on the device
+  (``ppgat_serve_topk``): user vector = mean of history rows, history masked to -1e9,
+  the k best descending with ties by smaller item index.
 """
 from __future__ import annotations
 
@@ -125,13 +126,41 @@ def export_item_embeddings(model, item_feats: torch.Tensor, edge_index: torch.Te
         return Z[model.n_users:].detach().cpu().numpy().astype(np.float32)
 
 
+def top_k_batch(item_vecs: torch.Tensor, histories: Sequence[Sequence[int]], k: int = 20):
+    """serving/runtime.py:56-76 for a batch of users on the device (ppgat_serve_topk): per
+    history, the mean of its rows, scores over every item, the history masked to -1e9, the
+    k best descending (ties by smaller index).  Returns (indices [B, k] int64, scores [B, k])."""
+    lib = _lib.load()
+    if not item_vecs.is_cuda or item_vecs.dtype != torch.float32:
+        raise RuntimeError("top_k_batch: fp32 ROCm item vectors required (no CPU path)")
+    iv = item_vecs.contiguous()
+    n_items, C = iv.shape
+    dev = iv.device
+    idx_out, sc_out = [], []
+    for b0 in range(0, len(histories), 256):
+        chunk = histories[b0:b0 + 256]
+        for h in chunk:
+            assert len(h) > 0, "Need at least one item id from user history"
+        lens = np.array([len(h) for h in chunk], np.int64)
+        ptr = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)])).to(dev)
+        hist = torch.from_numpy(np.concatenate([np.asarray(h, np.int64) for h in chunk])).to(dev)
+        B = len(chunk)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_serve_topk_workspace_bytes(n_items, C, B, ctypes.byref(nbytes)), "serve_topk_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        oi = torch.empty(B, k, dtype=torch.int32, device=dev)
+        os_ = torch.empty(B, k, dtype=torch.float32, device=dev)
+        _lib.check(lib.ppgat_serve_topk(iv.data_ptr(), n_items, C, ptr.data_ptr(), hist.data_ptr(), int(lens.max()), B,
+                                        int(k), oi.data_ptr(), os_.data_ptr(), ws.data_ptr(), nbytes.value,
+                                        _lib.stream_handle(dev)), "serve_topk")
+        idx_out.append(oi.long())
+        sc_out.append(os_)
+    return torch.cat(idx_out), torch.cat(sc_out)
+
+
 def top_k_for_user_items(item_vecs: torch.Tensor, item_ids, k: int = 20):
     """serving/runtime.py:56-76 on the device: (indices, scores) of the top-k items for the
-    mean of the history rows, history excluded, descending."""
+    mean of the history rows, history excluded, descending (ppgat_serve_topk)."""
     assert len(item_ids) > 0, "Need at least one item id from user history"
-    ids = torch.as_tensor(np.asarray(item_ids, dtype=np.int64), device=item_vecs.device)
-    user_vec = item_vecs[ids].mean(0)
-    scores = item_vecs @ user_vec
-    scores[ids] = -1e9
-    top = torch.topk(scores, k)
-    return top.indices.cpu().numpy(), top.values.cpu().numpy()
+    idx, sc = top_k_batch(item_vecs, [list(item_ids)], k)
+    return idx[0].cpu().numpy(), sc[0].cpu().numpy()

@@ -90,3 +90,31 @@ def test_vectorised_synthetic_graph_stats(pkg):
     # no duplicate (user, item) pairs
     key = ei[0, 0::2] * g.n_items + (ei[1, 0::2] - g.n_users)
     assert len(np.unique(key)) == len(key)
+
+
+def test_ui_edges_npz_roundtrip_and_reference_format(pkg, tmp_path):
+    """ui_edges.npz (graphs/build_ui_edges.py:50-85): the COO the reference builds -- rows are
+    first-appearance user ids, columns first-appearance item ids, data (rating - 1) / 4 as
+    float32 -- written with scipy's save_npz and read back without pickles."""
+    import scipy.sparse as sp
+    d = pkg.data
+    inter = d.synthetic_interactions_small(seed=0)
+    ui, maps = d.build_ui_edges(inter)
+    assert ui.shape == (maps["n_users"], maps["n_items"]) and ui.nnz == len(inter)
+    # restated independently: the reference's mapping + weight rule
+    uids = {u: k for k, u in enumerate(inter["user_id"].unique())}
+    iids = {a: k for k, a in enumerate(inter["asin"].unique())}
+    assert np.array_equal(ui.row, inter["user_id"].map(uids).to_numpy())
+    assert np.array_equal(ui.col, inter["asin"].map(iids).to_numpy())
+    assert np.array_equal(ui.data, ((inter["rating"].to_numpy() - 1.0) / 4.0).astype(np.float32))
+    path = tmp_path / "ui_edges.npz"
+    d.save_ui_edges(path, ui)
+    m = sp.load_npz(str(path))  # the format scipy (and the reference) reads
+    assert m.format == "coo" and m.dtype == np.float32
+    u, i, w, shape = d.load_ui_edges(path)
+    assert shape == ui.shape
+    assert np.array_equal(u, ui.row) and np.array_equal(i, ui.col) and np.array_equal(w, ui.data)
+    with np.load(path, allow_pickle=False) as z:  # a plain npz of arrays
+        assert set(z.files) >= {"row", "col", "data", "shape", "format"}
+    ei = d.edge_index_from_ui_edges(u, i, shape[0])
+    assert ei.shape == (2, 2 * len(u)) and np.array_equal(ei[0, 0::2], u) and np.array_equal(ei[1, 0::2], i + shape[0])

@@ -65,6 +65,31 @@ def test_serving_topk_matches_oracle(pkg, oracle, cuda):
         assert np.allclose(sc, rsc, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("C", [64, 128, 256])
+def test_serving_topk_batched_matches_oracle(pkg, oracle, cuda, C):
+    """ppgat_serve_topk over 300 histories (two launches of <= 256) on a 60k-item catalogue:
+    the top-20 of each equals serving/runtime.py's rule restated by the oracle (numpy float32);
+    a differing position counts as a near-tie only if the oracle's scores differ < 1e-6."""
+    rng = np.random.default_rng(C)
+    V = rng.standard_normal((60_000, C)).astype(np.float32)
+    hists = [rng.choice(60_000, int(rng.integers(1, 40)), replace=False).tolist() for _ in range(300)]
+    idx, sc = pkg.evaluation.top_k_batch(torch.from_numpy(V).to(cuda), hists, 20)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    near = 0
+    for b, h in enumerate(hists):
+        ridx, rsc = oracle.serving_topk(V, h, 20)
+        if np.array_equal(idx[b], ridx):
+            continue
+        uv = V[np.array(h)].mean(0)
+        s_ref = V.astype(np.float64) @ uv.astype(np.float64)
+        s_ref[np.array(h)] = -1e9
+        diff = idx[b] != ridx
+        assert np.all(np.abs(s_ref[idx[b][diff]] - s_ref[ridx[diff]]) < 1e-6 * np.abs(s_ref).max()), b
+        near += 1
+    assert near <= 3
+    assert np.all(np.diff(sc, axis=1) <= 0)
+
+
 def _write_cfg1_inputs(pkg, root):
     inter = pkg.data.synthetic_interactions_small(seed=0)
     maps = pkg.data.node_maps_from_interactions(inter)

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Halo exchange volume of the row-sharded partition (dist.build_halo_graph) for a config,
+computed on the host with the partition code itself (no GPU):
+
+    python tools/halo_stats.py --config 5 --world 8      # 200M-edge synthetic, d=256, heads=4
+    python tools/halo_stats.py --config 2 --world 8      # config 4 (config-2 graph)
+
+Per rank: own rows, halo rows received, rows sent, local (destination-owned) edges; bytes per
+layer and direction for the exchanged operand (x: C_in floats when H*C > C_in, else h)."""
+import argparse
+import importlib
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+pkg = importlib.import_module("plotpointe-gat-recommendation_amd")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=5)
+    ap.add_argument("--world", type=int, default=8)
+    args = ap.parse_args()
+    d = pkg.data
+    if args.config == 5:
+        g = d.synthetic_scaling_graph(1.0, seed=42)
+        row_bytes = 256 * 4  # x rows (H*C = 1024 > C_in = 256)
+    else:
+        g = d.synthetic_ui_graph(seed=42)
+        row_bytes = 128 * 4  # h rows (H*C = C_in)
+    N, nu, W = g.n_nodes, g.n_users, args.world
+    users = np.repeat(np.arange(nu, dtype=np.int64), np.diff(g.user_ptr))
+    items = g.user_items.astype(np.int64) + nu
+    # the U-I columns come in (u -> i, i -> u) pairs: each interaction is a message both ways
+    deg = np.bincount(users, minlength=N) * 2 + np.bincount(items, minlength=N) * 2 + 4.0
+    owner = np.empty(N, np.int32)
+    for a, b in ((0, nu), (nu, N)):
+        bnd = a + pkg.dist.partition_bounds(deg[a:b].astype(np.float64), W)
+        owner[a:b] = np.repeat(np.arange(W, dtype=np.int32), np.diff(bnd))
+    ou, oi = owner[users], owner[items]
+    out = []
+    for r in range(W):
+        own = int((owner == r).sum())
+        # edges homed at r: u -> i with owner(i) == r (sources: users), i -> u with owner(u) == r (sources: items)
+        m1 = oi == r
+        m2 = ou == r
+        halo_u = np.unique(users[m1 & (ou != r)])
+        halo_i = np.unique(items[m2 & (oi != r)])
+        # rows r sends: its users with an item elsewhere, its items with a user elsewhere (unique per peer)
+        s_u = np.unique(oi[(ou == r) & (oi != r)].astype(np.int64) * N + users[(ou == r) & (oi != r)]).size
+        s_i = np.unique(ou[(oi == r) & (ou != r)].astype(np.int64) * N + items[(oi == r) & (ou != r)]).size
+        n_halo = len(halo_u) + len(halo_i)
+        out.append({"rank": r, "own_rows": own, "halo_rows": n_halo, "sent_rows": s_u + s_i,
+                    "local_edges": int(m1.sum() + m2.sum()),
+                    "recv_GB_per_layer_dir": n_halo * row_bytes / 1e9, "send_GB_per_layer_dir": (s_u + s_i) * row_bytes / 1e9})
+        print(json.dumps(out[-1]), flush=True)
+    print(json.dumps({"config": args.config, "world": W, "nodes": N, "edges": 2 * len(users), "row_bytes": row_bytes,
+                      "max_recv_GB": max(o["recv_GB_per_layer_dir"] for o in out),
+                      "max_send_GB": max(o["send_GB_per_layer_dir"] for o in out),
+                      "max_local_edges": max(o["local_edges"] for o in out)}))
+
+
+if __name__ == "__main__":
+    main()
