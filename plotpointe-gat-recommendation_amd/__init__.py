@@ -8,7 +8,7 @@ import it is also registered as ``ppgat_amd``.
 """
 import sys as _sys
 
-from . import _lib, data, dist, evaluation, fusion, knn, optim, sampler  # noqa: F401
+from . import _lib, data, dist, evaluation, fusion, knn, optim, sampler, torch_ops  # noqa: F401
 from .conv import GATConv, SimpleGATLayer  # noqa: F401
 from .hip_ops import CSRGraph, csr_build, gat_aggregate, graph_cache  # noqa: F401
 from .model import CustomGAT, PyGGAT, bpr_loss  # noqa: F401

@@ -299,6 +299,8 @@ class HaloGraph:
     local_of: np.ndarray        # [N] int64: node id -> own row, -1 elsewhere (host)
     owner: np.ndarray           # [N] int32 node owner (host)
     loss_plans: dict = None
+    bwd_sched_own: object = None   # backward schedule over the own source rows
+    bwd_sched_halo: object = None  # ... over the halo source rows (row ids relative to n_own)
 
     @property
     def R(self) -> int:
@@ -323,7 +325,7 @@ class HaloGraph:
         from .hip_ops import XViews
         f, b = self.fwd_view, self.bwd_view
         return XViews(self.n_own, self.R, f.n_fwd_edges, f.col, f.csr_eid, f.fwd_sched, b.row, b.csc_eid, b.dz_slot,
-                      b.bwd_sched)
+                      b.bwd_sched, self.bwd_sched_own, self.bwd_sched_halo)
 
 
 def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,
@@ -375,12 +377,16 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     row, csc_eid, slot = G.row[:El].contiguous(), orig(G.csc_eid[:El]), G.csc2csr[:El].contiguous()
     fwd_view = LocalView(n_own, rowptr_own, col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
     bwd_view = LocalView(R, G.rowptr.contiguous(), col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
+    hg = HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan, fwd_view, bwd_view, local_of, owner, {})
     if sched_builder is not None:
         fwd_view.fwd_sched = sched_builder(rowptr_own, El)
         bwd_view.bwd_sched = sched_builder(bwd_view.colptr, El)
         bwd_view.fwd_sched = fwd_view.fwd_sched
-    return HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan, fwd_view, bwd_view, local_of, owner,
-                     {})
+        # the backward edge pass split by source class: halo sources first (their input
+        # gradients go back to their owners while the own sources are processed)
+        hg.bwd_sched_own = sched_builder(bwd_view.colptr[:n_own + 1].contiguous(), El)
+        hg.bwd_sched_halo = sched_builder(bwd_view.colptr[n_own:].contiguous(), El)
+    return hg
 
 
 # ---------------------------------------------------------------------------
@@ -426,6 +432,70 @@ class _LocalGAT(torch.autograd.Function):
                                       seed_buf=ctx.seed_buf)
         datt_src, datt_dst = st.bwd_epilogue(hg.bwd_view, h, a_s, a_d, ds_src, dz, grad_h, heads, C)
         return (grad_h, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                None, None, None, None, None, None, None, None)
+
+
+_COMM_STREAMS = {}
+
+
+def _comm_stream(dev) -> torch.cuda.Stream:
+    s = _COMM_STREAMS.get(dev.index)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _COMM_STREAMS[dev.index] = s
+    return s
+
+
+class _HaloLayerX(torch.autograd.Function):
+    """One multi-head layer on the halo partition, aggregate-then-transform (hip_ops.xgat_*):
+    forward = all_to_all of the halo rows of x, then the layer over [own | halo] sources;
+    backward = the halo sources' edge pass first, their input gradients sent back to the
+    owners on a communication stream (RCCL all_to_all) while the own sources' edge pass and
+    the weight-gradient GEMMs run, then the owners add the returned rows in peer order."""
+
+    @staticmethod
+    def forward(ctx, x_own, weight, att_src, att_dst, bias, hg: "HaloGraph", comm: "Comm", stages, heads: int,
+                C: int, slope: float, p: float, seed: int):
+        from .hip_ops import xgat_forward
+        plan = hg.plan
+        x_own = x_own.contiguous()
+        x_loc = torch.empty((plan.n_own + plan.n_recv, x_own.size(1)), dtype=x_own.dtype, device=x_own.device)
+        x_loc[:plan.n_own].copy_(x_own)
+        comm.all_to_all_rows(stages.gather_rows(x_own, plan.send_idx), plan.send_counts, plan.recv_counts,
+                             out=x_loc[plan.n_own:])
+        out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed)
+        ctx.hg, ctx.comm, ctx.stages = hg, comm, stages
+        ctx.att_shapes = (att_src.shape, att_dst.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .hip_ops import xgat_backward
+        hg, comm, st = ctx.hg, ctx.comm, ctx.stages
+        plan = hg.plan
+        dev = g.device
+        pending = {}
+
+        def send_back(dx_halo):
+            if comm.backend != "nccl" or not comm.active:
+                pending["ret"] = comm.all_to_all_rows(dx_halo, plan.recv_counts, plan.send_counts)
+                return
+            main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
+            cs.wait_stream(main)
+            dx_halo.record_stream(cs)
+            with torch.cuda.stream(cs):
+                pending["ret"] = comm.all_to_all_rows(dx_halo, plan.recv_counts, plan.send_counts)
+            pending["stream"] = cs
+
+        dx, dW, datt_src, datt_dst, dbias = xgat_backward(ctx.saved, g, ctx.needs_input_grad[4], halo_hook=send_back)
+        ctx.saved = None
+        dx_own = dx[:plan.n_own]
+        if "stream" in pending:
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(pending["stream"])
+            pending["ret"].record_stream(main)
+        st.return_add(dx_own, pending["ret"], plan.ret_ptr, plan.ret_pos)
+        return (dx_own, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
                 None, None, None, None, None, None, None, None)
 
 
@@ -514,13 +584,14 @@ class HaloPyGGAT(_ShardedBase):
             p = float(conv.dropout) if self.training else 0.0
             seed = self.layer_seed(conv)
             if self.exchanges_input(conv):
-                x_loc = exchange(x, hg.plan, self.comm, self.stages)
-                gat_x = getattr(self.stages, "gat_x", None)
-                out = gat_x(x_loc, conv, hg.xviews(), p, seed) if gat_x is not None else None
-                if out is not None:  # aggregate-then-transform on the local rows (no halo projection)
-                    x = out
+                if getattr(self.stages, "supports_x", lambda c: False)(conv):
+                    # aggregate-then-transform on the local rows: no halo projection, the
+                    # return of the halo gradients overlapped with the own rows' backward
+                    x = _HaloLayerX.apply(x, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg, self.comm,
+                                          self.stages, conv.heads, conv.out_channels, float(conv.negative_slope), p,
+                                          seed)
                     continue
-                h = self.stages.linear(x_loc, conv.lin.weight, None)
+                h = self.stages.linear(exchange(x, hg.plan, self.comm, self.stages), conv.lin.weight, None)
             else:
                 h = exchange(self.stages.linear(x, conv.lin.weight, None), hg.plan, self.comm, self.stages)
             x = _LocalGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, hg, self.stages, conv.heads,

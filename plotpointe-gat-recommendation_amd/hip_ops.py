@@ -754,6 +754,8 @@ class XViews:
     csc_eid: torch.Tensor
     dz_slot: torch.Tensor
     bwd_sched: Schedule
+    bwd_sched_own: Optional[Schedule] = None   # sources [0, n_dst) (halo partition)
+    bwd_sched_halo: Optional[Schedule] = None  # sources [n_dst, n_src), rows relative to n_dst
 
     @staticmethod
     def of_graph(g: "CSRGraph") -> "XViews":
@@ -765,6 +767,117 @@ def xgat_supported(in_channels: int, heads: int, channels: int) -> bool:
     return bool(_lib.load().ppgat_xgat_supported(int(in_channels), int(heads), int(channels)))
 
 
+def _xgat_edges_bwd(lib, sched: Schedule, v: "XViews", base_row: int, x, s_src, nstate, gt, A, S, dz, dx, H, K,
+                    slope, p, seed, seed_buf, st):
+    """ppgat_xgat_bwd_edges over one source schedule whose rows start at base_row."""
+    dev = x.device
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_xgat_bwd_workspace_bytes(sched.n_hub_items, K, ctypes.byref(nbytes)), "xgat_ws")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    cs = sched.cstruct()
+    E = v.n_edges
+    _lib.check(lib.ppgat_xgat_bwd_edges(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                        _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None, E, K, H,
+                                        x.data_ptr() + 4 * base_row * K, K, s_src.data_ptr() + 4 * base_row * H,
+                                        nstate.data_ptr(), gt.data_ptr(), A.data_ptr(), float(slope), float(p),
+                                        int(seed) & (2**64 - 1), _lib.ptr(seed_buf), dx.data_ptr() + 4 * base_row * K,
+                                        K, S.data_ptr() + 4 * base_row * 2 * H, 2 * H, dz.data_ptr(), ws.data_ptr(),
+                                        nbytes.value, st), "xgat_bwd_edges")
+
+
+def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
+                 seed: int):
+    """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state)."""
+    lib = _lib.load()
+    x = x.contiguous()
+    dev = x.device
+    K = x.size(1)
+    H = heads
+    _require(x.size(0) == v.n_src, f"x has {x.size(0)} rows, the edge lists {v.n_src} sources")
+    W = weight.detach().contiguous()
+    a_s = att_src.detach().reshape(H, C).contiguous()
+    a_d = att_dst.detach().reshape(H, C).contiguous()
+    b = bias.detach().contiguous() if bias is not None else None
+    st = _lib.stream_handle(dev)
+    A = torch.empty(2, H, K, dtype=torch.float32, device=dev)
+    Wt = torch.empty(H * K, C, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), H, C, K, A.data_ptr(),
+                                      Wt.data_ptr(), None, st), "xgat_weights")
+    s_src = torch.empty(v.n_src, H, dtype=torch.float32, device=dev)
+    s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_src, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
+                                     s_dst.data_ptr(), st), "xgat_scores")
+    agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
+    m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
+    inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
+    seed_buf = seed_buffer(p, dev)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_xgat_fwd_workspace_bytes(v.fwd_sched.n_hub_items, H, K, ctypes.byref(nbytes)), "xgat_ws")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    cs = v.fwd_sched.cstruct()
+    E = v.n_edges
+    _lib.check(lib.ppgat_xgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
+                                  _lib.ptr(v.csr_eid) if E else None, v.n_dst, E, K, H, x.data_ptr(), K,
+                                  s_src.data_ptr(), s_dst.data_ptr(), float(slope), float(p),
+                                  int(seed) & (2**64 - 1), _lib.ptr(seed_buf), agg.data_ptr(), m.data_ptr(),
+                                  inv_l.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_fwd")
+    out = gemm_nn(agg.view(v.n_dst, H * K), Wt, 0, C, alpha=1.0 / H, bias=b)
+    saved = dict(x=x, W=W, a_s=a_s, a_d=a_d, A=A, s_src=s_src, s_dst=s_dst, agg=agg, m=m, inv_l=inv_l,
+                 seed_buf=seed_buf, v=v, meta=(H, C, K, slope, p, seed, bias is not None))
+    return out, saved
+
+
+def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=None):
+    """Backward of the aggregate-then-transform layer -> (dx [n_src, C_in], dW, datt_src [H, C],
+    datt_dst [H, C], dbias).  With ``halo_hook`` and a view split into own sources [0, n_own)
+    and halo sources (XViews.bwd_sched_own / bwd_sched_halo), the halo rows' input gradients
+    are finished first and handed to halo_hook(dx_halo) -- which starts returning them to
+    their owners -- before the own rows' edge pass and the weight-gradient GEMMs run."""
+    lib = _lib.load()
+    x, W, a_s, a_d, A = saved["x"], saved["W"], saved["a_s"], saved["a_d"], saved["A"]
+    s_src, s_dst, agg, m, inv_l, v = saved["s_src"], saved["s_dst"], saved["agg"], saved["m"], saved["inv_l"], saved["v"]
+    H, C, K, slope, p, seed, has_bias = saved["meta"]
+    dev = x.device
+    st = _lib.stream_handle(dev)
+    g = g.contiguous()
+    Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
+               "xgat_weights")
+    gt = gemm_nn(g, Wg, 0, H * K)
+    nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_bwd_prologue(gt.data_ptr(), agg.data_ptr(), s_dst.data_ptr(), m.data_ptr(),
+                                           inv_l.data_ptr(), v.n_dst, K, H, nstate.data_ptr(), st), "xgat_bwd_prologue")
+    E = v.n_edges
+    S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
+    dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
+    args = (x, s_src, nstate, gt, A, S, dz, dx, H, K, slope, p, seed, saved["seed_buf"], st)
+    if halo_hook is not None and v.bwd_sched_halo is not None:
+        _xgat_edges_bwd(lib, v.bwd_sched_halo, v, v.n_dst, *args)
+        halo_hook(dx[v.n_dst:])
+        _xgat_edges_bwd(lib, v.bwd_sched_own, v, 0, *args)
+    else:
+        _xgat_edges_bwd(lib, v.bwd_sched, v, 0, *args)
+        if halo_hook is not None:
+            halo_hook(dx[v.n_dst:])
+    fs = v.fwd_sched.cstruct()
+    dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
+                                     dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
+    _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
+               "xgat_bwd_epilogue")
+    GV = gemm_tn(S, x)[0]
+    G = gemm_tn_big(g, agg.view(v.n_dst, H * K))
+    dW = torch.empty_like(W)
+    datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)
+    datt_dst = torch.empty(H, C, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_weight_grads(G.data_ptr(), GV.data_ptr(), W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(),
+                                           H, C, K, dW.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(), st),
+               "xgat_weight_grads")
+    dbias = colsum(g) if (has_bias and want_bias_grad) else None
+    return dx, dW, datt_src, datt_dst, dbias
+
+
 class GATLayerX(torch.autograd.Function):
     """x [n_src, C_in] -> out [n_dst, C]: GATConv with H heads in the aggregate-then-transform
     form (include/ppgat.h ppgat_xgat_*): the edge pass gathers x_j once per edge for all heads,
@@ -772,95 +885,16 @@ class GATLayerX(torch.autograd.Function):
     (GEMM), one edge pass by source, dW = g^T agg (TN GEMM) + attention terms."""
 
     @staticmethod
-    def forward(ctx, x, weight, att_src, att_dst, bias, v: XViews, heads: int, C: int, slope: float, p: float,
+    def forward(ctx, x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
                 seed: int):
-        lib = _lib.load()
-        x = x.contiguous()
-        dev = x.device
-        K = x.size(1)
-        H = heads
-        _require(x.size(0) == v.n_src, f"x has {x.size(0)} rows, the edge lists {v.n_src} sources")
-        W = weight.detach().contiguous()
-        a_s = att_src.detach().reshape(H, C).contiguous()
-        a_d = att_dst.detach().reshape(H, C).contiguous()
-        b = bias.detach().contiguous() if bias is not None else None
-        st = _lib.stream_handle(dev)
-        A = torch.empty(2, H, K, dtype=torch.float32, device=dev)
-        Wt = torch.empty(H * K, C, dtype=torch.float32, device=dev)
-        _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), H, C, K, A.data_ptr(),
-                                          Wt.data_ptr(), None, st), "xgat_weights")
-        s_src = torch.empty(v.n_src, H, dtype=torch.float32, device=dev)
-        s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
-        _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_src, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
-                                         s_dst.data_ptr(), st), "xgat_scores")
-        agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
-        m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
-        inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
-        seed_buf = seed_buffer(p, dev)
-        nbytes = ctypes.c_size_t(0)
-        _lib.check(lib.ppgat_xgat_fwd_workspace_bytes(v.fwd_sched.n_hub_items, H, K, ctypes.byref(nbytes)), "xgat_ws")
-        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
-        cs = v.fwd_sched.cstruct()
-        E = v.n_edges
-        _lib.check(lib.ppgat_xgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
-                                      _lib.ptr(v.csr_eid) if E else None, v.n_dst, E, K, H, x.data_ptr(), K,
-                                      s_src.data_ptr(), s_dst.data_ptr(), float(slope), float(p),
-                                      int(seed) & (2**64 - 1), _lib.ptr(seed_buf), agg.data_ptr(), m.data_ptr(),
-                                      inv_l.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_fwd")
-        out = gemm_nn(agg.view(v.n_dst, H * K), Wt, 0, C, alpha=1.0 / H, bias=b)
-        ctx.save_for_backward(x, W, a_s, a_d, A, s_src, s_dst, agg, m, inv_l)
-        ctx.v, ctx.seed_buf = v, seed_buf
-        ctx.meta = (H, C, K, slope, p, seed, bias is not None)
+        out, ctx.saved = xgat_forward(x, weight, att_src, att_dst, bias, v, heads, C, slope, p, seed)
         ctx.att_shapes = (att_src.shape, att_dst.shape)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        lib = _lib.load()
-        x, W, a_s, a_d, A, s_src, s_dst, agg, m, inv_l = ctx.saved_tensors
-        H, C, K, slope, p, seed, has_bias = ctx.meta
-        v = ctx.v
-        dev = x.device
-        st = _lib.stream_handle(dev)
-        g = g.contiguous()
-        Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
-        _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
-                   "xgat_weights")
-        gt = gemm_nn(g, Wg, 0, H * K)
-        nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
-        _lib.check(lib.ppgat_xgat_bwd_prologue(gt.data_ptr(), agg.data_ptr(), s_dst.data_ptr(), m.data_ptr(),
-                                               inv_l.data_ptr(), v.n_dst, K, H, nstate.data_ptr(), st),
-                   "xgat_bwd_prologue")
-        E = v.n_edges
-        S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
-        dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
-        dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
-        nbytes = ctypes.c_size_t(0)
-        _lib.check(lib.ppgat_xgat_bwd_workspace_bytes(v.bwd_sched.n_hub_items, K, ctypes.byref(nbytes)), "xgat_ws")
-        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
-        cs = v.bwd_sched.cstruct()
-        _lib.check(lib.ppgat_xgat_bwd_edges(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
-                                            _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None,
-                                            E, K, H, x.data_ptr(), K, s_src.data_ptr(), nstate.data_ptr(),
-                                            gt.data_ptr(), A.data_ptr(), float(slope), float(p),
-                                            int(seed) & (2**64 - 1), _lib.ptr(ctx.seed_buf), dx.data_ptr(), K,
-                                            S.data_ptr(), 2 * H, dz.data_ptr(), ws.data_ptr(), nbytes.value, st),
-                   "xgat_bwd_edges")
-        fs = v.fwd_sched.cstruct()
-        dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
-        _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
-                                         dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
-        _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
-                   "xgat_bwd_epilogue")
-        GV = gemm_tn(S, x)[0]
-        G = gemm_tn_big(g, agg.view(v.n_dst, H * K))
-        dW = torch.empty_like(W)
-        datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)
-        datt_dst = torch.empty(H, C, dtype=torch.float32, device=dev)
-        _lib.check(lib.ppgat_xgat_weight_grads(G.data_ptr(), GV.data_ptr(), W.data_ptr(), a_s.data_ptr(),
-                                               a_d.data_ptr(), H, C, K, dW.data_ptr(), datt_src.data_ptr(),
-                                               datt_dst.data_ptr(), st), "xgat_weight_grads")
-        dbias = colsum(g) if (has_bias and ctx.needs_input_grad[4]) else None
+        dx, dW, datt_src, datt_dst, dbias = xgat_backward(ctx.saved, g, ctx.needs_input_grad[4])
+        ctx.saved = None
         return (dx, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
                 None, None, None, None, None, None)
 
@@ -989,13 +1023,9 @@ class HipStages:
     def seed_buffer(self, p, device):
         return seed_buffer(p, device)
 
-    def gat_x(self, x_loc, conv, views, p, seed):
-        """The aggregate-then-transform layer over a rank's local edge lists, or None when the
-        shape is not supported (the caller then projects and runs the staged layer)."""
-        if not (conv.heads > 1 and xgat_supported(conv.in_channels, conv.heads, conv.out_channels)):
-            return None
-        return gat_layer_x(x_loc, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, views, conv.heads,
-                           conv.out_channels, float(conv.negative_slope), p, seed)
+    def supports_x(self, conv) -> bool:
+        """Whether the aggregate-then-transform kernels take this layer (dist.HaloPyGGAT)."""
+        return conv.heads > 1 and xgat_supported(conv.in_channels, conv.heads, conv.out_channels)
 
     def gather_rows(self, t, idx):
         """t[idx] (the all_to_all send buffer) through ppgat_rows_gather."""
