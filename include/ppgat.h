@@ -409,6 +409,25 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
                      const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
                      void* stream);
 
+/* ---- fusion MLP training: InfoNCE loss and backward, ReLU + dropout -----------------------
+ * Replaces: contrastive_fusion_loss + its autograd backward, embeddings/fuse_modal.py:39-72
+ *           (called by the training loop :179-214), and the ReLU/Dropout(0.1) of FusionMLP.mlp
+ *           (:27-29) in train mode.  The Linear layers around them run on ppgat_gemm_nn /
+ *           ppgat_gemm_tn_big / ppgat_colsum.
+ * ppgat_infonce: F = fused, T = txt_proj(txt), I = img_proj(img), each [B, D] (D = 128,
+ *   B <= 4096).  Fn, Tn, In = rows / max(||row||, 1e-12) (F.normalize); S_t = Fn Tn^T / tau,
+ *   S_i = Fn In^T / tau; loss_t = mean_b CE(S_t[b], b), loss_i likewise.
+ *   loss[3] = {(loss_t + loss_i) / 2, loss_t, loss_i} (device); dF, dT, dI = d loss / d(F, T, I).
+ *   Fixed-order reductions (deterministic).  Workspace queried first.
+ * ppgat_relu_dropout: backward 0: a = relu(z) * mask; backward 1: a <- a * mask * [z > 0] in place
+ *   (a holds dL/da on entry).  mask = 0 with probability p, else 1 / (1 - p), from a counter hash
+ *   of (seed, element index) -- the same draw forward and backward; p = 0 is plain ReLU. */
+int ppgat_infonce_workspace_bytes(int64_t batch, int dim, size_t* bytes);
+int ppgat_infonce(const float* fused, const float* txt_p, const float* img_p, int64_t batch, int dim, float tau,
+                  float* loss, float* d_fused, float* d_txt_p, float* d_img_p, void* workspace, size_t workspace_bytes,
+                  void* stream);
+int ppgat_relu_dropout(const float* z, int64_t n, float p, uint64_t seed, int backward, float* a, void* stream);
+
 /* ---- fp32 matrix-core GEMMs (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains) ---------------
  * Replaces: the hipBLAS/cuBLAS GEMMs of torch.nn.Linear in GATConv.lin at shapes past the fused
  *           128-column projection (config 5: lin 256 -> 1024, train_gat_pyg.py:77) and of
@@ -489,7 +508,8 @@ int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, con
 #define PPGAT_K_PROJ 10
 #define PPGAT_K_ADAM 11
 #define PPGAT_K_SAMPLE 12
-#define PPGAT_K_COUNT 13
+#define PPGAT_K_INFONCE 13
+#define PPGAT_K_COUNT 14
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

@@ -92,6 +92,9 @@ SIGNATURES = {
     "ppgat_serve_topk": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),
+    "ppgat_infonce_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_infonce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_relu_dropout": (c_int, [c_vp, c_i64, c_f, c_u64, c_int, c_vp, c_vp]),
     "ppgat_gemm_nn_supported": (c_int, [c_i64, c_int, c_int, c_int]),
     "ppgat_gemm_nn": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_int, c_f, c_vp, c_vp, c_i64, c_vp]),
     "ppgat_gemm_tn_big_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
@@ -117,7 +120,7 @@ SIGNATURES = {
 
 KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6, "sched": 7,
            "gemm_tn": 8, "fusion": 9, "proj": 10, "adam": 11,
-           "sample": 12}
+           "sample": 12, "infonce": 13}
 MODE_PYG, MODE_CUSTOM = 0, 1
 
 _lib = None

@@ -754,6 +754,41 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
   return PPGAT_OK;
 }
 
+int ppgat_infonce_workspace_bytes(int64_t batch, int dim, size_t* bytes) {
+  if (!bytes || !ppgat::infonce_shape_ok(batch, dim))
+    return fail(PPGAT_ERR_UNSUPPORTED, "infonce: needs dim 128 and 1 <= batch <= 4096");
+  *bytes = ppgat::infonce_workspace_bytes(batch);
+  return PPGAT_OK;
+}
+
+int ppgat_infonce(const float* fused, const float* txt_p, const float* img_p, int64_t batch, int dim, float tau,
+                  float* loss, float* d_fused, float* d_txt_p, float* d_img_p, void* workspace, size_t workspace_bytes,
+                  void* stream) {
+  if (!ppgat::infonce_shape_ok(batch, dim))
+    return fail(PPGAT_ERR_UNSUPPORTED, "infonce: needs dim 128 and 1 <= batch <= 4096");
+  if (!(tau > 0.f)) return fail(PPGAT_ERR_INVALID, "infonce: tau must be > 0");
+  if (!fused || !txt_p || !img_p || !loss || !d_fused || !d_txt_p || !d_img_p)
+    return fail(PPGAT_ERR_INVALID, "infonce: null pointer");
+  if (!al16(fused) || !al16(txt_p) || !al16(img_p) || !al16(d_fused) || !al16(d_txt_p) || !al16(d_img_p))
+    return fail(PPGAT_ERR_UNSUPPORTED, "infonce: 16-byte aligned rows");
+  if (!workspace || workspace_bytes < ppgat::infonce_workspace_bytes(batch))
+    return fail(PPGAT_ERR_INVALID, "infonce: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_INFONCE, st);
+  hipError_t e = ppgat::infonce(fused, txt_p, img_p, batch, tau, loss, d_fused, d_txt_p, d_img_p, workspace, st);
+  if (e != hipSuccess) return hip_fail(e, "infonce");
+  return PPGAT_OK;
+}
+
+int ppgat_relu_dropout(const float* z, int64_t n, float p, uint64_t seed, int backward, float* a, void* stream) {
+  if (n < 0 || !(p >= 0.f && p < 1.f) || (backward != 0 && backward != 1))
+    return fail(PPGAT_ERR_INVALID, "relu_dropout: n >= 0, 0 <= p < 1, backward 0 or 1");
+  if (n > 0 && (!z || !a)) return fail(PPGAT_ERR_INVALID, "relu_dropout: null pointer");
+  hipError_t e = ppgat::relu_dropout(z, n, p, seed, backward, a, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "relu_dropout");
+  return PPGAT_OK;
+}
+
 // ---- fp32 matrix-core GEMMs and the aggregate-then-transform multi-head layer ----------
 int ppgat_gemm_nn_supported(int64_t m, int k, int n, int b_layout) {
   return ppgat::gemm_nn_shape_ok(m, k, n, b_layout) ? 1 : 0;

@@ -130,22 +130,32 @@ hipError_t serve_topk(const float* iv, int64_t n_items, int C, const int64_t* hp
   const int64_t ipb = 256 / (C / 4);
   int64_t gs = (n_items + ipb - 1) / ipb;
   if (gs > 2048) gs = 2048;
-  const size_t lds = (size_t)B * C * 4;
-  switch (C) {
-    case 64:
-      hipLaunchKernelGGL(k_user_mean<64>, dim3(gm), dim3(256), 0, st, iv, n_items, hptr, hist, (int64_t)B, U);
-      hipLaunchKernelGGL(k_serve_scores<64>, dim3((unsigned)gs), dim3(256), lds, st, iv, n_items, U, B, scores);
-      break;
-    case 128:
-      hipLaunchKernelGGL(k_user_mean<128>, dim3(gm), dim3(256), 0, st, iv, n_items, hptr, hist, (int64_t)B, U);
-      hipLaunchKernelGGL(k_serve_scores<128>, dim3((unsigned)gs), dim3(256), lds, st, iv, n_items, U, B, scores);
-      break;
-    case 256:
-      hipLaunchKernelGGL(k_user_mean<256>, dim3(gm), dim3(256), 0, st, iv, n_items, hptr, hist, (int64_t)B, U);
-      hipLaunchKernelGGL(k_serve_scores<256>, dim3((unsigned)gs), dim3(256), lds, st, iv, n_items, U, B, scores);
-      break;
-    default:
-      return hipErrorInvalidValue;
+  // the users' rows live in LDS: at most 64 KB per launch (256 users at C = 64, 64 at C = 256)
+  const int ub = 65536 / (C * 4);
+  for (int b0 = 0; b0 < B; b0 += ub) {
+    const int nb = B - b0 < ub ? B - b0 : ub;
+    const size_t lds = (size_t)nb * C * 4;
+    const float* Ub = U + (int64_t)b0 * C;
+    float* sb = scores + (int64_t)b0 * n_items;
+    switch (C) {
+      case 64:
+        if (b0 == 0)
+          hipLaunchKernelGGL(k_user_mean<64>, dim3(gm), dim3(256), 0, st, iv, n_items, hptr, hist, (int64_t)B, U);
+        hipLaunchKernelGGL(k_serve_scores<64>, dim3((unsigned)gs), dim3(256), lds, st, iv, n_items, Ub, nb, sb);
+        break;
+      case 128:
+        if (b0 == 0)
+          hipLaunchKernelGGL(k_user_mean<128>, dim3(gm), dim3(256), 0, st, iv, n_items, hptr, hist, (int64_t)B, U);
+        hipLaunchKernelGGL(k_serve_scores<128>, dim3((unsigned)gs), dim3(256), lds, st, iv, n_items, Ub, nb, sb);
+        break;
+      case 256:
+        if (b0 == 0)
+          hipLaunchKernelGGL(k_user_mean<256>, dim3(gm), dim3(256), 0, st, iv, n_items, hptr, hist, (int64_t)B, U);
+        hipLaunchKernelGGL(k_serve_scores<256>, dim3((unsigned)gs), dim3(256), lds, st, iv, n_items, Ub, nb, sb);
+        break;
+      default:
+        return hipErrorInvalidValue;
+    }
   }
   if (max_hist > 0)
     hipLaunchKernelGGL(k_mask_history, dim3((unsigned)((max_hist + 255) / 256), (unsigned)B), dim3(256), 0, st, hptr,

@@ -137,6 +137,13 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
                       int normalize, float* out, float* z1_out, hipStream_t st);
 
+// fusion MLP training: InfoNCE loss + backward, ReLU/dropout (ppgat_infonce.hip)
+bool infonce_shape_ok(int64_t B, int D);
+size_t infonce_workspace_bytes(int64_t B);
+hipError_t infonce(const float* F, const float* T, const float* I, int64_t B, float tau, float* loss, float* dF,
+                   float* dT, float* dI, void* ws, hipStream_t st);
+hipError_t relu_dropout(const float* z, int64_t n, float p, uint64_t seed, int backward, float* a, hipStream_t st);
+
 // aggregate-then-transform multi-head layer and fp32 MFMA GEMMs (ppgat_xform.hip)
 hipError_t seed_snapshot(uint64_t seed, uint64_t* out, hipStream_t st);
 bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode);

@@ -6,14 +6,21 @@ embeddings/fuse_modal.py.
                              Eval-mode forward runs the fused fp32-MFMA kernel
                              (``ppgat_fusion_fwd``); train-mode forward uses torch ops
                              (dropout needs torch's RNG stream to match the reference).
-``contrastive_fusion_loss`` -- :39-72 (InfoNCE, tau = 0.07, both modalities).
+``contrastive_fusion_loss`` -- :39-72 (InfoNCE, tau = 0.07, both modalities), torch autograd.
+``fusion_train_step``      -- the same forward + loss + backward on the device kernels: the four
+                             Linear layers on the fp32 matrix-core GEMMs (ppgat_gemm_nn, weight
+                             grads ppgat_gemm_tn_big + ppgat_colsum), ReLU/Dropout and its
+                             backward (ppgat_relu_dropout, counter-hash mask), InfoNCE loss and
+                             gradient (ppgat_infonce).  Writes .grad; the loss stays on the device.
 ``infer_fused_embeddings``  -- :220-244: all items, mean-image fallback for items without an
                              image, L2-normalised; the per-row host->device image copy loop
                              becomes an index gather inside the kernel.
-``train_fusion``            -- :167-214 training loop (Adam, contiguous batches).
+``train_fusion``            -- :167-214 training loop (Adam, contiguous batches); native step
+                             by default, ``native=False`` keeps the torch-autograd step.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, Optional
 
 import numpy as np
@@ -21,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from . import hip_ops
 
 
 def fusion_forward(txt: torch.Tensor, img: Optional[torch.Tensor], W1, b1, W2, b2, normalize: bool,
@@ -89,13 +97,107 @@ def contrastive_fusion_loss(fused, txt_emb, img_emb, temperature=0.07):
     return loss, loss_txt.item(), loss_img.item()
 
 
+def infonce(fused: torch.Tensor, txt_p: torch.Tensor, img_p: torch.Tensor, temperature: float = 0.07):
+    """contrastive_fusion_loss forward and gradient on the device (ppgat_infonce) ->
+    (loss [3] = {loss, loss_txt, loss_img}, d_fused, d_txt_p, d_img_p)."""
+    lib = _lib.load()
+    for name, t in (("fused", fused), ("txt_p", txt_p), ("img_p", img_p)):
+        if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.is_contiguous()):
+            raise RuntimeError(f"infonce: {name} must be a contiguous fp32 ROCm [B, D] tensor (no CPU path)")
+    B, D = fused.shape
+    if txt_p.shape != (B, D) or img_p.shape != (B, D):
+        raise ValueError("infonce: fused, txt_p, img_p must share [B, D]")
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_infonce_workspace_bytes(B, D, ctypes.byref(nbytes)), "infonce_workspace_bytes")
+    dev = fused.device
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    loss = torch.empty(3, dtype=torch.float32, device=dev)
+    dF, dT, dI = (torch.empty(B, D, dtype=torch.float32, device=dev) for _ in range(3))
+    _lib.check(lib.ppgat_infonce(fused.data_ptr(), txt_p.data_ptr(), img_p.data_ptr(), B, D, float(temperature),
+                                 loss.data_ptr(), dF.data_ptr(), dT.data_ptr(), dI.data_ptr(), ws.data_ptr(),
+                                 nbytes.value, _lib.stream_handle(dev)), "infonce")
+    return loss, dF, dT, dI
+
+
+def relu_dropout(z: torch.Tensor, p: float, seed: int, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Forward (grad None): relu(z) * mask.  Backward: grad * mask * [z > 0], in place on grad.
+    The mask is a counter hash of (seed, element) (ppgat_relu_dropout), identical both ways."""
+    lib = _lib.load()
+    if not (z.is_cuda and z.dtype == torch.float32 and z.is_contiguous()):
+        raise RuntimeError("relu_dropout: contiguous fp32 ROCm tensor required (no CPU path)")
+    out = torch.empty_like(z) if grad is None else grad
+    if grad is not None and (grad.shape != z.shape or not grad.is_contiguous()):
+        raise ValueError("relu_dropout: grad must be contiguous and shaped like z")
+    _lib.check(lib.ppgat_relu_dropout(z.data_ptr(), z.numel(), float(p), int(seed) & (2**64 - 1),
+                                      0 if grad is None else 1, out.data_ptr(), _lib.stream_handle(z.device)),
+               "relu_dropout")
+    return out
+
+
+def _accumulate(p: torch.Tensor, g: torch.Tensor):
+    if p.grad is None:
+        p.grad = g
+    else:
+        p.grad.add_(g)
+
+
+def fusion_train_step(model: FusionMLP, txt: torch.Tensor, img: torch.Tensor, seed: int = 0,
+                      temperature: float = 0.07) -> torch.Tensor:
+    """One forward + contrastive loss + backward of FusionMLP on the device kernels (the
+    reference's opt.zero_grad/forward/loss/backward, fuse_modal.py:185-193, minus the step).
+    Dropout p is model.mlp[2].p (0 in eval-equivalent checks), drawn from ``seed``.
+    Accumulates into each parameter's .grad and returns the device loss [3] =
+    {loss, loss_txt, loss_img}."""
+    if not txt.is_cuda:
+        raise RuntimeError("fusion_train_step runs on ROCm devices only; there is no CPU path")
+    txt, img = txt.contiguous(), img.contiguous()
+    l1, l2 = model.mlp[0], model.mlp[3]
+    p = float(model.mlp[2].p) if model.training else 0.0
+    W1, b1, W2, b2 = (t.detach() for t in (l1.weight, l1.bias, l2.weight, l2.bias))
+    Wt, bt, Wi, bi = (t.detach() for t in (model.txt_proj.weight, model.txt_proj.bias, model.img_proj.weight,
+                                             model.img_proj.bias))
+    x = torch.cat([txt, img], 1)
+    z1 = hip_ops.gemm_nn(x, W1, 1, W1.size(0), bias=b1)                 # [B, hidden]
+    a = relu_dropout(z1, p, seed)
+    fused = hip_ops.gemm_nn(a, W2, 1, W2.size(0), bias=b2)              # [B, out]
+    tp = hip_ops.gemm_nn(txt, Wt, 1, Wt.size(0), bias=bt)
+    ip = hip_ops.gemm_nn(img, Wi, 1, Wi.size(0), bias=bi)
+    loss, dF, dT, dI = infonce(fused, tp, ip, temperature)
+    dW2, db2, _ = hip_ops.gemm_tn(dF, a, want_colsum=True)
+    da = hip_ops.gemm_nn(dF, W2, 0, W2.size(1))                         # dF W2 [B, hidden]
+    dz = relu_dropout(z1, p, seed, grad=da)
+    dW1, db1, _ = hip_ops.gemm_tn(dz, x, want_colsum=True)
+    dWt, dbt, _ = hip_ops.gemm_tn(dT, txt, want_colsum=True)
+    dWi, dbi, _ = hip_ops.gemm_tn(dI, img, want_colsum=True)
+    for prm, g in ((l1.weight, dW1), (l1.bias, db1), (l2.weight, dW2), (l2.bias, db2), (model.txt_proj.weight, dWt),
+                   (model.txt_proj.bias, dbt), (model.img_proj.weight, dWi), (model.img_proj.bias, dbi)):
+        _accumulate(prm, g)
+    return loss
+
+
 def train_fusion(model: FusionMLP, txt_aligned: torch.Tensor, img_aligned: torch.Tensor, epochs: int = 5,
-                 batch_size: int = 512, lr: float = 1e-3):
-    """fuse_modal.py:167-214 (tensors already on the device)."""
+                 batch_size: int = 512, lr: float = 1e-3, native: bool = True, seed: int = 0):
+    """fuse_modal.py:167-214 (tensors already on the device).  The native path keeps the
+    per-batch losses on the device and reads them once per epoch (the reference's
+    loss.item() per batch is a host sync per step)."""
     opt = torch.optim.Adam(model.parameters(), lr=lr)
     model.train()
     history = []
+    step = 0
     for _ in range(epochs):
+        if native:
+            acc = torch.zeros(3, dtype=torch.float32, device=txt_aligned.device)
+            nb = 0
+            for i in range(0, len(txt_aligned), batch_size):
+                bt, bi = txt_aligned[i:i + batch_size], img_aligned[i:i + batch_size]
+                opt.zero_grad(set_to_none=True)
+                acc += fusion_train_step(model, bt, bi, seed=(seed * 1_000_003 + step) & (2**64 - 1))
+                opt.step()
+                nb += 1
+                step += 1
+            tot, tt, ti = (acc / nb).tolist()
+            history.append((tot, tt, ti))
+            continue
         tot = tt = ti = 0.0
         nb = 0
         for i in range(0, len(txt_aligned), batch_size):

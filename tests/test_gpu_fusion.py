@@ -79,3 +79,71 @@ def test_training_step_loss_and_grads_vs_reference(pkg, gold, cuda):
     assert abs(loss.item() - float(gold["loss"])) <= 1e-5 * float(gold["loss"])
     for k, p in m.named_parameters():
         assert rel(p.grad, gold["grad__" + k]) <= 1e-4, k
+
+
+def _golden_params(gold, cuda):
+    return {k[4:]: torch.from_numpy(v).to(cuda) for k, v in gold.items() if k.startswith("sd__")}
+
+
+def test_native_training_step_vs_reference_golden(pkg, gold, cuda):
+    """fusion_train_step (matrix-core GEMMs + ppgat_relu_dropout + ppgat_infonce) at dropout 0
+    on the golden batch: loss and every gradient vs the reference's own (fuse_modal.py:39-72
+    imported by make_golden.py).  Loss 1e-5 relative, gradients 1e-4 (fp32 sums over B)."""
+    m = _model(pkg, gold, cuda).train()
+    m.mlp[2].p = 0.0
+    t = torch.from_numpy(gold["txt"][:256]).to(cuda)
+    im = torch.from_numpy(gold["img"][:256]).to(cuda)
+    loss = pkg.fusion.fusion_train_step(m, t, im).cpu()
+    assert abs(float(loss[0]) - float(gold["loss"])) <= 1e-5 * float(gold["loss"])
+    assert abs(float(loss[1]) - float(gold["loss_txt"])) <= 1e-5 * float(gold["loss_txt"])
+    assert abs(float(loss[2]) - float(gold["loss_img"])) <= 1e-5 * float(gold["loss_img"])
+    for k, p in m.named_parameters():
+        assert rel(p.grad, gold["grad__" + k]) <= 1e-4, (k, rel(p.grad, gold["grad__" + k]))
+
+
+@pytest.mark.parametrize("B,p", [(512, 0.1), (44, 0.1), (1, 0.0), (1000, 0.3)])
+def test_native_training_step_vs_fp64_oracle(pkg, oracle, gold, cuda, B, p):
+    """Reference batch size 512, the ragged tail batch (300 = 256 + 44), a single row and a
+    larger batch, with dropout: vs the fp64 restatement given the kernel's own mask (the mask
+    itself is checked bit-exact against the numpy hash restatement)."""
+    m = _model(pkg, gold, cuda).train()
+    m.mlp[2].p = p
+    g = torch.Generator().manual_seed(B)
+    t = torch.randn(B, 384, generator=g)
+    im = torch.randn(B, 512, generator=g)
+    seed = 0xABCDEF + B
+    loss = pkg.fusion.fusion_train_step(m, t.to(cuda), im.to(cuda), seed=seed).cpu()
+    ones = torch.ones(B, 256, device=cuda)
+    mask_dev = pkg.fusion.relu_dropout(ones, p, seed).cpu()
+    mask = oracle.mlp_dropout_scale(seed, B * 256, p).reshape(B, 256)
+    assert np.array_equal(mask_dev.numpy(), mask)
+    if p > 0:
+        assert abs(float((mask == 0).mean()) - p) < 0.02 + 3.0 / np.sqrt(B * 256)
+    P = {k: v.detach().double().cpu().requires_grad_(True) for k, v in m.named_parameters()}
+    ref, rt, ri = oracle.fusion_train_loss(P, t.double(), im.double(), 0.07, torch.from_numpy(mask).double())
+    ref.backward()
+    assert abs(float(loss[0]) - float(ref)) <= 1e-5 * max(float(ref), 1e-3)
+    assert abs(float(loss[1]) - float(rt)) <= 1e-5 * max(float(rt), 1e-3)
+    assert abs(float(loss[2]) - float(ri)) <= 1e-5 * max(float(ri), 1e-3)
+    for k, prm in m.named_parameters():
+        assert rel(prm.grad, P[k].grad) <= 1e-4, (k, rel(prm.grad, P[k].grad))
+
+
+def test_native_train_loop_matches_autograd_loop(pkg, gold, cuda):
+    """train_fusion native (device loss accumulation, device kernels) vs the torch-autograd loop
+    at dropout 0 from the same weights: per-epoch losses agree; the final weights agree to 1e-2
+    (Adam's g / sqrt(v) turns last-bit gradient differences on near-zero entries into
+    lr-sized steps, so the weights are a loose check)."""
+    g = torch.Generator().manual_seed(3)
+    txt = torch.randn(1300, 384, generator=g).to(cuda)
+    img = torch.randn(1300, 512, generator=g).to(cuda)
+    ms = []
+    for native in (True, False):
+        m = _model(pkg, gold, cuda)
+        m.mlp[2].p = 0.0
+        ms.append((m, pkg.fusion.train_fusion(m, txt, img, epochs=3, batch_size=512, native=native)))
+    (m1, h1), (m2, h2) = ms
+    for a, b in zip(h1, h2):
+        assert np.allclose(a, b, rtol=1e-4, atol=1e-5), (h1, h2)
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert rel(p1, p2) <= 1e-2, k

@@ -93,3 +93,28 @@ def test_serving_topk_and_rank(oracle):
     assert 0 not in idx and 1 not in idx and len(idx) == 3
     assert all(sc[i] >= sc[i + 1] for i in range(2))
     assert oracle.sampled_rank(np.array([1.0, 2.0, 1.0, 0.5])) == 2
+
+
+def test_fusion_train_loss_oracle_matches_reference_golden(oracle):
+    """fusion_train_loss (fp64) at dropout 0 vs the reference's own contrastive_fusion_loss and
+    autograd gradients on the golden batch (tests/golden/fusion_mlp.npz, first 256 rows)."""
+    g = dict(np.load(GOLDEN / "fusion_mlp.npz"))
+    P = {k[4:]: torch.from_numpy(v).double().requires_grad_(True) for k, v in g.items() if k.startswith("sd__")}
+    loss, lt, li = oracle.fusion_train_loss(P, torch.from_numpy(g["txt"][:256]).double(),
+                                            torch.from_numpy(g["img"][:256]).double())
+    loss.backward()
+    assert abs(float(loss) - float(g["loss"])) <= 1e-5 * float(g["loss"])
+    assert abs(float(lt) - float(g["loss_txt"])) <= 1e-5 * float(g["loss_txt"])
+    assert abs(float(li) - float(g["loss_img"])) <= 1e-5 * float(g["loss_img"])
+    for k, p in P.items():
+        ref = torch.from_numpy(g["grad__" + k]).double()
+        assert float((p.grad - ref).abs().max() / ref.abs().max()) <= 1e-4, k
+
+
+def test_mlp_dropout_mask_properties(oracle):
+    m = oracle.mlp_dropout_scale(77, 200_000, 0.1)
+    assert np.array_equal(m, oracle.mlp_dropout_scale(77, 200_000, 0.1))
+    assert abs(float((m == 0).mean()) - 0.1) < 0.005
+    assert set(np.unique(m).tolist()) == {0.0, float(np.float32(1) / np.float32(0.9))}
+    assert not np.array_equal(m, oracle.mlp_dropout_scale(78, 200_000, 0.1))
+    assert np.all(oracle.mlp_dropout_scale(77, 1000, 0.0) == 1.0)

@@ -19,6 +19,38 @@ pkg = importlib.import_module("plotpointe-gat-recommendation_amd")
 F = pkg.fusion
 
 
+def train_bench(dev, steps=30, B=512):
+    """One FusionMLP training step (fuse_modal.py:185-193, batch 512) native vs torch autograd;
+    Adam excluded from both (identical torch.optim)."""
+    rng = np.random.default_rng(1)
+    txt = torch.from_numpy(rng.standard_normal((B * steps, 384), dtype=np.float32)).to(dev)
+    img = torch.from_numpy(rng.standard_normal((B * steps, 512), dtype=np.float32)).to(dev)
+    torch.manual_seed(0)
+    m = F.FusionMLP(384, 512, 128, 256).to(dev).train()
+    out = {}
+    for name in ("native", "autograd"):
+        def step(i):
+            bt, bi = txt[i * B:(i + 1) * B], img[i * B:(i + 1) * B]
+            for p in m.parameters():
+                p.grad = None
+            if name == "native":
+                return F.fusion_train_step(m, bt, bi, seed=i)[0]
+            loss, _, _ = F.contrastive_fusion_loss(m(bt, bi), m.txt_proj(bt), m.img_proj(bi))
+            loss.backward()
+            return loss.detach()
+        for i in range(3):
+            step(i)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for i in range(steps):
+            step(i)
+        b.record()
+        torch.cuda.synchronize()
+        out[name + "_ms_per_step"] = a.elapsed_time(b) / steps
+    return out
+
+
 def main(iters=20):
     dev = torch.device("cuda")
     n_items, Dt, Di = 498_196, 384, 512
@@ -47,7 +79,13 @@ def main(iters=20):
                       "tflops": flop / (ms / 1e3) / 1e12, "mfma_fp32_peak_tflops": 157.3,
                       "mfma_frac": flop / (ms / 1e3) / 1e12 / 157.3,
                       "hbm_gbs": byts / (ms / 1e3) / 1e9}))
+    if "--train" in sys.argv:
+        print(json.dumps({"metric": "fusion MLP training step ms (batch 512, fwd + InfoNCE + bwd, no Adam)",
+                          **train_bench(dev)}))
 
 
 if __name__ == "__main__":
-    main()
+    it = 20
+    if "--iters" in sys.argv:
+        it = int(sys.argv[sys.argv.index("--iters") + 1])
+    main(it)
