@@ -356,6 +356,171 @@ __global__ void __launch_bounds__(256, PPGAT_PROJ16_OCC) k_proj16(ProjArg a) {
 }
 
 // ---------------------------------------------------------------------------
+// projection GEMM, one wave per 32-row tile (v_mfma_f32_32x32x2_f32), K in {64, 128}
+//
+// Same contract as k_proj16 (both modes, both epilogues).  Each wave owns 32 x 128 output
+// tiles with the full reduction: four 32 x 32 accumulator blocks (64 accumulation registers).
+// Reduction order per lane (r, hf): step s = 4 q + e takes k = 8 q + 4 hf + e, so lane (r, hf)
+// holds x[row r][8 q + 4 hf .. + 3] as one float4 per q (a wave's load q covers 32 B of each
+// of its 32 rows) and reads B'[32 cb + r][8 q + 4 hf .. + 3] from LDS as one ds_read_b128 per
+// four MFMAs of 64 cycles -- half the LDS reads per MFMA cycle of the 16 x 16 x 4 design.  The
+// next tile's x is loaded into each float4 right after its last use (one tile of x in
+// registers), the epilogue runs while the SIMD's other wave keeps the matrix pipe busy.
+// Node scores: 32 per-lane partial sums (16 rows x {src, dst}) reduced over the 32 lanes of
+// each half by transposing butterflies; each lane then stores one (row, vector) value.
+// ---------------------------------------------------------------------------
+template <int MODE, int KQ>
+__global__ void __launch_bounds__(256, 2) k_proj32(ProjArg a) {
+  constexpr int K = 8 * KQ;
+  constexpr int LD = K + 4;  // B' row stride: the 16 lanes of a ds_read_b128 group hit 64 banks
+  __shared__ float4 sW4[kPT * LD / 4];
+  __shared__ float sV[2][kPT];
+  float* sW = reinterpret_cast<float*>(sW4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int r = lane & 31, hf = lane >> 5;
+  if (MODE == 0) {
+    for (int idx = tid; idx < kPT * K / 4; idx += 256) {
+      const int j = idx / (K / 4), k4 = (idx % (K / 4)) * 4;
+      st4(&sW[j * LD + k4], ld4(a.W + (int64_t)j * a.ldw + k4));
+    }
+  } else {
+    for (int idx = tid; idx < kPT * K / 4; idx += 256) {
+      const int k = idx >> 5, j4 = (idx & 31) * 4;
+      const float4 v = ld4(a.W + (int64_t)k * a.ldw + j4);
+      sW[(j4 + 0) * LD + k] = v.x;
+      sW[(j4 + 1) * LD + k] = v.y;
+      sW[(j4 + 2) * LD + k] = v.z;
+      sW[(j4 + 3) * LD + k] = v.w;
+    }
+  }
+  const bool vec = a.att_src != nullptr;
+  if (vec && tid < 2 * kPT) {
+    const int k = tid & 127;
+    sV[tid >> 7][k] = (MODE == 1 && k >= K) ? 0.f : (tid < kPT ? a.att_src : a.att_dst)[k];
+  }
+  __syncthreads();
+  if (MODE == 1 && vec) {  // A[j] = sum_k att[k] W[k][j]
+    float s = 0.f;
+    const int j = tid & 127, v = tid >> 7;
+    for (int k = 0; k < K; ++k) s = fmaf(sV[v][k], sW[j * LD + k], s);
+    __syncthreads();
+    sV[v][j] = s;
+    __syncthreads();
+  }
+  float va[4], vb[4], bias[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int c = 32 * cb + r;
+    va[cb] = vec ? sV[0][c] : 0.f;
+    vb[cb] = vec ? sV[1][c] : 0.f;
+    bias[cb] = (MODE == 0 && a.bias) ? a.bias[c] : 0.f;
+  }
+  gfloat* const x0 = sgpr(a.x0);
+  gfloat* const x1 = sgpr(a.x1);
+  const int64_t ldx0 = sgpr(a.ldx0), ldx1 = sgpr(a.ldx1), split = sgpr(a.split), n = sgpr(a.n);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t tiles = (n + 31) / 32;
+  const int64_t iters = (tiles + nw - 1) / nw;  // the same for every wave
+  const float* sWl = sW + r * LD + 4 * hf;
+  // rows past n read row n - 1 (never stored)
+  auto row_src = [&](int64_t tile) -> gfloat* {
+    int64_t row = tile * 32 + r;
+    row = row < n ? row : n - 1;
+    return row < split ? x0 + row * ldx0 : x1 + (row - split) * ldx1;
+  };
+  float4 xr[KQ];
+  {
+    gfloat* src = row_src(wave);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) xr[q] = ld4(src + 8 * q + 4 * hf);
+  }
+  for (int64_t it = 0; it < iters; ++it) {
+    const int64_t t = wave + it * nw;
+    const int64_t row0 = t * 32;
+    float2 dv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dv[q] = make_float2(0.f, 0.f);
+    if (MODE == 1 && a.ds != nullptr) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        row = row < n ? row : n - 1;
+        dv[q] = *reinterpret_cast<const float2*>(a.ds + row * a.ldds);
+      }
+    }
+    gfloat* nsrc = row_src(t + nw);
+    f32x16 acc[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[cb][i] = 0.f;
+    // B' fragments one q ahead; the scheduling barrier keeps the compiler from hoisting every
+    // LDS read of the tile (256 registers) above the MFMAs, or sinking them onto their use
+    float4 bq[4], bn[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) bq[cb] = *reinterpret_cast<const float4*>(sWl + cb * 32 * LD);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      if (q + 1 < KQ) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) bn[cb] = *reinterpret_cast<const float4*>(sWl + cb * 32 * LD + 8 * (q + 1));
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the q + 1 reads stay ahead of the q MFMAs
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(comp(xr[q], e), comp(bq[cb], e), acc[cb]);
+      xr[q] = ld4(nsrc + 8 * q + 4 * hf);  // next tile, into the registers just consumed
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) bq[cb] = bn[cb];
+    }
+    // ---- epilogue ----
+    const int64_t live = row0 < n ? (n - row0 < 32 ? n - row0 : 32) : 0;
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc(a.y + (live ? row0 * a.ldy : 0), 0, (int)(live * a.ldy * 4),
+                                                      0x00020000);
+    const int64_t ldy = sgpr(a.ldy);
+    int voff = (int)((4 * hf * ldy + r) * 4);
+    asm volatile("" : "+v"(voff));  // per tile: keeps the 16 row offsets from being hoisted
+    float ps[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) ps[i] = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        float v = acc[cb][q];
+        if (MODE == 1) {
+          v = fmaf(dv[q].y, vb[cb], fmaf(dv[q].x, va[cb], v));
+        } else {
+          ps[q] = fmaf(v, va[cb], ps[q]);
+          ps[16 + q] = fmaf(v, vb[cb], ps[16 + q]);
+          v += bias[cb];
+        }
+        // every offset in the VGPR operand (the descriptor's range check clips the tail rows);
+        // the column block goes to the instruction's immediate offset
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry,
+                                              voff + (int)(((q & 3) + 8 * (q >> 2)) * ldy * 4) + 128 * cb, 0, 0);
+      }
+    if (MODE == 0 && vec) {
+      float res = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float v4[4] = {ps[4 * c], ps[4 * c + 1], ps[4 * c + 2], ps[4 * c + 3]};
+        const float s = transpose_reduce<32, 4>(v4, r);  // value 4 c + (r >> 3)
+        res = (r & 7) == c ? s : res;
+      }
+      const int v = 4 * (r & 7) + (r >> 3);
+      const int q = v & 15;
+      const int row = (q & 3) + 8 * (q >> 2) + 4 * hf;
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((v < 16 ? a.s_src : a.s_dst) + (live ? row0 : 0), 0,
+                                                        (int)(live * 4), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res), rs, row * 4, 0, 0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // out[M, K] = A^T B (+ V^T B, colsum A), M, K <= 128
 //
 // Workgroup = 8 waves = 4 pairs, one workgroup per CU (two waves per SIMD).  A pair owns a
@@ -743,6 +908,21 @@ __global__ void __launch_bounds__(256) k_adam(AdamArg a) {
 // ---- host launchers ----
 bool proj_shape_ok(int K, int ncols) { return K >= 4 && K <= kPT && K % 4 == 0 && ncols == kPT; }
 
+// the 32 x 32 x 2 kernel (k_proj32) for K in {64, 128}; PPGAT_PROJ_KERNEL=16 keeps k_proj16
+#ifndef PPGAT_PROJ_KERNEL
+#define PPGAT_PROJ_KERNEL 32
+#endif
+static bool proj32_ok(int K, int64_t ld0, int64_t ld1) {
+  return PPGAT_PROJ_KERNEL == 32 && (K == 64 || K == 128) && (ld0 % 4) == 0 && (ld1 % 4) == 0;
+}
+
+static unsigned proj32_grid(int64_t n) {
+  const int64_t tiles = (n + 31) / 32;
+  int64_t g = (tiles + 3) / 4;
+  if (g > 512) g = 512;  // persistent: two workgroups per CU over the 32-row tiles
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
 static unsigned proj16_grid(int64_t n) {
   const int64_t tiles = (n + 15) / 16;
   int64_t g = (tiles + 3) / 4;
@@ -758,7 +938,12 @@ hipError_t proj_fwd(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1
   a.x0 = x0; a.ldx0 = ldx0; a.x1 = x1 ? x1 : x0; a.ldx1 = x1 ? ldx1 : ldx0; a.split = x1 ? split : n; a.n = n;
   a.K = K; a.W = W; a.ldw = ldw; a.bias = bias; a.att_src = att_src; a.att_dst = att_dst;
   a.y = y; a.ldy = ldy; a.s_src = s_src; a.s_dst = s_dst;
-  hipLaunchKernelGGL(k_proj16<0>, dim3(proj16_grid(n)), dim3(256), 0, st, a);
+  if (proj32_ok(K, ldx0, x1 ? ldx1 : ldx0)) {
+    if (K == 128) hipLaunchKernelGGL((k_proj32<0, 16>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_proj32<0, 8>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_proj16<0>, dim3(proj16_grid(n)), dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -768,6 +953,11 @@ hipError_t proj_dx(const float* D, int64_t ldd, int64_t n, int K, const float* W
   ProjArg a{};
   a.x0 = D; a.ldx0 = ldd; a.x1 = D; a.ldx1 = ldd; a.split = n; a.n = n; a.K = K; a.W = W; a.ldw = ldw;
   a.att_src = att_src; a.att_dst = att_dst; a.ds = S; a.ldds = lds; a.y = y; a.ldy = ldy;
+  if (proj32_ok(K, ldd, ldd)) {
+    if (K == 128) hipLaunchKernelGGL((k_proj32<1, 16>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_proj32<1, 8>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_proj16<1>, dim3(proj16_grid(n)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -216,31 +216,53 @@ def make_plan(n_own: int, send_idx: np.ndarray, send_counts, recv_counts, device
 
 
 class _Exchange(torch.autograd.Function):
-    """[n_own, ...] own rows -> [n_own + n_recv, ...] = [own | rows received from the peers]."""
+    """[n_own, ...] own rows -> [n_own + sum n_recv (+ n_tail), ...] = [own | rows received
+    under each plan, in plan order | tail]: ``tail`` (nullable) are rows the rank computes
+    itself (the first layer's halo items, from the replicated item features)."""
 
     @staticmethod
-    def forward(ctx, t_own, plan: ExchangePlan, comm: "Comm", stages):
+    def forward(ctx, t_own, tail, plans, comm: "Comm", stages):
         t_own = t_own.contiguous()
-        out = torch.empty((plan.n_own + plan.n_recv,) + tuple(t_own.shape[1:]), dtype=t_own.dtype,
-                          device=t_own.device)
-        out[:plan.n_own].copy_(t_own)
-        send = stages.gather_rows(t_own, plan.send_idx)
-        comm.all_to_all_rows(send, plan.send_counts, plan.recv_counts, out=out[plan.n_own:])
-        ctx.plan, ctx.comm, ctx.stages = plan, comm, stages
+        n_tail = tail.size(0) if tail is not None else 0
+        n_own = plans[0].n_own
+        out = torch.empty((n_own + sum(p.n_recv for p in plans) + n_tail,) + tuple(t_own.shape[1:]),
+                          dtype=t_own.dtype, device=t_own.device)
+        out[:n_own].copy_(t_own)
+        off = n_own
+        for plan in plans:
+            send = stages.gather_rows(t_own, plan.send_idx)
+            comm.all_to_all_rows(send, plan.send_counts, plan.recv_counts, out=out[off:off + plan.n_recv])
+            off += plan.n_recv
+        if n_tail:
+            out[off:].copy_(tail)
+        ctx.plans, ctx.comm, ctx.stages, ctx.has_tail = plans, comm, stages, tail is not None
         return out
 
     @staticmethod
     def backward(ctx, g):
-        plan, comm, st = ctx.plan, ctx.comm, ctx.stages
+        plans, comm, st = ctx.plans, ctx.comm, ctx.stages
         g = g.contiguous()
-        g_own = g[:plan.n_own].clone()
-        ret = comm.all_to_all_rows(g[plan.n_own:], plan.recv_counts, plan.send_counts)
-        st.return_add(g_own, ret, plan.ret_ptr, plan.ret_pos)
-        return g_own, None, None, None
+        n_own = plans[0].n_own
+        g_own = g[:n_own].clone()
+        off = n_own
+        for plan in plans:  # each plan touches its own rows (users / items): independent sums
+            ret = comm.all_to_all_rows(g[off:off + plan.n_recv], plan.recv_counts, plan.send_counts)
+            st.return_add(g_own, ret, plan.ret_ptr, plan.ret_pos)
+            off += plan.n_recv
+        return g_own, (g[off:] if ctx.has_tail else None), None, None, None
 
 
 def exchange(t_own, plan: ExchangePlan, comm: "Comm", stages):
-    return _Exchange.apply(t_own, plan, comm, stages)
+    return _Exchange.apply(t_own, None, [plan], comm, stages)
+
+
+def halo_exchange(t_own, hg: "HaloGraph", comm: "Comm", stages, halo_items: Optional[torch.Tensor] = None):
+    """[own | halo users | halo items] rows of one layer: the halo users by the user plan's
+    all_to_all; the halo items by the item plan's, or -- first layer -- ``halo_items``
+    computed locally from the replicated item features (no exchange, no return)."""
+    if halo_items is not None:
+        return _Exchange.apply(t_own, halo_items, [hg.plan_u], comm, stages)
+    return _Exchange.apply(t_own, None, [hg.plan_u, hg.plan_i], comm, stages)
 
 
 # ---------------------------------------------------------------------------
@@ -292,19 +314,29 @@ class HaloGraph:
     n_users: int
     seg_bounds: list            # [user bounds [world+1], item bounds [world+1]] (node ids)
     n_own: int                  # own rows: users [u0, u1) then items [i0, i1)
-    n_halo: int
-    plan: ExchangePlan          # the layer halo exchange
+    n_halo: int                 # halo rows: users (by owner) then items (by owner)
+    plan_u: ExchangePlan        # the layer halo exchange of user rows
+    plan_i: ExchangePlan        # ... of item rows
     fwd_view: LocalView         # CSR over the own destination rows (n_rows = n_own)
     bwd_view: LocalView         # CSC over [own | halo] source rows (n_rows = n_own + n_halo)
     local_of: np.ndarray        # [N] int64: node id -> own row, -1 elsewhere (host)
     owner: np.ndarray           # [N] int32 node owner (host)
     loss_plans: dict = None
+    halo_items: torch.Tensor = None  # [n_halo_i] int64 item indices (node id - n_users) of the halo items
     bwd_sched_own: object = None   # backward schedule over the own source rows
     bwd_sched_halo: object = None  # ... over the halo source rows (row ids relative to n_own)
 
     @property
     def R(self) -> int:
         return self.n_own + self.n_halo
+
+    @property
+    def n_halo_u(self) -> int:
+        return self.plan_u.n_recv
+
+    @property
+    def n_send(self) -> int:
+        return self.plan_u.n_send + self.plan_i.n_send
 
     @property
     def bounds(self) -> np.ndarray:
@@ -355,17 +387,23 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     od, osrc = owner[dst], owner[src]
     loc = np.flatnonzero(od == rank)                       # edges homed here (destination owned)
     lsrc = src[loc]
-    halo = np.unique(lsrc[osrc[loc] != rank])              # ascending ids ...
-    halo = halo[np.argsort(owner[halo], kind="stable")]    # ... grouped by owner: the owner's row order
-    recv_counts = np.bincount(owner[halo], minlength=world)
+    halo = np.unique(lsrc[osrc[loc] != rank])              # ascending ids; users, then items,
+    halo_u, halo_i = halo[halo < nu], halo[halo >= nu]     # each grouped by owner (the owner's row order)
+    halo_u = halo_u[np.argsort(owner[halo_u], kind="stable")]
+    halo_i = halo_i[np.argsort(owner[halo_i], kind="stable")]
     lidx = local_of.copy()
-    lidx[halo] = n_own + np.arange(len(halo))
+    lidx[halo_u] = n_own + np.arange(len(halo_u))
+    lidx[halo_i] = n_own + len(halo_u) + np.arange(len(halo_i))
     # what this rank sends: its own sources of edges homed on other ranks, per peer, by id
     out_e = np.flatnonzero((osrc == rank) & (od != rank))
     key = np.unique(od[out_e].astype(np.int64) * N + src[out_e])
-    send_counts = np.bincount(key // N, minlength=world)
-    send_idx = local_of[key % N]
-    plan = make_plan(n_own, send_idx, send_counts, recv_counts, dev)
+    ids, peers = key % N, key // N
+    su = ids < nu
+    plan_u = make_plan(n_own, local_of[ids[su]], np.bincount(peers[su], minlength=world),
+                       np.bincount(owner[halo_u], minlength=world), dev)
+    plan_i = make_plan(n_own, local_of[ids[~su]], np.bincount(peers[~su], minlength=world),
+                       np.bincount(owner[halo_i], minlength=world), dev)
+    halo = np.concatenate([halo_u, halo_i])
     R = n_own + len(halo)
     ei_l = torch.from_numpy(np.stack([lidx[lsrc], lidx[dst[loc]]])).to(dev)
     El = len(loc)
@@ -377,7 +415,8 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     row, csc_eid, slot = G.row[:El].contiguous(), orig(G.csc_eid[:El]), G.csc2csr[:El].contiguous()
     fwd_view = LocalView(n_own, rowptr_own, col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
     bwd_view = LocalView(R, G.rowptr.contiguous(), col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
-    hg = HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan, fwd_view, bwd_view, local_of, owner, {})
+    hg = HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan_u, plan_i, fwd_view, bwd_view, local_of,
+                   owner, {}, torch.from_numpy(halo_i - nu).to(dev))
     if sched_builder is not None:
         fwd_view.fwd_sched = sched_builder(rowptr_own, El)
         bwd_view.bwd_sched = sched_builder(bwd_view.colptr, El)
@@ -448,54 +487,71 @@ def _comm_stream(dev) -> torch.cuda.Stream:
 
 class _HaloLayerX(torch.autograd.Function):
     """One multi-head layer on the halo partition, aggregate-then-transform (hip_ops.xgat_*):
-    forward = all_to_all of the halo rows of x, then the layer over [own | halo] sources;
-    backward = the halo sources' edge pass first, their input gradients sent back to the
-    owners on a communication stream (RCCL all_to_all) while the own sources' edge pass and
-    the weight-gradient GEMMs run, then the owners add the returned rows in peer order."""
+    forward = all_to_all of the halo rows of x (users, then items -- or, first layer, the
+    halo items' rows computed locally: ``x_halo_items``), then the layer over
+    [own | halo] sources; backward = the halo sources' edge pass first, their input gradients
+    sent back to the owners on a communication stream (RCCL all_to_all) while the own
+    sources' edge pass and the weight-gradient GEMMs run, then the owners add the returned
+    rows in peer order."""
 
     @staticmethod
-    def forward(ctx, x_own, weight, att_src, att_dst, bias, hg: "HaloGraph", comm: "Comm", stages, heads: int,
-                C: int, slope: float, p: float, seed: int):
+    def forward(ctx, x_own, x_halo_items, weight, att_src, att_dst, bias, hg: "HaloGraph", comm: "Comm", stages,
+                heads: int, C: int, slope: float, p: float, seed: int):
         from .hip_ops import xgat_forward
-        plan = hg.plan
+        plans = [hg.plan_u] if x_halo_items is not None else [hg.plan_u, hg.plan_i]
         x_own = x_own.contiguous()
-        x_loc = torch.empty((plan.n_own + plan.n_recv, x_own.size(1)), dtype=x_own.dtype, device=x_own.device)
-        x_loc[:plan.n_own].copy_(x_own)
-        comm.all_to_all_rows(stages.gather_rows(x_own, plan.send_idx), plan.send_counts, plan.recv_counts,
-                             out=x_loc[plan.n_own:])
+        x_loc = torch.empty((hg.R, x_own.size(1)), dtype=x_own.dtype, device=x_own.device)
+        x_loc[:hg.n_own].copy_(x_own)
+        off = hg.n_own
+        for plan in plans:
+            comm.all_to_all_rows(stages.gather_rows(x_own, plan.send_idx), plan.send_counts, plan.recv_counts,
+                                 out=x_loc[off:off + plan.n_recv])
+            off += plan.n_recv
+        if x_halo_items is not None and x_halo_items.size(0):
+            x_loc[off:].copy_(x_halo_items)
         out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed)
-        ctx.hg, ctx.comm, ctx.stages = hg, comm, stages
+        ctx.hg, ctx.comm, ctx.stages, ctx.plans = hg, comm, stages, plans
         ctx.att_shapes = (att_src.shape, att_dst.shape)
+        ctx.local_items = x_halo_items is not None
         return out
 
     @staticmethod
     def backward(ctx, g):
         from .hip_ops import xgat_backward
-        hg, comm, st = ctx.hg, ctx.comm, ctx.stages
-        plan = hg.plan
+        hg, comm, st, plans = ctx.hg, ctx.comm, ctx.stages, ctx.plans
         dev = g.device
         pending = {}
 
+        def a2a_back(dx_halo):
+            rets, off = [], 0
+            for plan in plans:
+                rets.append(comm.all_to_all_rows(dx_halo[off:off + plan.n_recv], plan.recv_counts, plan.send_counts))
+                off += plan.n_recv
+            return rets
+
         def send_back(dx_halo):
             if comm.backend != "nccl" or not comm.active:
-                pending["ret"] = comm.all_to_all_rows(dx_halo, plan.recv_counts, plan.send_counts)
+                pending["ret"] = a2a_back(dx_halo)
                 return
             main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
             cs.wait_stream(main)
             dx_halo.record_stream(cs)
             with torch.cuda.stream(cs):
-                pending["ret"] = comm.all_to_all_rows(dx_halo, plan.recv_counts, plan.send_counts)
+                pending["ret"] = a2a_back(dx_halo)
             pending["stream"] = cs
 
-        dx, dW, datt_src, datt_dst, dbias = xgat_backward(ctx.saved, g, ctx.needs_input_grad[4], halo_hook=send_back)
+        dx, dW, datt_src, datt_dst, dbias = xgat_backward(ctx.saved, g, ctx.needs_input_grad[5], halo_hook=send_back)
         ctx.saved = None
-        dx_own = dx[:plan.n_own]
+        dx_own = dx[:hg.n_own]
         if "stream" in pending:
             main = torch.cuda.current_stream(dev)
             main.wait_stream(pending["stream"])
-            pending["ret"].record_stream(main)
-        st.return_add(dx_own, pending["ret"], plan.ret_ptr, plan.ret_pos)
-        return (dx_own, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+            for r in pending["ret"]:
+                r.record_stream(main)
+        for plan, ret in zip(plans, pending["ret"]):
+            st.return_add(dx_own, ret, plan.ret_ptr, plan.ret_pos)
+        d_items = dx[hg.n_own + hg.n_halo_u:] if ctx.local_items else None
+        return (dx_own, d_items, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
                 None, None, None, None, None, None, None, None)
 
 
@@ -577,23 +633,35 @@ class HaloPyGGAT(_ShardedBase):
         """Exchange the pre-projection rows when they are narrower than h (H*C > C_in)."""
         return conv.heads * conv.out_channels > conv.in_channels
 
+    def halo_item_input(self, item_feats):
+        """The first layer's input rows of the halo items, item_proj(features) computed on this
+        rank (the item features are on every rank): they are neither received nor returned;
+        their gradient reaches item_proj here and is summed by the dense all-reduce."""
+        hg = self.dg
+        f = self.stages.gather_rows(item_feats, hg.halo_items)
+        return self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
+
     def forward(self, item_feats):
         hg = self.dg
         x = self.node_features(item_feats)
-        for conv in self.convs:
+        for li, conv in enumerate(self.convs):
             p = float(conv.dropout) if self.training else 0.0
             seed = self.layer_seed(conv)
+            xh = self.halo_item_input(item_feats) if li == 0 and hg.plan_i.n_recv else None
+            if li == 0 and xh is None:
+                xh = x.new_zeros(0, x.size(1))
             if self.exchanges_input(conv):
                 if getattr(self.stages, "supports_x", lambda c: False)(conv):
                     # aggregate-then-transform on the local rows: no halo projection, the
                     # return of the halo gradients overlapped with the own rows' backward
-                    x = _HaloLayerX.apply(x, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg, self.comm,
-                                          self.stages, conv.heads, conv.out_channels, float(conv.negative_slope), p,
-                                          seed)
+                    x = _HaloLayerX.apply(x, xh, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg,
+                                          self.comm, self.stages, conv.heads, conv.out_channels,
+                                          float(conv.negative_slope), p, seed)
                     continue
-                h = self.stages.linear(exchange(x, hg.plan, self.comm, self.stages), conv.lin.weight, None)
+                h = self.stages.linear(halo_exchange(x, hg, self.comm, self.stages, xh), conv.lin.weight, None)
             else:
-                h = exchange(self.stages.linear(x, conv.lin.weight, None), hg.plan, self.comm, self.stages)
+                hh = self.stages.linear(xh, conv.lin.weight, None) if xh is not None and xh.size(0) else xh
+                h = halo_exchange(self.stages.linear(x, conv.lin.weight, None), hg, self.comm, self.stages, hh)
             x = _LocalGAT.apply(h, conv.att_src, conv.att_dst, conv.bias, hg, self.stages, conv.heads,
                                 conv.out_channels, _lib.MODE_PYG, float(conv.negative_slope), p, seed)
         return x

@@ -72,7 +72,7 @@ def _worker(rank, world, port, out_dir, heads, ii):
     ug = model._user_rows_global(model.user_emb_local.grad, g.n_users)
     if rank == 0:
         torch.save({"Z": Zg, "loss": tot, "grads": grads, "user_grad": ug, "sd": sd, "bounds": hg.bounds,
-                    "n_halo": hg.n_halo, "n_send": hg.plan.n_send}, os.path.join(out_dir, "res.pt"))
+                    "n_halo": hg.n_halo, "n_send": hg.n_send}, os.path.join(out_dir, "res.pt"))
     dist.destroy_process_group()
 
 

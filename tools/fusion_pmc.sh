@@ -14,4 +14,5 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   i=$((i+1))
   (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o p -- python "$R/tools/bench_fusion.py" --iters 3 > "$OUT/p$i.log" 2>&1) || { echo "pass $i rc=$?"; exit 1; }
 done
+(cd /tmp && timeout -k 5 60 rocprofv3 -L > "$OUT/avail.txt" 2>&1) || echo "list rc=$?"
 echo done

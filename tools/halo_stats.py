@@ -54,10 +54,17 @@ def main():
         s_u = np.unique(oi[(ou == r) & (oi != r)].astype(np.int64) * N + users[(ou == r) & (oi != r)]).size
         s_i = np.unique(ou[(oi == r) & (ou != r)].astype(np.int64) * N + items[(oi == r) & (ou != r)]).size
         n_halo = len(halo_u) + len(halo_i)
-        out.append({"rank": r, "own_rows": own, "halo_rows": n_halo, "sent_rows": s_u + s_i,
+        out.append({"rank": r, "own_rows": own, "halo_rows": n_halo, "halo_users": len(halo_u),
+                    "halo_items": len(halo_i), "sent_rows": s_u + s_i, "sent_users": s_u, "sent_items": s_i,
                     "local_edges": int(m1.sum() + m2.sum()),
                     "recv_GB_per_layer_dir": n_halo * row_bytes / 1e9, "send_GB_per_layer_dir": (s_u + s_i) * row_bytes / 1e9})
         print(json.dumps(out[-1]), flush=True)
+    # per training step: layer 1 exchanges the user rows only (the halo items' input rows come
+    # from the replicated item features), layer 2 every halo row; each backward mirrors its
+    # forward.  An all_to_all ends with its busiest rank: max over ranks of max(send, recv).
+    l1 = max(max(o["halo_users"], o["sent_users"]) for o in out) * row_bytes / 1e9
+    l2 = max(max(o["halo_rows"], o["sent_rows"]) for o in out) * row_bytes / 1e9
+    print(json.dumps({"layer1_GB_busiest_rank": l1, "layer2_GB_busiest_rank": l2, "step_GB_busiest_rank": 2 * (l1 + l2)}))
     print(json.dumps({"config": args.config, "world": W, "nodes": N, "edges": 2 * len(users), "row_bytes": row_bytes,
                       "max_recv_GB": max(o["recv_GB_per_layer_dir"] for o in out),
                       "max_send_GB": max(o["send_GB_per_layer_dir"] for o in out),
