@@ -908,9 +908,11 @@ __global__ void __launch_bounds__(256) k_adam(AdamArg a) {
 // ---- host launchers ----
 bool proj_shape_ok(int K, int ncols) { return K >= 4 && K <= kPT && K % 4 == 0 && ncols == kPT; }
 
-// the 32 x 32 x 2 kernel (k_proj32) for K in {64, 128}; PPGAT_PROJ_KERNEL=16 keeps k_proj16
+// k_proj32 (32 x 32 x 2, K in {64, 128}) is built with PPGAT_PROJ_KERNEL=32 only: measured at
+// config 2 (profiles/r02/v4_gemm_ab.log) it is slower than k_proj16 -- 105.8 vs 99.4 us (x W^T
+// with scores) and 120.5 vs 104.6 us (dx) -- so k_proj16 stays the product kernel
 #ifndef PPGAT_PROJ_KERNEL
-#define PPGAT_PROJ_KERNEL 32
+#define PPGAT_PROJ_KERNEL 16
 #endif
 static bool proj32_ok(int K, int64_t ld0, int64_t ld1) {
   return PPGAT_PROJ_KERNEL == 32 && (K == 64 || K == 128) && (ld0 % 4) == 0 && (ld1 % 4) == 0;

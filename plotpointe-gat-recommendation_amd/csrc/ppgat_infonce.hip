@@ -46,17 +46,17 @@ __global__ void __launch_bounds__(256) k_rownorm3(const float* __restrict__ x0, 
   if (lane == 0) nrm[w] = n;
 }
 
-// S1 = A B1^T * scale, S2 = A B2^T * scale for A, B1, B2 [B, kD]: 64 x 64 output tiles, 16 per
-// thread (4 x 4), the k dimension staged through LDS in chunks of 32
+// S1 = A B1^T * scale, S2 = A B2^T * scale for A, B1, B2 [B, kD]: 32 x 32 output tiles (B^2/1024
+// workgroups: 256 at B = 512), 2 x 2 per thread per matrix, k staged through LDS in chunks of 32
 __global__ void __launch_bounds__(256) k_sim2(const float* __restrict__ A, const float* __restrict__ B1,
                                               const float* __restrict__ B2, int64_t B, float scale,
                                               float* __restrict__ S1, float* __restrict__ S2) {
-  __shared__ float sa[32][65], sb1[32][65], sb2[32][65];
+  __shared__ float sa[32][33], sb1[32][33], sb2[32][33];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
-  float acc1[4][4] = {}, acc2[4][4] = {};
+  const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
+  float acc1[2][2] = {}, acc2[2][2] = {};
   for (int k0 = 0; k0 < kD; k0 += 32) {
-    for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
       const int rr = e >> 5, kk = e & 31;
       const int64_t ra = r0 + rr, rb = c0 + rr;
       sa[kk][rr] = ra < B ? A[ra * kD + k0 + kk] : 0.f;
@@ -64,28 +64,22 @@ __global__ void __launch_bounds__(256) k_sim2(const float* __restrict__ A, const
       sb2[kk][rr] = rb < B ? B2[rb * kD + k0 + kk] : 0.f;
     }
     __syncthreads();
+#pragma unroll 8
     for (int kk = 0; kk < 32; ++kk) {
-      float a[4], b1[4], b2[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = sa[kk][ty + 16 * i];
-        b1[i] = sb1[kk][tx + 16 * i];
-        b2[i] = sb2[kk][tx + 16 * i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc1[i][j] = fmaf(a[i], b1[j], acc1[i][j]);
-          acc2[i][j] = fmaf(a[i], b2[j], acc2[i][j]);
-        }
+      const float a0 = sa[kk][ty], a1 = sa[kk][ty + 16];
+      const float p0 = sb1[kk][tx], p1 = sb1[kk][tx + 16];
+      const float q0 = sb2[kk][tx], q1 = sb2[kk][tx + 16];
+      acc1[0][0] = fmaf(a0, p0, acc1[0][0]); acc1[0][1] = fmaf(a0, p1, acc1[0][1]);
+      acc1[1][0] = fmaf(a1, p0, acc1[1][0]); acc1[1][1] = fmaf(a1, p1, acc1[1][1]);
+      acc2[0][0] = fmaf(a0, q0, acc2[0][0]); acc2[0][1] = fmaf(a0, q1, acc2[0][1]);
+      acc2[1][0] = fmaf(a1, q0, acc2[1][0]); acc2[1][1] = fmaf(a1, q1, acc2[1][1]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 2; ++j) {
       const int64_t r = r0 + ty + 16 * i, c = c0 + tx + 16 * j;
       if (r < B && c < B) {
         S1[r * B + c] = acc1[i][j] * scale;
@@ -151,48 +145,46 @@ __global__ void __launch_bounds__(256) k_ce_mean(const float* __restrict__ l, in
 }
 
 // out[r, d] (+)= scale * sum_k P(r, k) Q[k, d], P(r, k) = P[r * B + k] (TRANS 0) or P[k * B + r]
-// (TRANS 1); P [B, B], Q [B, kD]; 64-row x 128-col output tile, 8 x 4 per thread
+// (TRANS 1); P [B, B], Q [B, kD]; 16-row x 64-col output tiles (B/16 x 2 workgroups), 2 x 2
+// per thread, k staged through LDS in chunks of 32
 template <int TRANS>
 __global__ void __launch_bounds__(256) k_mm_bd(const float* __restrict__ P, const float* __restrict__ Q, int64_t B,
                                                float scale, int accumulate, float* __restrict__ out) {
-  __shared__ float sp[32][65];
-  __shared__ float sq[32][kD + 1];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 col groups x 8 row groups
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
-  float acc[8][4] = {};
+  __shared__ float sp[32][17];
+  __shared__ float sq[32][65];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // cols tx, tx + 32; rows ty, ty + 8
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+  const int c0 = blockIdx.y * 64;
+  float acc[2][2] = {};
   for (int64_t k0 = 0; k0 < B; k0 += 32) {
-    for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    for (int e = threadIdx.x; e < 16 * 32; e += 256) {
       // consecutive threads along P's contiguous index: k for TRANS 0, r for TRANS 1
-      const int rr = TRANS ? (e & 63) : (e >> 5), kk = TRANS ? (e >> 6) : (e & 31);
+      const int rr = TRANS ? (e & 15) : (e >> 5), kk = TRANS ? (e >> 4) : (e & 31);
       const int64_t r = r0 + rr, k = k0 + kk;
       sp[kk][rr] = (r < B && k < B) ? (TRANS ? P[k * B + r] : P[r * B + k]) : 0.f;
     }
-    for (int e = threadIdx.x; e < 32 * kD; e += 256) {
-      const int kk = e / kD, d = e % kD;
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int kk = e >> 6, d = e & 63;
       const int64_t k = k0 + kk;
-      sq[kk][d] = k < B ? Q[k * kD + d] : 0.f;
+      sq[kk][d] = k < B ? Q[k * kD + c0 + d] : 0.f;
     }
     __syncthreads();
+#pragma unroll 8
     for (int kk = 0; kk < 32; ++kk) {
-      float p[8], q[4];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) p[i] = sp[kk][ty + 8 * i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) q[j] = sq[kk][tx + 32 * j];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(p[i], q[j], acc[i][j]);
+      const float p0 = sp[kk][ty], p1 = sp[kk][ty + 8];
+      const float q0 = sq[kk][tx], q1 = sq[kk][tx + 32];
+      acc[0][0] = fmaf(p0, q0, acc[0][0]); acc[0][1] = fmaf(p0, q1, acc[0][1]);
+      acc[1][0] = fmaf(p1, q0, acc[1][0]); acc[1][1] = fmaf(p1, q1, acc[1][1]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < 2; ++i) {
     const int64_t r = r0 + ty + 8 * i;
     if (r >= B) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float* o = out + r * kD + tx + 32 * j;
+    for (int j = 0; j < 2; ++j) {
+      float* o = out + r * kD + c0 + tx + 32 * j;
       const float v = acc[i][j] * scale;
       *o = accumulate ? *o + v : v;
     }
@@ -272,16 +264,17 @@ hipError_t infonce(const float* F, const float* T, const float* I, int64_t B, fl
   const float* In = Y + 2 * B * kD;
   const unsigned w3 = (unsigned)((3 * B + 3) / 4);
   hipLaunchKernelGGL(k_rownorm3, dim3(w3), dim3(256), 0, st, F, T, I, B, Y, nrm);
-  const unsigned tb = (unsigned)((B + 63) / 64);
-  hipLaunchKernelGGL(k_sim2, dim3(tb, tb), dim3(256), 0, st, Fn, Tn, In, B, 1.f / tau, S1, S2);
+  const unsigned t32 = (unsigned)((B + 31) / 32);
+  hipLaunchKernelGGL(k_sim2, dim3(t32, t32), dim3(256), 0, st, Fn, Tn, In, B, 1.f / tau, S1, S2);
   hipLaunchKernelGGL(k_ce_rows, dim3((unsigned)B, 2), dim3(256), 0, st, S1, S2, B, 1.f / (2.f * (float)B), l);
   hipLaunchKernelGGL(k_ce_mean, dim3(1), dim3(256), 0, st, l, B, loss);
   // dFn = (dS_t Tn + dS_i In) / tau; dTn = dS_t^T Fn / tau; dIn = dS_i^T Fn / tau  (into dF, dT, dI)
   const float s = 1.f / tau;
-  hipLaunchKernelGGL(k_mm_bd<0>, dim3(tb), dim3(256), 0, st, S1, Tn, B, s, 0, dF);
-  hipLaunchKernelGGL(k_mm_bd<0>, dim3(tb), dim3(256), 0, st, S2, In, B, s, 1, dF);
-  hipLaunchKernelGGL(k_mm_bd<1>, dim3(tb), dim3(256), 0, st, S1, Fn, B, s, 0, dT);
-  hipLaunchKernelGGL(k_mm_bd<1>, dim3(tb), dim3(256), 0, st, S2, Fn, B, s, 0, dI);
+  const dim3 gm((unsigned)((B + 15) / 16), kD / 64);
+  hipLaunchKernelGGL(k_mm_bd<0>, gm, dim3(256), 0, st, S1, Tn, B, s, 0, dF);
+  hipLaunchKernelGGL(k_mm_bd<0>, gm, dim3(256), 0, st, S2, In, B, s, 1, dF);
+  hipLaunchKernelGGL(k_mm_bd<1>, gm, dim3(256), 0, st, S1, Fn, B, s, 0, dT);
+  hipLaunchKernelGGL(k_mm_bd<1>, gm, dim3(256), 0, st, S2, Fn, B, s, 0, dI);
   // normalisation backward, in place
   hipLaunchKernelGGL(k_norm_bwd3, dim3(w3), dim3(256), 0, st, Y, nrm, B, dF, dT, dI);
   return hipGetLastError();

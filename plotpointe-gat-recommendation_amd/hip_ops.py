@@ -607,7 +607,11 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
         # kernel (ppgat_gemm_tn_big); column sums and V^T B through the small kernels
         out = gemm_tn_big(A, B)
         cs = colsum(A) if want_colsum else None
-        vout = gemm_tn(V, B)[0] if nv else None
+        vout = None
+        if nv:  # V^T B by the small kernel, V padded to 4 columns (16-byte rows)
+            Vp = torch.zeros(N, 4, dtype=torch.float32, device=A.device)
+            Vp[:, :nv] = V
+            vout = gemm_tn(Vp, B)[0][:nv].contiguous()
         return out, cs, vout
     if V is not None:
         _require(V.is_cuda and V.dtype == torch.float32 and V.dim() == 2 and V.stride(1) == 1 and V.size(0) == N,
