@@ -7,188 +7,198 @@
 //   out_b = y_b / (||y_b|| + 1e-8)     (normalize != 0)
 //
 // fp32 in, fp32 out, v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains, no reduced precision, so
-// the result matches the fp32 reference to accumulation-order rounding).  One 256-thread
-// block = 64 rows: GEMM1 wave w owns hidden columns [64w, 64w+64) (2x2 tiles of 32x32),
-// K streamed in 32-wide LDS chunks (the cat() and the per-row image copy loop of the
-// reference are folded into the chunk loader); h stays on chip (LDS) for GEMM2 (wave w owns
-// output columns [32w, 32w+32)); bias, ReLU and the row L2 norm are epilogues.
-// Shapes: H1 == 4*64 = 256, Do == 4*32 = 128, Dt % 32 == 0, Di % 32 == 0 (the reference's
+// the result matches the fp32 reference to accumulation-order rounding).
+//
+// One 256-thread workgroup = 128 rows, wave w owns rows [32 w, 32 w + 32) end to end:
+//  GEMM1  x streams from HBM straight into MFMA operands (lane (r, hf) holds x[row r][k0 + 8 g
+//         + 4 hf .. + 3] as a float4: the reduction index is permuted identically on both
+//         operands), next chunk's x and W1 in flight while the current chunk's MFMAs run;
+//         W1 chunks (256 x 32) staged in LDS as [n][k] with row stride 36 (b128 reads, no bank
+//         conflicts); the wave's 32 x 256 pre-activation lives in 8 accumulator tiles.  The
+//         cat() and the per-row image copy loop of the reference become the row pointers.
+//  GEMM2  per 64 hidden columns: bias + ReLU, the wave's h slice transposed through its own LDS
+//         patch into the A-operand layout, W2's 128 x 64 slice staged once per workgroup, 4 x 4
+//         x 8 MFMAs into the 32 x 128 output tiles.
+//  norm   row sums of squares reduced inside the wave (DPP over the 32 column lanes).
+// LDS: max(W1 stage 36.9 KB, h patches 34.8 KB + W2 slice 34.8 KB) = 69.6 KB -> two
+// workgroups per CU (8 waves); 4 waves x 32 rows amortise each W1 chunk over 128 rows.
+// Shapes: H1 == 256, Do == 128, Dt % 32 == 0, Di % 32 == 0 (the reference's
 // 384 + 512 -> 256 -> 128).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
 
 #include "ppgat_internal.h"
+#include "ppgat_lanes.h"
 
 namespace ppgat {
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
-constexpr int BM = 64, BK = 32, H1 = 256, DO = 128;
-constexpr int SXP = BK + 1;   // padded row stride (floats) of the LDS chunks
-constexpr int SHP = H1 + 1;   // padded row stride of the on-chip hidden tile
+constexpr int BM = 128, BK = 32, H1 = 256, DO = 128;
+constexpr int LW1 = BK + 4;   // W1 stage row stride ([n][k] image)
+constexpr int HC = 64;        // hidden columns per GEMM2 step
+constexpr int LH = HC + 4;    // h patch / W2 slice row stride
+constexpr int kW1Floats = H1 * LW1;
+constexpr int kG2Floats = 4 * 32 * LH + DO * LH;
+constexpr int kLdsFloats = kW1Floats > kG2Floats ? kW1Floats : kG2Floats;
 
-__device__ __forceinline__ int row_of(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float comp(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int row_of(int q, int hf) { return (q & 3) + 8 * (q >> 2) + 4 * hf; }
 
-__global__ void __launch_bounds__(256) k_fusion_fwd(const float* __restrict__ txt, const float* __restrict__ img,
-                                                    const int32_t* __restrict__ img_index,
-                                                    const float* __restrict__ img_fallback, int64_t B, int Dt, int Di,
-                                                    const float* __restrict__ W1, const float* __restrict__ b1,
-                                                    const float* __restrict__ W2, const float* __restrict__ b2,
-                                                    int normalize, float* __restrict__ out,
-                                                    float* __restrict__ z1_out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sX = smem;                       // [BM][SXP]
-  float* sW = smem + BM * SXP;            // [H1][SXP]  (GEMM2: [DO][SXP])
-  float* sH = sW + H1 * SXP;              // [BM][SHP]
-  float* sN = sH + BM * SHP;              // [4][BM] row sums of squares
+__global__ void __launch_bounds__(256, 2) k_fusion_fwd(const float* __restrict__ txt, const float* __restrict__ img,
+                                                       const int32_t* __restrict__ img_index,
+                                                       const float* __restrict__ img_fallback, int64_t B, int Dt,
+                                                       int Di, const float* __restrict__ W1,
+                                                       const float* __restrict__ b1, const float* __restrict__ W2,
+                                                       const float* __restrict__ b2, int normalize,
+                                                       float* __restrict__ out, float* __restrict__ z1_out) {
+  __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t row0 = (int64_t)blockIdx.x * BM;
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * BM + 32 * w;
   const int K = Dt + Di;
-
-  f32x16 acc[2][2];
+  // this lane's x row (rows past B re-read row B - 1, never stored)
+  const int64_t b = row0 + r < B ? row0 + r : B - 1;
+  const float* trow = txt + b * Dt + 4 * hf;
+  const float* irow;
+  if (Di > 0) {
+    const int32_t ii = img_index ? img_index[b] : (int32_t)b;
+    irow = (ii >= 0 ? img + (int64_t)ii * Di : img_fallback) + 4 * hf;
+  } else {
+    irow = trow;
+  }
+  auto load_x = [&](int k0, float4 (&xv)[4]) {
+    const float* src = k0 < Dt ? trow + k0 : irow + (k0 - Dt);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
+  };
+  float4 wst[8];
+  auto load_w1 = [&](int k0) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  // ---- GEMM1: [BM x K] x [K x H1] ----
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    // X chunk: BM x BK = 512 float4; 2 per thread
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int idx = t * 256 + tid;
-      const int r = idx >> 3, c4 = (idx & 7) * 4;
-      const int64_t b = row0 + r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (b < B) {
-        const int k = k0 + c4;
-        if (k < Dt) {
-          v = *reinterpret_cast<const float4*>(txt + b * Dt + k);
-        } else {
-          const int32_t ii = img_index ? img_index[b] : (int32_t)b;
-          const float* src = ii >= 0 ? img + (int64_t)ii * Di : img_fallback;
-          v = *reinterpret_cast<const float4*>(src + (k - Dt));
-        }
-      }
-      float* d = sX + r * SXP + c4;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    for (int s = 0; s < 8; ++s) {
+      const int e = tid + 256 * s;
+      const int n = e >> 3, k4 = (e & 7) * 4;
+      wst[s] = ld4(W1 + (int64_t)n * K + k0 + k4);
     }
-    // W1 chunk: H1 x BK = 2048 float4; 8 per thread
+  };
+  auto store_w1 = [&]() {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int idx = t * 256 + tid;
-      const int j = idx >> 3, c4 = (idx & 7) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(W1 + (int64_t)j * K + k0 + c4);
-      float* d = sW + j * SXP + c4;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    for (int s = 0; s < 8; ++s) {
+      const int e = tid + 256 * s;
+      st4(&lds[(e >> 3) * LW1 + (e & 7) * 4], wst[s]);
+    }
+  };
+
+  // ---- GEMM1: z[32 rows x 256] per wave ----
+  f32x16 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+  float4 xa[4], xn[4];
+  load_x(0, xa);
+  load_w1(0);
+  store_w1();
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    const bool more = k0 + BK < K;
+    if (more) {
+      load_w1(k0 + BK);
+      load_x(k0 + BK, xn);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4 bv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) bv[t] = ld4(&lds[(32 * t + r) * LW1 + 8 * g + 4 * hf]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mfma(comp(xa[g], s), comp(bv[t], s), acc[t]);
     }
     __syncthreads();
-#pragma unroll 4
-    for (int kk = 0; kk < BK; kk += 2) {
-      const int kq = kk + (lane >> 5);
-      const float a0 = sX[(lane & 31) * SXP + kq];
-      const float a1 = sX[(32 + (lane & 31)) * SXP + kq];
-      const float w0 = sW[(64 * w + (lane & 31)) * SXP + kq];
-      const float w1 = sW[(64 * w + 32 + (lane & 31)) * SXP + kq];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, w0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, w1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, w0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, w1, acc[1][1], 0, 0, 0);
+    if (more) {
+      store_w1();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xa[g] = xn[g];
     }
     __syncthreads();
   }
-  // bias + ReLU -> sH (and the pre-activation for a training backward)
+
+  // ---- GEMM2: out[32 rows x 128] per wave, over four 64-column slices of h ----
+  float* hp = lds + w * 32 * LH;   // this wave's h patch [32 rows][LH]
+  float* w2s = lds + 4 * 32 * LH;  // W2 slice [128][LH]
+  f32x16 acc2[4];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int col = 64 * w + 32 * b + (lane & 31);
+  for (int c = 0; c < H1 / HC; ++c) {
+    // bias + ReLU of accumulator tiles 2c, 2c + 1 -> the patch (and z for a training backward)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int col = HC * c + 32 * tt + r;
       const float bias = b1[col];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * a + row_of(r, lane);
-        const float z = acc[a][b][r] + bias;
-        sH[row * SHP + col] = fmaxf(z, 0.f);
+      for (int q = 0; q < 16; ++q) {
+        const int row = row_of(q, hf);
+        const float z = acc[2 * c + tt][q] + bias;
+        hp[row * LH + 32 * tt + r] = fmaxf(z, 0.f);
         if (z1_out != nullptr && row0 + row < B) z1_out[(row0 + row) * H1 + col] = z;
       }
     }
-  // ---- GEMM2: [BM x H1] x [H1 x DO] ----
-  f32x16 acc2[2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc2[a][r] = 0.f;
-  for (int k0 = 0; k0 < H1; k0 += BK) {
-    // W2 chunk: DO x BK = 1024 float4; 4 per thread
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int idx = t * 256 + tid;
-      const int j = idx >> 3, c4 = (idx & 7) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(W2 + (int64_t)j * H1 + k0 + c4);
-      float* d = sW + j * SXP + c4;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    for (int s = 0; s < 8; ++s) {  // W2[:, 64 c .. 64 c + 63]: 2048 float4, 8 per thread
+      const int e = tid + 256 * s;
+      const int j = e >> 4, k4 = (e & 15) * 4;
+      st4(&w2s[j * LH + k4], ld4(W2 + (int64_t)j * H1 + HC * c + k4));
     }
     __syncthreads();
-#pragma unroll 4
-    for (int kk = 0; kk < BK; kk += 2) {
-      const int kq = kk + (lane >> 5);
-      const float a0 = sH[(lane & 31) * SHP + k0 + kq];
-      const float a1 = sH[(32 + (lane & 31)) * SHP + k0 + kq];
-      const float w0 = sW[(32 * w + (lane & 31)) * SXP + kq];
-      acc2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, w0, acc2[0], 0, 0, 0);
-      acc2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, w0, acc2[1], 0, 0, 0);
+#pragma unroll
+    for (int g = 0; g < HC / 8; ++g) {
+      const float4 av = ld4(&hp[r * LH + 8 * g + 4 * hf]);
+      float4 bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bv[u] = ld4(&w2s[(32 * u + r) * LH + 8 * g + 4 * hf]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc2[u] = mfma(comp(av, s), comp(bv[u], s), acc2[u]);
     }
     __syncthreads();
   }
-  // bias, row L2 norm (over the 4 waves' 32 columns each), store
-  const int col = 32 * w + (lane & 31);
-  const float bias2 = b2[col];
-  float ss[2][16];
+
+  // ---- bias, row L2 norm (inside the wave), store ----
+  float ss[16];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int q = 0; q < 16; ++q) ss[q] = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc2[a][r] += bias2;
-      ss[a][r] = acc2[a][r] * acc2[a][r];
+  for (int u = 0; u < 4; ++u) {
+    const float bias2 = b2[32 * u + r];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc2[u][q] += bias2;
+      ss[q] = fmaf(acc2[u][q], acc2[u][q], ss[q]);
     }
+  }
   if (normalize) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = ss[a][r];
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);  // within the 32-lane half
-        ss[a][r] = v;
-      }
-    if ((lane & 31) == 0) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sN[w * BM + 32 * a + row_of(r, lane)] = ss[a][r];
-    }
-    __syncthreads();
+    for (int q = 0; q < 16; ++q) ss[q] = 1.f / (sqrtf(group_reduce<Op::Sum, 1, 16>(ss[q])) + 1e-8f);
   }
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int q = 0; q < 16; ++q) {
+    const int64_t row = row0 + row_of(q, hf);
+    if (row >= B) continue;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = 32 * a + row_of(r, lane);
-      float v = acc2[a][r];
-      if (normalize) {
-        const float n2 = ((sN[row] + sN[BM + row]) + sN[2 * BM + row]) + sN[3 * BM + row];
-        v = v / (sqrtf(n2) + 1e-8f);
-      }
-      if (row0 + row < B) out[(row0 + row) * DO + col] = v;
-    }
+    for (int u = 0; u < 4; ++u) out[row * DO + 32 * u + r] = normalize ? acc2[u][q] * ss[q] : acc2[u][q];
+  }
 }
 
 }  // namespace
 
-size_t fusion_lds_bytes() { return (size_t)(BM * SXP + H1 * SXP + BM * SHP + 4 * BM) * 4; }
 
 bool fusion_shape_ok(int Dt, int Di, int h1, int d_out) {
   return h1 == H1 && d_out == DO && Dt >= 0 && Di >= 0 && Dt % BK == 0 && Di % BK == 0 && Dt + Di > 0;
@@ -198,15 +208,8 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
                       int normalize, float* out, float* z1_out, hipStream_t st) {
   if (B == 0) return hipSuccess;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_fusion_fwd),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)fusion_lds_bytes());
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(k_fusion_fwd, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), fusion_lds_bytes(), st, txt, img,
-                     img_index, img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);
+  hipLaunchKernelGGL(k_fusion_fwd, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), 0, st, txt, img, img_index,
+                     img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);
   return hipGetLastError();
 }
 

@@ -31,6 +31,16 @@ def _check_dev(name: str, t: torch.Tensor, dtype, device=None):
         _require(t.device == device, f"{name}: on {t.device}, expected {device}")
 
 
+def _check_rows(name: str, t: torch.Tensor, dtype, device=None):
+    """A 2-D operand passed with a row stride (column slices allowed): unit column stride."""
+    _require(isinstance(t, torch.Tensor), f"{name}: expected a tensor")
+    _require(t.is_cuda, f"{name}: ppgat runs on ROCm devices only (got {t.device}); there is no CPU path")
+    _require(t.dtype == dtype, f"{name}: expected {dtype}, got {t.dtype}")
+    _require(t.dim() == 2 and (t.stride(1) == 1 or t.size(1) <= 1), f"{name}: 2-D with unit column stride")
+    if device is not None:
+        _require(t.device == device, f"{name}: on {t.device}, expected {device}")
+
+
 # ---------------------------------------------------------------------------
 # graph preprocessing
 # ---------------------------------------------------------------------------
@@ -608,8 +618,8 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
         out = gemm_tn_big(A, B)
         cs = colsum(A) if want_colsum else None
         vout = None
-        if nv:  # V^T B by the small kernel, V padded to 4 columns (16-byte rows)
-            Vp = torch.zeros(N, 4, dtype=torch.float32, device=A.device)
+        if nv:  # V^T B by the small kernel, V padded to a multiple of 4 columns (16-byte rows)
+            Vp = torch.zeros(N, (nv + 3) // 4 * 4, dtype=torch.float32, device=A.device)
             Vp[:, :nv] = V
             vout = gemm_tn(Vp, B)[0][:nv].contiguous()
         return out, cs, vout
@@ -692,8 +702,8 @@ def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: floa
             bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """alpha x B (+ bias): B [K, n] row-major (b_layout 0) or [n, K] (b_layout 1: x B^T)."""
     lib = _lib.load()
-    _check_dev("x", x, torch.float32)
-    _check_dev("B", B, torch.float32, x.device)
+    _check_rows("x", x, torch.float32)
+    _check_rows("B", B, torch.float32, x.device)
     M, K = x.shape
     y = out if out is not None else torch.empty(M, n, dtype=torch.float32, device=x.device)
     ldb = B.stride(0)
@@ -710,8 +720,8 @@ def gemm_tn_big_supported(ma: int, nb: int) -> bool:
 def gemm_tn_big(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     """A [M, ma]^T B [M, nb] on the matrix cores (ppgat_gemm_tn_big), deterministic."""
     lib = _lib.load()
-    _check_dev("A", A, torch.float32)
-    _check_dev("B", B, torch.float32, A.device)
+    _check_rows("A", A, torch.float32)
+    _check_rows("B", B, torch.float32, A.device)
     M, ma = A.shape
     nb = B.size(1)
     nbytes = ctypes.c_size_t(0)
@@ -725,10 +735,14 @@ def gemm_tn_big(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
 
 
 def colsum(Y: torch.Tensor) -> torch.Tensor:
-    """Column sums of Y [n, c] (ppgat_colsum, c in {128, 256}; torch otherwise)."""
+    """Column sums of Y [n, c] (ppgat_colsum over 128- or 256-column slabs; torch for widths not a multiple of 128)."""
     lib = _lib.load()
-    _check_dev("Y", Y, torch.float32)
+    _check_rows("Y", Y, torch.float32)
     n, c = Y.shape
+    if c not in (128, 256) and c % 256 == 0:  # wider: 256-column slabs
+        return torch.cat([colsum(Y[:, s:s + 256]) for s in range(0, c, 256)])
+    if c not in (128, 256) and c % 128 == 0:
+        return torch.cat([colsum(Y[:, s:s + 128]) for s in range(0, c, 128)])
     if c not in (128, 256):
         return Y.sum(0)
     nbytes = ctypes.c_size_t(0)

@@ -161,8 +161,9 @@ def test_fused_layer_equals_unfused(pkg, cuda):
 
 
 def test_gemm_tn_large_shape_deterministic(pkg, cuda):
-    """Beyond one 128 x 128 tile gemm_tn goes through the library GEMM: fp32-accurate and
-    bitwise reproducible run to run (config 5's 1024 x 256 weight gradient, scaled down)."""
+    """Beyond one 128 x 128 tile gemm_tn goes through the matrix-core TN kernel
+    (ppgat_gemm_tn_big) with column-sliced operands: fp32-accurate and bitwise reproducible
+    run to run (config 5's 1024 x 256 weight gradient, scaled down)."""
     ops = _ops()
     g = torch.Generator().manual_seed(21)
     N = 100_000
