@@ -494,6 +494,19 @@ int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, con
                             const float* att_dst, int heads, int channels, int in_channels, float* dW, float* datt_src,
                             float* datt_dst, void* stream);
 
+/* ---- validation / debug build -----------------------------------------------------------
+ * ppgat_check_index_range: *n_bad = number of entries of idx (int32 when elem_bytes == 4,
+ *   int64 when 8) outside [lo, hi); synchronises the stream (a validation tool, not for use
+ *   inside a captured graph).  Used by the Python layer to validate graph views and exchange
+ *   plans when the library is a debug build.
+ * ppgat_debug_build: 1 for libppgat_debug.so (make debug: -O1 -g -DPPGAT_DEBUG=1), whose entry
+ *   points validate the index inputs whose bounds they know (BPR triples, eval users and
+ *   candidates, serving histories) and synchronise after their kernels, so an asynchronous
+ *   fault is reported by the entry point that launched it; 0 for libppgat.so. */
+int ppgat_debug_build(void);
+int ppgat_check_index_range(const void* idx, int elem_bytes, int64_t n, int64_t lo, int64_t hi, int64_t* n_bad,
+                            void* stream);
+
 /* ---- in-process kernel timing (HIP events on the launch stream) --------- */
 #define PPGAT_K_CSR 0
 #define PPGAT_K_SCORES 1

@@ -113,6 +113,8 @@ SIGNATURES = {
                                      c_f, c_f, c_u64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_xgat_bwd_epilogue": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp]),
     "ppgat_xgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_debug_build": (c_int, []),
+    "ppgat_check_index_range": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, ctypes.POINTER(c_i64), c_vp]),
     "ppgat_profile_enable": (c_int, [c_int]),
     "ppgat_profile_reset": (c_int, []),
     "ppgat_profile_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
@@ -170,6 +172,27 @@ def ptr(t) -> int:
 def stream_handle(device) -> int:
     import torch
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def debug_build() -> bool:
+    """True when the loaded library is libppgat_debug.so (PPGAT_LIB=.../libppgat_debug.so)."""
+    return bool(load().ppgat_debug_build())
+
+
+def check_index_range(t, lo: int, hi: int, what: str):
+    """Raise if any entry of the int32/int64 device tensor t is outside [lo, hi)
+    (ppgat_check_index_range; synchronises).  The debug build's graph/plan validation."""
+    import torch
+    lib = load()
+    if t is None or t.numel() == 0:
+        return
+    if t.dtype not in (torch.int32, torch.int64) or not t.is_cuda or not t.is_contiguous():
+        raise RuntimeError(f"check_index_range({what}): contiguous int32/int64 device tensor required")
+    n_bad = ctypes.c_int64(0)
+    check(lib.ppgat_check_index_range(t.data_ptr(), t.element_size(), t.numel(), int(lo), int(hi), ctypes.byref(n_bad),
+                                      stream_handle(t.device)), "check_index_range")
+    if n_bad.value:
+        raise RuntimeError(f"{what}: {n_bad.value} of {t.numel()} indices outside [{lo}, {hi})")
 
 
 def profile_enable(on: bool = True):

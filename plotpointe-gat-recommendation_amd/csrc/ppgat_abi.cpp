@@ -76,6 +76,10 @@ struct Timed {
     if (a) (void)hipEventRecord(a, st);
   }
   ~Timed() {
+#if PPGAT_DEBUG
+    // debug build: an asynchronous fault surfaces at the entry point that launched it
+    (void)hipStreamSynchronize(st);
+#endif
     if (!a) return;
     std::lock_guard<std::mutex> lk(g_prof.mu);
     hipEvent_t b = g_prof.get();
@@ -85,11 +89,38 @@ struct Timed {
   }
 };
 
+#ifndef PPGAT_DEBUG
+#define PPGAT_DEBUG 0
+#endif
+
+// debug build: index inputs with known bounds are validated before any launch
+int debug_range(const void* idx, int elem_bytes, int64_t n, int64_t lo, int64_t hi, const char* who, hipStream_t st) {
+  if (!PPGAT_DEBUG || n <= 0 || idx == nullptr) return 0;
+  int64_t bad = 0;
+  hipError_t e = ppgat::count_out_of_range(idx, elem_bytes, n, lo, hi, &bad, st);
+  if (e != hipSuccess) return hip_fail(e, who);
+  if (bad)
+    return fail(PPGAT_ERR_INVALID, std::string(who) + ": " + std::to_string(bad) + " of " + std::to_string(n) +
+                                       " indices outside [" + std::to_string(lo) + ", " + std::to_string(hi) + ")");
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
 
 int ppgat_version(void) { return 3; }
+
+int ppgat_debug_build(void) { return PPGAT_DEBUG ? 1 : 0; }
+
+int ppgat_check_index_range(const void* idx, int elem_bytes, int64_t n, int64_t lo, int64_t hi, int64_t* n_bad,
+                            void* stream) {
+  if (!n_bad || n < 0 || (elem_bytes != 4 && elem_bytes != 8) || (n > 0 && !idx))
+    return fail(PPGAT_ERR_INVALID, "check_index_range: bad arguments (elem_bytes 4 or 8)");
+  hipError_t e = ppgat::count_out_of_range(idx, elem_bytes, n, lo, hi, n_bad, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "check_index_range");
+  return PPGAT_OK;
+}
 
 const char* ppgat_last_error(void) { return g_err.c_str(); }
 
@@ -407,6 +438,12 @@ int ppgat_bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
                   float* loss, float* coef, int32_t* bad_count, void* workspace, size_t workspace_bytes,
                   void* stream) {
   if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_fwd")) return rc;
+  {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (int rc = debug_range(u, 8, n_samples, 0, n_users, "bpr_fwd: u", st)) return rc;
+    if (int rc = debug_range(i, 8, n_samples, 0, n_items, "bpr_fwd: i", st)) return rc;
+    if (int rc = debug_range(j, 8, n_samples, 0, n_items, "bpr_fwd: j", st)) return rc;
+  }
   if (row_map == nullptr ? n_rows != n_users + n_items : n_rows < 1)
     return fail(PPGAT_ERR_INVALID, "bpr_fwd: n_rows must be n_users + n_items without a row_map");
   if (loss_kind != 0 && loss_kind != 1) return fail(PPGAT_ERR_INVALID, "bpr_fwd: loss_kind must be 0 (bpr) or 1 (bce)");
@@ -701,6 +738,10 @@ int ppgat_sampled_rank(const float* Z, int64_t n_rows, int64_t n_users, int64_t 
   if (row_map == nullptr && n_rows != n_users + n_items)
     return fail(PPGAT_ERR_INVALID, "sampled_rank: n_rows must be n_users + n_items without a row_map");
   if (!Z || (n_eval > 0 && (!users || !cands || !rank))) return fail(PPGAT_ERR_INVALID, "sampled_rank: null pointer");
+  if (int rc = debug_range(users, 8, n_eval, 0, n_users, "sampled_rank: users", static_cast<hipStream_t>(stream)))
+    return rc;
+  if (int rc = debug_range(cands, 8, n_eval * n_cand, 0, n_items, "sampled_rank: cands", static_cast<hipStream_t>(stream)))
+    return rc;
   hipError_t e = ppgat::sampled_rank(Z, n_users, n_items, row_map, channels, users, cands, n_eval, n_cand, rank,
                                      static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "sampled_rank");
@@ -726,6 +767,15 @@ int ppgat_serve_topk(const float* item_vecs, int64_t n_items, int channels, cons
   size_t need = 0;
   ppgat_serve_topk_workspace_bytes(n_items, channels, n_users, &need);
   if (!workspace || workspace_bytes < need) return fail(PPGAT_ERR_INVALID, "serve_topk: workspace too small");
+  if (n_users > 0 && max_hist > 0) {
+    int64_t n_hist = 0;  // the CSR's last offset
+    if (PPGAT_DEBUG) {
+      if (hipMemcpy(&n_hist, hist_ptr + n_users, sizeof(n_hist), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(PPGAT_ERR_HIP, "serve_topk: reading hist_ptr");
+    }
+    if (int rc = debug_range(hist_items, 8, n_hist, 0, n_items, "serve_topk: hist_items", static_cast<hipStream_t>(stream)))
+      return rc;
+  }
   float* U = static_cast<float*>(workspace);
   float* scores = reinterpret_cast<float*>(static_cast<char*>(workspace) + align_up((size_t)n_users * channels * 4));
   hipError_t e = ppgat::serve_topk(item_vecs, n_items, channels, hist_ptr, hist_items, max_hist, n_users, k, U, scores,

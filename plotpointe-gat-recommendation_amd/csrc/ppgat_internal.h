@@ -137,6 +137,10 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
                       int normalize, float* out, float* z1_out, hipStream_t st);
 
+// index-range validation (ppgat_debug.hip)
+hipError_t count_out_of_range(const void* idx, int elem_bytes, int64_t n, int64_t lo, int64_t hi, int64_t* n_bad,
+                              hipStream_t st);
+
 // fusion MLP training: InfoNCE loss + backward, ReLU/dropout (ppgat_infonce.hip)
 bool infonce_shape_ok(int64_t B, int D);
 size_t infonce_workspace_bytes(int64_t B);

@@ -417,6 +417,14 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     bwd_view = LocalView(R, G.rowptr.contiguous(), col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
     hg = HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan_u, plan_i, fwd_view, bwd_view, local_of,
                    owner, {}, torch.from_numpy(halo_i - nu).to(dev))
+    if dev.type == "cuda" and _lib.debug_build():  # debug build: plans and views within bounds
+        for pname, plan in (("plan_u", plan_u), ("plan_i", plan_i)):
+            _lib.check_index_range(plan.send_idx, 0, n_own, f"halo.{pname}.send_idx")
+            _lib.check_index_range(plan.ret_pos, 0, max(plan.n_send, 1), f"halo.{pname}.ret_pos")
+        _lib.check_index_range(col, 0, R, "halo.col")
+        _lib.check_index_range(row, 0, n_own, "halo.row")
+        _lib.check_index_range(slot, 0, max(El, 1), "halo.dz_slot")
+        _lib.check_index_range(hg.halo_items, 0, N - nu, "halo.halo_items")
     if sched_builder is not None:
         fwd_view.fwd_sched = sched_builder(rowptr_own, El)
         bwd_view.bwd_sched = sched_builder(bwd_view.colptr, El)

@@ -157,7 +157,20 @@ def csr_build(edge_index: torch.Tensor, n_nodes: int, max_edges: int = MAX_EDGES
     with torch.cuda.device(dev):
         fs = schedule_build(rowptr, E, max_edges)
         bs = schedule_build(colptr, E, max_edges)
-    return CSRGraph(N, E, rowptr, col[:E], csr_eid[:E], colptr, row[:E], csc_eid[:E], csc2csr[:E], fs, bs)
+    G = CSRGraph(N, E, rowptr, col[:E], csr_eid[:E], colptr, row[:E], csc_eid[:E], csc2csr[:E], fs, bs)
+    if _lib.debug_build():
+        debug_validate_graph(G)
+    return G
+
+
+def debug_validate_graph(G: "CSRGraph"):
+    """Debug build (libppgat_debug.so): every index array of a graph view within its bounds
+    before any kernel reads it (ppgat_check_index_range)."""
+    N, E = G.n_nodes, G.n_edges
+    for name, t, hi in (("rowptr", G.rowptr, E + 1), ("colptr", G.colptr, E + 1), ("col", G.col, N),
+                        ("row", G.row, N), ("csr_eid", G.csr_eid, E), ("csc_eid", G.csc_eid, E),
+                        ("csc2csr", G.csc2csr, E)):
+        _lib.check_index_range(t, 0, hi, f"graph.{name}")
 
 
 class _GraphCache:

@@ -138,6 +138,35 @@ def build_model(cfg: Config, n_users: int, n_items: int, feat_dim: int):
     return m
 
 
+class _GlobalRows(torch.nn.Module):
+    """A row-sharded model seen as the single-GPU one by eval_sampled / export: forward returns
+    every node's rows on every rank (an all_gather; evaluation only, not the training path)."""
+
+    def __init__(self, sharded, to_global):
+        super().__init__()
+        self.sharded, self.to_global = sharded, to_global
+        self.n_users, self.n_items = sharded.n_users, sharded.n_items
+
+    def forward(self, item_feats, edge_index=None):
+        return self.to_global(self.sharded(item_feats), self.sharded.dg, self.sharded.comm)
+
+
+def _init_distributed(args):
+    """torch.distributed from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*): one
+    process per GPU; several ranks may share a GPU (gloo tests)."""
+    import torch.distributed as tdist
+    world = int(os.environ.get("WORLD_SIZE", args.world_size))
+    if world != args.world_size:
+        raise RuntimeError(f"--world-size {args.world_size} but WORLD_SIZE={world} (launch with torchrun)")
+    rank = int(os.environ.get("RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(device)
+    kw = {"device_id": device} if args.backend == "nccl" else {}
+    tdist.init_process_group(args.backend, rank=rank, world_size=world, **kw)
+    return rank, world, device
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="Train GAT (MI355X-native)")
     ap.add_argument("--project-id", default="local")
@@ -165,6 +194,12 @@ def main(argv=None):
     ap.add_argument("--fast-sampler", action="store_true",
                     help="BPR triples drawn on the GPU (ppgat_bpr_sample: same rule, counter-based stream)")
     ap.add_argument("--synthetic", choices=["cfg1", "cfg2"], default=None)
+    ap.add_argument("--world-size", type=int, default=1,
+                    help="ranks (one process per GPU, launched by torchrun); > 1 shards the model (dist.py)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend (nccl = RCCL on ROCm; gloo only for tests)")
+    ap.add_argument("--partition", choices=["auto", "replicated", "halo"], default="auto",
+                    help="auto: users sharded / items replicated for U-I graphs, halo otherwise")
     args = ap.parse_args(argv)
     cfg = Config(project_id=args.project_id, region=args.region, staging_prefix=args.staging_prefix,
                  graphs_prefix=args.graphs_prefix, embeddings_prefix=args.embeddings_prefix,
@@ -177,9 +212,19 @@ def main(argv=None):
     set_seed(cfg.seed)
     if not torch.cuda.is_available():
         raise RuntimeError("this trainer runs the HIP kernels: a ROCm GPU is required")
-    device = torch.device("cuda")
+    rank, world, device = 0, 1, torch.device("cuda")
+    if args.world_size > 1:
+        if cfg.model_family != "gat_pyg":
+            raise NotImplementedError("--world-size > 1: the sharded model is PyGGAT (--model-family gat_pyg)")
+        rank, world, device = _init_distributed(args)
+    lead = rank == 0
     tag = "GAT-PYG" if cfg.model_family == "gat_pyg" else "GAT-CUSTOM"
     run_id = f"{cfg.model_family}_d{cfg.hidden_dim}_{int(time.time())}"
+    if world > 1:  # one run id (checkpoint / metrics names) for every rank: rank 0's
+        import torch.distributed as tdist
+        ids = [run_id]
+        tdist.broadcast_object_list(ids, src=0)
+        run_id = ids[0]
     if args.structured_logs:
         log_event("run_start", run_id=run_id, model_family=cfg.model_family,
                   config={**cfg.__dict__, "device": str(device)})
@@ -189,7 +234,28 @@ def main(argv=None):
     item_feats = torch.tensor(feats_np, dtype=torch.float32).to(device)
     assert item_feats.shape[0] == n_items
     model = build_model(cfg, n_users, n_items, item_feats.size(1)).to(device)
-    opt = torch.optim.Adam(model.parameters(), lr=cfg.lr, weight_decay=cfg.l2)
+    sharded = None
+    if world > 1:
+        # every rank built the same full model (same seed); each keeps its shard
+        import importlib
+        dist_mod = importlib.import_module(model_mod.__name__.rsplit(".", 1)[0] + ".dist")
+        comm = dist_mod.Comm()
+        part = args.partition
+        if part == "auto":
+            part = "replicated"
+        if part == "replicated":
+            dg = dist_mod.build_replicated_graph(edge_index, n_users + n_items, n_users, world, rank)
+            sharded = dist_mod.ReplicatedPyGGAT(model, dg, comm)
+            loss_fn, to_global = dist_mod.replicated_bpr_loss, dist_mod.replicated_rows_to_global
+        else:
+            dg = dist_mod.build_halo_graph(edge_index, n_users + n_items, n_users, world, rank)
+            sharded = dist_mod.HaloPyGGAT(model, dg, comm)
+            loss_fn, to_global = dist_mod.halo_bpr_loss, dist_mod.halo_rows_to_global
+        eval_model = _GlobalRows(sharded, to_global)
+        opt = torch.optim.Adam(sharded.parameters(), lr=cfg.lr, weight_decay=cfg.l2)
+    else:
+        eval_model = model
+        opt = torch.optim.Adam(model.parameters(), lr=cfg.lr, weight_decay=cfg.l2)
     out_dir = _local(cfg.models_prefix)
     (out_dir / "checkpoints").mkdir(parents=True, exist_ok=True)
     best_path = out_dir / "checkpoints" / f"{run_id}.pt"
@@ -213,32 +279,63 @@ def main(argv=None):
             u = torch.from_numpy(u_arr).long().to(device)
             i = torch.from_numpy(i_arr).long().to(device)
             j = torch.from_numpy(j_arr).long().to(device)
-        Z = model(item_feats, edge_index)
-        loss = model_mod.bpr_loss(Z, n_users, u, i, j, cfg.loss)
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-        print(f"[{tag}][Epoch {epoch}] loss={loss.item():.4f} ({cfg.loss})")
-        model.eval()
-        val_metrics = evaluation.eval_sampled(model, cfg, item_feats, edge_index, tr, va, fast=args.fast_eval,
+        if sharded is None:
+            Z = model(item_feats, edge_index)
+            loss = model_mod.bpr_loss(Z, n_users, u, i, j, cfg.loss)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            loss_val = float(loss.item())
+        else:
+            # each rank: its own users' triples (the sum over ranks is the reference's mean),
+            # dense gradients all-reduced, user rows updated by their owner
+            sharded.train()
+            Zl = sharded(item_feats)
+            loss = loss_fn(Zl, sharded.dg, sharded.comm, u, i, j, n_users, n_items, loss=cfg.loss)
+            opt.zero_grad()
+            loss.backward()
+            sharded.allreduce_grads()
+            opt.step()
+            tot = loss.detach().clone()
+            sharded.comm.all_reduce_(tot)
+            loss_val = float(tot.item())
+        if lead:
+            print(f"[{tag}][Epoch {epoch}] loss={loss_val:.4f} ({cfg.loss})")
+        eval_model.eval()
+        val_metrics = evaluation.eval_sampled(eval_model, cfg, item_feats, edge_index, tr, va, fast=args.fast_eval,
                                               sampler=dev_sampler if args.device_eval else None,
                                               seed=cfg.seed + epoch)
-        print(f"[{tag}][Epoch {epoch}] val: {val_metrics}")
-        if args.structured_logs:
-            log_event("epoch_end", run_id=run_id, epoch=epoch, loss=float(loss.item()), val=val_metrics)
+        if lead:
+            print(f"[{tag}][Epoch {epoch}] val: {val_metrics}")
+        if args.structured_logs and lead:
+            log_event("epoch_end", run_id=run_id, epoch=epoch, loss=loss_val, val=val_metrics)
         if val_metrics.get("ndcg@20", 0.0) > best:
             best = val_metrics.get("ndcg@20", 0.0)
-            torch.save({"state_dict": model.state_dict(), "config": cfg.__dict__}, best_path)
-            print(f"[{tag}] Saved new best checkpoint")
+            sd = model.state_dict() if sharded is None else sharded.full_state_dict()  # collective when sharded
+            if lead:
+                torch.save({"state_dict": sd, "config": cfg.__dict__}, best_path)
+                print(f"[{tag}] Saved new best checkpoint")
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.barrier()  # rank 0's checkpoint is on disk
     ckpt = torch.load(best_path, map_location=device, weights_only=True)
     model.load_state_dict(ckpt["state_dict"])
-    model.eval()
-    test_metrics = evaluation.eval_sampled(model, cfg, item_feats, edge_index, tr, te, fast=args.fast_eval,
+    if sharded is not None:
+        with torch.no_grad():
+            sharded.user_emb_local.copy_(model.user_emb.weight[sharded.u0:sharded.u1])
+    eval_model.eval()
+    test_metrics = evaluation.eval_sampled(eval_model, cfg, item_feats, edge_index, tr, te, fast=args.fast_eval,
                                            sampler=dev_sampler if args.device_eval else None, seed=cfg.seed)
-    print(f"[{tag}] test: {test_metrics}")
+    if lead:
+        print(f"[{tag}] test: {test_metrics}")
     out = {"best_val_ndcg@20": float(best), "val": val_metrics, "test": test_metrics, "config": cfg.__dict__,
            "notes": f"One-backward-per-epoch with S sampled BPR triples; features={cfg.item_features}; "
                     f"loss={cfg.loss}"}
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+        if not lead:
+            return out
     with open(metrics_path, "w") as f:
         json.dump(out, f, indent=2)
     print(f"[{tag}] Complete. Wrote {best_path} and {metrics_path}")

@@ -22,6 +22,21 @@ def test_all_header_symbols_exported(pkg):
     assert set(names) == set(pkg._lib.SIGNATURES)
 
 
+def test_debug_build_exports_the_same_abi(pkg):
+    """libppgat_debug.so (make debug, built by __graft_entry__.build): same symbols, flagged."""
+    path = ROOT / "plotpointe-gat-recommendation_amd" / "libppgat_debug.so"
+    if not path.exists():
+        pytest.skip("debug library not built (make -C plotpointe-gat-recommendation_amd/csrc debug)")
+    dbg = ctypes.CDLL(str(path))
+    for n in _declared():
+        assert hasattr(dbg, n), n
+    assert dbg.ppgat_debug_build() == 1
+    assert pkg._lib.load().ppgat_debug_build() == 0
+    dbg.ppgat_check_index_range.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    assert dbg.ppgat_check_index_range(None, 3, 0, 0, 1, None, None) == 1  # invalid arguments, no GPU call
+
+
 def test_version_and_channels(pkg):
     lib = pkg._lib.load()
     assert lib.ppgat_version() == 3
