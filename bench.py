@@ -53,7 +53,9 @@ def parse():
                          "so the per-GPU work is the same at every N)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="committed PMC summary (default: profiles/r01_pmc_traffic.json for configs 2/3, "
+                         "profiles/r02/cfg5_pmc_traffic.json for config 5 at its default scale)")
     ap.add_argument("--partition", choices=["auto", "replicated", "halo"], default="auto",
                     help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
                          "'halo' = users and items row-sharded, RCCL all_to_all of the halo rows per layer "
@@ -351,8 +353,11 @@ def main():
     try:
         if dist_path:
             raise LookupError("the committed PMC summary is for the unsharded graph")
-        tj_ = json.loads(Path(args.traffic_json).read_text())
-        if tj_.get("config", 2) == args.config:  # PMC summaries are per workload
+        tj_path = args.traffic_json or str(ROOT / "profiles" / ("r02/cfg5_pmc_traffic.json" if args.config == 5
+                                                                else "r01_pmc_traffic.json"))
+        tj_ = json.loads(Path(tj_path).read_text())
+        if tj_.get("config", 2) == args.config and tj_.get("scale", scale if args.config == 5 else None) == (
+                scale if args.config == 5 else None):  # PMC summaries are per workload
             traffic = tj_.get("per_launch_bytes", {}).get(dom)
     except Exception:
         pass

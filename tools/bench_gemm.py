@@ -35,8 +35,11 @@ def main():
     ap.add_argument("--n", type=int, default=255_404)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--cfg5", action="store_true", help="config-5 share shapes of ppgat_gemm_nn, both B layouts")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if args.cfg5:
+        return cfg5(dev, args.iters)
     N = args.n
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(N, 128, device=dev, generator=g)
@@ -72,6 +75,27 @@ def main():
             if lib.ppgat_debug_clock_mhz(slot, 4096, ctypes.byref(mhz)) == 0:
                 out[f"clock_mhz_{name}"] = mhz.value
     print(json.dumps(out, indent=1))
+
+
+def cfg5(dev, iters):
+    """out = agg W_t / H ([1.875M, 1024] x [1024, 256]) and gt = g W_g ([1.875M, 256] x [256, 1024]),
+    B given as [K][N] (layout 0) or as its transpose [N][K] (layout 1)."""
+    M = 1_875_000
+    g = torch.Generator(device=dev).manual_seed(0)
+    res = {}
+    for name, K, Nc in (("out_1024x256", 1024, 256), ("gt_256x1024", 256, 1024)):
+        X = torch.randn(M, K, device=dev, generator=g)
+        B0 = torch.randn(K, Nc, device=dev, generator=g)
+        B1 = B0.t().contiguous()
+        y0 = ops.gemm_nn(X, B0, 0, Nc)
+        y1 = ops.gemm_nn(X, B1, 1, Nc)
+        assert torch.equal(y0, y1), name  # same products, same order
+        flop = 2.0 * M * K * Nc
+        for lay, B in ((0, B0), (1, B1)):
+            us = timeit(lambda: ops.gemm_nn(X, B, lay, Nc, out=y0), iters)
+            res[f"{name}_layout{lay}"] = {"us": us, "tflops": flop / us / 1e6}
+        del X, y0, y1
+    print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":

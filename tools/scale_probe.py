@@ -40,10 +40,11 @@ class NullComm:
         return t
 
     def all_to_all_rows(self, t, send_counts, recv_counts, out=None):
-        # stub: the received rows are left as they are (uninitialised); timing only
+        # stub: the received rows are zeros (valid row ids for the loss plan's id exchange);
+        # timing only
         n = int(sum(recv_counts))
         if out is None:
-            out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            out = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return out
 
     def all_to_all_counts(self, counts):
