@@ -160,8 +160,9 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
                                              int mode, float slope, float eps, float p, float inv_keep,
                                              uint64_t seed, float* __restrict__ out, float* __restrict__ m_out,
                                              float* __restrict__ invl_out, float* __restrict__ agg_out,
-                                             float* __restrict__ partial) {
+                                             float* __restrict__ partial, uint64_t* __restrict__ seed_out) {
   if (p > 0.f) seed = epoch_seed(seed);
+  if (seed_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) seed_out[0] = seed;  // the backward's mask seed
   using G = Geo<C>;
   __shared__ int2 rec[4][64];  // per wave: chunk edges {src row, weight}
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -255,8 +256,9 @@ __global__ void __launch_bounds__(256) k_fwd_short(Items it, int64_t first, cons
                                                    const float* __restrict__ bias, int mode, float slope, float eps,
                                                    float p, float inv_keep, uint64_t seed, float* __restrict__ out,
                                                    float* __restrict__ m_out, float* __restrict__ invl_out,
-                                                   float* __restrict__ agg_out) {
+                                                   float* __restrict__ agg_out, uint64_t* __restrict__ seed_out) {
   if (p > 0.f) seed = epoch_seed(seed);
+  if (seed_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) seed_out[0] = seed;  // the backward's mask seed
   constexpr int NV = C / 64;  // float4 columns per lane
   static_assert(NV >= 1, "k_fwd_short: C >= 64");
   __shared__ int2 rec[4][64];
@@ -1023,19 +1025,22 @@ hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid
                       float* agg, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
                       hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  if (seed_out != nullptr) hipLaunchKernelGGL(k_seed_snap, dim3(1), dim3(64), 0, st, seed, seed_out);
+  // the effective mask seed is written by block 0 of the first edge kernel launched (no
+  // separate launch); a graph without items snapshots it with k_seed_snap
   const int64_t n_long = short_begin(it, heads, C);
   const Items its{it.row, it.beg, it.end, n_long, it.n_hub_items};
+  if (seed_out != nullptr && it.n_items == 0) hipLaunchKernelGGL(k_seed_snap, dim3(1), dim3(64), 0, st, seed, seed_out);
   if (n_long > 0) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd<CC>, dim3(blocks_for(n_long * 64)), dim3(256), 0, st, its, col,
                                            eid, heads, h, ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m,
-                                           invl, agg, partial));
+                                           invl, agg, partial, seed_out));
   }
   if (n_long < it.n_items) {
     const Items all{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
     const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16);  // 4 waves x 4 items per block
     PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_fwd_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, col, eid, h,
-                                             ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m, invl, agg));
+                                             ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m, invl, agg,
+                                             n_long > 0 ? nullptr : seed_out));
   }
   if (n_hubs > 0) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,

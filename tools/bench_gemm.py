@@ -56,6 +56,8 @@ def main():
         "proj_dx": lambda: pkg._lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), 128, N, 128, W.data_ptr(), 128, 128,
                                                                       a_s.data_ptr(), a_d.data_ptr(), S.data_ptr(), 2,
                                                                       dx.data_ptr(), 128, st), "dx"),
+        "nn_fwd": lambda: ops.gemm_nn(x, W, 1, 128),
+        "nn_dx": lambda: ops.gemm_nn(D, W, 0, 128),
         "tn_dW_V": lambda: ops.gemm_tn(D, x, V=S),
         "tn_plain": lambda: ops.gemm_tn(D, x),
         "blas_fwd": lambda: torch.nn.functional.linear(x, W),

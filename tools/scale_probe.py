@@ -39,12 +39,15 @@ class NullComm:
     def all_reduce_(self, t, op=None):
         return t
 
+    own_id = 0  # a node id this rank owns (set after the graph is built): the stubbed id exchange
+
     def all_to_all_rows(self, t, send_counts, recv_counts, out=None):
-        # stub: the received rows are zeros (valid row ids for the loss plan's id exchange);
-        # timing only
+        # stub: received rows are zeros, received ids are an id this rank owns (so the loss
+        # plan's requests resolve to local rows); timing only
         n = int(sum(recv_counts))
         if out is None:
-            out = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            fill = self.own_id if not t.is_floating_point() else 0
+            out = torch.full((n,) + tuple(t.shape[1:]), fill, dtype=t.dtype, device=t.device)
         return out
 
     def all_to_all_counts(self, counts):
@@ -81,6 +84,7 @@ def main():
         n_edges = dg.view.n_fwd_edges
     else:
         dg = D.build_halo_graph(ei, g.n_nodes, g.n_users, args.world, args.rank)
+        comm.own_id = int(dg.owned()[1][0])  # first own item
         model = D.HaloPyGGAT(full, dg, comm)
         loss_fn = D.halo_bpr_loss
         n_edges = dg.fwd_view.n_fwd_edges

@@ -10,5 +10,6 @@ for rk in 0 7; do
   run probe_halo_r$rk 150 python -u tools/scale_probe.py --world 8 --rank $rk --partition halo --graph
 done
 run gemm5 300 python -u tools/bench_gemm.py --cfg5 --iters 5
+run gemm2 120 python -u tools/bench_gemm.py
 run bench5 400 python -u bench.py --config 5 --steps 10 --warmup 3
 echo done
