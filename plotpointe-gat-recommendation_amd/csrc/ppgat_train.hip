@@ -618,9 +618,12 @@ __global__ void __launch_bounds__(1024) k_split_reduce(SplitReduceArg arg, int64
 bool bpr_channels_ok(int C) { return C == 32 || C == 64 || C == 128 || C == 256; }
 
 // fixed grid (a function of S only): <= 1024 block partials for the one-block loss sum
+// one subgroup per triple up to 16384 workgroups: each triple is a chain of dependent loads
+// (ids -> row map -> rows), so the loss is latency-bound unless every triple is in flight at
+// once (1024 workgroups left 25 rounds of that chain at 200k triples: 44 us, now ~2 rounds)
 static int64_t bpr_fwd_blocks(int64_t S, int C) {
   const int64_t b = (S + 256 / (C / 4) - 1) / (256 / (C / 4));
-  return b < 1024 ? b : 1024;
+  return b < 16384 ? b : 16384;
 }
 
 // workspace: block_loss | keys | vals | skeys | scid | slots | radix sort
