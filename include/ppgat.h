@@ -441,6 +441,13 @@ int ppgat_relu_dropout(const float* z, int64_t n, float p, uint64_t seed, int ba
 int ppgat_gemm_nn_supported(int64_t m, int k, int n, int b_layout);
 int ppgat_gemm_nn(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
                   float alpha, const float* bias, float* y, int64_t ldy, void* stream);
+/* ppgat_gemm_nn_ws: the same product; with few output tiles (small m, e.g. a 512-row batch)
+ *   and a long reduction it splits k over workgroups into the workspace and sums the splits in
+ *   order (deterministic); workspace_bytes() returns 0 when no split is taken. */
+int ppgat_gemm_nn_workspace_bytes(int64_t m, int k, int n, size_t* bytes);
+int ppgat_gemm_nn_ws(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
+                     float alpha, const float* bias, float* y, int64_t ldy, void* workspace, size_t workspace_bytes,
+                     void* stream);
 int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes);
 int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb, float* out,
                       void* workspace, size_t workspace_bytes, void* stream);

@@ -97,6 +97,9 @@ SIGNATURES = {
     "ppgat_relu_dropout": (c_int, [c_vp, c_i64, c_f, c_u64, c_int, c_vp, c_vp]),
     "ppgat_gemm_nn_supported": (c_int, [c_i64, c_int, c_int, c_int]),
     "ppgat_gemm_nn": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_int, c_f, c_vp, c_vp, c_i64, c_vp]),
+    "ppgat_gemm_nn_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_gemm_nn_ws": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_int, c_f, c_vp, c_vp, c_i64, c_vp, c_sz,
+                                 c_vp]),
     "ppgat_gemm_tn_big_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_gemm_tn_big": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_colsum_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),

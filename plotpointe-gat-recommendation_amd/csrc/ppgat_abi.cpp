@@ -859,6 +859,32 @@ int ppgat_gemm_nn(const float* x, int64_t ldx, int64_t m, int k, const float* b,
   return PPGAT_OK;
 }
 
+int ppgat_gemm_nn_workspace_bytes(int64_t m, int k, int n, size_t* bytes) {
+  if (!bytes || !ppgat::gemm_nn_shape_ok(m, k, n, 0))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn_workspace_bytes: needs k % 32 == 0, n % 128 == 0");
+  *bytes = ppgat::gemm_nn_workspace_bytes(m, k, n);
+  return PPGAT_OK;
+}
+
+int ppgat_gemm_nn_ws(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
+                     float alpha, const float* bias, float* y, int64_t ldy, void* workspace, size_t workspace_bytes,
+                     void* stream) {
+  if (!ppgat::gemm_nn_shape_ok(m, k, n, b_layout))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn: needs k % 32 == 0, n % 128 == 0, b_layout 0 or 1");
+  if (ldx < k || (ldx % 4) || ldy < n || (ldy % 4) || (b_layout == 0 ? ldb < n : ldb < k) || (ldb % 4))
+    return fail(PPGAT_ERR_INVALID, "gemm_nn: bad leading dimension (>= width, multiple of 4)");
+  if (m > 0 && (!x || !b || !y)) return fail(PPGAT_ERR_INVALID, "gemm_nn: null pointer");
+  if (!al16(x) || !al16(b) || !al16(y)) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn: 16-byte aligned rows");
+  const size_t need = ppgat::gemm_nn_workspace_bytes(m, k, n);
+  if (need > 0 && (!workspace || workspace_bytes < need))
+    return fail(PPGAT_ERR_INVALID, "gemm_nn_ws: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ, st);
+  hipError_t e = ppgat::gemm_nn(x, ldx, m, k, b, ldb, b_layout, n, alpha, bias, y, ldy, st, need > 0 ? workspace : nullptr);
+  if (e != hipSuccess) return hip_fail(e, "gemm_nn_ws");
+  return PPGAT_OK;
+}
+
 int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes) {
   if (!bytes || m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
     return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big: needs ma, nb multiples of 128");

@@ -152,7 +152,9 @@ hipError_t relu_dropout(const float* z, int64_t n, float p, uint64_t seed, int b
 hipError_t seed_snapshot(uint64_t seed, uint64_t* out, hipStream_t st);
 bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode);
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
-                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st);
+                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st,
+                   void* ws = nullptr);
+size_t gemm_nn_workspace_bytes(int64_t M, int K, int N);
 bool gemm_tn_big_shape_ok(int Ma, int Nb);
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,

@@ -91,6 +91,9 @@ struct NnArg {
   int64_t ldy;
   int n_blocks;
   int64_t row_blocks;
+  int splits;     // > 1: split-K, raw partial tiles to part[split][M][N] (k_nn_split_sum finishes)
+  int k_per;      // reduction length per split (multiple of kGBK)
+  float* part;
 };
 
 // BMODE 0: B[k][n] = B[k * ldb + n] (image [k][n], b32 reads); 1: B[k][n] = B[n * ldb + k] (X W^T,
@@ -107,12 +110,22 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
   // XCD-aware order: blocks b, b + 8, b + 16, ... land on one XCD; the n blocks of a row block
   // are consecutive there, so its X rows are fetched from HBM once
   const int64_t b = blockIdx.x;
-  const int64_t idx = b >> 3;
-  const int64_t rb = (idx / a.n_blocks) * 8 + (b & 7);
+  int64_t rb;
+  int n0, split = 0;
+  if (a.splits > 1) {  // small M: (row block, n block, k split), splits fastest
+    split = (int)(b % a.splits);
+    const int64_t rest = b / a.splits;
+    n0 = (int)(rest % a.n_blocks) * BN;
+    rb = rest / a.n_blocks;
+  } else {
+    const int64_t idx = b >> 3;
+    rb = (idx / a.n_blocks) * 8 + (b & 7);
+    n0 = (int)(idx % a.n_blocks) * BN;
+  }
   if (rb >= a.row_blocks) return;
-  const int n0 = (int)(idx % a.n_blocks) * BN;
   const int64_t M = a.M;
-  const int K = a.K;
+  const int kbeg = split * a.k_per;
+  const int K = a.splits > 1 ? (kbeg + a.k_per < a.K ? kbeg + a.k_per : a.K) : a.K;
   const int64_t m = rb * kGBM + wv * 32 + r;
   const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
 
@@ -149,10 +162,14 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
   f32x16 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-  load_b(0);
+  if (kbeg > 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) xa[g] = ld4(xrow + kbeg + 8 * g);
+  }
+  load_b(kbeg);
   store_b();
   __syncthreads();
-  for (int kc = 0; kc < K; kc += kGBK) {
+  for (int kc = kbeg; kc < K; kc += kGBK) {
     const bool more = kc + kGBK < K;
     if (more) {
       load_b(kc + kGBK);
@@ -187,6 +204,19 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
     __syncthreads();
   }
   const int64_t row0 = rb * kGBM + wv * 32;
+  if (a.splits > 1) {
+    float* part = a.part + (int64_t)split * M * a.N;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        if (row < M) part[row * a.N + col] = acc[t][q];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = n0 + 32 * t + r;
@@ -197,6 +227,26 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
       if (row < M) a.Y[row * a.ldy + col] = fmaf(a.alpha, acc[t][q], bv);
     }
   }
+}
+
+// split-K finish: Y = alpha * sum_s part[s] (split order) + bias, float4 per thread
+__global__ void __launch_bounds__(256) k_nn_split_sum(const float* __restrict__ part, int64_t M, int N, int splits,
+                                                      float alpha, const float* __restrict__ bias,
+                                                      float* __restrict__ Y, int64_t ldy) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int n4 = N / 4;
+  if (e >= M * n4) return;
+  const int64_t row = e / n4;
+  const int c = (int)(e % n4) * 4;
+  const size_t stride = (size_t)M * N;
+  float4 s = ld4(part + row * N + c);
+  for (int k = 1; k < splits; ++k) s = add4(s, ld4(part + k * stride + row * N + c));
+  float4 o;
+  o.x = fmaf(alpha, s.x, bias ? bias[c] : 0.f);
+  o.y = fmaf(alpha, s.y, bias ? bias[c + 1] : 0.f);
+  o.z = fmaf(alpha, s.z, bias ? bias[c + 2] : 0.f);
+  o.w = fmaf(alpha, s.w, bias ? bias[c + 3] : 0.f);
+  st4(Y + row * ldy + c, o);
 }
 
 // ===========================================================================
@@ -755,8 +805,22 @@ bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode) {
   return M >= 0 && K >= kGBK && K % kGBK == 0 && N >= 128 && N % 128 == 0 && (bmode == 0 || bmode == 1);
 }
 
+// split-K for small M (few row blocks, long K): the partial tiles go to the caller's workspace
+int gemm_nn_splits(int64_t M, int K, int N) {
+  const int64_t tiles = (M + kGBM - 1) / kGBM * (N / (N % 256 == 0 ? 256 : 128));
+  if (tiles >= 128 || K < 4 * kGBK) return 1;
+  int s = 1;
+  while (s * 2 * tiles <= 256 && (K / kGBK) >= 4 * s * 2 && s < 32) s *= 2;  // >= 4 chunks per split
+  return s;
+}
+
+size_t gemm_nn_workspace_bytes(int64_t M, int K, int N) {
+  const int s = gemm_nn_splits(M, K, N);
+  return s > 1 ? align_up((size_t)s * M * N * 4) : 0;
+}
+
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
-                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st) {
+                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st, void* ws) {
   if (M <= 0) return hipSuccess;
   NnArg a{};
   a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.B = B; a.ldb = ldb; a.N = N; a.alpha = alpha; a.bias = bias;
@@ -765,7 +829,16 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
   const int64_t padded = (a.row_blocks + 7) / 8 * 8;
   const bool wide = N % 256 == 0;
   a.n_blocks = N / (wide ? 256 : 128);
-  const unsigned grid = (unsigned)(padded * a.n_blocks);
+  a.splits = ws != nullptr ? gemm_nn_splits(M, K, N) : 1;
+  if (a.splits > 1) {  // every split non-empty: splits = ceil(chunks / chunks per split)
+    const int chunks = K / kGBK;
+    const int per = (chunks + a.splits - 1) / a.splits;
+    a.k_per = per * kGBK;
+    a.splits = (chunks + per - 1) / per;
+    a.part = static_cast<float*>(ws);
+  }
+  const unsigned grid = a.splits > 1 ? (unsigned)(a.row_blocks * a.n_blocks * a.splits)
+                                     : (unsigned)(padded * a.n_blocks);
 #define PPGAT_NN(NT_, BM_) hipLaunchKernelGGL((k_gemm_nn<NT_, BM_>), dim3(grid), dim3(256), 0, st, a)
   if (wide) {
     if (bmode == 0) PPGAT_NN(8, 0); else PPGAT_NN(8, 1);
@@ -773,6 +846,11 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
     if (bmode == 0) PPGAT_NN(4, 0); else PPGAT_NN(4, 1);
   }
 #undef PPGAT_NN
+  if (a.splits > 1) {
+    const int64_t n4 = M * (N / 4);
+    hipLaunchKernelGGL(k_nn_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, M, N, a.splits,
+                       alpha, bias, Y, ldy);
+  }
   return hipGetLastError();
 }
 

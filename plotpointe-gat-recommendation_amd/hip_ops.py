@@ -720,9 +720,13 @@ def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: floa
     M, K = x.shape
     y = out if out is not None else torch.empty(M, n, dtype=torch.float32, device=x.device)
     ldb = B.stride(0)
-    _lib.check(lib.ppgat_gemm_nn(x.data_ptr(), x.stride(0) if M > 1 else K, M, K, B.data_ptr(), ldb, b_layout, n,
-                                 float(alpha), _lib.ptr(bias), y.data_ptr(), y.stride(0) if M > 1 else n,
-                                 _lib.stream_handle(x.device)), "gemm_nn")
+    nbytes = ctypes.c_size_t(0)
+    if gemm_nn_supported(M, K, n, b_layout):
+        _lib.check(lib.ppgat_gemm_nn_workspace_bytes(M, K, n, ctypes.byref(nbytes)), "gemm_nn_workspace_bytes")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=x.device) if nbytes.value else None
+    _lib.check(lib.ppgat_gemm_nn_ws(x.data_ptr(), x.stride(0) if M > 1 else K, M, K, B.data_ptr(), ldb, b_layout, n,
+                                    float(alpha), _lib.ptr(bias), y.data_ptr(), y.stride(0) if M > 1 else n,
+                                    _lib.ptr(ws), nbytes.value, _lib.stream_handle(x.device)), "gemm_nn")
     return y
 
 

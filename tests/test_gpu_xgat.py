@@ -39,6 +39,37 @@ def test_gemm_nn_vs_fp64(cuda, M, K, N, layout):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("M,K,N,layout", [(512, 896, 256, 1), (44, 896, 256, 1), (512, 128, 256, 0), (300, 512, 128, 1),
+                                          (1, 384, 128, 1), (1000, 1024, 512, 0)])
+def test_gemm_nn_split_k_vs_fp64(cuda, M, K, N, layout):
+    """Small M with a long reduction (the FusionMLP batch: 512 x 896 -> 256): ppgat_gemm_nn_ws
+    splits k over workgroups into the workspace and sums the splits in order; equals the
+    unsplit kernel to 1e-5 relative, the fp64 product to 1e-5, and is bitwise repeatable."""
+    import ctypes
+    ops = _ops()
+    lib = __import__("importlib").import_module("plotpointe-gat-recommendation_amd._lib").load()
+    nbytes = ctypes.c_size_t(0)
+    assert lib.ppgat_gemm_nn_workspace_bytes(M, K, N, ctypes.byref(nbytes)) == 0
+    if M * N <= 512 * 256 and K >= 256:
+        assert nbytes.value > 0  # the split path is taken
+    g = torch.Generator().manual_seed(M * 7 + K)
+    x = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N, generator=g, dtype=torch.float64) if layout == 0 else \
+        torch.randn(N, K, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    ref = 0.25 * (x @ (B if layout == 0 else B.t())) + bias
+    xs, Bs, bs = x.float().to(cuda), B.float().to(cuda), bias.float().to(cuda)
+    y = ops.gemm_nn(xs, Bs, layout, N, alpha=0.25, bias=bs)
+    assert rel(y, ref) <= 1e-5
+    assert torch.equal(y, ops.gemm_nn(xs, Bs, layout, N, alpha=0.25, bias=bs))
+    y1 = torch.empty(M, N, device=cuda)  # the unsplit kernel (no workspace) on the same operands
+    pkg_lib = __import__("importlib").import_module("plotpointe-gat-recommendation_amd._lib")
+    pkg_lib.check(lib.ppgat_gemm_nn(xs.data_ptr(), K if M == 1 else xs.stride(0), M, K, Bs.data_ptr(), Bs.stride(0),
+                                    layout, N, 0.25, bs.data_ptr(), y1.data_ptr(), N, pkg_lib.stream_handle(cuda)),
+                  "gemm_nn")
+    assert rel(y, y1.double()) <= 1e-5
+
+
 @pytest.mark.parametrize("M,Ma,Nb", [(5000, 256, 1024), (100_003, 256, 256), (77, 128, 128), (0, 128, 256)])
 def test_gemm_tn_big_and_colsum_vs_fp64(cuda, M, Ma, Nb):
     ops = _ops()
