@@ -144,29 +144,32 @@ __global__ void __launch_bounds__(256) k_ce_mean(const float* __restrict__ l, in
   }
 }
 
-// out[r, d] (+)= scale * sum_k P(r, k) Q[k, d], P(r, k) = P[r * B + k] (TRANS 0) or P[k * B + r]
-// (TRANS 1); P [B, B], Q [B, kD]; 16-row x 64-col output tiles (B/16 x 2 workgroups), 2 x 2
-// per thread, k staged through LDS in chunks of 32
+// part[z][r, d] = sum_{k in split z} P(r, k) Q[k, d], P(r, k) = P[r * B + k] (TRANS 0) or
+// P[k * B + r] (TRANS 1); P [B, B], Q [B, kD]; 16-row x 64-col output tiles, the reduction split
+// over gridDim.z (kper each, a multiple of 32) so a 512-row batch fills the chip; 2 x 2 per
+// thread, k staged through LDS in chunks of 32.  k_mm_sum adds the splits in order.
 template <int TRANS>
 __global__ void __launch_bounds__(256) k_mm_bd(const float* __restrict__ P, const float* __restrict__ Q, int64_t B,
-                                               float scale, int accumulate, float* __restrict__ out) {
+                                               int64_t kper, float* __restrict__ part) {
   __shared__ float sp[32][17];
   __shared__ float sq[32][65];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // cols tx, tx + 32; rows ty, ty + 8
   const int64_t r0 = (int64_t)blockIdx.x * 16;
   const int c0 = blockIdx.y * 64;
+  const int64_t kb = (int64_t)blockIdx.z * kper;
+  const int64_t ke = kb + kper < B ? kb + kper : B;
   float acc[2][2] = {};
-  for (int64_t k0 = 0; k0 < B; k0 += 32) {
+  for (int64_t k0 = kb; k0 < ke; k0 += 32) {
     for (int e = threadIdx.x; e < 16 * 32; e += 256) {
       // consecutive threads along P's contiguous index: k for TRANS 0, r for TRANS 1
       const int rr = TRANS ? (e & 15) : (e >> 5), kk = TRANS ? (e >> 4) : (e & 31);
       const int64_t r = r0 + rr, k = k0 + kk;
-      sp[kk][rr] = (r < B && k < B) ? (TRANS ? P[k * B + r] : P[r * B + k]) : 0.f;
+      sp[kk][rr] = (r < B && k < ke) ? (TRANS ? P[k * B + r] : P[r * B + k]) : 0.f;
     }
     for (int e = threadIdx.x; e < 32 * 64; e += 256) {
       const int kk = e >> 6, d = e & 63;
       const int64_t k = k0 + kk;
-      sq[kk][d] = k < B ? Q[k * kD + c0 + d] : 0.f;
+      sq[kk][d] = k < ke ? Q[k * kD + c0 + d] : 0.f;
     }
     __syncthreads();
 #pragma unroll 8
@@ -178,17 +181,27 @@ __global__ void __launch_bounds__(256) k_mm_bd(const float* __restrict__ P, cons
     }
     __syncthreads();
   }
+  float* out = part + (int64_t)blockIdx.z * B * kD;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int64_t r = r0 + ty + 8 * i;
     if (r >= B) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float* o = out + r * kD + c0 + tx + 32 * j;
-      const float v = acc[i][j] * scale;
-      *o = accumulate ? *o + v : v;
-    }
+    for (int j = 0; j < 2; ++j) out[r * kD + c0 + tx + 32 * j] = acc[i][j];
   }
+}
+
+// out[e] = scale * sum_{p < nparts} part[p][e]  (parts in order), float4 per thread
+__global__ void __launch_bounds__(256) k_mm_sum(const float* __restrict__ part, int nparts, int64_t n4, float scale,
+                                                float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n4) return;
+  float4 s = reinterpret_cast<const float4*>(part)[e];
+  for (int p = 1; p < nparts; ++p) {
+    const float4 v = reinterpret_cast<const float4*>(part)[(int64_t)p * n4 + e];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  reinterpret_cast<float4*>(out)[e] = make_float4(s.x * scale, s.y * scale, s.z * scale, s.w * scale);
 }
 
 // dx = (dy - y (y . dy)) / |x| (|x| > eps), dy / eps otherwise; one wave per row of the three
@@ -240,9 +253,17 @@ __global__ void __launch_bounds__(256) k_relu_drop(const float* __restrict__ z, 
 
 bool infonce_shape_ok(int64_t B, int D) { return B >= 1 && B <= 4096 && D == kD; }
 
+// reduction splits of the B x B products: k ranges of >= 64 (two LDS chunks), at most 8
+static int64_t mm_splits(int64_t B) {
+  int64_t s = (B + 63) / 64;
+  return s < 8 ? (s < 1 ? 1 : s) : 8;
+}
+static int64_t mm_kper(int64_t B) { return ((B + mm_splits(B) - 1) / mm_splits(B) + 31) / 32 * 32; }
+
 size_t infonce_workspace_bytes(int64_t B) {
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  return al(3 * B * kD * 4) + al(3 * B * 4) + 2 * al(B * B * 4) + al(2 * B * 4);
+  return al(3 * B * kD * 4) + al(3 * B * 4) + 2 * al(B * B * 4) + al(2 * B * 4) +
+         al((size_t)4 * mm_splits(B) * B * kD * 4);
 }
 
 // loss[3] = {loss, loss_t, loss_i}; dF, dT, dI = gradients of loss w.r.t. F, T, I (pre-normalisation)
@@ -259,6 +280,8 @@ hipError_t infonce(const float* F, const float* T, const float* I, int64_t B, fl
   float* S2 = reinterpret_cast<float*>(p);
   p += al(B * B * 4);
   float* l = reinterpret_cast<float*>(p);                 // [2, B]
+  p += al(2 * B * 4);
+  float* part = reinterpret_cast<float*>(p);              // [4 products][splits][B, D]
   const float* Fn = Y;
   const float* Tn = Y + B * kD;
   const float* In = Y + 2 * B * kD;
@@ -270,11 +293,19 @@ hipError_t infonce(const float* F, const float* T, const float* I, int64_t B, fl
   hipLaunchKernelGGL(k_ce_mean, dim3(1), dim3(256), 0, st, l, B, loss);
   // dFn = (dS_t Tn + dS_i In) / tau; dTn = dS_t^T Fn / tau; dIn = dS_i^T Fn / tau  (into dF, dT, dI)
   const float s = 1.f / tau;
-  const dim3 gm((unsigned)((B + 15) / 16), kD / 64);
-  hipLaunchKernelGGL(k_mm_bd<0>, gm, dim3(256), 0, st, S1, Tn, B, s, 0, dF);
-  hipLaunchKernelGGL(k_mm_bd<0>, gm, dim3(256), 0, st, S2, In, B, s, 1, dF);
-  hipLaunchKernelGGL(k_mm_bd<1>, gm, dim3(256), 0, st, S1, Fn, B, s, 0, dT);
-  hipLaunchKernelGGL(k_mm_bd<1>, gm, dim3(256), 0, st, S2, Fn, B, s, 0, dI);
+  const int64_t ns = mm_splits(B), kper = mm_kper(B);
+  const int64_t nz = (B + kper - 1) / kper;  // non-empty splits
+  const size_t pstride = (size_t)ns * B * kD;
+  const dim3 gm((unsigned)((B + 15) / 16), kD / 64, (unsigned)nz);
+  hipLaunchKernelGGL(k_mm_bd<0>, gm, dim3(256), 0, st, S1, Tn, B, kper, part);
+  hipLaunchKernelGGL(k_mm_bd<0>, gm, dim3(256), 0, st, S2, In, B, kper, part + (size_t)nz * B * kD);
+  hipLaunchKernelGGL(k_mm_bd<1>, gm, dim3(256), 0, st, S1, Fn, B, kper, part + 2 * pstride);
+  hipLaunchKernelGGL(k_mm_bd<1>, gm, dim3(256), 0, st, S2, Fn, B, kper, part + 3 * pstride);
+  const int64_t n4 = B * kD / 4;
+  const unsigned g4 = (unsigned)((n4 + 255) / 256);
+  hipLaunchKernelGGL(k_mm_sum, dim3(g4), dim3(256), 0, st, part, (int)(2 * nz), n4, s, dF);  // S1 Tn + S2 In
+  hipLaunchKernelGGL(k_mm_sum, dim3(g4), dim3(256), 0, st, part + 2 * pstride, (int)nz, n4, s, dT);
+  hipLaunchKernelGGL(k_mm_sum, dim3(g4), dim3(256), 0, st, part + 3 * pstride, (int)nz, n4, s, dI);
   // normalisation backward, in place
   hipLaunchKernelGGL(k_norm_bwd3, dim3(w3), dim3(256), 0, st, Y, nrm, B, dF, dT, dI);
   return hipGetLastError();
