@@ -119,6 +119,25 @@ def host_cores() -> int:
     return max(1, n)
 
 
+def measured_copy_gbs(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
+    """STREAM-like device copy (read + write bytes / time) on this box, beside the spec peak
+    (SURVEY.md 8(d)): a 1 GiB buffer copied `reps` times, HIP events on the current stream."""
+    n = nbytes // 4
+    src = torch.ones(n, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    b.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2.0 * n * 4 * reps / (a.elapsed_time(b) / 1e3) / 1e9
+    del src, dst
+    return gbs
+
+
 def cpu_baseline(g: data.UIGraph, feats: np.ndarray, hidden: int, layers: int, budget_s: float):
     """Oracle (torch CPU restatement of PyG GATConv, oracle/gat_oracle.py) fwd+bwd of the
     L GAT layers, on a bounded prefix sample of the same graph: median of 5 timed
@@ -361,6 +380,7 @@ def main():
             traffic = tj_.get("per_launch_bytes", {}).get(dom)
     except Exception:
         pass
+    copy_gbs = measured_copy_gbs(dev) if rank == 0 else None
     if args.config == 5:
         metric = "edges/sec GAT fwd+bwd, d=256 heads=4, 200M-edge synthetic (config 5)"
         workload = (f"cfg5 x{scale:g}: PyGGAT train step (fwd+BPR+bwd+Adam), {g.n_users:,} users + {g.n_items:,} "
@@ -403,7 +423,8 @@ def main():
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algo_bytes_per_launch": ab, "avg_launch_ms": avg_s * 1e3, "launches": dom_n},
+                     "algo_bytes_per_launch": ab, "avg_launch_ms": avg_s * 1e3, "launches": dom_n,
+                     "measured_copy_gbs": copy_gbs},
         "loss": float(loss.item()),
         "optimizer": "Adam (libppgat device kernel, torch.optim.Adam semantics)",
     }
