@@ -112,7 +112,7 @@ def test_native_training_step_vs_fp64_oracle(pkg, oracle, gold, cuda, B, p):
     t = torch.randn(B, 384, generator=g)
     im = torch.randn(B, 512, generator=g)
     seed = 0xABCDEF + B
-    loss = pkg.fusion.fusion_train_step(m, t.to(cuda), im.to(cuda), seed=seed).cpu()
+    loss = pkg.fusion.fusion_train_step(m, t.to(cuda), im.to(cuda), seed=seed).detach().cpu()
     ones = torch.ones(B, 256, device=cuda)
     mask_dev = pkg.fusion.relu_dropout(ones, p, seed).cpu()
     mask = oracle.mlp_dropout_scale(seed, B * 256, p).reshape(B, 256)
@@ -122,7 +122,7 @@ def test_native_training_step_vs_fp64_oracle(pkg, oracle, gold, cuda, B, p):
     P = {k: v.detach().double().cpu().requires_grad_(True) for k, v in m.named_parameters()}
     ref, rt, ri = oracle.fusion_train_loss(P, t.double(), im.double(), 0.07, torch.from_numpy(mask).double())
     ref.backward()
-    assert abs(float(loss[0]) - float(ref)) <= 1e-5 * max(float(ref), 1e-3)
+    assert abs(float(loss[0]) - float(ref.detach())) <= 1e-5 * max(float(ref.detach()), 1e-3)
     assert abs(float(loss[1]) - float(rt)) <= 1e-5 * max(float(rt), 1e-3)
     assert abs(float(loss[2]) - float(ri)) <= 1e-5 * max(float(ri), 1e-3)
     for k, prm in m.named_parameters():

@@ -82,7 +82,7 @@ def test_graph_replay_equals_eager_steps(pkg, cuda):
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
-        return loss
+        return loss.detach()  # no autograd graph kept alive across steps (a capture hazard)
 
     try:
         side = torch.cuda.Stream(cuda)
