@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=None,
-                    help="committed PMC summary (default: profiles/r01_pmc_traffic.json for configs 2/3, "
+                    help="committed PMC summary (default: profiles/r02/cfg2_pmc_traffic.json for config 2, "
                          "profiles/r02/cfg5_pmc_traffic.json for config 5 at its default scale)")
     ap.add_argument("--partition", choices=["auto", "replicated", "halo"], default="auto",
                     help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
@@ -372,8 +372,8 @@ def main():
     try:
         if dist_path:
             raise LookupError("the committed PMC summary is for the unsharded graph")
-        tj_path = args.traffic_json or str(ROOT / "profiles" / ("r02/cfg5_pmc_traffic.json" if args.config == 5
-                                                                else "r01_pmc_traffic.json"))
+        tj_path = args.traffic_json or str(ROOT / "profiles" / "r02" / ("cfg5_pmc_traffic.json" if args.config == 5
+                                                                       else "cfg2_pmc_traffic.json"))
         tj_ = json.loads(Path(tj_path).read_text())
         if tj_.get("config", 2) == args.config and tj_.get("scale", scale if args.config == 5 else None) == (
                 scale if args.config == 5 else None):  # PMC summaries are per workload
