@@ -486,12 +486,6 @@ int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const in
                    int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
                    const float* s_dst, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
                    float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream);
-/* ppgat_xgat_bwd_gt: gt = g w_grad (the GEMM above) with D[i][h] = gt_i^h . agg_i^h formed in the GEMM's
- * epilogue while the tile is in registers, then nstate -- the same gt and nstate as ppgat_gemm_nn +
- * ppgat_xgat_bwd_prologue without re-reading gt.  D [n_dst, H] is caller scratch. */
-int ppgat_xgat_bwd_gt(const float* g, int64_t ldg, int64_t n_dst, int channels, const float* w_grad, int heads,
-                      int in_channels, const float* agg, const float* s_dst, const float* m, const float* inv_l,
-                      float* gt, float* D, float* nstate, void* stream);
 int ppgat_xgat_bwd_prologue(const float* gt, const float* agg, const float* s_dst, const float* m, const float* inv_l,
                             int64_t n_dst, int in_channels, int heads, float* nstate, void* stream);
 int ppgat_xgat_bwd_workspace_bytes(int64_t n_hub_items, int in_channels, size_t* bytes);

@@ -1001,22 +1001,6 @@ int ppgat_xgat_bwd_prologue(const float* gt, const float* agg, const float* s_ds
   return PPGAT_OK;
 }
 
-int ppgat_xgat_bwd_gt(const float* g, int64_t ldg, int64_t n_dst, int channels, const float* w_grad, int heads,
-                      int in_channels, const float* agg, const float* s_dst, const float* m, const float* inv_l,
-                      float* gt, float* D, float* nstate, void* stream) {
-  if (!ppgat::xgat_shape_ok(in_channels, heads, channels)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_gt: shape");
-  if (n_dst < 0 || ldg < channels || (ldg % 4)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_gt: bad sizes");
-  if (n_dst > 0 && (!g || !w_grad || !agg || !s_dst || !m || !inv_l || !gt || !D || !nstate))
-    return fail(PPGAT_ERR_INVALID, "xgat_bwd_gt: null pointer");
-  if (!al16(g) || !al16(w_grad) || !al16(gt)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_gt: 16-byte aligned rows");
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  Timed t(PPGAT_K_PROJ, st);
-  hipError_t e = ppgat::xgat_bwd_gt(g, ldg, n_dst, channels, w_grad, heads, in_channels, agg, s_dst, m, inv_l, gt, D,
-                                    nstate, st);
-  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_gt");
-  return PPGAT_OK;
-}
-
 int ppgat_xgat_bwd_workspace_bytes(int64_t n_hub_items, int in_channels, size_t* bytes) {
   if (!bytes || n_hub_items < 0 || in_channels < 1) return fail(PPGAT_ERR_INVALID, "xgat_bwd_ws: bad args");
   *bytes = partial_bytes(n_hub_items, 1, in_channels);

@@ -153,7 +153,7 @@ hipError_t seed_snapshot(uint64_t seed, uint64_t* out, hipStream_t st);
 bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode);
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
                    float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st,
-                   void* ws = nullptr, const float* dot_with = nullptr, float* dot_out = nullptr);
+                   void* ws = nullptr);
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N);
 bool gemm_tn_big_shape_ok(int Ma, int Nb);
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
@@ -168,9 +168,6 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
                     int H, const float* s_src, const float* s_dst, float slope, float p, uint64_t seed,
                     const uint64_t* seed_in, float* agg, float* m, float* invl, float* partial,
                     const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
-hipError_t xgat_bwd_gt(const float* g, int64_t ldg, int64_t n, int C, const float* w_grad, int H, int K,
-                       const float* agg, const float* s_dst, const float* m, const float* invl, float* gt, float* D,
-                       float* nstate, hipStream_t st);
 hipError_t xgat_bwd_pro(const float* gt, const float* agg, const float* s_dst, const float* m, const float* invl,
                         int64_t n, int K, int H, float* nstate, hipStream_t st);
 hipError_t xgat_bwd_edges(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,

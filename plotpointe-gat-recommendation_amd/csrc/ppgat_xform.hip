@@ -70,34 +70,6 @@ __device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t eid, uint32_
   return u >= p ? inv_keep : 0.f;
 }
 
-// transposing reduction of 16 per-lane values over the lanes sl with bit OFF, OFF/2, ... 8
-// set, then over lanes 1..4 (see k_bwd_x): returns how many values (from `base`) each lane holds
-template <int OFF, int N>
-__device__ __forceinline__ int tr_reduce(float (&v)[16], int sl, int& base) {
-  if constexpr (OFF >= 8 && N > 1) {
-    constexpr int Hh = N / 2;
-    const bool bit = (sl & OFF) != 0;
-#pragma unroll
-    for (int t = 0; t < Hh; ++t) {
-      if constexpr (OFF >= 16) {
-        float r0, r1;
-        row_swap<OFF>(v[t], v[Hh + t], r0, r1);
-        v[t] = r0 + r1;
-      } else {
-        const float send = bit ? v[t] : v[Hh + t];
-        const float keep = bit ? v[Hh + t] : v[t];
-        v[t] = keep + dpp<0x128>(send);
-      }
-    }
-    if (bit) base += Hh;
-    return tr_reduce<OFF / 2, Hh>(v, sl, base);
-  } else {
-#pragma unroll
-    for (int t = 0; t < N; ++t) v[t] = group_reduce<Op::Sum, 1, 4>(v[t]);
-    return N;
-  }
-}
-
 // ===========================================================================
 // NN GEMM: Y[M, N] = alpha X[M, K] B + bias
 // ===========================================================================
@@ -122,10 +94,6 @@ struct NnArg {
   int splits;     // > 1: split-K, raw partial tiles to part[split][M][N] (k_nn_split_sum finishes)
   int k_per;      // reduction length per split (multiple of kGBK)
   float* part;
-  // optional row-dot epilogue (no split): dot_out[row * (N / BN) + n_block] =
-  // sum over the block's columns of Y[row][col] * dot_with[row * ldy + col]  (fixed order)
-  const float* dot_with;
-  float* dot_out;
 };
 
 // BMODE 0: B[k][n] = B[k * ldb + n] (image [k][n], b32 reads); 1: B[k][n] = B[n * ldb + k] (X W^T,
@@ -249,9 +217,6 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
     }
     return;
   }
-  float dp[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) dp[q] = 0.f;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = n0 + 32 * t + r;
@@ -259,25 +224,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
-      const float y = fmaf(a.alpha, acc[t][q], bv);
-      if (row < M) a.Y[row * a.ldy + col] = y;
-      if (a.dot_with != nullptr) dp[q] = fmaf(y, a.dot_with[(row < M ? row : M - 1) * a.ldy + col], dp[q]);
-    }
-  }
-  if (a.dot_with != nullptr) {
-    // sum each row's 32 column lanes (within the lane half hf): transposing butterfly, then
-    // lane (t = lane & 7) < R holds row value vbase + t
-    int vbase = 0;
-    const int R = tr_reduce<16, 16>(dp, lane, vbase);
-    const int t = lane & 7;
-    if (t < R) {
-      float dv = dp[0];
-#pragma unroll
-      for (int c = 1; c < 4; ++c)
-        if (c == t) dv = dp[c];
-      const int q = vbase + t;
-      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
-      if (row < M) a.dot_out[row * (a.N / BN) + n0 / BN] = dv;
+      if (row < M) a.Y[row * a.ldy + col] = fmaf(a.alpha, acc[t][q], bv);
     }
   }
 }
@@ -580,14 +527,6 @@ __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restr
   }
 }
 
-// nstate[i][h] = {s_dst, m, inv_l, D} with D computed by the gt GEMM's row-dot epilogue
-__global__ void __launch_bounds__(256) k_bwd_x_state(const float* __restrict__ D, const float* __restrict__ s_dst,
-                                                     const float* __restrict__ m, const float* __restrict__ invl,
-                                                     int64_t n_pairs, float4* __restrict__ nstate) {
-  const int64_t pr = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (pr < n_pairs) nstate[pr] = make_float4(s_dst[pr], m[pr], invl[pr], D[pr]);
-}
-
 // backward prologue: nstate[i][h] = {s_dst, m, inv_l, D = gt_i^h . ax_i^h}; one wave per row
 template <int K, int H>
 __global__ void __launch_bounds__(256) k_bwd_x_pro(const float* __restrict__ gt, const float* __restrict__ agg,
@@ -623,6 +562,32 @@ __global__ void __launch_bounds__(256) k_bwd_x_pro(const float* __restrict__ gt,
 // with a transposing butterfly.  Writes dx_j = sum beta gt + sum_h ds_src^h A_src^h (hub
 // pieces: [msg (K) | ds_h (H <= 4)] partials), ds_src[j][h], and dz at each edge's CSR slot.
 // ---------------------------------------------------------------------------
+template <int OFF, int N>
+__device__ __forceinline__ int tr_reduce(float (&v)[16], int sl, int& base) {
+  if constexpr (OFF >= 8 && N > 1) {
+    constexpr int Hh = N / 2;
+    const bool bit = (sl & OFF) != 0;
+#pragma unroll
+    for (int t = 0; t < Hh; ++t) {
+      if constexpr (OFF >= 16) {
+        float r0, r1;
+        row_swap<OFF>(v[t], v[Hh + t], r0, r1);
+        v[t] = r0 + r1;
+      } else {
+        const float send = bit ? v[t] : v[Hh + t];
+        const float keep = bit ? v[Hh + t] : v[t];
+        v[t] = keep + dpp<0x128>(send);
+      }
+    }
+    if (bit) base += Hh;
+    return tr_reduce<OFF / 2, Hh>(v, sl, base);
+  } else {
+#pragma unroll
+    for (int t = 0; t < N; ++t) v[t] = group_reduce<Op::Sum, 1, 4>(v[t]);
+    return N;
+  }
+}
+
 template <int K, int H>
 __global__ void __launch_bounds__(256) k_bwd_x(XItems it, const int32_t* __restrict__ row,
                                                const int32_t* __restrict__ csc_eid,
@@ -855,8 +820,7 @@ size_t gemm_nn_workspace_bytes(int64_t M, int K, int N) {
 }
 
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
-                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st, void* ws,
-                   const float* dot_with, float* dot_out) {
+                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st, void* ws) {
   if (M <= 0) return hipSuccess;
   NnArg a{};
   a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.B = B; a.ldb = ldb; a.N = N; a.alpha = alpha; a.bias = bias;
@@ -865,10 +829,7 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
   const int64_t padded = (a.row_blocks + 7) / 8 * 8;
   const bool wide = N % 256 == 0;
   a.n_blocks = N / (wide ? 256 : 128);
-  a.dot_with = dot_with;
-  a.dot_out = dot_out;
-  a.splits = (ws != nullptr && dot_with == nullptr) ? gemm_nn_splits(M, K, N) : 1;
-  if (dot_with != nullptr && !wide) return hipErrorInvalidValue;  // the row dot works per 256-column block
+  a.splits = ws != nullptr ? gemm_nn_splits(M, K, N) : 1;
   if (a.splits > 1) {  // every split non-empty: splits = ceil(chunks / chunks per split)
     const int chunks = K / kGBK;
     const int per = (chunks + a.splits - 1) / a.splits;
@@ -968,21 +929,6 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
   if (e != hipSuccess) return e;
   (void)K;
   return launch_fwd_merge(256, hub_row, hub_ptr, n_hubs, H, partial, 1e-16f, m, invl, agg, st);
-}
-
-// gt = g W_grad (GEMM, one 256-column block per head) with D[i][h] = gt_i^h . agg_i^h in its
-// epilogue (agg read while the tile is in registers: gt is never re-read), then nstate
-hipError_t xgat_bwd_gt(const float* g, int64_t ldg, int64_t n, int C, const float* w_grad, int H, int K,
-                       const float* agg, const float* s_dst, const float* m, const float* invl, float* gt, float* D,
-                       float* nstate, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipError_t e = gemm_nn(g, ldg, n, C, w_grad, (int64_t)H * K, 0, H * K, 1.f, nullptr, gt, (int64_t)H * K, st, nullptr,
-                         agg, D);
-  if (e != hipSuccess) return e;
-  const int64_t pairs = n * H;
-  hipLaunchKernelGGL(k_bwd_x_state, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, st, D, s_dst, m, invl, pairs,
-                     reinterpret_cast<float4*>(nstate));
-  return hipGetLastError();
 }
 
 hipError_t xgat_bwd_pro(const float* gt, const float* agg, const float* s_dst, const float* m, const float* invl,

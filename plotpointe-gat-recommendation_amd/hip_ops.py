@@ -878,13 +878,10 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
                "xgat_weights")
-    # gt = g W_grad with D = gt . agg per (row, head) in the GEMM epilogue, then nstate
-    gt = torch.empty(v.n_dst, H * K, dtype=torch.float32, device=dev)
-    Dh = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
+    gt = gemm_nn(g, Wg, 0, H * K)
     nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_xgat_bwd_gt(g.data_ptr(), C, v.n_dst, C, Wg.data_ptr(), H, K, agg.data_ptr(), s_dst.data_ptr(),
-                                     m.data_ptr(), inv_l.data_ptr(), gt.data_ptr(), Dh.data_ptr(), nstate.data_ptr(),
-                                     st), "xgat_bwd_gt")
+    _lib.check(lib.ppgat_xgat_bwd_prologue(gt.data_ptr(), agg.data_ptr(), s_dst.data_ptr(), m.data_ptr(),
+                                           inv_l.data_ptr(), v.n_dst, K, H, nstate.data_ptr(), st), "xgat_bwd_prologue")
     E = v.n_edges
     S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)

@@ -24,8 +24,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=5)
     ap.add_argument("--world", type=int, default=8)
-    ap.add_argument("--node-weight", type=float, default=4.0,
-                    help="per-node weight added to the degree in the partition (dist.build_halo_graph node_weight)")
     args = ap.parse_args()
     d = pkg.data
     if args.config == 5:
@@ -38,7 +36,7 @@ def main():
     users = np.repeat(np.arange(nu, dtype=np.int64), np.diff(g.user_ptr))
     items = g.user_items.astype(np.int64) + nu
     # the U-I columns come in (u -> i, i -> u) pairs: each interaction is a message both ways
-    deg = np.bincount(users, minlength=N) * 2 + np.bincount(items, minlength=N) * 2 + args.node_weight
+    deg = np.bincount(users, minlength=N) * 2 + np.bincount(items, minlength=N) * 2 + 4.0
     owner = np.empty(N, np.int32)
     for a, b in ((0, nu), (nu, N)):
         bnd = a + pkg.dist.partition_bounds(deg[a:b].astype(np.float64), W)
