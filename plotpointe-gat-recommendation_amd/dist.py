@@ -832,6 +832,9 @@ def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int,
         from .hip_ops import CSRGraph
         graph = CSRGraph(R, El, view.rowptr, view.col, view.csr_eid, view.colptr, view.row, view.csc_eid,
                          view.dz_slot, view.fwd_sched, view.bwd_sched)
+        if not bool((~su & ~du).any()):  # bipartite (no I-I columns): item sources reach users only
+            graph.bwd_split = (RU, sched_builder(view.colptr[:RU + 1].contiguous(), El),
+                               sched_builder(view.colptr[RU:].contiguous(), El))
     rp = G.rowptr.to(torch.int64)
     item_live = (rp[RU + 1:] - rp[RU:-1]) > 0
     return RepGraph(world, rank, N, E, nu, ni, ub, RU, RU_max, view, row_map.to(torch.int32), item_live, ub, graph)
@@ -869,6 +872,25 @@ class RepHooks:
     def reduce_grad(self, g):
         if self.comm.active:
             self.comm.all_reduce_(g[self.RU:])
+
+    def async_capable(self) -> bool:
+        """RCCL on device tensors: the item-row all_reduce can run on the communication stream."""
+        return self.comm.active and self.comm.backend == "nccl"
+
+    def reduce_grad_async(self, g):
+        """all_reduce of the item rows of g on the communication stream, after the main
+        stream's work so far; ``wait`` joins it back."""
+        dev = g.device
+        main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
+        cs.wait_stream(main)
+        g.record_stream(cs)
+        with torch.cuda.stream(cs):
+            self.comm.all_reduce_(g[self.RU:])
+        return (main, cs)
+
+    def wait(self, pending):
+        main, cs = pending
+        main.wait_stream(cs)
 
 
 def _merge_item_rows(rg: RepGraph, comm: Comm, out, m, inv_l, agg, bias, heads: int, C: int):

@@ -110,6 +110,11 @@ class CSRGraph:
     csc2csr: torch.Tensor
     fwd_sched: Schedule = None
     bwd_sched: Schedule = None
+    # replicated-item partition (dist.build_replicated_graph) of a bipartite graph: (RU, pass-B
+    # schedule over the user sources [0, RU), over the item sources [RU, N) with rows relative
+    # to RU).  Item sources only reach user destinations, so their edge pass can run before the
+    # item rows of grad_out are all-reduced (hip_ops.GATLayer.backward overlaps the two).
+    bwd_split: tuple = None
 
     @property
     def device(self):
@@ -321,6 +326,40 @@ def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope
     return GATAggregate.apply(h, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed)
 
 
+def _bwd_edges_src(g: CSRGraph, sched: Schedule, r0: int, h, s_src, nstate, grad_out, D, S, dz, heads, channels,
+                   mode, slope, p, seed, seed_buf=None):
+    """Pass B over the source rows of ``sched`` (row ids relative to r0; edge slots and
+    destination rows absolute) into D, S[:, :H] and dz."""
+    lib = _lib.load()
+    dev = h.device
+    E, HC = g.n_edges, heads * channels
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_fwd_workspace_bytes(sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
+               "workspace_bytes")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    cs = sched.cstruct()
+    st = _lib.stream_handle(dev)
+    _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(g.row) if E else None,
+                                   _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, E, heads,
+                                   channels, h.data_ptr() + 4 * r0 * HC, s_src.data_ptr() + 4 * r0 * heads,
+                                   nstate.data_ptr(), grad_out.data_ptr(),
+                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                   D.data_ptr() + 4 * r0 * HC, HC,
+                                   S.data_ptr() + 4 * r0 * 2 * heads, 2 * heads, dz.data_ptr(), ws.data_ptr(),
+                                   nbytes.value, st),
+               "bwd_edges")
+
+
+def _bwd_dst_sum(g: CSRGraph, dz, S, heads):
+    lib = _lib.load()
+    dev = dz.device
+    fs = g.fwd_sched.cstruct()
+    dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), g.n_nodes, heads, dz.data_ptr(), S.data_ptr() + 4 * heads,
+                                     2 * heads, dws.data_ptr(), dws.numel() * 4, _lib.stream_handle(dev)),
+               "bwd_dst_sum")
+
+
 def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channels, mode, slope, p, seed,
                    seed_buf=None):
     """Pass B into D [N, HC] (dh_msg) and S[:, :H] (ds_src); the destination sum into
@@ -329,21 +368,9 @@ def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channel
     lib = _lib.load()
     dev = h.device
     N, E, HC = g.n_nodes, g.n_edges, heads * channels
-    sched = g.bwd_sched
-    nbytes = ctypes.c_size_t(0)
-    _lib.check(lib.ppgat_fwd_workspace_bytes(sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
-               "workspace_bytes")
-    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
     dz = torch.empty(max(E, 1) * heads, dtype=torch.float32, device=dev)
-    cs = sched.cstruct()
-    st = _lib.stream_handle(dev)
-    _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(g.row) if E else None,
-                                   _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, E, heads,
-                                   channels, h.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), grad_out.data_ptr(),
-                                   mode, float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
-                                   D.data_ptr(), HC,
-                                   S.data_ptr(), 2 * heads, dz.data_ptr(), ws.data_ptr(), nbytes.value, st),
-               "bwd_edges")
+    _bwd_edges_src(g, g.bwd_sched, 0, h, s_src, nstate, grad_out, D, S, dz, heads, channels, mode, slope, p, seed,
+                   seed_buf)
     fs = g.fwd_sched.cstruct()
     dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), N, heads, dz.data_ptr(), S.data_ptr() + 4 * heads, 2 * heads,
@@ -529,8 +556,15 @@ class GATLayer(torch.autograd.Function):
         K = x.size(1)
         HC = heads * C
         rep = ctx.rep
+        # replicated items over RCCL on a bipartite graph: the item rows' all_reduce runs on the
+        # communication stream while the item sources' edge pass (user destinations only) runs
+        overlap = rep is not None and g.bwd_split is not None and rep.async_capable()
+        pending = None
         if rep is not None:  # item rows of grad_out: per-rank partial sums -> the full gradient
-            rep.reduce_grad(g_out)
+            if overlap:
+                pending = rep.reduce_grad_async(g_out)
+            else:
+                rep.reduce_grad(g_out)
         # prologue: packed per-node state (+ dbias)
         want_db = has_bias and ctx.needs_input_grad[4]
         nstate = torch.empty(N, heads, 4, dtype=torch.float32, device=dev)
@@ -547,18 +581,30 @@ class GATLayer(torch.autograd.Function):
                                               heads, C, mode, nstate.data_ptr() + 16 * r0 * heads, _lib.ptr(db),
                                               _lib.ptr(part), _lib.stream_handle(dev)), "bwd_prologue")
 
+        D = torch.empty(N, HC, dtype=torch.float32, device=dev)
+        S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
         if rep is None:
             prologue(0, N, dbias)
+            _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed, ctx.seed_buf)
         else:  # the replicated item rows enter dbias on one rank only
             RU = rep.RU
             db_i = torch.empty(C, dtype=torch.float32, device=dev) if (want_db and rep.rank == 0) else None
             prologue(0, RU, dbias)
-            prologue(RU, N, db_i)
+            if overlap:
+                RUs, sched_u, sched_i = g.bwd_split
+                dz = torch.empty(max(g.n_edges, 1) * heads, dtype=torch.float32, device=dev)
+                _bwd_edges_src(g, sched_i, RU, h, s_src, nstate, g_out, D, S, dz, heads, C, mode, slope, p, seed,
+                               ctx.seed_buf)
+                rep.wait(pending)
+                prologue(RU, N, db_i)
+                _bwd_edges_src(g, sched_u, 0, h, s_src, nstate, g_out, D, S, dz, heads, C, mode, slope, p, seed,
+                               ctx.seed_buf)
+                _bwd_dst_sum(g, dz, S, heads)
+            else:
+                prologue(RU, N, db_i)
+                _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed, ctx.seed_buf)
             if db_i is not None:
                 dbias = dbias + db_i
-        D = torch.empty(N, HC, dtype=torch.float32, device=dev)
-        S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
-        _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed, ctx.seed_buf)
         need_dx = ctx.needs_input_grad[0] or (had_items and ctx.needs_input_grad[12])
         dx = None
         if need_dx:
