@@ -356,7 +356,10 @@ def main():
     value = E * args.layers * K / el  # the whole job: every edge of the global graph, once per layer
     dom = max(("fwd", "bwd_src", "bwd_epi"), key=lambda k: kern[k][0])
     dom_ms, dom_n = kern[dom]
-    avg_s = dom_ms / max(dom_n, 1) / 1e3
+    # one layer pass may be several launches (the sharded backward runs halo / item sources
+    # first and the rest after the exchange): average per layer pass, K steps x L layers
+    passes = args.steps * args.layers
+    avg_s = dom_ms / max(passes, 1) / 1e3
     if dist_path:
         # rank 0's kernels run over its local graph: price them on its own rows and edges
         if part == "replicated":
@@ -424,6 +427,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algo_bytes_per_launch": ab, "avg_launch_ms": avg_s * 1e3, "launches": dom_n,
+                     "launches_per_layer_pass": dom_n / max(passes, 1),
                      "measured_copy_gbs": copy_gbs},
         "loss": float(loss.item()),
         "optimizer": "Adam (libppgat device kernel, torch.optim.Adam semantics)",

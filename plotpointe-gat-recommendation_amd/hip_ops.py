@@ -371,10 +371,7 @@ def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channel
     dz = torch.empty(max(E, 1) * heads, dtype=torch.float32, device=dev)
     _bwd_edges_src(g, g.bwd_sched, 0, h, s_src, nstate, grad_out, D, S, dz, heads, channels, mode, slope, p, seed,
                    seed_buf)
-    fs = g.fwd_sched.cstruct()
-    dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), N, heads, dz.data_ptr(), S.data_ptr() + 4 * heads, 2 * heads,
-                                     dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
+    _bwd_dst_sum(g, dz, S, heads)
 
 
 def project_supported(k: int, out_cols: int) -> bool:
