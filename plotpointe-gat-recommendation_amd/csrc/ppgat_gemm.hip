@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
@@ -903,6 +905,487 @@ __global__ void __launch_bounds__(256) k_adam(AdamArg a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 GEMMs on the bf16 matrix cores: three-term split ("bf16x6")
+//
+// Every fp32 operand v is cut into three bf16 terms, h = rne(v), m = rne(v - h),
+// l = rne(v - h - m) (the two differences are exact), so v = h + m + l + e with
+// |e| <= 2^-24 |v| -- fp32's own rounding unit.  A product a b is formed as the six terms of
+// order <= 2 (l_a h_b, h_a l_b, m_a m_b, m_a h_b, h_a m_b, h_a h_b, smallest first) on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation; the dropped terms (m l, l m, l l) are
+// <= 2^-24 |a b| together.  Each bf16 product is exact in fp32, so the result carries fp32
+// GEMM accuracy (tests: vs the fp64 oracle at the fp32 path's tolerances) at 16/6 = 2.7x the
+// fp32 MFMA rate (MI355X_MICROARCH.md: 16x16x32 bf16 = 16 cycles, 16x16x4 f32 = 32 cycles per
+// SIMD).  Not bitwise equal to the fp32 FMA chain of k_proj16 (different summation order).
+// ---------------------------------------------------------------------------
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
+using f32x2e = __attribute__((ext_vector_type(2))) float;
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // v_cvt_pk_bf16_f32 (rne)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2e{a, b}, bf16x2));
+}
+__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
+// 8 fp32 values (element j of the fragment = p.x, p.y, ..., q.w) -> three bf16x8 terms
+__device__ __forceinline__ void split3(const float4& p, const float4& q, u32x4& h, u32x4& m, u32x4& l) {
+  const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t hh = pk_bf16(v[2 * i], v[2 * i + 1]);
+    const float r0 = v[2 * i] - bf_lo(hh), r1 = v[2 * i + 1] - bf_hi(hh);
+    const uint32_t mm = pk_bf16(r0, r1);
+    h[i] = hh;
+    m[i] = mm;
+    l[i] = pk_bf16(r0 - bf_lo(mm), r1 - bf_hi(mm));
+  }
+}
+__device__ __forceinline__ f32x4 mfma_bf(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_x6(const u32x4& ah, const u32x4& am, const u32x4& al, const u32x4& bh,
+                                         const u32x4& bm, const u32x4& bl, f32x4 c) {
+  c = mfma_bf(al, bh, c);
+  c = mfma_bf(ah, bl, c);
+  c = mfma_bf(am, bm, c);
+  c = mfma_bf(am, bh, c);
+  c = mfma_bf(ah, bm, c);
+  return mfma_bf(ah, bh, c);
+}
+
+// LDS image of the split B' (three parts, [128 rows][128 k] bf16, 256-B rows, no padding).
+// 16-B unit of (row n, reduction index k) within its row: the lane (jl = l & 15, kq = l >> 4)
+// reads unit 4 kq + s of row 16 cb + jl for k step s; rotating by jl and swapping the kq
+// pairs {0,1}, {2,3} of rows jl in [4, 12) makes the 16 lanes of every ds_read_b128 group
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) land on 16 distinct 16-B bank slots.
+__host__ __device__ constexpr int xs_unit(int n, int k) {
+  return (4 * ((k >> 5) ^ ((((n & 15) >= 4) && ((n & 15) < 12)) ? 1 : 0)) + ((k >> 3) & 3) + (n & 15)) & 15;
+}
+constexpr int kXsPart = kPT * kPT * 2;  // bytes per split part
+constexpr int kXsWaves = 8;
+
+// ---------------------------------------------------------------------------
+// projection GEMM on the split bf16 matrix cores (same contract as k_proj16, both modes)
+//
+// One workgroup per CU (96 KB of split B' in LDS), 8 waves, each wave persistent over 16-row
+// tiles.  The product is computed transposed: A = B' (output column n on the lane's row
+// slot), B = x (row jl of the tile on the lane's column slot), so the accumulator of column
+// block cb holds y[row jl][16 cb + 4 kq + q] in register q -- one float4 store per block --
+// and the node scores reduce over the four kq lane groups only.  x: lane (jl, kq) loads
+// x[row][32 kq .. 32 kq + 31] (8 float4, the reduction index permuted as in k_proj16), the
+// next tile's x in flight during the MFMAs; k step s uses its float4 pair 2 s, 2 s + 1.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ void __launch_bounds__(64 * kXsWaves, 1) k_projx(ProjArg a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char xs_lds[];
+  unsigned char* sW = xs_lds;                                          // 3 parts
+  float* sV = reinterpret_cast<float*>(xs_lds + 3 * kXsPart);          // [2][128] att / A
+  float* sB = sV + 2 * kPT;                                            // [128] bias
+  float* sP = sB + kPT;  // mode 1: [2][16][128] partial A = att W per 8-k chunk
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int jl = lane & 15, kq = lane >> 4;
+  const int K = a.K;
+  // ---- stage split B'[n][k] (zero past K) ----
+  for (int idx = tid; idx < kPT * 16; idx += 64 * kXsWaves) {
+    const int n = idx & 127, c = idx >> 7, k0 = 8 * c;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), q = p;
+    if (MODE == 0) {
+      if (k0 < K) p = ld4(a.W + (int64_t)n * a.ldw + k0);
+      if (k0 + 4 < K) q = ld4(a.W + (int64_t)n * a.ldw + k0 + 4);
+    } else {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = (k0 + j < K) ? a.W[(int64_t)(k0 + j) * a.ldw + n] : 0.f;
+      p = make_float4(t[0], t[1], t[2], t[3]);
+      q = make_float4(t[4], t[5], t[6], t[7]);
+      if (a.att_src) {  // partial A_v[n] over this 8-k chunk (summed over the chunks in order below)
+        float ps = 0.f, pd = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (k0 + j < K) {
+            ps = fmaf(a.att_src[k0 + j], t[j], ps);
+            pd = fmaf(a.att_dst[k0 + j], t[j], pd);
+          }
+        }
+        sP[c * kPT + n] = ps;
+        sP[16 * kPT + c * kPT + n] = pd;
+      }
+    }
+    u32x4 h, m, l;
+    split3(p, q, h, m, l);
+    const int off = n * 256 + xs_unit(n, k0) * 16;
+    *reinterpret_cast<u32x4*>(sW + off) = h;
+    *reinterpret_cast<u32x4*>(sW + kXsPart + off) = m;
+    *reinterpret_cast<u32x4*>(sW + 2 * kXsPart + off) = l;
+  }
+  const bool vec = a.att_src != nullptr;
+  if (tid < 2 * kPT) {
+    const int j = tid & 127, v = tid >> 7;
+    float s = 0.f;
+    if (vec) {
+      const float* att = v ? a.att_dst : a.att_src;
+      if (MODE == 0) {
+        s = att[j];
+      }
+    }
+    sV[v * kPT + j] = s;
+  } else if (tid < 3 * kPT) {
+    const int j = tid - 2 * kPT;
+    sB[j] = (MODE == 0 && a.bias) ? a.bias[j] : 0.f;
+  }
+  __syncthreads();
+  if (MODE == 1 && vec && tid < 2 * kPT) {  // A_v[j] = sum_k att_v[k] W[k][j], 8-k chunks in order
+    const int j = tid & 127, v = tid >> 7;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s += sP[v * 16 * kPT + c * kPT + j];
+    sV[v * kPT + j] = s;
+  }
+  if (MODE == 1) __syncthreads();
+
+  gfloat* const x0 = sgpr(a.x0);
+  gfloat* const x1 = sgpr(a.x1);
+  const int64_t ldx0 = sgpr(a.ldx0), ldx1 = sgpr(a.ldx1), split = sgpr(a.split), n = sgpr(a.n);
+  const int64_t nw = (int64_t)gridDim.x * kXsWaves;
+  const int64_t wave = (int64_t)blockIdx.x * kXsWaves + __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t tiles = (n + 15) / 16;
+  int aoff[4];  // byte offset of this lane's A unit for k step s (column block 0)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) aoff[s] = jl * 256 + xs_unit(jl, 32 * kq + 8 * s) * 16;
+
+  auto load_x = [&](int64_t tile, float4 (&xv)[8]) {
+    int64_t row = tile * 16 + jl;
+    row = row < n ? row : n - 1;
+    gfloat* src = row < split ? x0 + row * ldx0 : x1 + (row - split) * ldx1;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = 32 * kq + 4 * q;
+      xv[q] = ld4(src + (c < K ? c : K - 4));
+    }
+  };
+
+  // one tile's MFMAs and epilogue; the caller keeps the next tile's x in flight in the other
+  // register buffer (ping-pong, so no copy makes the loop wait for the prefetch)
+  auto tile_body = [&](int64_t t, const float4 (&xr)[8]) {
+    float2 dv = make_float2(0.f, 0.f);
+    const int64_t row = t * 16 + jl;
+    if (MODE == 1) dv = *reinterpret_cast<const float2*>(a.ds + (row < n ? row : n - 1) * a.ldds);
+    f32x4 acc[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 32 (k step, column block) steps; the next step's three A units are read from LDS while
+    // the current step's six MFMAs run
+    auto read_a = [&](int idx, u32x4 (&f)[3]) {
+      const unsigned char* pa = sW + aoff[idx >> 3] + (idx & 7) * 16 * 256;
+      f[0] = *reinterpret_cast<const u32x4*>(pa);
+      f[1] = *reinterpret_cast<const u32x4*>(pa + kXsPart);
+      f[2] = *reinterpret_cast<const u32x4*>(pa + 2 * kXsPart);
+    };
+    u32x4 fa[3], bh, bm, bl;
+    read_a(0, fa);
+#pragma unroll
+    for (int idx = 0; idx < 32; ++idx) {
+      const int s = idx >> 3, cb = idx & 7;
+      if (cb == 0) split3(xr[2 * s], xr[2 * s + 1], bh, bm, bl);
+      u32x4 fn[3];
+      if (idx < 31) read_a(idx + 1, fn);
+      acc[cb] = mfma_x6(fa[0], fa[1], fa[2], bh, bm, bl, acc[cb]);
+      __builtin_amdgcn_sched_barrier(0);  // keep each LDS read one step ahead (no hoisting)
+      if (idx < 31) {
+        fa[0] = fn[0];
+        fa[1] = fn[1];
+        fa[2] = fn[2];
+      }
+    }
+    // ---- epilogue: lane holds y[row][16 cb + 4 kq + q] ----
+    float ps = 0.f, pd = 0.f;
+    float* yrow = a.y + (row < n ? row : 0) * a.ldy;
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      const int c0 = 16 * cb + 4 * kq;
+      const float4 va = *reinterpret_cast<const float4*>(sV + c0);
+      const float4 vb = *reinterpret_cast<const float4*>(sV + kPT + c0);
+      float4 o;
+      if (MODE == 0) {
+        const float4 bb = *reinterpret_cast<const float4*>(sB + c0);
+        ps = fmaf(acc[cb][0], va.x, fmaf(acc[cb][1], va.y, fmaf(acc[cb][2], va.z, fmaf(acc[cb][3], va.w, ps))));
+        pd = fmaf(acc[cb][0], vb.x, fmaf(acc[cb][1], vb.y, fmaf(acc[cb][2], vb.z, fmaf(acc[cb][3], vb.w, pd))));
+        o = make_float4(acc[cb][0] + bb.x, acc[cb][1] + bb.y, acc[cb][2] + bb.z, acc[cb][3] + bb.w);
+      } else {
+        o = make_float4(fmaf(dv.y, vb.x, fmaf(dv.x, va.x, acc[cb][0])), fmaf(dv.y, vb.y, fmaf(dv.x, va.y, acc[cb][1])),
+                        fmaf(dv.y, vb.z, fmaf(dv.x, va.z, acc[cb][2])), fmaf(dv.y, vb.w, fmaf(dv.x, va.w, acc[cb][3])));
+      }
+      if (row < n) st4(yrow + c0, o);
+    }
+    if (MODE == 0 && vec) {
+      ps += __shfl_xor(ps, 16);
+      pd += __shfl_xor(pd, 16);
+      ps += __shfl_xor(ps, 32);
+      pd += __shfl_xor(pd, 32);
+      if (row < n && kq == 0) a.s_src[row] = ps;
+      if (row < n && kq == 1) a.s_dst[row] = pd;
+    }
+  };
+  float4 xa[8], xb[8];
+  int64_t t = wave;
+  if (t < tiles) load_x(t, xa);
+  while (t < tiles) {
+    if (t + nw < tiles) load_x(t + nw, xb);
+    tile_body(t, xa);
+    t += nw;
+    if (t >= tiles) break;
+    if (t + nw < tiles) load_x(t + nw, xa);
+    tile_body(t, xb);
+    t += nw;
+  }
+}
+constexpr size_t kXsLds = 3 * kXsPart + (3 + 32) * kPT * sizeof(float);
+
+// ---------------------------------------------------------------------------
+// weight-gradient GEMM on the split bf16 matrix cores (same contract and partial layout as
+// k_tn128): out = A^T B, + V^T B and colsum(A) on the VALU in fp32.
+//
+// v_mfma_f32_32x32x16_bf16 sums over 16 rows per instruction: lane (r, hf) holds rows
+// 8 hf + j (j = 0..7) of a 16-row step.  A'[m = 64 mh + 2 r + i] and B'[k = 4 r + kb] as in
+// k_tn128, so per row a lane loads one float2 of A and one float4 of B, and the three bf16
+// terms of each operand fragment are formed from eight rows of one column.  4 waves per
+// workgroup (two pairs of m halves), one workgroup per CU with 512 registers per wave: the
+// 128 accumulators, two 32-row batches of operands (one in flight) and the split terms.
+// Pair partials are summed through LDS in pair order, then the ordered split reduction
+// k_tn_reduce (deterministic).
+// ---------------------------------------------------------------------------
+constexpr int kTnxWaves = 4;
+constexpr int kTnxSteps = 1;              // MFMA k steps (16 rows each) per batch
+constexpr int kTnxRows = 16 * kTnxSteps;  // rows per batch
+
+__device__ __forceinline__ f32x16 mfma32_bf(const u32x4& a, const u32x4& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32_x6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+  c = mfma32_bf(a[2], b[0], c);
+  c = mfma32_bf(a[0], b[2], c);
+  c = mfma32_bf(a[1], b[1], c);
+  c = mfma32_bf(a[1], b[0], c);
+  c = mfma32_bf(a[0], b[1], c);
+  return mfma32_bf(a[0], b[0], c);
+}
+
+struct TnxBatch {
+  float2 av[kTnxSteps][8];
+  float4 bv[kTnxSteps][8];
+  float vv[kTnxSteps][8];
+};
+
+template <bool HASV>
+__device__ __forceinline__ void tnx_compute(f32x16 (&acc)[2][4], float4& vacc, float2& csum, const TnxBatch& b) {
+#pragma unroll
+  for (int t = 0; t < kTnxSteps; ++t) {
+    u32x4 fa[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = i ? b.av[t][j].y : b.av[t][j].x;
+      split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), fa[i][0], fa[i][1], fa[i][2]);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = comp(b.bv[t][j], kb);
+      u32x4 fb[3];
+      split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), fb[0], fb[1], fb[2]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][kb] = mfma32_x6(fa[i], fb, acc[i][kb]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (HASV) {
+        vacc.x = fmaf(b.vv[t][j], b.bv[t][j].x, vacc.x);
+        vacc.y = fmaf(b.vv[t][j], b.bv[t][j].y, vacc.y);
+        vacc.z = fmaf(b.vv[t][j], b.bv[t][j].z, vacc.z);
+        vacc.w = fmaf(b.vv[t][j], b.bv[t][j].w, vacc.w);
+      }
+      csum.x += b.av[t][j].x;
+      csum.y += b.av[t][j].y;
+    }
+  }
+}
+
+template <int NV, bool MASK>
+__global__ void __launch_bounds__(64 * kTnxWaves, 1) k_tnx(TnArg a) {
+  __shared__ float sR[kPT][kPT + 4];
+  __shared__ float sVr[kTnxWaves / 2][2][kPT];
+  __shared__ float sC[kTnxWaves / 2][kPT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int mh = w & 1, pr = w >> 1;
+  const int64_t pid = (int64_t)blockIdx.x * (kTnxWaves / 2) + pr;
+  const int64_t n_beg = pid * a.rows_per_pair;
+  const int64_t n_end = min(a.n, n_beg + a.rows_per_pair);
+  const int mcol = 64 * mh + 2 * r;
+  const bool am = !MASK || mcol < a.M, bk = !MASK || 4 * r < a.K;
+  const int acol = am ? mcol : 0, bcol = bk ? 4 * r : 0;
+  const bool hasv = mh < NV;
+  const int vcol = hasv ? mh : 0;
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  float4 vacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 csum = make_float2(0.f, 0.f);
+  for (int seg = 0; seg < 2; ++seg) {
+    const int64_t r0 = seg == 0 ? n_beg : max(n_beg, a.split);
+    const int64_t r1 = seg == 0 ? min(n_end, a.split) : n_end;
+    if (r0 >= r1) continue;
+    const float* bbase = seg == 0 ? a.B : a.B1;
+    const int64_t ldb = seg == 0 ? a.ldb : a.ldb1;
+    const int64_t boff = seg == 0 ? 0 : a.split;
+    const int64_t full = (r1 - r0) / kTnxRows;
+    // lane's row for (t, j) of a batch starting at row b: b + 16 t + 8 hf + j
+    auto load = [&](int64_t b0, TnxBatch& bt, bool tail) {
+#pragma unroll
+      for (int t = 0; t < kTnxSteps; ++t)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          int64_t row = b0 + 16 * t + 8 * hf + j;
+          const bool ok = !tail || row < r1;
+          row = ok ? row : r0;
+          const float2 va = *reinterpret_cast<const float2*>(a.A + row * a.lda + acol);
+          const float4 vb = ld4(bbase + (row - boff) * ldb + bcol);
+          const float vv = NV > 0 ? a.V[row * a.ldv + vcol] : 0.f;
+          if (MASK || tail) {
+            bt.av[t][j] = (ok && am) ? va : make_float2(0.f, 0.f);
+            bt.bv[t][j] = (ok && bk) ? vb : make_float4(0.f, 0.f, 0.f, 0.f);
+            bt.vv[t][j] = ok ? vv : 0.f;
+          } else {
+            bt.av[t][j] = va;
+            bt.bv[t][j] = vb;
+            bt.vv[t][j] = vv;
+          }
+        }
+    };
+    // fast path: buffer loads from descriptors based at the batch's first row, so a lane's
+    // addresses are one 32-bit lane offset plus a scalar row offset (no 64-bit address
+    // registers per row)
+    const uint32_t lane_a = (uint32_t)((8 * hf * a.lda + acol) * 4);
+    const uint32_t lane_b = (uint32_t)((8 * hf * ldb + bcol) * 4);
+    const uint32_t lane_v = (uint32_t)((8 * hf * a.ldv + vcol) * 4);
+    auto load_fast = [&](int64_t b0, TnxBatch& bt) {
+      const auto rA = __builtin_amdgcn_make_buffer_rsrc((void*)(a.A + b0 * a.lda), 0, 0x7fffffff, 0x00020000);
+      const auto rB = __builtin_amdgcn_make_buffer_rsrc((void*)(bbase + (b0 - boff) * ldb), 0, 0x7fffffff, 0x00020000);
+      const auto rV = __builtin_amdgcn_make_buffer_rsrc((void*)(a.V + b0 * a.ldv), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < kTnxSteps; ++t)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int rr = 16 * t + j;
+          const auto va = __builtin_amdgcn_raw_buffer_load_b64(rA, lane_a, (int)(rr * a.lda * 4), 0);
+          const auto vb = __builtin_amdgcn_raw_buffer_load_b128(rB, lane_b, (int)(rr * ldb * 4), 0);
+          bt.av[t][j] = make_float2(__uint_as_float(va[0]), __uint_as_float(va[1]));
+          bt.bv[t][j] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
+                                    __uint_as_float(vb[3]));
+          bt.vv[t][j] = NV > 0 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rV, lane_v, (int)(rr * a.ldv * 4), 0))
+                               : 0.f;
+        }
+    };
+    if (MASK) {  // rare shapes (M or K < 128): no batch in flight (the masks cost the registers)
+      for (int64_t bi = 0; bi < full; ++bi) {
+        TnxBatch cur;
+        load(r0 + bi * kTnxRows, cur, false);
+        tnx_compute<NV != 0>(acc, vacc, csum, cur);
+      }
+    } else if (full > 0) {  // ring of three buffers: two batches in flight during the MFMAs
+      TnxBatch b0, b1, b2;
+      load_fast(r0, b0);
+      if (full > 1) load_fast(r0 + kTnxRows, b1);
+      int64_t bi = 0;
+      while (true) {
+        if (bi + 2 < full) load_fast(r0 + (bi + 2) * kTnxRows, b2);
+        __builtin_amdgcn_sched_barrier(0);
+        tnx_compute<NV != 0>(acc, vacc, csum, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++bi >= full) break;
+        if (bi + 2 < full) load_fast(r0 + (bi + 2) * kTnxRows, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        tnx_compute<NV != 0>(acc, vacc, csum, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++bi >= full) break;
+        if (bi + 2 < full) load_fast(r0 + (bi + 2) * kTnxRows, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        tnx_compute<NV != 0>(acc, vacc, csum, b2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++bi >= full) break;
+      }
+    }
+    const int64_t t0 = r0 + full * kTnxRows;
+    if (t0 < r1) {
+      TnxBatch tb;
+      load(t0, tb, true);
+      tnx_compute<NV != 0>(acc, vacc, csum, tb);
+    }
+  }
+  // ---- workgroup reduction through LDS, pairs in order ----
+  auto put = [&](bool add) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = 64 * mh + 2 * acc_row(q, hf) + i;
+        float4 v = make_float4(acc[i][0][q], acc[i][1][q], acc[i][2][q], acc[i][3][q]);
+        float* dst = &sR[m][4 * r];
+        if (add) {
+          const float4 o = *reinterpret_cast<const float4*>(dst);
+          v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        }
+        st4(dst, v);
+      }
+  };
+  if (pr == 0) put(false);
+  __syncthreads();
+  if (pr == 1) put(true);
+  {
+    float t[4] = {vacc.x, vacc.y, vacc.z, vacc.w};
+    float c[2] = {csum.x, csum.y};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x0, x1;
+      row_swap<32>(t[e], t[e], x0, x1);
+      t[e] = x0 + x1;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float x0, x1;
+      row_swap<32>(c[e], c[e], x0, x1);
+      c[e] = x0 + x1;
+    }
+    if (hf == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sVr[pr][mh][4 * r + e] = hasv ? t[e] : 0.f;
+      sC[pr][mcol] = c[0];
+      sC[pr][mcol + 1] = c[1];
+    }
+  }
+  __syncthreads();
+  float* P = a.part + (int64_t)blockIdx.x * kPT * kPT;
+  for (int idx = tid; idx < kPT * kPT / 4; idx += 64 * kTnxWaves) {
+    const int m = idx >> 5, k4 = (idx & 31) * 4;
+    st4(P + m * kPT + k4, *reinterpret_cast<const float4*>(&sR[m][k4]));
+  }
+  if (tid < 2 * kPT) {
+    const int v = tid >> 7, k = tid & 127;
+    a.vpart[((int64_t)blockIdx.x * 2 + v) * kPT + k] = sVr[0][v][k] + sVr[1][v][k];
+  }
+  if (a.cpart && tid < kPT) a.cpart[(int64_t)blockIdx.x * kPT + tid] = sC[0][tid] + sC[1][tid];
+}
+
 }  // namespace
 
 // ---- host launchers ----
@@ -925,6 +1408,33 @@ static unsigned proj32_grid(int64_t n) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
+// Which projection kernel runs: the split-bf16 matrix-core kernel k_projx (default) or the
+// fp32 MFMA kernel k_proj16 (PPGAT_GEMM=fp32: exact fp32 FMA chains).  Read once per process.
+bool gemm_split_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PPGAT_GEMM");
+    return !(e && strcmp(e, "fp32") == 0);
+  }();
+  return on;
+}
+
+static bool projx_ok(const float* y, int64_t ldy) {
+  return gemm_split_enabled() && (ldy % 4) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+}
+
+template <int MODE>
+static void launch_projx(const ProjArg& a, hipStream_t st) {
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_projx<MODE>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXsLds) == hipSuccess;
+  }();
+  (void)attr;
+  const int64_t tiles = (a.n + 15) / 16;
+  int64_t g = (tiles + kXsWaves - 1) / kXsWaves;
+  if (g > 256) g = 256;  // one workgroup per CU, persistent over the 16-row tiles
+  hipLaunchKernelGGL(k_projx<MODE>, dim3((unsigned)(g < 1 ? 1 : g)), dim3(64 * kXsWaves), kXsLds, st, a);
+}
+
 static unsigned proj16_grid(int64_t n) {
   const int64_t tiles = (n + 15) / 16;
   int64_t g = (tiles + 3) / 4;
@@ -940,7 +1450,9 @@ hipError_t proj_fwd(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1
   a.x0 = x0; a.ldx0 = ldx0; a.x1 = x1 ? x1 : x0; a.ldx1 = x1 ? ldx1 : ldx0; a.split = x1 ? split : n; a.n = n;
   a.K = K; a.W = W; a.ldw = ldw; a.bias = bias; a.att_src = att_src; a.att_dst = att_dst;
   a.y = y; a.ldy = ldy; a.s_src = s_src; a.s_dst = s_dst;
-  if (proj32_ok(K, ldx0, x1 ? ldx1 : ldx0)) {
+  if (projx_ok(y, ldy)) {
+    launch_projx<0>(a, st);
+  } else if (proj32_ok(K, ldx0, x1 ? ldx1 : ldx0)) {
     if (K == 128) hipLaunchKernelGGL((k_proj32<0, 16>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_proj32<0, 8>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
   } else {
@@ -955,6 +1467,10 @@ hipError_t proj_dx(const float* D, int64_t ldd, int64_t n, int K, const float* W
   ProjArg a{};
   a.x0 = D; a.ldx0 = ldd; a.x1 = D; a.ldx1 = ldd; a.split = n; a.n = n; a.K = K; a.W = W; a.ldw = ldw;
   a.att_src = att_src; a.att_dst = att_dst; a.ds = S; a.ldds = lds; a.y = y; a.ldy = ldy;
+  if (projx_ok(y, ldy)) {
+    launch_projx<1>(a, st);
+    return hipGetLastError();
+  }
   if (proj32_ok(K, ldd, ldd)) {
     if (K == 128) hipLaunchKernelGGL((k_proj32<1, 16>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_proj32<1, 8>), dim3(proj32_grid(n)), dim3(256), 0, st, a);
@@ -1005,6 +1521,18 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
                    : nullptr;
   const bool mask = M != kPT || K != kPT;
   const int NVk = nv;
+  if (gemm_split_enabled()) {
+    const int64_t pairs_x = nb * (kTnxWaves / 2);
+    a.rows_per_pair = ((N + pairs_x - 1) / pairs_x + kTnxRows - 1) / kTnxRows * kTnxRows;
+#define PPGAT_TNX(NV_, MASK_) \
+  hipLaunchKernelGGL((k_tnx<NV_, MASK_>), dim3((unsigned)nb), dim3(64 * kTnxWaves), 0, st, a)
+    if (mask) {
+      if (NVk == 0) PPGAT_TNX(0, true); else if (NVk == 1) PPGAT_TNX(1, true); else PPGAT_TNX(2, true);
+    } else {
+      if (NVk == 0) PPGAT_TNX(0, false); else if (NVk == 1) PPGAT_TNX(1, false); else PPGAT_TNX(2, false);
+    }
+#undef PPGAT_TNX
+  } else {
 #define PPGAT_TN(NV_, MASK_) \
   hipLaunchKernelGGL((k_tn128<NV_, MASK_>), dim3((unsigned)nb), dim3(64 * kTnWaves), 0, st, a)
   if (mask) {
@@ -1013,6 +1541,7 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
     if (NVk == 0) PPGAT_TN(0, false); else if (NVk == 1) PPGAT_TN(1, false); else PPGAT_TN(2, false);
   }
 #undef PPGAT_TN
+  }
   TnReduceArg ra{};
   ra.part = a.part; ra.vpart = a.vpart; ra.cpart = a.cpart; ra.splits = nb; ra.M = M; ra.K = K; ra.nv = nv;
   ra.out = out; ra.vout = vout; ra.colsum = colsum;
