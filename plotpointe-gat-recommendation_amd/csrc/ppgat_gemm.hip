@@ -34,6 +34,7 @@
 
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
+#include "ppgat_split.h"
 
 // Projection kernel occupancy: 2 waves per SIMD (256 VGPRs, two workgroups per CU).
 #ifndef PPGAT_PROJ16_OCC
@@ -906,54 +907,11 @@ __global__ void __launch_bounds__(256) k_adam(AdamArg a) {
 }
 
 // ---------------------------------------------------------------------------
-// fp32 GEMMs on the bf16 matrix cores: three-term split ("bf16x6")
-//
-// Every fp32 operand v is cut into three bf16 terms, h = rne(v), m = rne(v - h),
-// l = rne(v - h - m) (the two differences are exact), so v = h + m + l + e with
-// |e| <= 2^-24 |v| -- fp32's own rounding unit.  A product a b is formed as the six terms of
-// order <= 2 (l_a h_b, h_a l_b, m_a m_b, m_a h_b, h_a m_b, h_a h_b, smallest first) on
-// v_mfma_f32_16x16x32_bf16 with fp32 accumulation; the dropped terms (m l, l m, l l) are
-// <= 2^-24 |a b| together.  Each bf16 product is exact in fp32, so the result carries fp32
-// GEMM accuracy (tests: vs the fp64 oracle at the fp32 path's tolerances) at 16/6 = 2.7x the
-// fp32 MFMA rate (MI355X_MICROARCH.md: 16x16x32 bf16 = 16 cycles, 16x16x4 f32 = 32 cycles per
-// SIMD).  Not bitwise equal to the fp32 FMA chain of k_proj16 (different summation order).
+// fp32 GEMMs on the bf16 matrix cores: three-term split ("bf16x6", ppgat_split.h)
 // ---------------------------------------------------------------------------
-using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
-using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
-using f32x2e = __attribute__((ext_vector_type(2))) float;
-
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // v_cvt_pk_bf16_f32 (rne)
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2e{a, b}, bf16x2));
-}
-__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
-
-// 8 fp32 values (element j of the fragment = p.x, p.y, ..., q.w) -> three bf16x8 terms
-__device__ __forceinline__ void split3(const float4& p, const float4& q, u32x4& h, u32x4& m, u32x4& l) {
-  const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t hh = pk_bf16(v[2 * i], v[2 * i + 1]);
-    const float r0 = v[2 * i] - bf_lo(hh), r1 = v[2 * i + 1] - bf_hi(hh);
-    const uint32_t mm = pk_bf16(r0, r1);
-    h[i] = hh;
-    m[i] = mm;
-    l[i] = pk_bf16(r0 - bf_lo(mm), r1 - bf_hi(mm));
-  }
-}
-__device__ __forceinline__ f32x4 mfma_bf(const u32x4& a, const u32x4& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                 0, 0, 0);
-}
-__device__ __forceinline__ f32x4 mfma_x6(const u32x4& ah, const u32x4& am, const u32x4& al, const u32x4& bh,
-                                         const u32x4& bm, const u32x4& bl, f32x4 c) {
-  c = mfma_bf(al, bh, c);
-  c = mfma_bf(ah, bl, c);
-  c = mfma_bf(am, bm, c);
-  c = mfma_bf(am, bh, c);
-  c = mfma_bf(ah, bm, c);
-  return mfma_bf(ah, bh, c);
-}
+using split::mfma32_x6;
+using split::mfma_x6;
+using split::split3;
 
 // LDS image of the split B' (three parts, [128 rows][128 k] bf16, 256-B rows, no padding).
 // 16-B unit of (row n, reduction index k) within its row: the lane (jl = l & 15, kq = l >> 4)
@@ -987,6 +945,30 @@ __global__ void __launch_bounds__(64 * kXsWaves, 1) k_projx(ProjArg a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int jl = lane & 15, kq = lane >> 4;
   const int K = a.K;
+  gfloat* const x0 = sgpr(a.x0);
+  gfloat* const x1 = sgpr(a.x1);
+  const int64_t ldx0 = sgpr(a.ldx0), ldx1 = sgpr(a.ldx1), split = sgpr(a.split), n = sgpr(a.n);
+  const int64_t nw = (int64_t)gridDim.x * kXsWaves;
+  const int64_t wave = (int64_t)blockIdx.x * kXsWaves + __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t tiles = (n + 15) / 16;
+  int aoff[4];  // byte offset of this lane's A unit for k step s (column block 0)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) aoff[s] = jl * 256 + xs_unit(jl, 32 * kq + 8 * s) * 16;
+
+  auto load_x = [&](int64_t tile, float4 (&xv)[8]) {
+    int64_t row = tile * 16 + jl;
+    row = row < n ? row : n - 1;
+    gfloat* src = row < split ? x0 + row * ldx0 : x1 + (row - split) * ldx1;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = 32 * kq + 4 * q;
+      xv[q] = ld4(src + (c < K ? c : K - 4));
+    }
+  };
+
+  // the first tile's x is in flight while B' is staged
+  float4 xa[8], xb[8];
+  if (wave < tiles) load_x(wave, xa);
   // ---- stage split B'[n][k] (zero past K) ----
   for (int idx = tid; idx < kPT * 16; idx += 64 * kXsWaves) {
     const int n = idx & 127, c = idx >> 7, k0 = 8 * c;
@@ -1044,27 +1026,6 @@ __global__ void __launch_bounds__(64 * kXsWaves, 1) k_projx(ProjArg a) {
     sV[v * kPT + j] = s;
   }
   if (MODE == 1) __syncthreads();
-
-  gfloat* const x0 = sgpr(a.x0);
-  gfloat* const x1 = sgpr(a.x1);
-  const int64_t ldx0 = sgpr(a.ldx0), ldx1 = sgpr(a.ldx1), split = sgpr(a.split), n = sgpr(a.n);
-  const int64_t nw = (int64_t)gridDim.x * kXsWaves;
-  const int64_t wave = (int64_t)blockIdx.x * kXsWaves + __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t tiles = (n + 15) / 16;
-  int aoff[4];  // byte offset of this lane's A unit for k step s (column block 0)
-#pragma unroll
-  for (int s = 0; s < 4; ++s) aoff[s] = jl * 256 + xs_unit(jl, 32 * kq + 8 * s) * 16;
-
-  auto load_x = [&](int64_t tile, float4 (&xv)[8]) {
-    int64_t row = tile * 16 + jl;
-    row = row < n ? row : n - 1;
-    gfloat* src = row < split ? x0 + row * ldx0 : x1 + (row - split) * ldx1;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = 32 * kq + 4 * q;
-      xv[q] = ld4(src + (c < K ? c : K - 4));
-    }
-  };
 
   // one tile's MFMAs and epilogue; the caller keeps the next tile's x in flight in the other
   // register buffer (ping-pong, so no copy makes the loop wait for the prefetch)
@@ -1128,9 +1089,7 @@ __global__ void __launch_bounds__(64 * kXsWaves, 1) k_projx(ProjArg a) {
       if (row < n && kq == 1) a.s_dst[row] = pd;
     }
   };
-  float4 xa[8], xb[8];
   int64_t t = wave;
-  if (t < tiles) load_x(t, xa);
   while (t < tiles) {
     if (t + nw < tiles) load_x(t + nw, xb);
     tile_body(t, xa);
@@ -1159,19 +1118,6 @@ constexpr size_t kXsLds = 3 * kXsPart + (3 + 32) * kPT * sizeof(float);
 constexpr int kTnxWaves = 4;
 constexpr int kTnxSteps = 1;              // MFMA k steps (16 rows each) per batch
 constexpr int kTnxRows = 16 * kTnxSteps;  // rows per batch
-
-__device__ __forceinline__ f32x16 mfma32_bf(const u32x4& a, const u32x4& b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                 0, 0, 0);
-}
-__device__ __forceinline__ f32x16 mfma32_x6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
-  c = mfma32_bf(a[2], b[0], c);
-  c = mfma32_bf(a[0], b[2], c);
-  c = mfma32_bf(a[1], b[1], c);
-  c = mfma32_bf(a[1], b[0], c);
-  c = mfma32_bf(a[0], b[1], c);
-  return mfma32_bf(a[0], b[0], c);
-}
 
 struct TnxBatch {
   float2 av[kTnxSteps][8];

@@ -151,6 +151,8 @@ hipError_t relu_dropout(const float* z, int64_t n, float p, uint64_t seed, int b
 // aggregate-then-transform multi-head layer and fp32 MFMA GEMMs (ppgat_xform.hip)
 hipError_t seed_snapshot(uint64_t seed, uint64_t* out, hipStream_t st);
 bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode);
+// split-bf16 matrix-core GEMMs on (default) or the fp32 MFMA kernels (PPGAT_GEMM=fp32)
+bool gemm_split_enabled();
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
                    float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st,
                    void* ws = nullptr);

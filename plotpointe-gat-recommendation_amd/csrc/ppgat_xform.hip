@@ -33,6 +33,7 @@
 
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
+#include "ppgat_split.h"
 
 namespace ppgat {
 namespace {
@@ -200,6 +201,152 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nn(NnArg a) {
       store_b();
 #pragma unroll
       for (int g = 0; g < 4; ++g) xa[g] = xn[g];
+    }
+    __syncthreads();
+  }
+  const int64_t row0 = rb * kGBM + wv * 32;
+  if (a.splits > 1) {
+    float* part = a.part + (int64_t)split * M * a.N;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        if (row < M) part[row * a.N + col] = acc[t][q];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 32 * t + r;
+    const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      if (row < M) a.Y[row * a.ldy + col] = fmaf(a.alpha, acc[t][q], bv);
+    }
+  }
+}
+
+// NN GEMM on the split bf16 matrix cores (ppgat_split.h), same contract, block order and
+// split-K partials as k_gemm_nn.  v_mfma_f32_32x32x16_bf16: lane (r, hf) holds A[row r][8 hf + j]
+// and B[8 hf + j][col r]; a 32-deep k chunk is two MFMA steps u, and lane half hf's element j
+// of step u is k = 16 u + 4 hf + (j & 3) + 8 (j >> 2) -- exactly the two float4 xa[2u], xa[2u+1]
+// a lane already streams from its X row.  The B chunk is split once per workgroup while being
+// staged: three bf16 images [n][kk] with kk the position of k in that order (80-B rows: the 16
+// lanes of every ds_read_b128 group hit distinct bank slots), one b128 read per part per tile.
+template <int NT, int BMODE, int KC>
+__global__ void __launch_bounds__(256, 2) k_gemm_nnx(NnArg a) {
+  constexpr int BN = 32 * NT;
+  constexpr int LDK = KC + 8;             // bf16 per image row (KC + 8 pad: an odd number of 16-B units)
+  constexpr int PART = BN * LDK;          // bf16 per part
+  constexpr int G = BN * (KC / 4) / 256;  // 4-k groups staged per thread per chunk
+  constexpr int XG = KC / 8;              // float4 of X per lane per chunk
+  __shared__ __attribute__((aligned(16))) uint16_t sB[3 * PART];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t b = blockIdx.x;
+  int64_t rb;
+  int n0, split = 0;
+  if (a.splits > 1) {
+    split = (int)(b % a.splits);
+    const int64_t rest = b / a.splits;
+    n0 = (int)(rest % a.n_blocks) * BN;
+    rb = rest / a.n_blocks;
+  } else {
+    const int64_t idx = b >> 3;
+    rb = (idx / a.n_blocks) * 8 + (b & 7);
+    n0 = (int)(idx % a.n_blocks) * BN;
+  }
+  if (rb >= a.row_blocks) return;
+  const int64_t M = a.M;
+  const int kbeg = split * a.k_per;
+  const int K = a.splits > 1 ? (kbeg + a.k_per < a.K ? kbeg + a.k_per : a.K) : a.K;
+  const int64_t m = rb * kGBM + wv * 32 + r;
+  const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;
+
+  // staged group e = tid + 256 s: column n, reduction indices 4 q .. 4 q + 3 of the chunk
+  auto grp = [&](int s, int& n, int& q) {
+    const int e = tid + 256 * s;
+    if (BMODE == 0) { n = e % BN; q = e / BN; }                   // a k row is contiguous in n
+    else { n = e / (KC / 4); q = e % (KC / 4); }                 // an n row is contiguous in k
+  };
+  float4 bst[G];
+  auto load_b = [&](int kc) {
+#pragma unroll
+    for (int s = 0; s < G; ++s) {
+      int n, q;
+      grp(s, n, q);
+      if (BMODE == 0) {
+        const float* p = a.B + (int64_t)(kc + 4 * q) * a.ldb + n0 + n;
+        bst[s] = make_float4(p[0], p[a.ldb], p[2 * a.ldb], p[3 * a.ldb]);
+      } else {
+        bst[s] = ld4(a.B + (int64_t)(n0 + n) * a.ldb + kc + 4 * q);
+      }
+    }
+  };
+  auto store_b = [&]() {
+#pragma unroll
+    for (int s = 0; s < G; ++s) {
+      int n, q;
+      grp(s, n, q);
+      const int kk = 16 * (q >> 2) + 8 * (q & 1) + 4 * ((q >> 1) & 1);
+      const float v[4] = {bst[s].x, bst[s].y, bst[s].z, bst[s].w};
+      uint2 h, mm, l;
+      uint32_t* ph = &h.x;
+      uint32_t* pm = &mm.x;
+      uint32_t* pl = &l.x;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t hh = split::pk_bf16(v[2 * i], v[2 * i + 1]);
+        const float r0 = v[2 * i] - split::bf_lo(hh), r1 = v[2 * i + 1] - split::bf_hi(hh);
+        const uint32_t m2 = split::pk_bf16(r0, r1);
+        ph[i] = hh;
+        pm[i] = m2;
+        pl[i] = split::pk_bf16(r0 - split::bf_lo(m2), r1 - split::bf_hi(m2));
+      }
+      const int off = n * LDK + kk;
+      *reinterpret_cast<uint2*>(&sB[off]) = h;
+      *reinterpret_cast<uint2*>(&sB[PART + off]) = mm;
+      *reinterpret_cast<uint2*>(&sB[2 * PART + off]) = l;
+    }
+  };
+  float4 xa[XG], xn[XG];
+#pragma unroll
+  for (int g = 0; g < XG; ++g) xa[g] = ld4(xrow + kbeg + 8 * g);
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+  load_b(kbeg);
+  store_b();
+  __syncthreads();
+  for (int kc = kbeg; kc < K; kc += KC) {
+    const bool more = kc + KC < K;
+    if (more) {
+      load_b(kc + KC);
+#pragma unroll
+      for (int g = 0; g < XG; ++g) xn[g] = ld4(xrow + kc + KC + 8 * g);
+    }
+#pragma unroll
+    for (int u = 0; u < KC / 16; ++u) {
+      split::u32x4 fx[3];
+      split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int off = (32 * t + r) * LDK + 16 * u + 8 * hf;
+        split::u32x4 fb[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[p] = *reinterpret_cast<const split::u32x4*>(&sB[p * PART + off]);
+        acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_b();
+#pragma unroll
+      for (int g = 0; g < XG; ++g) xa[g] = xn[g];
     }
     __syncthreads();
   }
@@ -837,6 +984,23 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
     a.splits = (chunks + per - 1) / per;
     a.part = static_cast<float*>(ws);
   }
+  if (gemm_split_enabled()) {  // split bf16 matrix cores, two workgroups per CU
+    a.n_blocks = N / 128;
+    // 256-wide tiles when N allows (measured at config-5 shapes: 5.6-6.5 ms against 5.9-7.0 for
+    // 128-wide tiles or 64-deep k chunks, profiles/r02/v13_gemm_split_cfg5.log)
+    const bool w8 = N % 256 == 0;
+    if (w8) a.n_blocks = N / 256;
+    const unsigned gv = a.splits > 1 ? (unsigned)(a.row_blocks * a.n_blocks * a.splits)
+                                     : (unsigned)(padded * a.n_blocks);
+#define PPGAT_NNX(NT_, KC_)                                                                     \
+  do {                                                                                          \
+    if (bmode == 0) hipLaunchKernelGGL((k_gemm_nnx<NT_, 0, KC_>), dim3(gv), dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((k_gemm_nnx<NT_, 1, KC_>), dim3(gv), dim3(256), 0, st, a);            \
+  } while (0)
+    if (w8) PPGAT_NNX(8, 32);
+    else PPGAT_NNX(4, 32);
+#undef PPGAT_NNX
+  } else {
   const unsigned grid = a.splits > 1 ? (unsigned)(a.row_blocks * a.n_blocks * a.splits)
                                      : (unsigned)(padded * a.n_blocks);
 #define PPGAT_NN(NT_, BM_) hipLaunchKernelGGL((k_gemm_nn<NT_, BM_>), dim3(grid), dim3(256), 0, st, a)
@@ -846,6 +1010,7 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
     if (bmode == 0) PPGAT_NN(4, 0); else PPGAT_NN(4, 1);
   }
 #undef PPGAT_NN
+  }
   if (a.splits > 1) {
     const int64_t n4 = M * (N / 4);
     hipLaunchKernelGGL(k_nn_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, M, N, a.splits,

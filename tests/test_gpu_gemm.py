@@ -1,7 +1,14 @@
 """Projection GEMMs, weight-gradient assembly and the device Adam (GPU), against fp64 torch
 restatements of the same ops (GATConv.lin + node scores, its input/weight gradients,
-torch.optim.Adam).  Tolerance: max-abs error / max-abs reference <= 1e-5 (fp32 MFMA)."""
+torch.optim.Adam).  Tolerance: max-abs error / max-abs reference <= 1e-5.  The default
+GEMM family is the split-bf16 matrix-core one (csrc/ppgat_split.h); test_both_gemm_families
+runs the config-2 and config-5 shapes once per family (PPGAT_GEMM is read once per process)."""
+import json
+import os
+import subprocess
+import sys
 from importlib import import_module
+from pathlib import Path
 
 import pytest
 import torch
@@ -176,3 +183,24 @@ def test_gemm_tn_large_shape_deterministic(pkg, cuda):
     assert rel(vo, A[:, 1024:1032].t() @ B) <= 1e-5
     out2, cs2, vo2 = ops.gemm_tn(Ad[:, :1024], Bd, want_colsum=True, V=Ad[:, 1024:1032])
     assert torch.equal(out, out2) and torch.equal(cs, cs2) and torch.equal(vo, vo2)
+
+
+@pytest.mark.parametrize("family", ["split", "fp32"])
+def test_both_gemm_families(cuda, family):
+    """Projection (x W^T + scores, + bias), dx and weight-gradient GEMMs at config-2 rows, and
+    the config-5 NN shapes, in a fresh process per family: both within 2e-6 of fp64 (tighter
+    than the suite's 1e-5), bitwise repeatable, the two B layouts of the NN GEMM identical."""
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, PPGAT_GEMM=family)
+    res = {}
+    for extra in ([], ["--cfg5"]):
+        out = subprocess.run([sys.executable, str(root / "tools" / "gemm_split_check.py"), "--iters", "3"] + extra,
+                             env=env, capture_output=True, text=True, timeout=300, cwd=str(root))
+        assert out.returncode == 0, out.stderr[-2000:]
+        res.update(json.loads(out.stdout.strip().splitlines()[-1]))
+    assert res["mode"] == family
+    for k, v in res.items():
+        if k.endswith("_err"):
+            assert v <= (5e-6 if k == "tn_big_err" else 2e-6), (k, v)
+    assert res["fwd_bitwise_repeat"]
+    assert res["out_1024x256_layouts_equal"] and res["gt_256x1024_layouts_equal"]

@@ -36,13 +36,48 @@ def rel(a, b):
     return float((a.double() - b).abs().max() / b.abs().max())
 
 
+def cfg5(dev, iters):
+    """Config-5 share shapes (M = 1.875M rows): out = agg W_t ([M, 1024] x [1024, 256]) and
+    gt = g W_g ([M, 256] x [256, 1024]) through ppgat_gemm_nn (both B layouts), and the weight
+    gradient G = g^T agg ([M, 256]^T [M, 1024], ppgat_gemm_tn_big); errors vs fp64 on 4096
+    sampled rows (NN) and on the whole product (TN)."""
+    M = 1_875_000
+    g = torch.Generator(device=dev).manual_seed(0)
+    out = {"mode": os.environ.get("PPGAT_GEMM", "split"), "cfg": 5}
+    rows = torch.randint(0, M, (4096,), device=dev, generator=g)
+    for name, K, Nc in (("out_1024x256", 1024, 256), ("gt_256x1024", 256, 1024)):
+        X = torch.randn(M, K, device=dev, generator=g)
+        B0 = torch.randn(K, Nc, device=dev, generator=g) * 0.05
+        B1 = B0.t().contiguous()
+        y0 = ops.gemm_nn(X, B0, 0, Nc)
+        y1 = ops.gemm_nn(X, B1, 1, Nc)
+        out[f"{name}_layouts_equal"] = bool(torch.equal(y0, y1))
+        out[f"{name}_err"] = rel(y0[rows], X[rows].double() @ B0.double())
+        for lay, B in ((0, B0), (1, B1)):
+            us = timeit(lambda: ops.gemm_nn(X, B, lay, Nc, out=y0), iters)
+            out[f"{name}_layout{lay}_us"] = us
+            out[f"{name}_layout{lay}_tflops"] = 2.0 * M * K * Nc / us / 1e6
+        del X, y0, y1
+    A = torch.randn(M, 256, device=dev, generator=g)
+    Bt = torch.randn(M, 1024, device=dev, generator=g)
+    G = ops.gemm_tn_big(A, Bt)
+    out["tn_big_err"] = rel(G, A.double().t() @ Bt.double())
+    us = timeit(lambda: ops.gemm_tn_big(A, Bt), iters)
+    out["tn_big_us"] = us
+    out["tn_big_tflops"] = 2.0 * M * 256 * 1024 / us / 1e6
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=255_404)
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cfg5", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if args.cfg5:
+        return cfg5(dev, max(3, args.iters // 4))
     N, K = args.n, args.k
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(N, K, device=dev, generator=g)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Session 17: split-bf16 NN GEMM (k_gemm_nnx) at config-5 shapes vs the fp32 kernels; config-5 bench.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$(pwd); mkdir -p gpurun_out/s17; export TMPDIR=/tmp
+run() { local name=$1 to=$2; shift 2; timeout -k 10 "$to" "$@" > gpurun_out/s17/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -3 gpurun_out/s17/$name.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
+run cfg5_split 200 python -u tools/gemm_split_check.py --cfg5
+PPGAT_GEMM=fp32 run cfg5_fp32 200 python -u tools/gemm_split_check.py --cfg5
+run pytest 300 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_xgat.py tests/test_gpu_fusion.py -m gpu -q -rf --timeout 170 --timeout-method thread
+run bench5 300 python -u bench.py --config 5 --steps 10 --warmup 3 --cpu-baseline-seconds 0
+echo done
