@@ -30,6 +30,7 @@
 
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
+#include "ppgat_split.h"
 
 namespace ppgat {
 namespace {
@@ -197,6 +198,195 @@ __global__ void __launch_bounds__(256, 2) k_fusion_fwd(const float* __restrict__
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// The same MLP on the split bf16 matrix cores (ppgat_split.h: fp32 products as six bf16
+// MFMAs of three-term splits, fp32 accumulation), same contract and row ownership.
+//  GEMM1  v_mfma_f32_32x32x16_bf16, 32-deep k chunks = two MFMA steps u; lane half hf's
+//         element j of step u is k = 16 u + 4 hf + (j & 3) + 8 (j >> 2), i.e. the float4 pair
+//         xa[2u], xa[2u + 1] the lane streams from its x row; the W1 chunk is split once per
+//         workgroup while staged: three bf16 images [n][kk] (80-B rows, conflict-free b128 reads).
+//  GEMM2  per 32 hidden columns (one accumulator tile): bias + ReLU into the wave's fp32 patch,
+//         W2's 128 x 32 slice staged split; the patch is read back as float4 pairs in the same
+//         k order and split per lane.
+// LDS 61.4 KB (GEMM1 images; GEMM2 reuses it: patches 18.4 KB + W2 images 30.7 KB) -> two
+// workgroups per CU.
+// ---------------------------------------------------------------------------
+constexpr int XLD = BK + 8;                 // bf16 per image row
+constexpr int XP1 = H1 * XLD;               // bf16 per W1 image part
+constexpr int XP2 = DO * XLD;               // bf16 per W2 image part
+constexpr int XLH = BK + 4;                 // fp32 patch row stride
+constexpr int kXLdsBytes = 3 * XP1 * 2;
+
+__device__ __forceinline__ int xkk(int q) { return 16 * (q >> 2) + 8 * (q & 1) + 4 * ((q >> 1) & 1); }
+
+// split 4 consecutive-k values of one image row into the three parts at kk position xkk(q)
+__device__ __forceinline__ void put_split4(uint16_t* img, int part, int row, int q, const float4& f) {
+  const float v[4] = {f.x, f.y, f.z, f.w};
+  uint2 h, m, l;
+  uint32_t* ph = &h.x;
+  uint32_t* pm = &m.x;
+  uint32_t* pl = &l.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const uint32_t hh = split::pk_bf16(v[2 * i], v[2 * i + 1]);
+    const float e0 = v[2 * i] - split::bf_lo(hh), e1 = v[2 * i + 1] - split::bf_hi(hh);
+    const uint32_t mm = split::pk_bf16(e0, e1);
+    ph[i] = hh;
+    pm[i] = mm;
+    pl[i] = split::pk_bf16(e0 - split::bf_lo(mm), e1 - split::bf_hi(mm));
+  }
+  const int off = row * XLD + xkk(q);
+  *reinterpret_cast<uint2*>(&img[off]) = h;
+  *reinterpret_cast<uint2*>(&img[part + off]) = m;
+  *reinterpret_cast<uint2*>(&img[2 * part + off]) = l;
+}
+
+__global__ void __launch_bounds__(256, 2) k_fusion_fwdx(const float* __restrict__ txt, const float* __restrict__ img,
+                                                        const int32_t* __restrict__ img_index,
+                                                        const float* __restrict__ img_fallback, int64_t B, int Dt,
+                                                        int Di, const float* __restrict__ W1,
+                                                        const float* __restrict__ b1, const float* __restrict__ W2,
+                                                        const float* __restrict__ b2, int normalize,
+                                                        float* __restrict__ out, float* __restrict__ z1_out) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kXLdsBytes / 2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * BM + 32 * w;
+  const int K = Dt + Di;
+  const int64_t b = row0 + r < B ? row0 + r : B - 1;
+  const float* trow = txt + b * Dt + 4 * hf;
+  const float* irow;
+  if (Di > 0) {
+    const int32_t ii = img_index ? img_index[b] : (int32_t)b;
+    irow = (ii >= 0 ? img + (int64_t)ii * Di : img_fallback) + 4 * hf;
+  } else {
+    irow = trow;
+  }
+  auto load_x = [&](int k0, float4 (&xv)[4]) {
+    const float* src = k0 < Dt ? trow + k0 : irow + (k0 - Dt);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
+  };
+  float4 wst[8];  // W1 chunk: group e = tid + 256 s -> row n = e >> 3, k group q = e & 7
+  auto load_w1 = [&](int k0) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int e = tid + 256 * s;
+      wst[s] = ld4(W1 + (int64_t)(e >> 3) * K + k0 + (e & 7) * 4);
+    }
+  };
+  auto store_w1 = [&]() {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int e = tid + 256 * s;
+      put_split4(lds, XP1, e >> 3, e & 7, wst[s]);
+    }
+  };
+
+  // ---- GEMM1 ----
+  f32x16 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+  float4 xa[4], xn[4];
+  load_x(0, xa);
+  load_w1(0);
+  store_w1();
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    const bool more = k0 + BK < K;
+    if (more) {
+      load_w1(k0 + BK);
+      load_x(k0 + BK, xn);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      split::u32x4 fx[3];
+      split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int off = (32 * t + r) * XLD + 16 * u + 8 * hf;
+        split::u32x4 fb[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[p] = *reinterpret_cast<const split::u32x4*>(&lds[p * XP1 + off]);
+        acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_w1();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xa[g] = xn[g];
+    }
+    __syncthreads();
+  }
+
+  // ---- GEMM2 over eight 32-column slices of h ----
+  float* hp = reinterpret_cast<float*>(lds) + w * 32 * XLH;     // this wave's patch [32][XLH]
+  uint16_t* w2i = lds + (4 * 32 * XLH * 4) / 2;                 // W2 slice images [3][128][XLD]
+  f32x16 acc2[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
+#pragma unroll
+  for (int c = 0; c < H1 / BK; ++c) {
+    const int col = BK * c + r;
+    const float bias = b1[col];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = row_of(q, hf);
+      const float z = acc[c][q] + bias;
+      hp[row * XLH + r] = fmaxf(z, 0.f);
+      if (z1_out != nullptr && row0 + row < B) z1_out[(row0 + row) * H1 + col] = z;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {  // W2[:, 32 c .. 32 c + 31]: 1024 groups of 4 k, 4 per thread
+      const int e = tid + 256 * s;
+      put_split4(w2i, XP2, e >> 3, e & 7, ld4(W2 + (int64_t)(e >> 3) * H1 + BK * c + (e & 7) * 4));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      split::u32x4 fh[3];
+      split::split3(ld4(&hp[r * XLH + 16 * u + 4 * hf]), ld4(&hp[r * XLH + 16 * u + 8 + 4 * hf]), fh[0], fh[1],
+                    fh[2]);
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        const int off = (32 * uu + r) * XLD + 16 * u + 8 * hf;
+        split::u32x4 fb[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[p] = *reinterpret_cast<const split::u32x4*>(&w2i[p * XP2 + off]);
+        acc2[uu] = split::mfma32_x6(fh, fb, acc2[uu]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- bias, row L2 norm (inside the wave), store ----
+  float ss[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) ss[q] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float bias2 = b2[32 * u + r];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc2[u][q] += bias2;
+      ss[q] = fmaf(acc2[u][q], acc2[u][q], ss[q]);
+    }
+  }
+  if (normalize) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ss[q] = 1.f / (sqrtf(group_reduce<Op::Sum, 1, 16>(ss[q])) + 1e-8f);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t row = row0 + row_of(q, hf);
+    if (row >= B) continue;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) out[row * DO + 32 * u + r] = normalize ? acc2[u][q] * ss[q] : acc2[u][q];
+  }
+}
+
 }  // namespace
 
 
@@ -208,8 +398,12 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
                       int normalize, float* out, float* z1_out, hipStream_t st) {
   if (B == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fusion_fwd, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), 0, st, txt, img, img_index,
-                     img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);
+  if (gemm_split_enabled())
+    hipLaunchKernelGGL(k_fusion_fwdx, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), 0, st, txt, img, img_index,
+                       img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);
+  else
+    hipLaunchKernelGGL(k_fusion_fwd, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), 0, st, txt, img, img_index,
+                       img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);
   return hipGetLastError();
 }
 
