@@ -299,17 +299,26 @@ __global__ void __launch_bounds__(256, 2) k_fusion_fwdx(const float* __restrict_
       load_w1(k0 + BK);
       load_x(k0 + BK, xn);
     }
+    // (u, t) steps; the next step's W1 units are read while this step's six MFMAs run
+    auto read_w = [&](int idx, split::u32x4 (&f)[3]) {
+      const int off = (32 * (idx & 7) + r) * XLD + 16 * (idx >> 3) + 8 * hf;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      split::u32x4 fx[3];
-      split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&lds[p * XP1 + off]);
+    };
+    split::u32x4 fx[3], fb[3];
+    read_w(0, fb);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int off = (32 * t + r) * XLD + 16 * u + 8 * hf;
-        split::u32x4 fb[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) fb[p] = *reinterpret_cast<const split::u32x4*>(&lds[p * XP1 + off]);
-        acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+    for (int idx = 0; idx < 16; ++idx) {
+      const int u = idx >> 3, t = idx & 7;
+      if (t == 0) split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+      split::u32x4 fn[3];
+      if (idx + 1 < 16) read_w(idx + 1, fn);
+      acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (idx + 1 < 16) {
+        fb[0] = fn[0];
+        fb[1] = fn[1];
+        fb[2] = fn[2];
       }
     }
     __syncthreads();

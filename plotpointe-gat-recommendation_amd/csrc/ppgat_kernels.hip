@@ -97,6 +97,30 @@ __device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t eid, uint32_
   return u >= p ? inv_keep : 0.f;
 }
 
+// Streamed (once-touched) rows of the edge kernels -- the forward's output rows, pass B's own
+// source rows h_j and dh_j -- with the non-temporal hint when PPGAT_NT_STREAM=1, so they do
+// not push the gathered table (h forward, grad_out in pass B) out of the Infinity Cache.
+#ifndef PPGAT_NT_STREAM
+#define PPGAT_NT_STREAM 1
+#endif
+__device__ __forceinline__ float4 ld4s(const float* p) {
+#if PPGAT_NT_STREAM
+  using v4 = __attribute__((ext_vector_type(4))) float;
+  const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ void st4s(float* p, float4 a) {
+#if PPGAT_NT_STREAM
+  using v4 = __attribute__((ext_vector_type(4))) float;
+  __builtin_nontemporal_store(v4{a.x, a.y, a.z, a.w}, reinterpret_cast<v4*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = a;
+#endif
+}
+
 template <int C>
 struct Geo {
   static constexpr int LPR = C / 4;              // lanes per row (float4 each)
@@ -235,7 +259,7 @@ __global__ void __launch_bounds__(256) k_fwd(Items it, const int32_t* __restrict
   if (hub) return;
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
-  if (sg == 0) st4(out + i * C + sl * 4, osum);
+  if (sg == 0) st4s(out + i * C + sl * 4, osum);
 }
 
 // ---------------------------------------------------------------------------
@@ -314,7 +338,7 @@ __global__ void __launch_bounds__(256) k_fwd_short(Items it, int64_t first, cons
     const int col4 = (ql + 16 * c) * 4;
     const float4 a = mul4(acc[c], invl);
     if (agg_out != nullptr) st4(agg_out + i * C + col4, a);
-    st4(out + i * C + col4, bias != nullptr ? add4(a, ld4(bias + col4)) : a);
+    st4s(out + i * C + col4, bias != nullptr ? add4(a, ld4(bias + col4)) : a);
   }
   if (ql == 0) {
     m_out[i] = (pyg && re > rs) ? m : 0.f;
@@ -384,7 +408,7 @@ __global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ h
   if (out == nullptr) return;  // aggregate-then-transform: the per-head aggregates only
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
-  if (sg == 0) st4(out + i * C + sl * 4, osum);
+  if (sg == 0) st4s(out + i * C + sl * 4, osum);
 }
 
 // ---------------------------------------------------------------------------
@@ -417,7 +441,7 @@ __global__ void __launch_bounds__(256) k_bwd_pro(const float* __restrict__ grad_
       if (pr < pairs) {
         const int64_t n = pr / heads;
         g[u] = ld4(grad_out + n * C + sl * 4);
-        a[u] = agg != nullptr ? ld4(agg + pr * C + sl * 4) : ld4(out + n * C + sl * 4);
+        a[u] = agg != nullptr ? ld4s(agg + pr * C + sl * 4) : ld4s(out + n * C + sl * 4);  // read once here
       }
     }
 #pragma unroll
@@ -481,7 +505,7 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
   const bool hub = w < it.n_hub_items;
   for (int hd = 0; hd < heads; ++hd) {
     const float ss = s_src[j * heads + hd];
-    const float4 hv = ld4(h + (j * heads + hd) * C + sl * 4);
+    const float4 hv = ld4s(h + (j * heads + hd) * C + sl * 4);
     float4 acc = f4(0.f);
     float ds = 0.f;
     for (int base = cs; base < ce; base += 64) {
@@ -540,7 +564,7 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
       if (lane == 0) s[C] = ds;
       continue;
     }
-    if (sg == 0) st4(dh + j * ld_dh + hd * C + sl * 4, acc);
+    if (sg == 0) st4s(dh + j * ld_dh + hd * C + sl * 4, acc);
     if (lane == 0) ds_src[j * ld_ds + hd] = ds;
   }
 }
@@ -574,7 +598,7 @@ __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, 
   const float ss = s_src[j];
   float4 hv[NV];
 #pragma unroll
-  for (int c = 0; c < NV; ++c) hv[c] = ld4(h + j * C + (ql + 16 * c) * 4);
+  for (int c = 0; c < NV; ++c) hv[c] = ld4s(h + j * C + (ql + 16 * c) * 4);
   const int k = rs + ql;
   const bool valid = k < re;
   const int i = valid ? row[k] : 0;
@@ -635,7 +659,7 @@ __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, 
   ds = group_reduce<Op::Sum, 1, 8>(ds);
   if (!live) return;
 #pragma unroll
-  for (int c = 0; c < NV; ++c) st4(dh + j * ld_dh + (ql + 16 * c) * 4, acc[c]);
+  for (int c = 0; c < NV; ++c) st4s(dh + j * ld_dh + (ql + 16 * c) * 4, acc[c]);
   if (ql == 0) ds_src[j * ld_ds] = ds;
 }
 
@@ -820,7 +844,7 @@ __global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ h
     }
     if (q < p1) acc = add4(acc, ld4(partial + ((int64_t)q * heads + hd) * (C + 4) + sl * 4));
     acc = across_subgroups<G::LPR>(add4(acc, acc2));
-    if (sg == 0) st4(dh + j * ld_dh + hd * C + sl * 4, acc);
+    if (sg == 0) st4s(dh + j * ld_dh + hd * C + sl * 4, acc);
     if (lane == 0) ds_src[j * ld_ds + hd] = ds;
   }
 }

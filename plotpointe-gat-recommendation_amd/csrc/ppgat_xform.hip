@@ -329,17 +329,28 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nnx(NnArg a) {
 #pragma unroll
       for (int g = 0; g < XG; ++g) xn[g] = ld4(xrow + kc + KC + 8 * g);
     }
+    // (u, t) steps in order; the next step's three B units are read from LDS while the
+    // current step's six MFMAs run (a read waited on right before its MFMAs exposes the LDS
+    // latency against only six MFMAs)
+    auto read_b = [&](int idx, split::u32x4 (&f)[3]) {
+      const int off = (32 * (idx % NT) + r) * LDK + 16 * (idx / NT) + 8 * hf;
 #pragma unroll
-    for (int u = 0; u < KC / 16; ++u) {
-      split::u32x4 fx[3];
-      split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sB[p * PART + off]);
+    };
+    split::u32x4 fx[3], fb[3];
+    read_b(0, fb);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int off = (32 * t + r) * LDK + 16 * u + 8 * hf;
-        split::u32x4 fb[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) fb[p] = *reinterpret_cast<const split::u32x4*>(&sB[p * PART + off]);
-        acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+    for (int idx = 0; idx < (KC / 16) * NT; ++idx) {
+      const int u = idx / NT, t = idx % NT;
+      if (t == 0) split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+      split::u32x4 fn[3];
+      if (idx + 1 < (KC / 16) * NT) read_b(idx + 1, fn);
+      acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (idx + 1 < (KC / 16) * NT) {
+        fb[0] = fn[0];
+        fb[1] = fn[1];
+        fb[2] = fn[2];
       }
     }
     __syncthreads();
