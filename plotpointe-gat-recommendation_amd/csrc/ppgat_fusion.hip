@@ -219,6 +219,10 @@ constexpr int XLH = BK + 4;                 // fp32 patch row stride
 constexpr int kXLdsBytes = 3 * XP1 * 2;
 
 __device__ __forceinline__ int xkk(int q) { return 16 * (q >> 2) + 8 * (q & 1) + 4 * ((q >> 1) & 1); }
+// staging group e (8 per image row: k groups q = e & 7) -> image row.  Rows n and n + 4 share
+// each 16-lane ds_write_b64 group, 80 dwords apart (16 mod 32): conflict-free writes, and every
+// 8 lanes still read one 128-B row segment from global memory.
+__device__ __forceinline__ int xrow(int e) { return 8 * (e >> 6) + ((((e >> 3) & 1) << 2) | ((e >> 4) & 3)); }
 
 // split 4 consecutive-k values of one image row into the three parts at kk position xkk(q)
 __device__ __forceinline__ void put_split4(uint16_t* img, int part, int row, int q, const float4& f) {
@@ -268,19 +272,19 @@ __global__ void __launch_bounds__(256, 2) k_fusion_fwdx(const float* __restrict_
 #pragma unroll
     for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
   };
-  float4 wst[8];  // W1 chunk: group e = tid + 256 s -> row n = e >> 3, k group q = e & 7
+  float4 wst[8];  // W1 chunk: group e = tid + 256 s -> row xrow(e), k group q = e & 7
   auto load_w1 = [&](int k0) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int e = tid + 256 * s;
-      wst[s] = ld4(W1 + (int64_t)(e >> 3) * K + k0 + (e & 7) * 4);
+      wst[s] = ld4(W1 + (int64_t)xrow(e) * K + k0 + (e & 7) * 4);
     }
   };
   auto store_w1 = [&]() {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int e = tid + 256 * s;
-      put_split4(lds, XP1, e >> 3, e & 7, wst[s]);
+      put_split4(lds, XP1, xrow(e), e & 7, wst[s]);
     }
   };
 
@@ -350,7 +354,7 @@ __global__ void __launch_bounds__(256, 2) k_fusion_fwdx(const float* __restrict_
 #pragma unroll
     for (int s = 0; s < 4; ++s) {  // W2[:, 32 c .. 32 c + 31]: 1024 groups of 4 k, 4 per thread
       const int e = tid + 256 * s;
-      put_split4(w2i, XP2, e >> 3, e & 7, ld4(W2 + (int64_t)(e >> 3) * H1 + BK * c + (e & 7) * 4));
+      put_split4(w2i, XP2, xrow(e), e & 7, ld4(W2 + (int64_t)xrow(e) * H1 + BK * c + (e & 7) * 4));
     }
     __syncthreads();
 #pragma unroll

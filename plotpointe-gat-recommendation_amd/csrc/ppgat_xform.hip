@@ -271,7 +271,10 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nnx(NnArg a) {
   auto grp = [&](int s, int& n, int& q) {
     const int e = tid + 256 * s;
     if (BMODE == 0) { n = e % BN; q = e / BN; }                   // a k row is contiguous in n
-    else { n = e / (KC / 4); q = e % (KC / 4); }                 // an n row is contiguous in k
+    else if (KC == 32) {  // an n row is contiguous in k; rows n, n + 4 share a 16-lane write group
+      n = 8 * (e >> 6) + ((((e >> 3) & 1) << 2) | ((e >> 4) & 3));  // (80 dwords apart: no bank conflict)
+      q = e & 7;
+    } else { n = e / (KC / 4); q = e % (KC / 4); }
   };
   float4 bst[G];
   auto load_b = [&](int kc) {
