@@ -1109,13 +1109,14 @@ constexpr size_t kXsLds = 3 * kXsPart + (3 + 32) * kPT * sizeof(float);
 // v_mfma_f32_32x32x16_bf16 sums over 16 rows per instruction: lane (r, hf) holds rows
 // 8 hf + j (j = 0..7) of a 16-row step.  A'[m = 64 mh + 2 r + i] and B'[k = 4 r + kb] as in
 // k_tn128, so per row a lane loads one float2 of A and one float4 of B, and the three bf16
-// terms of each operand fragment are formed from eight rows of one column.  4 waves per
-// workgroup (two pairs of m halves), one workgroup per CU with 512 registers per wave: the
-// 128 accumulators, two 32-row batches of operands (one in flight) and the split terms.
+// terms of each operand fragment are formed from eight rows of one column.  WV = 8 waves per
+// workgroup (four pairs of m halves, two waves per SIMD), one workgroup per CU: 128
+// accumulators and one 16-row batch per wave, the SIMD's other wave hiding the load latency.
+// WV = 4 (masked shapes): 512 registers per wave, a ring of three batches (two in flight).
 // Pair partials are summed through LDS in pair order, then the ordered split reduction
 // k_tn_reduce (deterministic).
 // ---------------------------------------------------------------------------
-constexpr int kTnxWaves = 4;
+
 constexpr int kTnxSteps = 1;              // MFMA k steps (16 rows each) per batch
 constexpr int kTnxRows = 16 * kTnxSteps;  // rows per batch
 
@@ -1161,16 +1162,17 @@ __device__ __forceinline__ void tnx_compute(f32x16 (&acc)[2][4], float4& vacc, f
   }
 }
 
-template <int NV, bool MASK>
-__global__ void __launch_bounds__(64 * kTnxWaves, 1) k_tnx(TnArg a) {
+template <int NV, bool MASK, int WV>
+__global__ void __launch_bounds__(64 * WV, 1) k_tnx(TnArg a) {
+  constexpr bool RING = WV == 4;  // 8 waves (2 per SIMD): no batches in flight, the other wave hides latency
   __shared__ float sR[kPT][kPT + 4];
-  __shared__ float sVr[kTnxWaves / 2][2][kPT];
-  __shared__ float sC[kTnxWaves / 2][kPT];
+  __shared__ float sVr[WV / 2][2][kPT];
+  __shared__ float sC[WV / 2][kPT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
   const int mh = w & 1, pr = w >> 1;
-  const int64_t pid = (int64_t)blockIdx.x * (kTnxWaves / 2) + pr;
+  const int64_t pid = (int64_t)blockIdx.x * (WV / 2) + pr;
   const int64_t n_beg = pid * a.rows_per_pair;
   const int64_t n_end = min(a.n, n_beg + a.rows_per_pair);
   const int mcol = 64 * mh + 2 * r;
@@ -1242,7 +1244,13 @@ __global__ void __launch_bounds__(64 * kTnxWaves, 1) k_tnx(TnArg a) {
                                : 0.f;
         }
     };
-    if (MASK) {  // rare shapes (M or K < 128): no batch in flight (the masks cost the registers)
+    if (!MASK && !RING) {
+      for (int64_t bi = 0; bi < full; ++bi) {
+        TnxBatch cur;
+        load_fast(r0 + bi * kTnxRows, cur);
+        tnx_compute<NV != 0>(acc, vacc, csum, cur);
+      }
+    } else if (MASK) {  // rare shapes (M or K < 128): no batch in flight (the masks cost the registers)
       for (int64_t bi = 0; bi < full; ++bi) {
         TnxBatch cur;
         load(r0 + bi * kTnxRows, cur, false);
@@ -1297,6 +1305,12 @@ __global__ void __launch_bounds__(64 * kTnxWaves, 1) k_tnx(TnArg a) {
   if (pr == 0) put(false);
   __syncthreads();
   if (pr == 1) put(true);
+  if (WV == 8) {
+    __syncthreads();
+    if (pr == 2) put(true);
+    __syncthreads();
+    if (pr == 3) put(true);
+  }
   {
     float t[4] = {vacc.x, vacc.y, vacc.z, vacc.w};
     float c[2] = {csum.x, csum.y};
@@ -1321,15 +1335,21 @@ __global__ void __launch_bounds__(64 * kTnxWaves, 1) k_tnx(TnArg a) {
   }
   __syncthreads();
   float* P = a.part + (int64_t)blockIdx.x * kPT * kPT;
-  for (int idx = tid; idx < kPT * kPT / 4; idx += 64 * kTnxWaves) {
+  for (int idx = tid; idx < kPT * kPT / 4; idx += 64 * WV) {
     const int m = idx >> 5, k4 = (idx & 31) * 4;
     st4(P + m * kPT + k4, *reinterpret_cast<const float4*>(&sR[m][k4]));
   }
   if (tid < 2 * kPT) {
     const int v = tid >> 7, k = tid & 127;
-    a.vpart[((int64_t)blockIdx.x * 2 + v) * kPT + k] = sVr[0][v][k] + sVr[1][v][k];
+    float sv = sVr[0][v][k] + sVr[1][v][k];
+    if (WV == 8) sv = (sv + sVr[2][v][k]) + sVr[3][v][k];
+    a.vpart[((int64_t)blockIdx.x * 2 + v) * kPT + k] = sv;
   }
-  if (a.cpart && tid < kPT) a.cpart[(int64_t)blockIdx.x * kPT + tid] = sC[0][tid] + sC[1][tid];
+  if (a.cpart && tid < kPT) {
+    float sc = sC[0][tid] + sC[1][tid];
+    if (WV == 8) sc = (sc + sC[2][tid]) + sC[3][tid];
+    a.cpart[(int64_t)blockIdx.x * kPT + tid] = sc;
+  }
 }
 
 }  // namespace
@@ -1468,10 +1488,17 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
   const bool mask = M != kPT || K != kPT;
   const int NVk = nv;
   if (gemm_split_enabled()) {
-    const int64_t pairs_x = nb * (kTnxWaves / 2);
+    // 8 waves (two per SIMD, no batch in flight: the other wave hides the latency) measured
+    // 84.5 vs 94-96 us at config 2 against 4 waves with two batches in flight
+    // (profiles/r02/v17_tnx_waves.log); the masked shapes keep 4 waves (8 would spill)
+    const int wv = mask ? 4 : 8;
+    const int64_t pairs_x = nb * (wv / 2);
     a.rows_per_pair = ((N + pairs_x - 1) / pairs_x + kTnxRows - 1) / kTnxRows * kTnxRows;
-#define PPGAT_TNX(NV_, MASK_) \
-  hipLaunchKernelGGL((k_tnx<NV_, MASK_>), dim3((unsigned)nb), dim3(64 * kTnxWaves), 0, st, a)
+#define PPGAT_TNX(NV_, MASK_)                                                                        \
+  do {                                                                                               \
+    if (wv == 8) hipLaunchKernelGGL((k_tnx<NV_, MASK_, 8>), dim3((unsigned)nb), dim3(512), 0, st, a); \
+    else hipLaunchKernelGGL((k_tnx<NV_, MASK_, 4>), dim3((unsigned)nb), dim3(256), 0, st, a);         \
+  } while (0)
     if (mask) {
       if (NVk == 0) PPGAT_TNX(0, true); else if (NVk == 1) PPGAT_TNX(1, true); else PPGAT_TNX(2, true);
     } else {
