@@ -421,6 +421,8 @@ def main():
         "hip_graph": graph is not None,
         "formulation": ("aggregate-then-transform (x_j gathered once per edge for all heads)" if xform_k else
                         "transform-then-aggregate (h_j gathered per edge)"),
+        "gemm": ("fp32 MFMA (PPGAT_GEMM=fp32)" if os.environ.get("PPGAT_GEMM") == "fp32" else
+                 "fp32 results on bf16 MFMA, three-term split, 6 products (DESIGN.md 4.3)"),
         "kernel_timing": kern_src,
         "fused_kernel_edges_per_sec": E * args.layers * K / (fused_ms / 1e3) if fused_ms else None,
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},
