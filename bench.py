@@ -74,16 +74,20 @@ def parse():
 # ---------------------------------------------------------------------------
 # algorithmic bytes per launch (DESIGN.md "Kernels and their rooflines")
 # ---------------------------------------------------------------------------
-def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool, xform_k: int = 0) -> float:
+def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool, xform_k: int = 0,
+               dz_slot: bool = False) -> float:
     """Algorithmic bytes per launch.  xform_k > 0: the aggregate-then-
-    transform kernels (heads > 1, x rows of xform_k floats gathered instead of h rows)."""
+    transform kernels (heads > 1, x rows of xform_k floats gathered instead of h rows).
+    dz_slot: pass B reads each edge's dz position (the sharded layouts); otherwise dz is stored
+    at the edge's own CSC position (no index read)."""
     d = 4 if dropout else 0
+    sl = 4 if dz_slot else 0
     if xform_k:
         K = xform_k
         if kernel == "fwd":    # k_fwd_x: col, s_src[H], x_j | sched, s_dst[H], agg[H, K], m, inv_l
             return E * (4 + 4 * H + 4 * K + d) + N * (12 + 4 * H + 4 * H * K + 8 * H)
-        if kernel == "bwd_src":  # k_bwd_x: row, slot, nstate[H], gt_i[H, K], dz[H] | sched, x, s_src, dx, S
-            return E * (8 + 16 * H + 4 * H * K + 4 * H + d) + N * (12 + 4 * K + 4 * H + 4 * K + 4 * H)
+        if kernel == "bwd_src":  # k_bwd_x: row, (slot), nstate[H], gt_i[H, K], dz[H] | sched, x, s_src, dx, S
+            return E * (4 + sl + 16 * H + 4 * H * K + 4 * H + d) + N * (12 + 4 * K + 4 * H + 4 * K + 4 * H)
         if kernel == "bwd_pro":  # gt, agg in; s_dst, m, inv_l in; nstate out
             return N * (8 * H * K + 12 * H + 16 * H)
         if kernel == "scores":
@@ -94,11 +98,11 @@ def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool, xform
         per_n = 8 + 4 * H + 4 * C + 8 * H
         return E * per_e + N * per_n
     if kernel == "bwd_src":
-        per_e = 4 + 4 + 4 * H * 4 + 4 * C + 4 * H + d
+        per_e = 4 + sl + 4 * H * 4 + 4 * C + 4 * H + d  # row, (slot), nstate, g_i, dz
         per_n = 8 + 4 * H + 4 * H * C * 2 + 4 * H
         return E * per_e + N * per_n
-    if kernel == "bwd_epi":
-        return E * 4 * H + N * (8 + 4 * H + 4 * H * C * 3)
+    if kernel == "bwd_epi":  # (+ the csr2csc index per edge when dz is in CSC order)
+        return E * (4 * H + (0 if dz_slot else 4)) + N * (8 + 4 * H + 4 * H * C * 3)
     if kernel == "bwd_pro":
         return N * (4 * C + 4 * C + 4 * H)
     if kernel == "scores":
@@ -367,7 +371,7 @@ def main():
         else:
             v = dg.fwd_view if dom == "fwd" else dg.bwd_view
         ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
-                        args.attn_dropout > 0, xform_k)
+                        args.attn_dropout > 0, xform_k, dz_slot=part != "replicated")
     else:
         ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k)
     achieved = ab / avg_s / 1e9

@@ -163,6 +163,8 @@ int ppgat_bwd(const ppgat_schedule* src_sched, const int32_t* rowptr, const int3
  *  edges over the rank's own SOURCE rows (CSC slice; `row` indexes the gathered dst space,
  *  dz_slot gives each edge's position in a [world x max-local-edges] dz buffer that is then
  *  reduce-scattered), epilogue over the own destination rows with the local dz.
+ *  dz_slot == NULL: each edge's dz goes to its own CSC position (read back through
+ *  ppgat_bwd_dst_sum_csc); csc2csr as dz_slot gives the CSR-order layout of ppgat_bwd_dst_sum.
  *  nstate: [N_dst, H] float4 {s_dst, m, inv_l, D}.  grad_bias (nullable) needs bias_part
  *  [ppgat_bwd_partial_rows(n) * C]; epilogue part: [ppgat_bwd_partial_rows(n) * 2*H*C].
  */
@@ -187,6 +189,16 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
  *   datt_src[h] = W_h (ds_src^T x)[h],  datt_dst[h] = W_h (ds_dst^T x)[h]. */
 int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
                       int64_t ld_ds_dst, void* workspace, size_t workspace_bytes, void* stream);
+/* Same sums with dz in CSC (source) order -- the layout ppgat_bwd_edges writes when dz_slot is
+ * NULL (contiguous per-edge stores instead of a 4-B scatter per edge): CSR slot k of a
+ * destination reads dz[csr2csc[k]], csr2csc = the inverse of ppgat_csr_build's csc2csr
+ * (ppgat_invert_index).  Same summation order, so the result equals ppgat_bwd_dst_sum's on the
+ * CSR-order layout bit for bit. */
+int ppgat_bwd_dst_sum_csc(const ppgat_schedule* fwd_sched, int64_t n_nodes, int64_t n_edges, int heads,
+                          const float* dz, const int32_t* csr2csc, float* ds_dst, int64_t ld_ds_dst,
+                          void* workspace, size_t workspace_bytes, void* stream);
+/* inverse[index[k]] = k for a permutation index of [0, n) (int32). */
+int ppgat_invert_index(const int32_t* index, int64_t n, int32_t* inverse, void* stream);
 int ppgat_bwd_epilogue(const int32_t* rowptr, int64_t n_nodes, int heads, int channels, const float* h,
                        const float* att_src, const float* att_dst, const float* ds_src, const float* dz,
                        float* grad_h, float* grad_att_src, float* grad_att_dst, float* part, void* stream);

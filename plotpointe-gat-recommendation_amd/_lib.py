@@ -53,6 +53,8 @@ SIGNATURES = {
     "ppgat_bwd_edges": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f,
                                 c_u64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_bwd_dst_sum": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_vp, c_sz, c_vp]),
+    "ppgat_bwd_dst_sum_csc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_sz, c_vp]),
+    "ppgat_invert_index": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "ppgat_bwd_epilogue": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp]),
     "ppgat_bpr_workspace_bytes": (c_int, [c_i64, c_i64, c_int, ctypes.POINTER(c_sz)]),

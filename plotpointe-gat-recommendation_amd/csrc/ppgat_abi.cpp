@@ -297,7 +297,7 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
   if (int rc = check_sched(src_sched, 0, "bwd_edges")) return rc;
   if (src_sched->n_items > 0 && (!h || !s_src || !grad_h || !ds_src))
     return fail(PPGAT_ERR_INVALID, "bwd_edges: null pointer");
-  if (n_edges > 0 && (!row || !dz_slot || !nstate || !grad_out || !dz))
+  if (n_edges > 0 && (!row || !nstate || !grad_out || !dz))  // dz_slot NULL: dz in CSC order
     return fail(PPGAT_ERR_INVALID, "bwd_edges: null edge pointer");
   if (dropout_p > 0.f && n_edges > 0 && !csc_eid) return fail(PPGAT_ERR_INVALID, "bwd_edges: dropout needs csc_eid");
   if (src_sched->n_hub_items > 0 &&
@@ -320,8 +320,9 @@ int ppgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, const i
   return PPGAT_OK;
 }
 
-int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
-                      int64_t ld_ds_dst, void* workspace, size_t workspace_bytes, void* stream) {
+static int bwd_dst_sum_impl(const ppgat_schedule* fwd_sched, int64_t n_nodes, int heads, const float* dz,
+                            const int32_t* csr2csc, float* ds_dst, int64_t ld_ds_dst, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   if (n_nodes < 0 || heads < 1 || ld_ds_dst < heads) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: bad sizes");
   if (int rc = check_sched(fwd_sched, n_nodes, "bwd_dst_sum")) return rc;
   if (n_nodes > 0 && !ds_dst) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum: null pointer");
@@ -332,9 +333,34 @@ int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int head
   Timed t(PPGAT_K_BWD_EPI, st);
   const ppgat::ItemsArg it{fwd_sched->item_row, fwd_sched->item_beg, fwd_sched->item_end, fwd_sched->n_items,
                            fwd_sched->n_hub_items, fwd_sched->n_long_items};
-  hipError_t e = ppgat::launch_dst_sum(it, heads, dz, ds_dst, ld_ds_dst, static_cast<float*>(workspace),
+  hipError_t e = ppgat::launch_dst_sum(it, heads, dz, csr2csc, ds_dst, ld_ds_dst, static_cast<float*>(workspace),
                                        fwd_sched->hub_row, fwd_sched->hub_ptr, fwd_sched->n_hubs, st);
   if (e != hipSuccess) return hip_fail(e, "bwd_dst_sum");
+  return PPGAT_OK;
+}
+
+int ppgat_bwd_dst_sum(const ppgat_schedule* fwd_sched, int64_t n_nodes, int heads, const float* dz, float* ds_dst,
+                      int64_t ld_ds_dst, void* workspace, size_t workspace_bytes, void* stream) {
+  return bwd_dst_sum_impl(fwd_sched, n_nodes, heads, dz, nullptr, ds_dst, ld_ds_dst, workspace, workspace_bytes,
+                          stream);
+}
+
+int ppgat_bwd_dst_sum_csc(const ppgat_schedule* fwd_sched, int64_t n_nodes, int64_t n_edges, int heads,
+                          const float* dz, const int32_t* csr2csc, float* ds_dst, int64_t ld_ds_dst, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  if (n_edges > 0 && !csr2csc) return fail(PPGAT_ERR_INVALID, "bwd_dst_sum_csc: null csr2csc");
+  if (int rc = debug_range(csr2csc, 4, n_edges, 0, n_edges, "bwd_dst_sum_csc: csr2csc",
+                           static_cast<hipStream_t>(stream)))
+    return rc;
+  return bwd_dst_sum_impl(fwd_sched, n_nodes, heads, dz, csr2csc, ds_dst, ld_ds_dst, workspace, workspace_bytes,
+                          stream);
+}
+
+int ppgat_invert_index(const int32_t* index, int64_t n, int32_t* inverse, void* stream) {
+  if (n < 0 || (n > 0 && (!index || !inverse))) return fail(PPGAT_ERR_INVALID, "invert_index: bad arguments");
+  if (int rc = debug_range(index, 4, n, 0, n, "invert_index: index", static_cast<hipStream_t>(stream))) return rc;
+  hipError_t e = ppgat::launch_invert_index(index, n, inverse, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "invert_index");
   return PPGAT_OK;
 }
 
@@ -1020,7 +1046,7 @@ int ppgat_xgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, co
   if (int rc = check_sched(src_sched, 0, "xgat_bwd_edges")) return rc;
   if (src_sched->n_items > 0 && (!x || !s_src || !att_proj || !dx || !S))
     return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: null pointer");
-  if (n_edges > 0 && (!row || !dz_slot || !nstate || !gt || !dz))
+  if (n_edges > 0 && (!row || !nstate || !gt || !dz))  // dz_slot NULL: dz in CSC order
     return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: null edge pointer");
   if (dropout_p > 0.f && (!seed_used || (n_edges > 0 && !csc_eid)))
     return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges: dropout needs seed_used and csc_eid");

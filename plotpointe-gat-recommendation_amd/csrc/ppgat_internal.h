@@ -41,8 +41,10 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
                           float* dh, int64_t ld_dh,
                           float* ds_src, int64_t ld_ds, float* dz, float* partial, const int32_t* hub_row,
                           const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
-hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, float* ds_dst, int64_t ld, float* partial,
-                          const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
+hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const int32_t* csr2csc, float* ds_dst,
+                          int64_t ld, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                          hipStream_t st);
+hipError_t launch_invert_index(const int32_t* p, int64_t n, int32_t* inv, hipStream_t st);
 int64_t epi_blocks(int64_t n);
 hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, const float* h, const float* as,
                           const float* ad, const float* ds_src, const float* dz, float* dh, float* partial,

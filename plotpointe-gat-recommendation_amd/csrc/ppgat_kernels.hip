@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
         const float e = logit(z, slope, mode);
         const float af = expf(e - st.y) * st.z;
         const float dm = p > 0.f ? drop_scale(seed, (uint32_t)csc_eid[k], (uint32_t)hd, p, inv_keep) : 1.f;
-        slot = csc2csr[k];
+        slot = csc2csr != nullptr ? csc2csr[k] : k;  // NULL: dz in CSC order
         bg = af * dm * gscale;
         const float a1 = af * dlogit(z, slope, mode);
         c1 = a1 * dm * gscale;
@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, 
     const float z = ss + st.x;
     const float af = expf(logit(z, slope, mode) - st.y) * st.z;
     const float dm = p > 0.f ? drop_scale(seed, (uint32_t)csc_eid[k], 0u, p, inv_keep) : 1.f;
-    slot = csc2csr[k];
+    slot = csc2csr != nullptr ? csc2csr[k] : k;  // NULL: dz in CSC order
     bg = af * dm * gscale;
     const float a1 = af * dlogit(z, slope, mode);
     c1 = a1 * dm * gscale;
@@ -742,7 +742,7 @@ __global__ void __launch_bounds__(256) k_bwd_src_mh(Items it, const int32_t* __r
     const int k = base + lane;
     const bool valid = k < ce;
     const int i = valid ? row[k] : 0;
-    const int slot = valid ? csc2csr[k] : 0;
+    const int slot = valid ? (csc2csr != nullptr ? csc2csr[k] : k) : 0;  // NULL: dz in CSC order
     const uint32_t eid = (valid && p > 0.f) ? (uint32_t)csc_eid[k] : 0u;
 #pragma unroll
     for (int hd = 0; hd < H; ++hd) {
@@ -958,9 +958,14 @@ __global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ p
 // hub pieces leave a partial that k_dst_merge adds up in piece order (deterministic).
 // Written with row stride ld.
 // ---------------------------------------------------------------------------
+template <bool PERM>
 __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const float* __restrict__ dz,
+                                                 const int32_t* __restrict__ csr2csc,
                                                  float* __restrict__ ds_dst, int64_t ld,
                                                  float* __restrict__ partial) {
+  // PERM: dz is in CSC (source) order, as pass B wrote it contiguously; CSR slot k reads
+  // dz[csr2csc[k]] (same summation order as the CSR-order layout: bitwise equal results)
+  auto at = [&](int k) -> int64_t { return PERM ? (int64_t)csr2csc[k] : (int64_t)k; };
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pr = t >> 4;
   const int l = (int)(t & 15);
@@ -974,12 +979,12 @@ __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const floa
     const int rs = it.beg[w], re = it.end[w];
     int k = rs + l;
     for (; k + 48 < re; k += 64) {
-      x0 += dz[(int64_t)k * heads + hd];
-      x1 += dz[(int64_t)(k + 16) * heads + hd];
-      x2 += dz[(int64_t)(k + 32) * heads + hd];
-      x3 += dz[(int64_t)(k + 48) * heads + hd];
+      x0 += dz[at(k) * heads + hd];
+      x1 += dz[at(k + 16) * heads + hd];
+      x2 += dz[at(k + 32) * heads + hd];
+      x3 += dz[at(k + 48) * heads + hd];
     }
-    for (; k < re; k += 16) x0 += dz[(int64_t)k * heads + hd];
+    for (; k < re; k += 16) x0 += dz[at(k) * heads + hd];
   }
   float x = (x0 + x1) + (x2 + x3);
   x = group_reduce<Op::Sum, 1, 8>(x);  // the 16 lanes of a DPP row
@@ -1152,16 +1157,33 @@ hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, co
   return hipGetLastError();
 }
 
-hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, float* ds_dst, int64_t ld, float* partial,
-                          const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const int32_t* csr2csc, float* ds_dst,
+                          int64_t ld, float* partial, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs,
+                          hipStream_t st) {
   const int64_t pairs = it.n_items * heads;
   if (pairs == 0) return hipSuccess;
   const Items items{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-  hipLaunchKernelGGL(k_dst_sum, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, ds_dst, ld,
-                     partial);
+  if (csr2csc != nullptr)
+    hipLaunchKernelGGL(k_dst_sum<true>, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, csr2csc,
+                       ds_dst, ld, partial);
+  else
+    hipLaunchKernelGGL(k_dst_sum<false>, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, csr2csc,
+                       ds_dst, ld, partial);
   if (n_hubs > 0)
     hipLaunchKernelGGL(k_dst_merge, dim3(blocks_for(n_hubs * heads)), dim3(256), 0, st, hub_row, hub_ptr, n_hubs,
                        heads, partial, ds_dst, ld);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_invert_index(const int32_t* __restrict__ p, int64_t n,
+                                                      int32_t* __restrict__ inv) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) inv[p[k]] = (int32_t)k;
+}
+
+hipError_t launch_invert_index(const int32_t* p, int64_t n, int32_t* inv, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_invert_index, dim3(blocks_for(n)), dim3(256), 0, st, p, n, inv);
   return hipGetLastError();
 }
 

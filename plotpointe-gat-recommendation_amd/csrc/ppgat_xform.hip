@@ -782,7 +782,7 @@ __global__ void __launch_bounds__(256) k_bwd_x(XItems it, const int32_t* __restr
     const int k = base + lane;
     const bool valid = k < ce;
     const int i = valid ? row[k] : 0;
-    const int slot = valid ? csc2csr[k] : 0;
+    const int slot = valid ? (csc2csr != nullptr ? csc2csr[k] : k) : 0;  // NULL: dz in CSC order
     const uint32_t e_id = (valid && p > 0.f) ? (uint32_t)csc_eid[k] : 0u;
 #pragma unroll
     for (int h = 0; h < H; ++h) {

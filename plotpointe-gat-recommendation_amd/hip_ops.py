@@ -115,6 +115,9 @@ class CSRGraph:
     # to RU).  Item sources only reach user destinations, so their edge pass can run before the
     # item rows of grad_out are all-reduced (hip_ops.GATLayer.backward overlaps the two).
     bwd_split: tuple = None
+    # CSC position of each CSR slot (the inverse of csc2csr): pass B writes dz contiguously in
+    # CSC order and the destination sums read it through this (_csr2csc builds it once)
+    csr2csc: torch.Tensor = None
 
     @property
     def device(self):
@@ -165,7 +168,20 @@ def csr_build(edge_index: torch.Tensor, n_nodes: int, max_edges: int = MAX_EDGES
     G = CSRGraph(N, E, rowptr, col[:E], csr_eid[:E], colptr, row[:E], csc_eid[:E], csc2csr[:E], fs, bs)
     if _lib.debug_build():
         debug_validate_graph(G)
+    with torch.cuda.device(dev):
+        _csr2csc(G)
     return G
+
+
+def _csr2csc(g) -> torch.Tensor:
+    """g.csr2csc, built on the device from g.csc2csr on first use (ppgat_invert_index)."""
+    if g.csr2csc is None:
+        E = g.n_edges
+        inv = torch.empty(max(E, 1), dtype=torch.int32, device=g.csc2csr.device)
+        _lib.check(_lib.load().ppgat_invert_index(_lib.ptr(g.csc2csr) if E else None, E, inv.data_ptr(),
+                                                  _lib.stream_handle(inv.device)), "invert_index")
+        g.csr2csc = inv[:E]
+    return g.csr2csc
 
 
 def debug_validate_graph(G: "CSRGraph"):
@@ -329,7 +345,8 @@ def gat_aggregate(h, att_src, att_dst, bias, graph, heads, channels, mode, slope
 def _bwd_edges_src(g: CSRGraph, sched: Schedule, r0: int, h, s_src, nstate, grad_out, D, S, dz, heads, channels,
                    mode, slope, p, seed, seed_buf=None):
     """Pass B over the source rows of ``sched`` (row ids relative to r0; edge slots and
-    destination rows absolute) into D, S[:, :H] and dz."""
+    destination rows absolute) into D, S[:, :H] and dz -- dz in CSC order (dz_slot NULL: one
+    contiguous store per edge instead of a 4-B scatter to its CSR slot)."""
     lib = _lib.load()
     dev = h.device
     E, HC = g.n_edges, heads * channels
@@ -340,7 +357,7 @@ def _bwd_edges_src(g: CSRGraph, sched: Schedule, r0: int, h, s_src, nstate, grad
     cs = sched.cstruct()
     st = _lib.stream_handle(dev)
     _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), _lib.ptr(g.row) if E else None,
-                                   _lib.ptr(g.csc_eid) if E else None, _lib.ptr(g.csc2csr) if E else None, E, heads,
+                                   _lib.ptr(g.csc_eid) if E else None, None, E, heads,
                                    channels, h.data_ptr() + 4 * r0 * HC, s_src.data_ptr() + 4 * r0 * heads,
                                    nstate.data_ptr(), grad_out.data_ptr(),
                                    mode, float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
@@ -355,9 +372,10 @@ def _bwd_dst_sum(g: CSRGraph, dz, S, heads):
     dev = dz.device
     fs = g.fwd_sched.cstruct()
     dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), g.n_nodes, heads, dz.data_ptr(), S.data_ptr() + 4 * heads,
-                                     2 * heads, dws.data_ptr(), dws.numel() * 4, _lib.stream_handle(dev)),
-               "bwd_dst_sum")
+    E = g.n_edges
+    _lib.check(lib.ppgat_bwd_dst_sum_csc(ctypes.byref(fs), g.n_nodes, E, heads, dz.data_ptr(),
+                                         _lib.ptr(_csr2csc(g)) if E else None, S.data_ptr() + 4 * heads, 2 * heads,
+                                         dws.data_ptr(), dws.numel() * 4, _lib.stream_handle(dev)), "bwd_dst_sum_csc")
 
 
 def _bwd_edges_dst(g: CSRGraph, h, s_src, nstate, grad_out, D, S, heads, channels, mode, slope, p, seed,
@@ -834,11 +852,13 @@ class XViews:
     bwd_sched: Schedule
     bwd_sched_own: Optional[Schedule] = None   # sources [0, n_dst) (halo partition)
     bwd_sched_halo: Optional[Schedule] = None  # sources [n_dst, n_src), rows relative to n_dst
+    # dz_slot None: dz in CSC order, summed per destination through csr2csc
+    csr2csc: Optional[torch.Tensor] = None
 
     @staticmethod
     def of_graph(g: "CSRGraph") -> "XViews":
-        return XViews(g.n_nodes, g.n_nodes, g.n_edges, g.col, g.csr_eid, g.fwd_sched, g.row, g.csc_eid, g.csc2csr,
-                      g.bwd_sched)
+        return XViews(g.n_nodes, g.n_nodes, g.n_edges, g.col, g.csr_eid, g.fwd_sched, g.row, g.csc_eid, None,
+                      g.bwd_sched, csr2csc=_csr2csc(g))
 
 
 def xgat_supported(in_channels: int, heads: int, channels: int) -> bool:
@@ -940,8 +960,13 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
             halo_hook(dx[v.n_dst:])
     fs = v.fwd_sched.cstruct()
     dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
-                                     dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
+    if v.dz_slot is None:
+        _lib.check(lib.ppgat_bwd_dst_sum_csc(ctypes.byref(fs), v.n_dst, E, H, dz.data_ptr(),
+                                             _lib.ptr(v.csr2csc) if E else None, S.data_ptr() + 4 * H, 2 * H,
+                                             dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum_csc")
+    else:
+        _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
+                                         dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
     _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
                "xgat_bwd_epilogue")
     GV = gemm_tn(S, x)[0]

@@ -323,3 +323,55 @@ def test_config3_ui_plus_ii_edges_model(pkg, oracle, cuda):
     for k, v in m.named_parameters():
         tol = 1e-4 if v.dim() != 2 else 1e-5
         assert rel(v.grad, P[k].grad) <= tol, k
+
+
+@pytest.mark.parametrize("heads,C", [(1, 128), (2, 64)])
+def test_dz_csc_order_equals_csr_order(pkg, cuda, heads, C):
+    """Pass B with dz_slot NULL (dz stored contiguously in CSC order) + ppgat_bwd_dst_sum_csc
+    gives bit for bit the dh / ds_src / ds_dst of dz_slot = csc2csr (CSR-order scatter) +
+    ppgat_bwd_dst_sum, on a hub-heavy graph with dropout (the product path uses the former)."""
+    import ctypes
+    hip_ops, _lib = pkg.hip_ops, pkg._lib
+    lib = _lib.load()
+    rng = np.random.default_rng(7)
+    n, e = 3000, 40000
+    ei = _rand_graph(rng, n, e, "hub")
+    ei = np.concatenate([ei, ei[::-1]], axis=1)  # hubs on both sides (pass B's and the dst sum's)
+    g = hip_ops.csr_build(torch.from_numpy(ei).to(cuda), n)
+    E, HC = g.n_edges, heads * C
+    assert torch.equal(g.csr2csc.long()[g.csc2csr.long()], torch.arange(E, device=cuda))
+    gen = torch.Generator(device=cuda).manual_seed(3)
+    h = torch.randn(n, HC, device=cuda, generator=gen)
+    s_src = torch.randn(n, heads, device=cuda, generator=gen)
+    nstate = torch.randn(n, heads, 4, device=cuda, generator=gen)
+    nstate[..., 2] = nstate[..., 2].abs() + 0.1
+    grad_out = torch.randn(n, C, device=cuda, generator=gen)
+    outs = []
+    for csr_order in (True, False):
+        D = torch.zeros(n, HC, device=cuda)
+        S = torch.zeros(n, 2 * heads, device=cuda)
+        dz = torch.full((E * heads,), float("nan"), device=cuda)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_fwd_workspace_bytes(g.bwd_sched.n_hub_items, heads, C, ctypes.byref(nbytes)), "ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=cuda)
+        cs = g.bwd_sched.cstruct()
+        st = _lib.stream_handle(cuda)
+        _lib.check(lib.ppgat_bwd_edges(ctypes.byref(cs), g.row.data_ptr(), g.csc_eid.data_ptr(),
+                                       g.csc2csr.data_ptr() if csr_order else None, E, heads, C, h.data_ptr(),
+                                       s_src.data_ptr(), nstate.data_ptr(), grad_out.data_ptr(), 0, 0.2, 0.1, 1234,
+                                       None, D.data_ptr(), HC, S.data_ptr(), 2 * heads, dz.data_ptr(), ws.data_ptr(),
+                                       nbytes.value, st), "bwd_edges")
+        fs = g.fwd_sched.cstruct()
+        dws = torch.empty(max(g.fwd_sched.n_hub_items * heads, 1), device=cuda)
+        if csr_order:
+            _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), n, heads, dz.data_ptr(), S.data_ptr() + 4 * heads,
+                                             2 * heads, dws.data_ptr(), dws.numel() * 4, st), "dst_sum")
+        else:
+            _lib.check(lib.ppgat_bwd_dst_sum_csc(ctypes.byref(fs), n, E, heads, dz.data_ptr(), g.csr2csc.data_ptr(),
+                                                 S.data_ptr() + 4 * heads, 2 * heads, dws.data_ptr(),
+                                                 dws.numel() * 4, st), "dst_sum_csc")
+        torch.cuda.synchronize()
+        outs.append((D, S, dz.view(E, heads)))
+    (D0, S0, dz0), (D1, S1, dz1) = outs
+    assert torch.equal(D0, D1) and torch.equal(S0, S1)
+    assert torch.equal(dz1, dz0[g.csc2csr.long()])  # the CSC-order store is the CSR layout permuted
