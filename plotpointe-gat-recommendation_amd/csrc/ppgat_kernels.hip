@@ -994,6 +994,42 @@ __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const floa
   }
 }
 
+// heads in {2, 4}: one 16-lane group per item for all heads, each edge's H logit gradients
+// loaded as one vector (dz rows of H floats), the same per-head summation order as k_dst_sum
+template <bool PERM, int H>
+__global__ void __launch_bounds__(256) k_dst_sum_vh(Items it, const float* __restrict__ dz,
+                                                    const int32_t* __restrict__ csr2csc, float* __restrict__ ds_dst,
+                                                    int64_t ld, float* __restrict__ partial) {
+  using V = __attribute__((ext_vector_type(H))) float;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t w = t >> 4;
+  const int l = (int)(t & 15);
+  const bool live = w < it.n_items;
+  auto at = [&](int k) -> int64_t { return PERM ? (int64_t)csr2csc[k] : (int64_t)k; };
+  const V* dzv = reinterpret_cast<const V*>(dz);
+  V x0 = {}, x1 = {}, x2 = {}, x3 = {};
+  if (live) {
+    const int rs = it.beg[w], re = it.end[w];
+    int k = rs + l;
+    for (; k + 48 < re; k += 64) {
+      x0 += dzv[at(k)];
+      x1 += dzv[at(k + 16)];
+      x2 += dzv[at(k + 32)];
+      x3 += dzv[at(k + 48)];
+    }
+    for (; k < re; k += 16) x0 += dzv[at(k)];
+  }
+  const V xs = (x0 + x1) + (x2 + x3);
+#pragma unroll
+  for (int hd = 0; hd < H; ++hd) {
+    const float x = group_reduce<Op::Sum, 1, 8>(xs[hd]);
+    if (live && l == 0) {
+      if (w < it.n_hub_items) partial[w * H + hd] = x;
+      else ds_dst[(int64_t)it.row[w] * ld + hd] = x;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_dst_merge(const int32_t* __restrict__ hub_row,
                                                    const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
                                                    const float* __restrict__ partial, float* __restrict__ ds_dst,
@@ -1163,7 +1199,15 @@ hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const 
   const int64_t pairs = it.n_items * heads;
   if (pairs == 0) return hipSuccess;
   const Items items{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-  if (csr2csc != nullptr)
+  const bool aligned = (reinterpret_cast<uintptr_t>(dz) % (4 * heads)) == 0;
+  if (csr2csc != nullptr && (heads == 2 || heads == 4) && aligned) {
+    if (heads == 2)
+      hipLaunchKernelGGL((k_dst_sum_vh<true, 2>), dim3(blocks_for(it.n_items * 16)), dim3(256), 0, st, items, dz,
+                         csr2csc, ds_dst, ld, partial);
+    else
+      hipLaunchKernelGGL((k_dst_sum_vh<true, 4>), dim3(blocks_for(it.n_items * 16)), dim3(256), 0, st, items, dz,
+                         csr2csc, ds_dst, ld, partial);
+  } else if (csr2csc != nullptr)
     hipLaunchKernelGGL(k_dst_sum<true>, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, csr2csc,
                        ds_dst, ld, partial);
   else

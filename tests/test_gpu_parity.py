@@ -325,7 +325,7 @@ def test_config3_ui_plus_ii_edges_model(pkg, oracle, cuda):
         assert rel(v.grad, P[k].grad) <= tol, k
 
 
-@pytest.mark.parametrize("heads,C", [(1, 128), (2, 64)])
+@pytest.mark.parametrize("heads,C", [(1, 128), (2, 64), (4, 32)])
 def test_dz_csc_order_equals_csr_order(pkg, cuda, heads, C):
     """Pass B with dz_slot NULL (dz stored contiguously in CSC order) + ppgat_bwd_dst_sum_csc
     gives bit for bit the dh / ds_src / ds_dst of dz_slot = csc2csr (CSR-order scatter) +
