@@ -345,6 +345,18 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
   __syncthreads();
   if (b0 >= total) return;
   const int len = (int)min((int64_t)kChunk, total - b0);
+  // rows no contribution reaches are zeroed here instead of by a memset of the whole dZ:
+  // each segment start zeroes the rows between the previous key and its own (the sentinel key
+  // n_rows closes the last gap; without sentinels the last contribution zeroes the tail), so
+  // every row of [0, n_rows) is written exactly once
+  for (int q = 0; q < len; ++q) {
+    const int32_t r = s_dst[sg][q];
+    const int64_t prev = q > 0 ? (int64_t)s_dst[sg][q - 1] : (b0 > 0 ? (int64_t)skey[b0 - 1] : -1);
+    const int64_t hi = min((int64_t)r, n_rows);
+    for (int64_t z = prev + 1; z < hi; ++z) st4(dZ + z * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (b0 + q == total - 1 && r < n_rows)
+      for (int64_t z = (int64_t)r + 1; z < n_rows; ++z) st4(dZ + z * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+  }
   const bool starts_before = b0 > 0 && skey[b0 - 1] == s_dst[sg][0];
   const bool ends_after = b0 + len < total && skey[b0 + len] == s_dst[sg][len - 1];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -658,8 +670,8 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
                    const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
   const int64_t N = n_rows;
-  hipError_t err = hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);
-  if (err != hipSuccess || S == 0) return err;
+  if (S == 0) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_chunks zeroes the gaps
+  hipError_t err = hipSuccess;
   const int64_t total = 4 * S;
   const int64_t chunks = (total + kChunk - 1) / kChunk;
   char* p = static_cast<char*>(ws) + align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4);
