@@ -832,6 +832,8 @@ def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int,
         from .hip_ops import CSRGraph
         graph = CSRGraph(R, El, view.rowptr, view.col, view.csr_eid, view.colptr, view.row, view.csc_eid,
                          view.dz_slot, view.fwd_sched, view.bwd_sched)
+        graph.fwd_split = (RU, sched_builder(view.rowptr[:RU + 1].contiguous(), El),
+                           sched_builder(view.rowptr[RU:].contiguous(), El))
         if not bool((~su & ~du).any()):  # bipartite (no I-I columns): item sources reach users only
             graph.bwd_split = (RU, sched_builder(view.colptr[:RU + 1].contiguous(), El),
                                sched_builder(view.colptr[RU:].contiguous(), El))
@@ -868,6 +870,19 @@ class RepHooks:
         _lib.check(lib.ppgat_rep_merge(1, *args), "rep_merge")
         self.comm.all_reduce_(pack)
         _lib.check(lib.ppgat_rep_merge(2, *args), "rep_merge")
+
+    def merge_fwd_async(self, out, m, inv_l, agg, bias, heads: int, C: int):
+        """merge_fwd on the communication stream, after the main stream's work so far (the
+        item destinations' forward); ``wait`` joins it back.  It touches the item rows only."""
+        dev = out.device
+        main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
+        cs.wait_stream(main)
+        for t in (out, m, inv_l, agg, bias):
+            if t is not None:
+                t.record_stream(cs)
+        with torch.cuda.stream(cs):
+            self.merge_fwd(out, m, inv_l, agg, bias, heads, C)
+        return (main, cs)
 
     def reduce_grad(self, g):
         if self.comm.active:

@@ -115,6 +115,10 @@ class CSRGraph:
     # to RU).  Item sources only reach user destinations, so their edge pass can run before the
     # item rows of grad_out are all-reduced (hip_ops.GATLayer.backward overlaps the two).
     bwd_split: tuple = None
+    # the same partition's forward split by destination class: (RU, schedule over the user
+    # destinations [0, RU), over the item destinations [RU, N) with rows relative to RU).  The
+    # item rows' cross-rank merge (two all_reduces) then runs while the user rows aggregate.
+    fwd_split: tuple = None
     # CSC position of each CSR slot (the inverse of csc2csr): pass B writes dz contiguously in
     # CSC order and the destination sums read it through this (_csr2csc builds it once)
     csr2csc: torch.Tensor = None
@@ -247,27 +251,43 @@ def seed_buffer(dropout_p: float, device) -> Optional[torch.Tensor]:
 
 def gat_fwd(g: CSRGraph, h, s_src, s_dst, bias, heads: int, channels: int, mode: int, slope: float,
             dropout_p: float, seed: int, want_agg: bool, seed_buf: Optional[torch.Tensor] = None):
-    lib = _lib.load()
     N = g.n_nodes
     dev = h.device
     _require(h.size(0) == N, f"x has {h.size(0)} rows but the graph has {N} nodes")
+    out, m, inv_l, agg = _fwd_outputs(N, heads, channels, want_agg, dev)
+    _fwd_rows(g, g.fwd_sched, 0, N, h, s_src, s_dst, bias, heads, channels, mode, slope, dropout_p, seed, seed_buf,
+              out, m, inv_l, agg)
+    return out, m, inv_l, agg
+
+
+def _fwd_outputs(N: int, heads: int, channels: int, want_agg: bool, dev):
     out = torch.empty(N, channels, dtype=torch.float32, device=dev)
     m = torch.empty(N, heads, dtype=torch.float32, device=dev)
     inv_l = torch.empty(N, heads, dtype=torch.float32, device=dev)
     agg = torch.empty(N, heads, channels, dtype=torch.float32, device=dev) if want_agg else None
-    sched = g.fwd_sched
+    return out, m, inv_l, agg
+
+
+def _fwd_rows(g: CSRGraph, sched: Schedule, r0: int, n: int, h, s_src, s_dst, bias, heads: int, channels: int,
+              mode: int, slope: float, dropout_p: float, seed: int, seed_buf, out, m, inv_l, agg):
+    """The forward over the destination rows [r0, r0 + n) of ``sched`` (row ids relative to
+    r0; edge slots and source rows absolute): destination-indexed pointers are offset by r0."""
+    lib = _lib.load()
+    dev = h.device
+    HC = heads * channels
     nbytes = ctypes.c_size_t(0)
     _lib.check(lib.ppgat_fwd_workspace_bytes(sched.n_hub_items, heads, channels, ctypes.byref(nbytes)),
                "fwd_workspace_bytes")
     ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
     cs = sched.cstruct()
     _lib.check(lib.ppgat_fwd(ctypes.byref(cs), _lib.ptr(g.col) if g.n_edges else None,
-                             _lib.ptr(g.csr_eid) if g.n_edges else None, N, g.n_edges, heads, channels,
-                             h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(), _lib.ptr(bias), mode, float(slope),
-                             float(dropout_p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf), out.data_ptr(),
-                             m.data_ptr(), inv_l.data_ptr(), _lib.ptr(agg), ws.data_ptr(), nbytes.value,
+                             _lib.ptr(g.csr_eid) if g.n_edges else None, n, g.n_edges, heads, channels,
+                             h.data_ptr(), s_src.data_ptr(), s_dst.data_ptr() + 4 * r0 * heads, _lib.ptr(bias), mode,
+                             float(slope), float(dropout_p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                             out.data_ptr() + 4 * r0 * channels, m.data_ptr() + 4 * r0 * heads,
+                             inv_l.data_ptr() + 4 * r0 * heads,
+                             agg.data_ptr() + 4 * r0 * HC if agg is not None else None, ws.data_ptr(), nbytes.value,
                              _lib.stream_handle(dev)), "gat_fwd")
-    return out, m, inv_l, agg
 
 
 def gat_bwd(g: CSRGraph, h, s_src, s_dst, att_src, att_dst, bias, out, agg, m, inv_l, grad_out, heads: int,
@@ -543,10 +563,24 @@ class GATLayer(torch.autograd.Function):
             s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
         need = any(ctx.needs_input_grad[:5]) or (had_items and ctx.needs_input_grad[12])
         ctx.seed_buf = seed_buffer(dropout_p, x.device) if need else None
-        out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed,
-                                     want_agg=(need or rep is not None) and heads > 1, seed_buf=ctx.seed_buf)
-        if rep is not None:  # replicated item rows (dist.py): merge their softmax over the ranks
-            rep.merge_fwd(out, m, inv_l, agg, b, heads, channels)
+        want_agg = (need or rep is not None) and heads > 1
+        if rep is not None and graph.fwd_split is not None and rep.async_capable():
+            # replicated item rows over RCCL: the item destinations first, their merge on the
+            # communication stream, the user destinations meanwhile on this one
+            RU, sched_u, sched_i = graph.fwd_split
+            N = graph.n_nodes
+            _require(h.size(0) == N, f"x has {h.size(0)} rows but the graph has {N} nodes")
+            out, m, inv_l, agg = _fwd_outputs(N, heads, channels, want_agg, x.device)
+            fa = (h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed, ctx.seed_buf, out, m, inv_l, agg)
+            _fwd_rows(graph, sched_i, RU, N - RU, *fa)
+            pending = rep.merge_fwd_async(out, m, inv_l, agg, b, heads, channels)
+            _fwd_rows(graph, sched_u, 0, RU, *fa)
+            rep.wait(pending)
+        else:
+            out, m, inv_l, agg = gat_fwd(graph, h, s_src, s_dst, b, heads, channels, mode, slope, dropout_p, seed,
+                                         want_agg=want_agg, seed_buf=ctx.seed_buf)
+            if rep is not None:  # replicated item rows (dist.py): merge their softmax over the ranks
+                rep.merge_fwd(out, m, inv_l, agg, b, heads, channels)
         if need:
             empty = torch.empty(0, device=x.device)
             ctx.save_for_backward(x, x_items if x_items is not None else empty, W, h, a_s, a_d, s_src, s_dst, out, m,
