@@ -832,8 +832,11 @@ def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int,
         from .hip_ops import CSRGraph
         graph = CSRGraph(R, El, view.rowptr, view.col, view.csr_eid, view.colptr, view.row, view.csc_eid,
                          view.dz_slot, view.fwd_sched, view.bwd_sched)
-        graph.fwd_split = (RU, sched_builder(view.rowptr[:RU + 1].contiguous(), El),
-                           sched_builder(view.rowptr[RU:].contiguous(), El))
+        # opt-in (PPGAT_FWD_SPLIT=1): measured 0.06-0.08 ms/step of fork/join and split-launch
+        # cost per rank, more than the user rows hide from the merge at N >= 4
+        if os.environ.get("PPGAT_FWD_SPLIT", "0") == "1":
+            graph.fwd_split = (RU, sched_builder(view.rowptr[:RU + 1].contiguous(), El),
+                               sched_builder(view.rowptr[RU:].contiguous(), El))
         if not bool((~su & ~du).any()):  # bipartite (no I-I columns): item sources reach users only
             graph.bwd_split = (RU, sched_builder(view.colptr[:RU + 1].contiguous(), El),
                                sched_builder(view.colptr[RU:].contiguous(), El))

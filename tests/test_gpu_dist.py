@@ -126,9 +126,12 @@ def _check(res, ref):
 
 
 @pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (4, "halo"), (1, "replicated"), (2, "replicated"),
-                                        (1, "replicated-staged")])
+                                        (1, "replicated-staged"), (1, "replicated-fsplit"),
+                                        (2, "replicated-fsplit")])
 def test_sharded_world1_rccl(cuda, tmp_path, monkeypatch, heads, part):
     monkeypatch.setenv("PPGAT_COMM_ALWAYS", "1")  # run every collective through RCCL at world 1
+    # fsplit: the forward split by destination class, the item-row merge on the comm stream
+    monkeypatch.setenv("PPGAT_FWD_SPLIT", "1" if part.endswith("fsplit") else "0")
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)

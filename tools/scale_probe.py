@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph (as bench.py for N>1)")
+    ap.add_argument("--streams", action="store_true",
+                    help="report the stub as RCCL so the comm-stream overlaps (fwd_split / bwd_split) run as at N>1")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = data.synthetic_ui_graph(seed=42)
@@ -76,6 +78,8 @@ def main():
     full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=128, hidden=128, layers=2, heads=1,
                       attn_dropout=0.1).to(dev)
     comm = NullComm(args.world, args.rank)
+    if args.streams:
+        comm.backend = "nccl"
     D = pkg.dist
     if args.partition == "replicated":
         dg = D.build_replicated_graph(ei, g.n_nodes, g.n_users, args.world, args.rank)
