@@ -1,9 +1,9 @@
 #!/bin/bash
-# Session 44: forward split by destination class (replicated partition, item-row merge
+# Session 44 (also the final check): forward split by destination class (replicated partition, item-row merge
 # overlapped with the user destinations) -- dist tests first, then the full GPU suite + bench.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=gpurun_out/s44; mkdir -p $OUT
+OUT=gpurun_out/${SESS_OUT:-s44}; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 240 --timeout-method thread > $OUT/dist.log 2>&1 || { echo "dist rc=$?"; tail -30 $OUT/dist.log; exit 1; }
 tail -3 $OUT/dist.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/gpu.log 2>&1 || { echo "gpu rc=$?"; tail -30 $OUT/gpu.log; exit 1; }
