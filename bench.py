@@ -263,7 +263,7 @@ def main():
         if dist_path:
             Z = model(feats)
             loss_fn = pkg.dist.replicated_bpr_loss if part == "replicated" else pkg.dist.halo_bpr_loss
-            loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
+            loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items, plan_key="bench")  # fixed triples
             opt.zero_grad(set_to_none=True)
             loss.backward()
             model.allreduce_grads()

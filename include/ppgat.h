@@ -513,6 +513,18 @@ int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, con
                             const float* att_dst, int heads, int channels, int in_channels, float* dW, float* datt_src,
                             float* datt_dst, void* stream);
 
+/* ---- multi-head layer, transform-then-aggregate (H*C <= C_in, or the replicated partition) ----
+ * Replaces: the input-gradient terms of GATConv's attention logits (PyG, train_gat_pyg.py:77;
+ *   SURVEY.md Appendix B): dx = D W + ds_src A_src + ds_dst A_dst, with D W on ppgat_gemm_nn.
+ * ppgat_att_proj: att_proj [2, H, C_in] = [W_h^T att_src[h]; W_h^T att_dst[h]] for any shape
+ *   (W [H*C, C_in] row-major, att [H, C]).
+ * ppgat_rows_rank_update: dx[i][k] += sum_{v < nv} S[i][v] A[v][k] (v ascending) over n_rows
+ *   rows, nv <= 16, k % 4 == 0, 16-byte aligned A / dx rows.  Deterministic. */
+int ppgat_att_proj(const float* w, const float* att_src, const float* att_dst, int heads, int channels,
+                   int in_channels, float* att_proj, void* stream);
+int ppgat_rows_rank_update(const float* S, int64_t lds, int nv, const float* A, int64_t lda, int64_t n_rows, int k,
+                           float* dx, int64_t lddx, void* stream);
+
 /* ---- validation / debug build -----------------------------------------------------------
  * ppgat_check_index_range: *n_bad = number of entries of idx (int32 when elem_bytes == 4,
  *   int64 when 8) outside [lo, hi); synchronises the stream (a validation tool, not for use

@@ -1092,6 +1092,30 @@ int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, con
   return PPGAT_OK;
 }
 
+int ppgat_att_proj(const float* w, const float* att_src, const float* att_dst, int heads, int channels,
+                   int in_channels, float* att_proj, void* stream) {
+  if (heads < 1 || channels < 1 || in_channels < 1) return fail(PPGAT_ERR_INVALID, "att_proj: bad sizes");
+  if (!w || !att_src || !att_dst || !att_proj) return fail(PPGAT_ERR_INVALID, "att_proj: null pointer");
+  hipError_t e = ppgat::att_proj(w, att_src, att_dst, heads, channels, in_channels, att_proj,
+                                 static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "att_proj");
+  return PPGAT_OK;
+}
+
+int ppgat_rows_rank_update(const float* S, int64_t lds, int nv, const float* A, int64_t lda, int64_t n_rows, int k,
+                           float* dx, int64_t lddx, void* stream) {
+  if (n_rows < 0 || nv < 0 || nv > 16 || k < 4 || (k % 4)) return fail(PPGAT_ERR_INVALID, "rows_rank_update: bad sizes");
+  if (lds < nv || lda < k || (lda % 4) || lddx < k || (lddx % 4))
+    return fail(PPGAT_ERR_INVALID, "rows_rank_update: bad leading dimension");
+  if (n_rows > 0 && nv > 0 && (!S || !A || !dx)) return fail(PPGAT_ERR_INVALID, "rows_rank_update: null pointer");
+  if ((A && !al16(A)) || (dx && !al16(dx))) return fail(PPGAT_ERR_UNSUPPORTED, "rows_rank_update: 16-byte aligned rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ, st);
+  hipError_t e = ppgat::rank_update(S, lds, nv, A, lda, n_rows, k, dx, lddx, st);
+  if (e != hipSuccess) return hip_fail(e, "rows_rank_update");
+  return PPGAT_OK;
+}
+
 int ppgat_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
   g_prof.on = on != 0;

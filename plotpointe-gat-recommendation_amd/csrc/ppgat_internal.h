@@ -159,6 +159,11 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
                    float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st,
                    void* ws = nullptr);
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N);
+// A [2H, K] = [W_h^T att_src[h]; W_h^T att_dst[h]] (any shape) and dx += S A (rank nv <= 16)
+hipError_t att_proj(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
+                    hipStream_t st);
+hipError_t rank_update(const float* S, int64_t lds, int nv, const float* A, int64_t lda, int64_t n, int K, float* dx,
+                       int64_t lddx, hipStream_t st);
 bool gemm_tn_big_shape_ok(int Ma, int Nb);
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,

@@ -910,6 +910,22 @@ __global__ void __launch_bounds__(256) k_bwd_x_epi(const float* __restrict__ S, 
   st4(dx + i * lddx + c4, v);
 }
 
+// dx[i][k] += sum_{v < nv} S[i][v] A[v][k] (v ascending): the rank-nv attention terms of a
+// multi-head layer's input gradient, dx = D W + S [A_src; A_dst], after the D W GEMM.  One
+// thread per float4 of dx, nv <= 16 runtime (the transform-then-aggregate layer, any K % 4).
+__global__ void __launch_bounds__(256) k_rank_update(const float* __restrict__ S, int64_t lds, int nv,
+                                                     const float* __restrict__ A, int64_t lda, int64_t n, int K,
+                                                     float* __restrict__ dx, int64_t lddx) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int q = K / 4;
+  const int64_t i = t / q;
+  if (i >= n) return;
+  const int c4 = (int)(t % q) * 4;
+  float4 v = ld4(dx + i * lddx + c4);
+  for (int r = 0; r < nv; ++r) v = fma4(S[i * lds + r], ld4(A + r * lda + c4), v);
+  st4(dx + i * lddx + c4, v);
+}
+
 // dW[h C + c][k] = G[c][h K + k] * gs + att_src[h][c] GV[h][k] + att_dst[h][c] GV[H + h][k];
 // datt_v[h][c] = sum_k W[h C + c][k] GV[v H + h][k].  One wave per (h, c) row of W.
 __global__ void __launch_bounds__(256) k_wgrad_x(const float* __restrict__ G, const float* __restrict__ GV,
@@ -1146,6 +1162,23 @@ hipError_t xgat_bwd_epi(const float* S, int64_t lds, const float* A_dst, int64_t
   const int64_t th = n * (K / 4);
   PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_x_epi<256, HH>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, S, lds,
                                  A_dst, n, dx, lddx));
+  return hipGetLastError();
+}
+
+hipError_t att_proj(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
+                    hipStream_t st) {
+  const int64_t na = (int64_t)2 * H * K;
+  if (na > 0) hipLaunchKernelGGL(k_att_proj, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, st, W, att_src, att_dst,
+                                 H, C, K, A);
+  return hipGetLastError();
+}
+
+hipError_t rank_update(const float* S, int64_t lds, int nv, const float* A, int64_t lda, int64_t n, int K, float* dx,
+                       int64_t lddx, hipStream_t st) {
+  if (n <= 0 || nv <= 0) return hipSuccess;
+  const int64_t th = n * (K / 4);
+  hipLaunchKernelGGL(k_rank_update, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, S, lds, nv, A, lda, n, K, dx,
+                     lddx);
   return hipGetLastError();
 }
 

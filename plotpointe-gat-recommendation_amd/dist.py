@@ -675,13 +675,20 @@ class HaloPyGGAT(_ShardedBase):
         return x
 
 
-def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j):
+def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j, plan_key=None):
     """Exchange plan + row map for the triples of this rank's own users: the item rows they
-    read that other ranks own come by one all_to_all (requests exchanged once per triple set)."""
-    key = (u.data_ptr(), i.data_ptr(), j.data_ptr(), int(u.numel()), u._version, i._version, j._version)
-    hit = hg.loss_plans.get(key)
-    if hit is not None:
-        return hit
+    read that other ranks own come by one all_to_all.
+
+    Reuse across calls is keyed ONLY on the caller's ``plan_key`` (e.g. the epoch of the
+    triple draw, or a constant for a fixed triple set), which the caller passes identically on
+    every rank -- the cache decision then agrees across ranks by construction, so no rank can
+    skip the request exchange while another enters it.  Tensor identity (data_ptr/_version)
+    is not a key: a new draw written in place (the device sampler) or placed at a freed
+    address would hit a stale plan.  ``plan_key=None`` rebuilds the plan on every call."""
+    if plan_key is not None:
+        hit = hg.loss_plans.get(plan_key)
+        if hit is not None:
+            return hit
     nu, N = hg.n_users, hg.n_nodes
     (u0, u1), _ = hg.owned()
     un, inn, jn = (t.detach().cpu().numpy().astype(np.int64) for t in (u, i, j))
@@ -703,18 +710,20 @@ def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j):
     rmap[req] = hg.n_own + np.arange(len(req))
     res = (plan, torch.from_numpy(rmap.astype(np.int32)).to(dev))
     hg.loss_plans.clear()  # one live triple set at a time (an epoch's draw)
-    hg.loss_plans[key] = res
+    if plan_key is not None:
+        hg.loss_plans[plan_key] = res
     return res
 
 
 def halo_bpr_loss(Z_own, hg: HaloGraph, comm: "Comm", u, i, j, n_users: int, n_items: int, loss: str = "bpr",
-                  stages=None):
+                  stages=None, plan_key=None):
     """The BPR/BCE loss of train_gat_pyg.py:313-322 over row-sharded Z: each rank takes the
-    triples of its own users; the ranks' returned values add up to the reference's mean."""
+    triples of its own users; the ranks' returned values add up to the reference's mean.
+    ``plan_key``: identifies the triple set, the same value on every rank (see _loss_plan)."""
     if stages is None:
         from .hip_ops import HipStages
         stages = HipStages()
-    plan, rmap = _loss_plan(hg, comm, u, i, j)
+    plan, rmap = _loss_plan(hg, comm, u, i, j, plan_key)
     Zl = exchange(Z_own, plan, comm, stages)
     return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss)
 
@@ -1027,9 +1036,10 @@ class ReplicatedPyGGAT(_ShardedBase):
 
 
 def replicated_bpr_loss(Z_local, rg: RepGraph, comm: Comm, u, i, j, n_users: int, n_items: int,
-                        loss: str = "bpr", stages=None):
+                        loss: str = "bpr", stages=None, plan_key=None):
     """The BPR/BCE loss of train_gat_pyg.py:313-322: each rank takes the triples of its own
-    users against its (replicated) item rows -- no exchange; the ranks' values add up to
+    users against its (replicated) item rows -- no exchange (so no plan: ``plan_key`` is
+    accepted for the halo loss's signature and unused); the ranks' values add up to
     the reference's mean loss and their item-row gradients are partial sums (merged by the
     next layer backward's all_reduce)."""
     if stages is None:

@@ -3,10 +3,11 @@ embeddings/fuse_modal.py.
 
 ``FusionMLP``             -- :18-36, same modules/keys (mlp.0, mlp.3, txt_proj, img_proj) and
                              construction order (seeded construction = reference weights).
-                             Eval-mode forward runs the fused fp32-MFMA kernel
-                             (``ppgat_fusion_fwd``); train-mode forward uses torch ops
-                             (dropout needs torch's RNG stream to match the reference).
-``contrastive_fusion_loss`` -- :39-72 (InfoNCE, tau = 0.07, both modalities), torch autograd.
+                             Eval-mode forward runs the fused matrix-core kernel
+                             (``ppgat_fusion_fwd``); train-mode forward is autograd over the
+                             ppgat GEMMs (hip_ops.linear) with torch's Dropout (its RNG stream).
+``contrastive_fusion_loss`` -- :39-72 (InfoNCE, tau = 0.07, both modalities), autograd; the
+                             similarity products on the ppgat GEMM.
 ``fusion_train_step``      -- the same forward + loss + backward on the device kernels: the four
                              Linear layers on the fp32 matrix-core GEMMs (ppgat_gemm_nn, weight
                              grads ppgat_gemm_tn_big + ppgat_colsum), ReLU/Dropout and its
@@ -72,11 +73,21 @@ class FusionMLP(nn.Module):
         self.img_proj = nn.Linear(img_dim, output_dim)
         self.text_dim, self.img_dim = text_dim, img_dim
 
+    def project_txt(self, t):
+        """txt_proj (fuse_modal.py:31) on the ppgat GEMM."""
+        return hip_ops.linear(t.contiguous(), self.txt_proj.weight, self.txt_proj.bias)
+
+    def project_img(self, t):
+        """img_proj (fuse_modal.py:32) on the ppgat GEMM."""
+        return hip_ops.linear(t.contiguous(), self.img_proj.weight, self.img_proj.bias)
+
     def forward(self, text_emb, img_emb):
-        if self.training or not text_emb.is_cuda:
-            if not text_emb.is_cuda:
-                raise RuntimeError("FusionMLP runs on ROCm devices only; there is no CPU path")
-            return self.mlp(torch.cat([text_emb, img_emb], dim=-1))
+        if not text_emb.is_cuda:
+            raise RuntimeError("FusionMLP runs on ROCm devices only; there is no CPU path")
+        if self.training:  # autograd through the ppgat GEMMs; Dropout keeps torch's RNG draw (:29)
+            l1, l2 = self.mlp[0], self.mlp[3]
+            h = torch.relu(hip_ops.linear(torch.cat([text_emb, img_emb], dim=-1), l1.weight, l1.bias))
+            return hip_ops.linear(self.mlp[2](h), l2.weight, l2.bias)
         return fusion_forward(text_emb, img_emb, self.mlp[0].weight, self.mlp[0].bias, self.mlp[3].weight,
                               self.mlp[3].bias, normalize=False)
 
@@ -88,8 +99,9 @@ def contrastive_fusion_loss(fused, txt_emb, img_emb, temperature=0.07):
     fused_norm = F.normalize(fused, dim=-1)
     txt_norm = F.normalize(txt_emb, dim=-1)
     img_norm = F.normalize(img_emb, dim=-1)
-    sim_fused_txt = torch.matmul(fused_norm, txt_norm.T) / temperature
-    sim_fused_img = torch.matmul(fused_norm, img_norm.T) / temperature
+    # fused_norm @ txt_norm.T as x W^T on ppgat_gemm_nn, differentiable in both operands
+    sim_fused_txt = hip_ops.linear(fused_norm.contiguous(), txt_norm.contiguous()) / temperature
+    sim_fused_img = hip_ops.linear(fused_norm.contiguous(), img_norm.contiguous()) / temperature
     labels = torch.arange(batch_size, device=fused.device)
     loss_txt = F.cross_entropy(sim_fused_txt, labels)
     loss_img = F.cross_entropy(sim_fused_img, labels)
@@ -204,7 +216,7 @@ def train_fusion(model: FusionMLP, txt_aligned: torch.Tensor, img_aligned: torch
             bt, bi = txt_aligned[i:i + batch_size], img_aligned[i:i + batch_size]
             opt.zero_grad()
             fused = model(bt, bi)
-            loss, lt, li = contrastive_fusion_loss(fused, model.txt_proj(bt), model.img_proj(bi))
+            loss, lt, li = contrastive_fusion_loss(fused, model.project_txt(bt), model.project_img(bi))
             loss.backward()
             opt.step()
             tot += loss.item(); tt += lt; ti += li

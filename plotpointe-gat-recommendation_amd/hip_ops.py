@@ -559,7 +559,7 @@ class GATLayer(torch.autograd.Function):
             if x_items is not None:
                 x = torch.cat([x, x_items], 0)
                 x_items = None
-            h = torch.nn.functional.linear(x, W)
+            h = mm_nn(x, W, 1, heads * channels)  # ppgat_gemm_nn (zero-padded where the shape needs it)
             s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
         need = any(ctx.needs_input_grad[:5]) or (had_items and ctx.needs_input_grad[12])
         ctx.seed_buf = seed_buffer(dropout_p, x.device) if need else None
@@ -663,11 +663,13 @@ class GATLayer(torch.autograd.Function):
                                                        a_d.data_ptr(), S.data_ptr(), 2, dx.data_ptr(), K,
                                                        _lib.stream_handle(dev)), "project_bwd_input")
             else:
-                # W_aug = [W; A_src; A_dst],  A[hd] = sum_c att[hd, c] W[hd*C + c, :]
-                Wv = W.view(heads, C, K)
-                A_s = torch.einsum("hc,hck->hk", a_s, Wv)
-                A_d = torch.einsum("hc,hck->hk", a_d, Wv)
-                dx = torch.addmm(S @ torch.cat([A_s, A_d], 0), D, W)
+                # dx = D W + S [A_src; A_dst] with A_v[hd] = sum_c att_v[hd, c] W[hd*C + c, :]:
+                # ppgat_gemm_nn, then the rank-2H attention terms in place (ppgat_rows_rank_update)
+                dx = mm_nn(D, W, 0, K)
+                if K % 4 == 0:
+                    rank_update_(dx, S, att_proj(W, a_s, a_d, heads, C))
+                else:  # odd widths: the rank-2H terms through the padded GEMM as well
+                    dx += mm_nn(S, att_proj(W, a_s, a_d, heads, C), 0, K)
         def wgrad():
             G, _, GV = gemm_tn(D, x, V=S, B_items=xi if seg else None)
             return weight_grads(G, GV, W, a_s, a_d, heads, C)
@@ -757,10 +759,10 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
 
 
 class _Linear(torch.autograd.Function):
-    """y = x W^T + b on the fp32 matrix cores: the fused 128-column projection
-    (ppgat_project) or the general GEMM (ppgat_gemm_nn, config 5's 256-wide layers); dx by
-    ppgat_gemm_nn, dW (and db) through ppgat_gemm_tn (N = 10^5..10^7 rows split over the
-    chip).  Shapes outside both kernels (tests' odd widths) use torch's GEMM."""
+    """y = x W^T + b on the matrix cores: the fused 128-column projection (ppgat_project) or
+    the general GEMM (ppgat_gemm_nn, config 5's 256-wide layers; other widths zero-padded by
+    ``mm_nn``); dx by ppgat_gemm_nn, dW (and db) through ppgat_gemm_tn (N = 10^5..10^7 rows
+    split over the chip).  No vendor BLAS on any shape."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -773,7 +775,7 @@ class _Linear(torch.autograd.Function):
             return project(x, W, b)
         if gemm_nn_supported(x.size(0), x.size(1), weight.size(0), 1):
             return gemm_nn(x, W, 1, weight.size(0), bias=b)
-        return torch.nn.functional.linear(x, weight, bias)
+        return mm_nn(x, W, 1, weight.size(0), bias=b)
 
     @staticmethod
     def backward(ctx, g):
@@ -785,7 +787,7 @@ class _Linear(torch.autograd.Function):
             if gemm_nn_supported(g.size(0), g.size(1), W.size(1), 0):
                 dx = gemm_nn(g, W, 0, W.size(1))
             else:
-                dx = g @ weight
+                dx = mm_nn(g, W, 0, W.size(1))
         dW = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dW, db, _ = gemm_tn(g, x, want_colsum=ctx.has_bias)
@@ -823,6 +825,62 @@ def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: floa
                                     float(alpha), _lib.ptr(bias), y.data_ptr(), y.stride(0) if M > 1 else n,
                                     _lib.ptr(ws), nbytes.value, _lib.stream_handle(x.device)), "gemm_nn")
     return y
+
+
+def _aligned_rows(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1 and (t.size(0) <= 1 or t.stride(0) % 4 == 0) and t.data_ptr() % 16 == 0
+
+
+def mm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: float = 1.0,
+          bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """alpha x B (+ bias) for ANY shape on ppgat_gemm_nn: the reduction width is zero-padded to
+    a multiple of 32 and the output width to a multiple of 128 where the kernel needs it (the
+    padding adds exact zeros, so the result is the unpadded product).  B [K, n] (b_layout 0)
+    or [n, K] (b_layout 1, i.e. x B^T).  No vendor BLAS on any shape."""
+    _require(x.is_cuda and x.dtype == torch.float32 and x.dim() == 2, "mm_nn: x must be a 2-D fp32 ROCm tensor")
+    M, K = x.shape
+    if M == 0:
+        return torch.zeros(0, n, dtype=torch.float32, device=x.device)
+    Kp, Np = -(-max(K, 1) // 32) * 32, -(-max(n, 1) // 128) * 128
+    if Kp != K or not _aligned_rows(x):
+        xp = torch.zeros(M, Kp, dtype=torch.float32, device=x.device)
+        xp[:, :K] = x
+        x = xp
+    B = B.detach()
+    if Kp != K or Np != n or not _aligned_rows(B):
+        Bp = torch.zeros((Kp, Np) if b_layout == 0 else (Np, Kp), dtype=torch.float32, device=x.device)
+        if b_layout == 0:
+            Bp[:K, :n] = B
+        else:
+            Bp[:n, :K] = B
+        B = Bp
+    if bias is not None and Np != n:
+        bias = torch.cat([bias.detach().reshape(-1), bias.new_zeros(Np - n)])
+    y = gemm_nn(x, B, b_layout, Np, alpha=alpha, bias=bias.detach().contiguous() if bias is not None else None)
+    return y if Np == n else y[:, :n].contiguous()
+
+
+def att_proj(W: torch.Tensor, a_s: torch.Tensor, a_d: torch.Tensor, heads: int, channels: int) -> torch.Tensor:
+    """[2H, K] = [W_h^T att_src[h]; W_h^T att_dst[h]] (ppgat_att_proj)."""
+    lib = _lib.load()
+    K = W.size(1)
+    A = torch.empty(2 * heads, K, dtype=torch.float32, device=W.device)
+    _lib.check(lib.ppgat_att_proj(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), heads, channels, K, A.data_ptr(),
+                                  _lib.stream_handle(W.device)), "att_proj")
+    return A
+
+
+def rank_update_(dx: torch.Tensor, S: torch.Tensor, A: torch.Tensor) -> torch.Tensor:
+    """dx += S A in place (ppgat_rows_rank_update; S [n, nv] with nv <= 16, A [nv, K])."""
+    lib = _lib.load()
+    n, K = dx.shape
+    nv = S.size(1)
+    _require(K % 4 == 0 and _aligned_rows(dx) and A.is_contiguous() and S.stride(1) == 1 and nv <= 16,
+             "rank_update_: dx rows 16-byte aligned with K % 4 == 0, nv <= 16")
+    _lib.check(lib.ppgat_rows_rank_update(S.data_ptr(), S.stride(0) if n > 1 else nv, nv, A.data_ptr(), K, n, K,
+                                          dx.data_ptr(), dx.stride(0) if n > 1 else K, _lib.stream_handle(dx.device)),
+               "rows_rank_update")
+    return dx
 
 
 def gemm_tn_big_supported(ma: int, nb: int) -> bool:

@@ -7,7 +7,8 @@ and ``save_npz`` exactly as build_ii_knn.py:104-116 writes it.
 
 Steps (build_ii_knn.py line refs): rows normalised as e / (||e|| + 1e-8) (:57-59) and again
 by sklearn's cosine_similarity (:76); per block of query rows the similarity block
-E_q E^T is one library GEMM (hipBLASLt, fp32); the selection -- self excluded, top-k,
+E_q E^T is one ``ppgat_gemm_nn`` launch (fp32 results on the matrix cores; the rows are
+zero-padded once to the kernel's widths, exact zeros); the selection -- self excluded, top-k,
 sorted, thresholded (:79-95) -- is libppgat's ``ppgat_knn_topk`` kernel.  The full n x n
 matrix is never materialised (block_rows x n at a time).
 """
@@ -16,6 +17,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from . import hip_ops
 
 
 def build_ii_knn(embeddings: torch.Tensor, k: int = 20, min_similarity: float = 0.3, block_rows: int = 8192):
@@ -34,10 +36,14 @@ def build_ii_knn(embeddings: torch.Tensor, k: int = 20, min_similarity: float = 
     sim = torch.empty(n, k, dtype=torch.float32, device=dev)
     cnt = torch.empty(n, dtype=torch.int32, device=dev)
     st = _lib.stream_handle(dev)
+    d = ex.size(1)
+    n_p, d_p = -(-n // 128) * 128, -(-max(d, 1) // 32) * 32
+    exp = torch.zeros(n_p, d_p, dtype=torch.float32, device=dev)  # padded rows/columns are exact zeros
+    exp[:n, :d] = ex
     for q0 in range(0, n, block_rows):
         q1 = min(q0 + block_rows, n)
-        S = ex[q0:q1] @ ex.t()
-        _lib.check(lib.ppgat_knn_topk(S.data_ptr(), n, q1 - q0, n, q0, k, float(min_similarity),
+        S = hip_ops.gemm_nn(exp[q0:q1], exp, 1, n_p)  # [q, n_p]: the similarity block, columns >= n unused
+        _lib.check(lib.ppgat_knn_topk(S.data_ptr(), n_p, q1 - q0, n, q0, k, float(min_similarity),
                                       idx[q0:].data_ptr(), sim[q0:].data_ptr(), cnt[q0:].data_ptr(), st),
                    "knn_topk")
     keep = torch.arange(k, device=dev)[None, :] < cnt[:, None].to(torch.int64)

@@ -291,7 +291,8 @@ def main(argv=None):
             # dense gradients all-reduced, user rows updated by their owner
             sharded.train()
             Zl = sharded(item_feats)
-            loss = loss_fn(Zl, sharded.dg, sharded.comm, u, i, j, n_users, n_items, loss=cfg.loss)
+            loss = loss_fn(Zl, sharded.dg, sharded.comm, u, i, j, n_users, n_items, loss=cfg.loss,
+                           plan_key=epoch)  # one triple draw per epoch, the same epoch on every rank
             opt.zero_grad()
             loss.backward()
             sharded.allreduce_grads()

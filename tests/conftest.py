@@ -34,6 +34,35 @@ def cuda():
     return torch.device("cuda:0")
 
 
+def row_rel(a, b):
+    """Per-row relative error max_i |a_i - b_i| / |b_i| (2-norms, fp64) over the rows of the
+    reference ``b`` with a nonzero norm, and the largest |a_i| over the rows where |b_i| == 0
+    (those must come out zero too).  Returns (max_rel, argmax_row, zero_rows_max_abs)."""
+    import numpy as np
+    import torch
+    a = a.detach().double().cpu().numpy() if torch.is_tensor(a) else np.asarray(a, np.float64)
+    b = b.detach().double().cpu().numpy() if torch.is_tensor(b) else np.asarray(b, np.float64)
+    a, b = a.reshape(len(a), -1), b.reshape(len(b), -1)
+    nb = np.linalg.norm(b, axis=1)
+    nz = nb > 0
+    r = np.linalg.norm(a - b, axis=1)[nz] / nb[nz]
+    zmax = float(np.abs(a[~nz]).max()) if (~nz).any() else 0.0
+    if r.size == 0:
+        return 0.0, -1, zmax
+    k = int(np.argmax(r))
+    return float(r[k]), int(np.flatnonzero(nz)[k]), zmax
+
+
+def write_report(name: str, record: dict):
+    """Parity figures of a GPU test, as JSON under gpurun_out/parity/ (merged back from the GPU
+    box; the committed copies live in profiles/)."""
+    import json
+    out = ROOT / "gpurun_out" / "parity"
+    out.mkdir(parents=True, exist_ok=True)
+    (out / f"{name}.json").write_text(json.dumps(record, indent=2, default=float))
+    print(f"[parity] {name}: {json.dumps(record, default=float)}")
+
+
 @pytest.fixture(autouse=True)
 def _seeded():
     """Every test starts from the same global RNG state, so inputs drawn without an explicit

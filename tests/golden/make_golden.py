@@ -19,6 +19,12 @@ reference's outputs), written as .npz / .json next to this script:
                      build_edge_index (:166-175), sample_bpr_epoch (:213-224, seed 42),
                      CustomGAT (:96-115) init at seed 42, eval forward Z, one BPR+Adam
                      step with attn dropout 0, eval_sampled (:184-210) metrics.
+  trajectory_cfg1.*  the reference's main() (:227-400) for 20 epochs on the config-1
+                     inputs (attn dropout 0, --eval-neg-k 100): the best checkpoint's
+                     export forward, per-epoch loss / val metrics, test metrics; run twice
+                     (default and 1 torch thread) to record the reference's own spread.
+
+    python tests/golden/make_golden.py trajectory    # only the trajectory fixture
 """
 from __future__ import annotations
 
@@ -296,15 +302,184 @@ def knn_case():
     print(f"knn: {m.nnz} edges over {n} items")
 
 
+def trajectory_case(ref, epochs: int = 20):
+    """The reference trainer's own ``main()`` (train_gat_custom.py:227-400) end to end on the
+    config-1 synthetic inputs: ``epochs`` epochs of one 200k-triple BPR batch + Adam, eval each
+    epoch (``--eval-neg-k 100``), best-val checkpoint, reload, test eval, metrics JSON.  GCS is
+    replaced by local files (downloads copy our inputs, uploads are no-ops) and the attention
+    dropout of every ``layer.drop`` is set to 0 after construction (no RNG drawn: the torch
+    stream only initialises the model).  The export forward of the best checkpoint
+    (tools/export_item_embeddings.py:136-142, CustomGAT branch) gives the final item rows.
+
+    Written: ``trajectory_cfg1.npz`` (final item embeddings, the best checkpoint's
+    state_dict, the per-epoch training loss recomputed from the captured Z and triples with
+    the reference's own expression) and ``trajectory_cfg1.json`` (the metrics JSON the
+    reference wrote, minus its time-stamped run id, plus every epoch's val metrics)."""
+    import os
+    import shutil
+    import tempfile
+
+    data = _pkg()
+    work = Path(tempfile.mkdtemp())
+    inter = data.synthetic_interactions_small(seed=0)
+    maps = data.node_maps_from_interactions(inter)
+    src = work / "src"
+    src.mkdir()
+    inter.to_parquet(src / "interactions.parquet")
+    with open(src / "node_maps.json", "w") as f:
+        json.dump({k: v for k, v in maps.items() if not k.startswith("idx_to")}, f)
+    feats = np.random.RandomState(0).standard_normal((maps["n_items"], 384)).astype(np.float32)
+    np.save(src / "txt_interacted.npy", feats)
+
+    class _Blob:
+        def __init__(self, name):
+            self.name = name
+
+        def download_to_filename(self, path):
+            shutil.copy(src / Path(self.name).name, path)
+
+        def upload_from_filename(self, path):
+            pass
+
+    class _Bucket:
+        def blob(self, name):
+            return _Blob(name)
+
+    class _Client:
+        def __init__(self, *a, **k):
+            pass
+
+        def bucket(self, name):
+            return _Bucket()
+
+    rec = {"val": [], "loss": [], "triples": None}
+    base_gat, base_eval, base_sample = ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch
+
+    class _NoDropGAT(base_gat):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            for layer in self.layers:
+                layer.drop.p = 0.0
+
+        def forward(self, item_feats, edge_index):
+            Z = super().forward(item_feats, edge_index)
+            if self.training:  # the epoch's training forward: recompute the loss as main() does
+                u, i, j = (torch.from_numpy(a).long() for a in rec["triples"])
+                with torch.no_grad():
+                    U, I = Z[:self.n_users], Z[self.n_users:]
+                    pos = (U[u] * I[i]).sum(dim=-1)
+                    neg = (U[u] * I[j]).sum(dim=-1)
+                    rec["loss"].append(float(-torch.log(torch.sigmoid(pos - neg) + 1e-8).mean()))
+            return Z
+
+    def _eval(*a, **k):
+        m = base_eval(*a, **k)
+        rec["val"].append(m)
+        return m
+
+    def _sample(*a, **k):
+        rec["triples"] = base_sample(*a, **k)
+        return rec["triples"]
+
+    old_storage = ref.storage
+    ref.storage = types.SimpleNamespace(Client=_Client)
+    ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch = _NoDropGAT, _eval, _sample
+    argv, cwd = sys.argv, os.getcwd()
+    try:
+        os.chdir(work)
+        sys.argv = ["train_gat_custom.py", "--project-id", "local", "--staging-prefix", "gs://b/staging",
+                    "--graphs-prefix", "gs://b/graphs", "--embeddings-prefix", "gs://b/emb",
+                    "--models-prefix", "gs://b/models", "--epochs", str(epochs), "--eval-neg-k", "100",
+                    "--item-features", "txt", "--seed", "42"]
+        ref.main()
+        metrics = json.loads((work / "tmp" / "metrics_gat_custom.json").read_text())
+        ckpt = torch.load(work / "tmp" / "gat_custom_best.pt", map_location="cpu", weights_only=True)
+        # export forward (tools/export_item_embeddings.py:136-142) with the reference's CustomGAT
+        n_users, n_items = int(maps["n_users"]), int(maps["n_items"])
+        model = base_gat(n_users, n_items, item_feat_dim=384, hidden=ckpt["config"].get("hidden_dim", 128),
+                         layers=ckpt["config"].get("layers", 2))
+        model.load_state_dict(ckpt["state_dict"])
+        model.eval()
+        train_raw, _, _ = ref.build_splits(pd_read(work / "tmp" / "interactions.parquet"))
+        u2i = {k: int(v) for k, v in maps["user_to_idx"].items()}
+        i2i = {k: int(v) for k, v in maps["item_to_idx"].items()}
+        tr = {}
+        for u_raw, items in train_raw.items():
+            ii = [i2i[str(t)] for t in items if str(t) in i2i]
+            if str(u_raw) in u2i and ii:
+                tr[u2i[str(u_raw)]] = np.array(ii, dtype=np.int64)
+        ei = ref.build_edge_index(n_users, n_items, tr)
+        with torch.no_grad():
+            Z = model(torch.from_numpy(feats), ei)
+            I = Z[n_users:].detach().cpu().numpy().astype(np.float32)
+            U = Z[:n_users].detach().cpu().numpy().astype(np.float32)
+    finally:
+        sys.argv = argv
+        os.chdir(cwd)
+        ref.storage = old_storage
+        ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch = base_gat, base_eval, base_sample
+        shutil.rmtree(work, ignore_errors=True)
+    best_epoch = 1 + int(np.argmax([v["ndcg@20"] for v in rec["val"][:epochs]]))
+    metrics["config"] = {k: v for k, v in metrics["config"].items() if not k.endswith("_prefix")}
+    metrics["val_per_epoch"] = rec["val"][:epochs]
+    metrics["best_epoch"] = best_epoch
+    metrics["torch_threads"] = torch.get_num_threads()
+    print(f"trajectory ({torch.get_num_threads()} threads): {epochs} epochs, best epoch {best_epoch}, "
+          f"loss {rec['loss'][0]:.6f} -> {rec['loss'][-1]:.6f}, test {metrics['test']}")
+    arrays = dict(item_embeddings=I, user_embeddings=U, loss=np.array(rec["loss"], np.float64),
+                  **{"best__" + k: v.numpy() for k, v in ckpt["state_dict"].items()})
+    return arrays, metrics
+
+
+def trajectory_fixture(ref, epochs: int = 20):
+    """Two runs of the reference trainer that differ only in torch's CPU thread count (the
+    default, then 1): the reference's own run-to-run spread.  Its float reductions
+    (``index_add_`` / ``scatter_add_`` / GEMM) change order with the thread count, and Adam
+    turns the resulting sign noise of near-zero gradients into lr-sized steps, so two runs of
+    the REFERENCE differ after 20 epochs; the GPU test measures our trainer against this
+    envelope.  The default-thread run is the primary fixture, the 1-thread run is ``t1__*``."""
+    threads = torch.get_num_threads()
+    arr, met = trajectory_case(ref, epochs)
+    torch.set_num_threads(1)
+    try:
+        arr1, met1 = trajectory_case(ref, epochs)
+    finally:
+        torch.set_num_threads(threads)
+    nz = np.linalg.norm(arr["item_embeddings"], axis=1) > 0
+    d = arr["item_embeddings"].astype(np.float64) - arr1["item_embeddings"]
+    spread = float((np.linalg.norm(d, axis=1)[nz] / np.linalg.norm(arr["item_embeddings"], axis=1)[nz]).max())
+    met["reference_self_spread"] = {
+        "what": "max over nonzero final item rows of |Z_a - Z_b| / |Z_a|, reference run with the default "
+                "torch thread count vs 1 thread",
+        "item_row_rel": spread,
+        "t1_val_per_epoch": met1["val_per_epoch"], "t1_test": met1["test"], "t1_best_epoch": met1["best_epoch"]}
+    np.savez_compressed(HERE / "trajectory_cfg1.npz", **arr,
+                        t1__item_embeddings=arr1["item_embeddings"], t1__user_embeddings=arr1["user_embeddings"],
+                        t1__loss=arr1["loss"])
+    with open(HERE / "trajectory_cfg1.json", "w") as f:
+        json.dump(met, f, indent=2)
+    print(f"trajectory: reference self-spread (threads {threads} vs 1) {spread:.3e} per item row")
+
+
+def pd_read(path):
+    import pandas as pd
+    return pd.read_parquet(path)
+
+
 def main():
+    only = sys.argv[1:]
+    ref = load_reference_custom()
+    if only == ["trajectory"]:
+        trajectory_fixture(ref)
+        return
     knn_case()
     fusion_case()
-    ref = load_reference_custom()
     layer_case(ref, "small_c8", 0, 300, 3000, 8, "uniform")
     layer_case(ref, "uniform_c128", 1, 1200, 12000, 128, "uniform")
     layer_case(ref, "skewed_c128", 2, 1000, 9000, 128, "skewed")
     layer_case(ref, "clamp_c128", 3, 500, 4000, 128, "uniform", x_scale=6.0)
     plumbing_case(ref)
+    trajectory_fixture(ref)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,6 @@ tests/_cpu_stages.py; the orchestration (partition, padded ids, sliced CSR/CSC, 
 collectives, loss split, grad all-reduce, state_dict gathering) is the product code."""
 import importlib
 import os
-import socket
 import sys
 from pathlib import Path
 
@@ -18,12 +17,15 @@ import torch.multiprocessing as mp
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _master_store():
+    """TCPStore server on a port the OS picks at bind time, held by the test process (the
+    ranks join it as clients: no window in which another process can take the port)."""
+    return dist.TCPStore("127.0.0.1", 0, None, is_master=True, wait_for_workers=False)
+
+
+def _join(rank, world, port):
+    store = dist.TCPStore("127.0.0.1", port, None, is_master=False)
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
 
 
 def _setup(n_users=300, n_items=120, n_int=3000, heads=1, C=32, ii=False):
@@ -48,9 +50,7 @@ def _setup(n_users=300, n_items=120, n_int=3000, heads=1, C=32, ii=False):
 def _worker(rank, world, port, out_dir, heads, ii):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _join(rank, world, port)
     torch.set_num_threads(1)
     from _cpu_stages import CpuStages, csr_builder
     pkg, g, ei, feats, full, (u, i, j) = _setup(heads=heads, ii=ii)
@@ -106,9 +106,10 @@ def test_halo_matches_unsharded_oracle(tmp_path, world, heads, ii):
     the halo rows per layer (h when H*C <= C_in, pre-lin x otherwise: heads 2/4 here), the
     reverse all_to_all of their gradients, the item rows of the loss by all_to_all; forward,
     loss, every gradient == the unsharded fp64 oracle, with attention dropout."""
-    port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path), heads, ii), nprocs=world, join=True,
+    store = _master_store()
+    mp.start_processes(_worker, args=(world, store.port, str(tmp_path), heads, ii), nprocs=world, join=True,
                        start_method="spawn")
+    del store
     res = torch.load(tmp_path / "res.pt", weights_only=False)
     Zr, lr, gr, full = _reference(heads, ii)
     assert len(res["bounds"]) == world + 1
@@ -129,9 +130,7 @@ def test_halo_matches_unsharded_oracle(tmp_path, world, heads, ii):
 def _rep_worker(rank, world, port, out_dir, heads, ii):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _join(rank, world, port)
     torch.set_num_threads(1)
     from _cpu_stages import CpuStages, csr_builder
     pkg, g, ei, feats, full, (u, i, j) = _setup(heads=heads, ii=ii)
@@ -166,8 +165,10 @@ def test_replicated_items_matches_unsharded(tmp_path, world, heads, ii):
     the cross-rank softmax merge of item rows, loss over own users, item-row grad
     all_reduce per layer backward, dense all_reduce == the unsharded oracle (fp64), with
     attention dropout; ii: config 3's item-item columns (homed by destination item)."""
-    mp.start_processes(_rep_worker, args=(world, _free_port(), str(tmp_path), heads, ii), nprocs=world, join=True,
+    store = _master_store()
+    mp.start_processes(_rep_worker, args=(world, store.port, str(tmp_path), heads, ii), nprocs=world, join=True,
                        start_method="spawn")
+    del store
     res = torch.load(tmp_path / "res.pt", weights_only=False)
     Zr, lr, gr, full = _reference(heads, ii)
     for r in range(1, world):

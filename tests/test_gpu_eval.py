@@ -147,7 +147,6 @@ def test_trainer_two_ranks_matches_single_gpu(pkg, cuda, tmp_path, capsys, parti
     seeded inputs (1e-5 at epoch 1, before any update; 1e-4 after the Adam steps), and its
     validation / test metrics agree (ranks can flip on near-ties: 0.02)."""
     import importlib
-    import socket
     import subprocess
     import sys
     from pathlib import Path
@@ -162,12 +161,9 @@ def test_trainer_two_ranks_matches_single_gpu(pkg, cuda, tmp_path, capsys, parti
     single = train.main(common + ["--models-prefix", str(tmp_path / "m1")])
     ev1 = [json.loads(ln) for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
     loss1 = [e["loss"] for e in ev1 if e.get("event") == "epoch_end"]
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    # c10d rendezvous on 127.0.0.1:0: the agent binds the port itself
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "plotpointe-gat-recommendation_amd.train"]
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1", "-m", "plotpointe-gat-recommendation_amd.train"]
     cmd += common + ["--models-prefix", str(tmp_path / "m2"), "--world-size", "2", "--backend", "gloo",
                      "--partition", partition]
     env = dict(__import__("os").environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=str(root))

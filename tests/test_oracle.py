@@ -118,3 +118,29 @@ def test_mlp_dropout_mask_properties(oracle):
     assert set(np.unique(m).tolist()) == {0.0, float(np.float32(1) / np.float32(0.9))}
     assert not np.array_equal(m, oracle.mlp_dropout_scale(78, 200_000, 0.1))
     assert np.all(oracle.mlp_dropout_scale(77, 1000, 0.0) == 1.0)
+
+
+def test_chunked_oracle_equals_whole_graph(oracle):
+    """pyg_gat_conv_chunked (destination blocks, used as the config-5 full-size checker) gives
+    the whole-graph oracle's output, dx and parameter gradients, with dropout and hub rows."""
+    g = _load("skewed_c128")
+    rng = np.random.default_rng(4)
+    H, C, Cin = 2, 16, 24
+    n = g["x"].shape[0]
+    ei = torch.from_numpy(g["edge_index"])
+    x = torch.from_numpy(rng.standard_normal((n, Cin))).double()
+    G = torch.from_numpy(rng.standard_normal((n, C))).double()
+    P = {"lin.weight": torch.from_numpy(rng.standard_normal((H * C, Cin)) * 0.2),
+         "att_src": torch.from_numpy(rng.standard_normal((1, H, C)) * 0.2),
+         "att_dst": torch.from_numpy(rng.standard_normal((1, H, C)) * 0.2),
+         "bias": torch.from_numpy(rng.standard_normal(C) * 0.1)}
+    out_c, dx_c, gr_c = oracle.pyg_gat_conv_chunked(P, x, ei, G, H, 0.1, 77, max_edges=700)
+    Q = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    xw = x.clone().requires_grad_(True)
+    out = oracle.pyg_gat_conv(xw, ei, Q["lin.weight"], Q["att_src"], Q["att_dst"], Q["bias"], H, dropout_p=0.1,
+                              seed=77)
+    (out * G).sum().backward()
+    assert _rel(out_c, out.detach()) <= 1e-12
+    assert _rel(dx_c, xw.grad) <= 1e-12
+    for k in P:
+        assert _rel(gr_c[k], Q[k].grad) <= 1e-11, k

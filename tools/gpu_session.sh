@@ -8,6 +8,7 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 STEPS="${STEPS:-tests smoke bench prof}"
+TESTS="${TESTS:-tests}"   # the 'sel' step: the test files / node ids to run
 BENCH_ARGS="${BENCH_ARGS:---steps 20 --warmup 5}"
 run() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
@@ -28,6 +29,7 @@ for s in $STEPS; do
     gemm) run pytest_gemm 300 python -u -m pytest tests/test_gpu_gemm.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     sampler) run pytest_sampler 300 python -u -m pytest tests/test_sampler.py "tests/test_gpu_eval.py::test_trainer_device_sampler" -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     bsampler) run bench_sampler 300 python tools/bench_sampler.py ;;
+    sel) run pytest_sel 1100 python -u -m pytest $TESTS -m gpu -v -s -rf --durations=15 --timeout 170 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
