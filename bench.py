@@ -350,6 +350,9 @@ def main():
         tt = tt.to(dev) if args.dist_backend == "nccl" else tt
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         el = float(tt.item())
+    loss_val = loss.detach().clone()
+    if dist_path:  # each rank's loss covers its own users' triples: the job's loss is their sum
+        comm.all_reduce_(loss_val)
     K = args.steps
     H, C = args.heads, args.hidden
     # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
@@ -435,7 +438,7 @@ def main():
                      "algo_bytes_per_launch": ab, "avg_launch_ms": avg_s * 1e3, "launches": dom_n,
                      "launches_per_layer_pass": dom_n / max(passes, 1),
                      "measured_copy_gbs": copy_gbs},
-        "loss": float(loss.item()),
+        "loss": float(loss_val.item()),
         "optimizer": "Adam (libppgat device kernel, torch.optim.Adam semantics)",
     }
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0 and args.config != 5:

@@ -345,18 +345,6 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
   __syncthreads();
   if (b0 >= total) return;
   const int len = (int)min((int64_t)kChunk, total - b0);
-  // rows no contribution reaches are zeroed here instead of by a memset of the whole dZ:
-  // each segment start zeroes the rows between the previous key and its own (the sentinel key
-  // n_rows closes the last gap; without sentinels the last contribution zeroes the tail), so
-  // every row of [0, n_rows) is written exactly once
-  for (int q = 0; q < len; ++q) {
-    const int32_t r = s_dst[sg][q];
-    const int64_t prev = q > 0 ? (int64_t)s_dst[sg][q - 1] : (b0 > 0 ? (int64_t)skey[b0 - 1] : -1);
-    const int64_t hi = min((int64_t)r, n_rows);
-    for (int64_t z = prev + 1; z < hi; ++z) st4(dZ + z * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
-    if (b0 + q == total - 1 && r < n_rows)
-      for (int64_t z = (int64_t)r + 1; z < n_rows; ++z) st4(dZ + z * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
-  }
   const bool starts_before = b0 > 0 && skey[b0 - 1] == s_dst[sg][0];
   const bool ends_after = b0 + len < total && skey[b0 + len] == s_dst[sg][len - 1];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -385,6 +373,28 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
         seg_start = q + 1;
       }
     }
+  }
+}
+
+// Rows no contribution reaches: zero, one subgroup per row, membership by a binary search of
+// the sorted keys (lower bound).  Row-parallel whatever the key distribution -- a rank whose
+// triples are all sentinels, few triples, or a huge Z -- and every row of [0, n_rows) is still
+// written exactly once (by k_bpr_chunks / k_bpr_fixup, or here), so no memset of dZ.
+template <int C>
+__global__ void __launch_bounds__(256) k_bpr_zero_untouched(const int32_t* __restrict__ skey, int64_t total,
+                                                            int64_t n_rows, float* __restrict__ dZ) {
+  constexpr int LPR = C / 4;
+  constexpr int SPB = 256 / LPR;
+  const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
+  for (int64_t r = (int64_t)blockIdx.x * SPB + sg; r < n_rows; r += (int64_t)gridDim.x * SPB) {
+    int64_t lo = 0, hi = total;  // first position with skey >= r
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)skey[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < total && (int64_t)skey[lo] == r) continue;
+    st4(dZ + r * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
   }
 }
 
@@ -670,7 +680,7 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
                    const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
   const int64_t N = n_rows;
-  if (S == 0) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_chunks zeroes the gaps
+  if (S == 0) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_zero_untouched
   hipError_t err = hipSuccess;
   const int64_t total = 4 * S;
   const int64_t chunks = (total + kChunk - 1) / kChunk;
@@ -698,6 +708,9 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
     hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, skeys, scid, total, u, i, j, n_users, n_items,
                        row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, slots);
     hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, N, dZ);
+    int64_t gz = (N + SPB - 1) / SPB;
+    if (gz > 4096) gz = 4096;
+    if (N > 0) hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, skeys, total, N, dZ);
   });
   return hipGetLastError();
 }

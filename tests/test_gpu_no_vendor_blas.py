@@ -82,7 +82,7 @@ def test_every_gemm_is_a_ppgat_kernel(pkg, cuda):
         single = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=100, hidden=64, layers=2, heads=4,
                             attn_dropout=0.1).to(cuda).train()  # H*C = 256 > 64: aggregate-then-transform
         cust = pkg.CustomGAT(g.n_users, g.n_items, item_feat_dim=100, hidden=128, layers=2).to(cuda).train()
-        fm = pkg.FusionMLP(384, 512, 128, 256).to(cuda)
+        fm = pkg.fusion.FusionMLP(384, 512, 128, 256).to(cuda)
         txt = torch.randn(300, 384, device=cuda)
         img = torch.randn(300, 512, device=cuda)
         emb = torch.randn(3000, 64, device=cuda)

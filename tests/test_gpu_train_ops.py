@@ -131,6 +131,27 @@ def test_bpr_large_row_space(pkg, oracle, cuda):
     assert rel(Zd.grad, Z64.grad) <= 1e-5
 
 
+@pytest.mark.gpu
+def test_bpr_sparse_keys_zero_untouched_rows(pkg, oracle, cuda):
+    """Three triples over 500k rows: almost every row of dZ is reached by no contribution and
+    must be written as zero (k_bpr_zero_untouched, row-parallel) -- on memory the caching
+    allocator hands back dirty (NaN-filled) on purpose."""
+    rng = np.random.default_rng(3)
+    n_users, n_items, S, C = 400_000, 100_000, 3, 128
+    dirty = torch.full(((n_users + n_items) * C * 2,), float("nan"), device=cuda)
+    del dirty
+    u = torch.from_numpy(rng.integers(0, n_users, S))
+    i = torch.from_numpy(rng.integers(0, n_items, S))
+    j = torch.from_numpy(rng.integers(0, n_items, S))
+    Z64 = torch.from_numpy(rng.standard_normal((n_users + n_items, C)) * 0.3).requires_grad_(True)
+    Zd = Z64.detach().float().to(cuda).requires_grad_(True)
+    pkg.bpr_loss(Zd, n_users, u.to(cuda), i.to(cuda), j.to(cuda)).backward()
+    oracle.bpr_loss(Z64, n_users, u, i, j).backward()
+    assert torch.isfinite(Zd.grad).all()
+    assert rel(Zd.grad, Z64.grad) <= 1e-5
+    assert int((Zd.grad != 0).any(1).sum()) <= 3 * S
+
+
 def _two_layer_grads(pkg, cuda, steps=1, zero=True):
     g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
     ei = torch.from_numpy(g.edge_index_numpy()).to(cuda)

@@ -144,3 +144,26 @@ def test_chunked_oracle_equals_whole_graph(oracle):
     assert _rel(dx_c, xw.grad) <= 1e-12
     for k in P:
         assert _rel(gr_c[k], Q[k].grad) <= 1e-11, k
+
+
+def test_kink_band_options(oracle):
+    """kink_rel marks the logits within fp32 resolution of the LeakyReLU kink; without a forced
+    slope the layer is unchanged (bitwise), with one the band's logit gradient takes it."""
+    g = _load("uniform_c128")
+    x = torch.from_numpy(g["x"]).double()
+    ei = torch.from_numpy(g["edge_index"])
+    W = torch.from_numpy(g["lin_weight"]).double()
+    a_s = torch.from_numpy(g["a_src"]).double().view(1, 1, -1)
+    a_d = torch.from_numpy(g["a_dst"]).double().view(1, 1, -1)
+    b = torch.zeros(W.size(0), dtype=torch.float64)
+    base = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1)
+    kc = []
+    same = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_rel=1e-3, kink_count=kc)
+    assert torch.equal(base, same) and kc[0] > 0
+    # a band covering every edge at slope 1: the layer without the LeakyReLU
+    lin = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_rel=1e9, kink_slope=1.0)
+    ref = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, negative_slope=1.0)
+    assert torch.allclose(lin, ref, rtol=0, atol=1e-12)
+    lo = torch.tensor([1.0, 2.0]); hi = torch.tensor([1.0, 3.0])
+    assert oracle.kink_interval_error(torch.tensor([1.0, 2.5]), lo, hi) == 0.0
+    assert abs(oracle.kink_interval_error(torch.tensor([1.0, 3.5]), lo, hi) - 0.25) < 1e-12
