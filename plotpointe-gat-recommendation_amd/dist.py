@@ -357,7 +357,7 @@ class HaloGraph:
         from .hip_ops import XViews
         f, b = self.fwd_view, self.bwd_view
         return XViews(self.n_own, self.R, f.n_fwd_edges, f.col, f.csr_eid, f.fwd_sched, b.row, b.csc_eid, b.dz_slot,
-                      b.bwd_sched, self.bwd_sched_own, self.bwd_sched_halo)
+                      b.bwd_sched, self.bwd_sched_own, self.bwd_sched_halo, rowptr=f.rowptr)
 
 
 def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,

@@ -243,6 +243,27 @@ def node_scores(h: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, h
     return s_src, s_dst
 
 
+# Test instrumentation (None in normal runs): a list that receives, per GAT layer call, the side
+# of the LeakyReLU kink each edge's logit z = s_src[j] + s_dst[i] fell on in THIS forward --
+# (edge_index column ids [E_local] int64, z > 0 [E_local, heads] bool), z formed exactly as the
+# edge kernels form it (one fp32 add of the same node terms).  The full-size gradient checks
+# hand it to the oracle (oracle/gat_oracle.py kink_pos): a logit within fp32 resolution of 0 may
+# take either side in any fp32 implementation, and the logit gradient depends on the side.
+KINK_TAP: Optional[list] = None
+
+
+def _tap_kinks(rowptr, col, csr_eid, s_src, s_dst, heads: int):
+    if KINK_TAP is None or col is None or rowptr is None:
+        return
+    n = rowptr.numel() - 1
+    E = int(col.numel())
+    if E == 0:
+        return
+    dst = torch.repeat_interleave(torch.arange(n, device=col.device), (rowptr[1:] - rowptr[:-1]).long())[:E]
+    z = s_src.reshape(-1, heads)[col[:E].long()] + s_dst.reshape(-1, heads)[dst]
+    KINK_TAP.append((csr_eid[:E].long().clone(), z > 0))
+
+
 def seed_buffer(dropout_p: float, device) -> Optional[torch.Tensor]:
     """Device slot for the effective mask seed a forward used (include/ppgat.h ppgat_fwd
     seed_used), handed to its backward; None without dropout."""
@@ -561,6 +582,7 @@ class GATLayer(torch.autograd.Function):
                 x_items = None
             h = mm_nn(x, W, 1, heads * channels)  # ppgat_gemm_nn (zero-padded where the shape needs it)
             s_src, s_dst = node_scores(h, a_s, a_d, heads, channels)
+        _tap_kinks(graph.rowptr, graph.col, graph.csr_eid, s_src, s_dst, heads)
         need = any(ctx.needs_input_grad[:5]) or (had_items and ctx.needs_input_grad[12])
         ctx.seed_buf = seed_buffer(dropout_p, x.device) if need else None
         want_agg = (need or rep is not None) and heads > 1
@@ -946,11 +968,12 @@ class XViews:
     bwd_sched_halo: Optional[Schedule] = None  # sources [n_dst, n_src), rows relative to n_dst
     # dz_slot None: dz in CSC order, summed per destination through csr2csc
     csr2csc: Optional[torch.Tensor] = None
+    rowptr: Optional[torch.Tensor] = None  # CSR row pointers over the destinations (KINK_TAP only)
 
     @staticmethod
     def of_graph(g: "CSRGraph") -> "XViews":
         return XViews(g.n_nodes, g.n_nodes, g.n_edges, g.col, g.csr_eid, g.fwd_sched, g.row, g.csc_eid, None,
-                      g.bwd_sched, csr2csc=_csr2csc(g))
+                      g.bwd_sched, csr2csc=_csr2csc(g), rowptr=g.rowptr)
 
 
 def xgat_supported(in_channels: int, heads: int, channels: int) -> bool:
@@ -997,6 +1020,7 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_src, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
                                      s_dst.data_ptr(), st), "xgat_scores")
+    _tap_kinks(v.rowptr, v.col, v.csr_eid, s_src, s_dst, H)
     agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
     m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
     inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
@@ -1252,6 +1276,7 @@ class HipStages:
     def fwd(self, v, h_full, s_src_full, s_dst, bias, heads, channels, mode, slope, p, seed, want_agg, seed_buf=None):
         lib = _lib.load()
         dev = h_full.device
+        _tap_kinks(v.rowptr, v.col, v.csr_eid, s_src_full, s_dst, heads)
         R = v.n_rows
         out = torch.empty(R, channels, dtype=torch.float32, device=dev)
         m = torch.empty(R, heads, dtype=torch.float32, device=dev)

@@ -53,6 +53,20 @@ def row_rel(a, b):
     return float(r[k]), int(np.flatnonzero(nz)[k]), zmax
 
 
+def kink_sides(entries, n_edges: int, heads: int, n_layers: int):
+    """Per layer, the LeakyReLU side [E, heads] bool the HIP kernels took (hip_ops.KINK_TAP
+    entries of one forward, in layer order; ``entries`` may concatenate several ranks' lists,
+    each rank contributing its own edges of every layer)."""
+    import torch
+    out = []
+    for l in range(n_layers):
+        pos = torch.zeros(n_edges, heads, dtype=torch.bool)
+        for eids, p in entries[l::n_layers] if isinstance(entries[0], tuple) else [e[l] for e in entries]:
+            pos[eids.cpu()] = p.cpu().view(-1, heads)
+        out.append(pos)
+    return out
+
+
 def write_report(name: str, record: dict):
     """Parity figures of a GPU test, as JSON under gpurun_out/parity/ (merged back from the GPU
     box; the committed copies live in profiles/)."""

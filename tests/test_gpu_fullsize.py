@@ -29,7 +29,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import row_rel, write_report
+from conftest import kink_sides, row_rel, write_report
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(170)]
 
@@ -42,6 +42,10 @@ def rel(a, b):
 
 def _conv_mod():
     return importlib.import_module("plotpointe-gat-recommendation_amd.conv")
+
+
+def _ops():
+    return importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
 
 
 @pytest.fixture(scope="module")
@@ -69,62 +73,61 @@ def _train_step_check(pkg, oracle, cuda, g, ei_np, feats_np, triples, name):
     tu, ti, tj = (torch.from_numpy(a) for a in triples)
     # device step: the two layers' dropout seeds are drawn from torch's CPU generator
     torch.manual_seed(777)
-    Z = m(feats.to(cuda), ei.to(cuda))
+    _ops().KINK_TAP = []  # the LeakyReLU side of every logit in this forward (for the oracle)
+    try:
+        Z = m(feats.to(cuda), ei.to(cuda))
+        sides = kink_sides(_ops().KINK_TAP, ei_np.shape[1], 1, 2)
+    finally:
+        _ops().KINK_TAP = None
     loss = pkg.bpr_loss(Z, g.n_users, tu.to(cuda), ti.to(cuda), tj.to(cuda))
     loss.backward()
     torch.cuda.synchronize()
     torch.manual_seed(777)
     seeds = [_conv_mod()._dropout_seed() for _ in range(2)]
-    ref = _oracle_step(oracle, m, feats, ei, triples, g.n_users, seeds, cuda)
-    Zr, lr = ref["lo"]["Z"], ref["lo"]["loss"]
+    P = {k: v.detach().double().to(cuda).requires_grad_(True) for k, v in m.named_parameters()}
+    kst = []
+    Zr = oracle.pyg_gat_model(P, feats.double().to(cuda), ei.to(cuda), 2, 1, dropout_p=0.1, seeds=seeds,
+                              kink_pos=sides, kink_stats=kst)
+    lr_t = oracle.bpr_loss(Zr, g.n_users, *(torch.from_numpy(a).to(cuda) for a in triples))
+    lr_t.backward()
+    lr, Zr = float(lr_t), Zr.detach().cpu()
+    grads = {k: v.grad.cpu() for k, v in P.items()}
     r_items, worst, zmax = row_rel(Z[g.n_users:], Zr[g.n_users:])
     r_users = row_rel(Z[:g.n_users], Zr[:g.n_users])[0]
-    gerr = {k: oracle.kink_interval_error(v.grad, ref["lo"]["grads"][k], ref["hi"]["grads"][k])
-            for k, v in m.named_parameters()}
     write_report(name, {"Z_rel": rel(Z, Zr), "item_row_rel_max": r_items, "item_worst_row": worst,
                         "item_zero_rows_max_abs": zmax, "user_row_rel_max": r_users,
-                        "loss_rel": abs(loss.item() - lr) / abs(lr), "kink_band_edges": ref["kinks"],
-                        "grad_rel": gerr, "oracle": "fp64 torch ops on the device, kink band at each slope"})
+                        "loss_rel": abs(loss.item() - lr) / abs(lr),
+                        "kink_ties_per_layer": [{"edges": n, "max_abs_z_rel": r} for n, r in kst],
+                        "grad_rel": {k: rel(v.grad, grads[k]) for k, v in m.named_parameters()},
+                        "oracle": "fp64 torch ops on the device, LeakyReLU sides as the kernels took them"})
+    for n, r in kst:  # the kernels' side differs from the fp64 sign only at fp32 ties of the logit
+        assert r <= KINK_TIE, (n, r)
     assert rel(Z, Zr) <= 1e-5
     assert r_items <= 1e-5 and r_users <= 1e-5, (r_items, worst, r_users)
     assert abs(loss.item() - lr) <= 1e-5 * abs(lr)
     for k, v in m.named_parameters():
         tol = 1e-5 if v.dim() == 2 else 1e-4
+        ref = grads[k]
         if k.endswith("att_dst"):
             # datt_src and datt_dst are sums of the same per-edge logit gradients dz (over a
             # source's out-edges / a destination's in-edges).  Where every in-edge of a
             # destination sits on one side of the LeakyReLU, its dz sum cancels exactly, and
             # datt_dst is rounding only (1.4e-18 in the fp64 oracle at config 3, layer 2):
             # its error is judged on the scale of the pair
-            lo = ref["lo"]["grads"]
-            pair = max(float(lo[k].abs().max()), float(lo[k.replace("att_dst", "att_src")].abs().max()))
-            assert gerr[k] * float(lo[k].abs().max()) <= tol * pair, (k, gerr[k])
+            scale = max(float(ref.abs().max()), float(grads[k.replace("att_dst", "att_src")].abs().max()))
+            err = float((v.grad.detach().double().cpu() - ref).abs().max())
+            assert err <= tol * scale, (k, err, scale)
             continue
-        assert gerr[k] <= tol, (k, gerr[k])
+        assert rel(v.grad, ref) <= tol, (k, rel(v.grad, ref))
 
 
-KINK_REL = 2e-6  # the LeakyReLU kink band, relative to sum_c |h_c att_c| of the two node terms
-
-
-def _oracle_step(oracle, m, feats, ei, triples, n_users, seeds, dev):
-    """The fp64 oracle of one training step (forward, BPR, backward) with the LeakyReLU kink
-    band at slope 0.2 ("lo") and at slope 1 ("hi"): an edge whose logit is within fp32
-    resolution of 0 may take either side in any fp32 implementation (ours and the reference's
-    alike), so a gradient element passes when it lies within the two (oracle.kink_interval_error).
-    Runs on ``dev`` in fp64 (the device oracle equals the CPU one to 1e-15: tools/diag_parity.py)."""
-    tu, ti, tj = (torch.from_numpy(a).to(dev) for a in triples)
-    out = {"kinks": None}
-    for side, slope in (("lo", 0.2), ("hi", 1.0)):
-        P = {k: v.detach().double().to(dev).requires_grad_(True) for k, v in m.named_parameters()}
-        kc = []
-        Zr = oracle.pyg_gat_model(P, feats.double().to(dev), ei.to(dev), 2, 1, dropout_p=0.1, seeds=seeds,
-                                  kink_rel=KINK_REL, kink_slope=slope, kink_count=kc)
-        lr = oracle.bpr_loss(Zr, n_users, tu, ti, tj)
-        lr.backward()
-        out[side] = {"Z": Zr.detach().cpu(), "loss": float(lr), "grads": {k: v.grad.cpu() for k, v in P.items()}}
-        out["kinks"] = kc
-        del P, Zr, lr
-    return out
+# The LeakyReLU kink: where the fp64 logit z = a_src + a_dst is within fp32 resolution of 0, an
+# fp32 implementation (ours, and the reference's own fp32 CPU path) may land on either side, and
+# the logit gradient takes slope 1 or 0.2 accordingly (tools/diag_parity.py found such single
+# edges behind the only large gradient differences at configs 4 and 5).  The oracle therefore
+# takes the side the kernels took (hip_ops.KINK_TAP), and every edge where that side differs
+# from the fp64 sign must be a tie: |z| <= KINK_TIE * (|a_src| + |a_dst|).
+KINK_TIE = 1e-5
 
 
 def test_cfg2_full_eval_embeddings_and_top20(pkg, oracle, cuda, cfg2):
@@ -213,7 +216,12 @@ def test_cfg5_share_layer_full_gradients(pkg, oracle, cuda):
         ei = torch.from_numpy(ei_np).to(cuda)
         xd = x.to(cuda).requires_grad_(True)
         Gd = Gup.to(cuda)
-        out = conv(xd, ei)
+        _ops().KINK_TAP = []
+        try:
+            out = conv(xd, ei)
+            sides = kink_sides(_ops().KINK_TAP, E, H, 1)
+        finally:
+            _ops().KINK_TAP = None
         (out * Gd).sum().backward()
         torch.cuda.synchronize()
         res1 = (out.detach().clone(), xd.grad.clone(), conv.lin.weight.grad.clone(), conv.att_src.grad.clone(),
@@ -231,21 +239,19 @@ def test_cfg5_share_layer_full_gradients(pkg, oracle, cuda):
     del out, out2, res2, xd
     torch.cuda.empty_cache()
     P = {k: v.detach() for k, v in conv.named_parameters()}
-    refs, kinks = {}, None
-    for side, slope in (("lo", 0.2), ("hi", 1.0)):  # the LeakyReLU kink band at each slope (_oracle_step)
-        kc = []
-        out_r, dx_r, grads = oracle.pyg_gat_conv_chunked(P, x.to(cuda), ei, Gd, H, 0.1, 424242, kink_rel=KINK_REL,
-                                                         kink_slope=slope, kink_count=kc)
-        refs[side] = [t.cpu() for t in (out_r, dx_r, grads["lin.weight"], grads["att_src"], grads["att_dst"],
-                                        grads["bias"])]
-        kinks = sum(kc)
-        del out_r, dx_r, grads
-        torch.cuda.empty_cache()
-    errs = {n: oracle.kink_interval_error(a, lo, hi) for n, a, lo, hi in zip(names, res1, refs["lo"], refs["hi"])}
-    rows = {"out": row_rel(res1[0], refs["lo"][0])[0]}
+    kst = []
+    out_r, dx_r, grads = oracle.pyg_gat_conv_chunked(P, x.to(cuda), ei, Gd, H, 0.1, 424242, kink_pos=sides[0].to(cuda),
+                                                     kink_stats=kst)
+    refs = (out_r, dx_r, grads["lin.weight"], grads["att_src"], grads["att_dst"], grads["bias"])
+    errs = {n: rel(a, b) for n, a, b in zip(names, res1, refs)}
+    rows = {"out": row_rel(res1[0], refs[0])[0]}
+    ties = sum(n for n, _ in kst)
+    worst_tie = max((r for _, r in kst), default=0.0)
     write_report("cfg5_share_layer", {"edges": E, "nodes": N, "heads": H, "channels": C, "rel": errs,
-                                      "row_rel_max": rows, "kink_band_edge_heads": kinks,
-                                      "oracle": "chunked fp64 pyg_gat_conv on the device, kink band at each slope"})
+                                      "row_rel_max": rows, "kink_ties": ties, "kink_tie_max_abs_z_rel": worst_tie,
+                                      "oracle": "chunked fp64 pyg_gat_conv on the device, LeakyReLU sides as the "
+                                                "kernels took them"})
+    assert worst_tie <= KINK_TIE, worst_tie
     tol = {"out": 1e-5, "dx": 1e-5, "lin.weight": 1e-5, "att_src": 1e-4, "att_dst": 1e-4, "bias": 1e-5}
     for n in names:
         assert errs[n] <= tol[n], (n, errs[n])

@@ -146,9 +146,9 @@ def test_chunked_oracle_equals_whole_graph(oracle):
         assert _rel(gr_c[k], Q[k].grad) <= 1e-11, k
 
 
-def test_kink_band_options(oracle):
-    """kink_rel marks the logits within fp32 resolution of the LeakyReLU kink; without a forced
-    slope the layer is unchanged (bitwise), with one the band's logit gradient takes it."""
+def test_kink_sides_option(oracle):
+    """kink_pos = the fp64 signs leaves the layer unchanged (bitwise) and reports no tie; all
+    sides forced to slope 1 gives the layer without the LeakyReLU; flipped sides are reported."""
     g = _load("uniform_c128")
     x = torch.from_numpy(g["x"]).double()
     ei = torch.from_numpy(g["edge_index"])
@@ -156,14 +156,17 @@ def test_kink_band_options(oracle):
     a_s = torch.from_numpy(g["a_src"]).double().view(1, 1, -1)
     a_d = torch.from_numpy(g["a_dst"]).double().view(1, 1, -1)
     b = torch.zeros(W.size(0), dtype=torch.float64)
+    h = x @ W.t()
+    z = (h @ a_s.view(-1))[ei[0]] + (h @ a_d.view(-1))[ei[1]]
     base = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1)
-    kc = []
-    same = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_rel=1e-3, kink_count=kc)
-    assert torch.equal(base, same) and kc[0] > 0
-    # a band covering every edge at slope 1: the layer without the LeakyReLU
-    lin = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_rel=1e9, kink_slope=1.0)
+    st = []
+    same = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_pos=(z > 0).view(-1, 1), kink_stats=st)
+    assert torch.equal(base, same) and st == [(0, 0.0)]
+    lin = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_pos=torch.ones(ei.size(1), 1, dtype=torch.bool))
     ref = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, negative_slope=1.0)
     assert torch.allclose(lin, ref, rtol=0, atol=1e-12)
-    lo = torch.tensor([1.0, 2.0]); hi = torch.tensor([1.0, 3.0])
-    assert oracle.kink_interval_error(torch.tensor([1.0, 2.5]), lo, hi) == 0.0
-    assert abs(oracle.kink_interval_error(torch.tensor([1.0, 3.5]), lo, hi) - 0.25) < 1e-12
+    st = []
+    flip = (z > 0).view(-1, 1).clone()
+    flip[:3] = ~flip[:3]
+    oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_pos=flip, kink_stats=st)
+    assert st[0][0] == 3 and st[0][1] > 0
