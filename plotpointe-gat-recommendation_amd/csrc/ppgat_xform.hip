@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
@@ -378,6 +380,143 @@ __global__ void __launch_bounds__(256, 2) k_gemm_nnx(NnArg a) {
     }
     return;
   }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 32 * t + r;
+    const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      if (row < M) a.Y[row * a.ldy + col] = fmaf(a.alpha, acc[t][q], bv);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// NN GEMM on the split bf16 matrix cores, B pre-split once per call (the large-M shapes:
+// config 5's [1.9M x 1024] x [1024 x 256] and [1.9M x 256] x [256 x 1024]).
+//
+// k_gemm_nnx splits its 32-deep B chunk while staging it (per workgroup, per chunk: ~1.8 VALU
+// instructions per MFMA, PMC profiles/r03/v1_gemm_nnx_cfg5_pmc.json: MFMA busy 0.49) and
+// stages it through registers with two barriers per chunk.  Here:
+//  * k_nnx_presplit writes the three bf16 images of every (column block, k chunk) to the
+//    workspace ONCE per call, in exactly the LDS layout k_gemm_nnx uses (80-B rows, the
+//    permuted reduction order), so the products are the same -- bitwise equal results;
+//  * k_gemm_nnp stages them with global_load_lds_dwordx4 (an image is a contiguous byte
+//    range, so the lane-linear LDS destination is the image itself), two LDS buffers, one
+//    barrier per chunk, 8 waves (256 rows) sharing every staged chunk.
+// ---------------------------------------------------------------------------
+constexpr int kPBM = 256;  // rows per k_gemm_nnp workgroup (8 waves x 32)
+
+template <int NT>
+struct NnpImg {
+  static constexpr int KC = 32, BN = 32 * NT, LDK = KC + 8, PART = BN * LDK, ELEMS = 3 * PART, BYTES = 2 * ELEMS;
+  static_assert(BYTES % 1024 == 0, "an image is a whole number of 1-KB wave copies");
+};
+
+template <int NT, int BMODE>
+__global__ void __launch_bounds__(256) k_nnx_presplit(const float* __restrict__ B, int64_t ldb, int K, int N,
+                                                      uint16_t* __restrict__ img) {
+  using I = NnpImg<NT>;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * (K / 4)) return;
+  const int ng = (int)(t % N), kq = (int)(t / N);
+  const int k0 = 4 * kq, c = k0 / I::KC, q = (k0 % I::KC) / 4;
+  const int nb = ng / I::BN, n = ng % I::BN;
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = BMODE == 0 ? B[(int64_t)(k0 + j) * ldb + ng] : B[(int64_t)ng * ldb + k0 + j];
+  uint2 h, mm, l;
+  uint32_t* ph = &h.x;
+  uint32_t* pm = &mm.x;
+  uint32_t* pl = &l.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const uint32_t hh = split::pk_bf16(v[2 * i], v[2 * i + 1]);
+    const float r0 = v[2 * i] - split::bf_lo(hh), r1 = v[2 * i + 1] - split::bf_hi(hh);
+    const uint32_t m2 = split::pk_bf16(r0, r1);
+    ph[i] = hh;
+    pm[i] = m2;
+    pl[i] = split::pk_bf16(r0 - split::bf_lo(m2), r1 - split::bf_hi(m2));
+  }
+  const int kk = 16 * (q >> 2) + 8 * (q & 1) + 4 * ((q >> 1) & 1);
+  uint16_t* base = img + ((int64_t)nb * (K / I::KC) + c) * I::ELEMS + n * I::LDK + kk;
+  *reinterpret_cast<uint2*>(base) = h;
+  *reinterpret_cast<uint2*>(base + I::PART) = mm;
+  *reinterpret_cast<uint2*>(base + 2 * I::PART) = l;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(512, 1) k_gemm_nnp(NnArg a, const uint16_t* __restrict__ img) {
+  using I = NnpImg<NT>;
+  constexpr int KC = I::KC, LDK = I::LDK, PART = I::PART, NI = I::BYTES / 1024;
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][I::ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int64_t rb = (idx / a.n_blocks) * 8 + (b & 7);  // XCD-aware: a row block's column blocks share an L2
+  const int nb = (int)(idx % a.n_blocks);
+  if (rb >= a.row_blocks) return;
+  const int64_t M = a.M;
+  const int K = a.K, chunks = K / KC;
+  const int64_t m = rb * kPBM + wv * 32 + r;
+  const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
+  const char* gimg = reinterpret_cast<const char*>(img + (int64_t)nb * chunks * I::ELEMS);
+  auto issue = [&](int c, int buf) {  // chunk c's three images -> sB[buf], 1 KB per wave instruction
+    const char* src = gimg + (int64_t)c * I::BYTES + lane * 16;
+    char* dst = reinterpret_cast<char*>(sB[buf]);
+    for (int i = wv; i < NI; i += 8)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+  };
+  float4 xa[4], xn[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) xa[g] = ld4(xrow + 8 * g);
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+  issue(0, 0);
+  __syncthreads();  // vmcnt(0): chunk 0 and the first x fragments have landed
+  for (int c = 0; c < chunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < chunks;
+    if (more) {
+      issue(c + 1, buf ^ 1);  // the buffer every wave finished reading before the last barrier
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xn[g] = ld4(xrow + (c + 1) * KC + 8 * g);
+    }
+    const uint16_t* sb = sB[buf];
+    auto read_b = [&](int i, split::u32x4 (&f)[3]) {
+      const int off = (32 * (i % NT) + r) * LDK + 16 * (i / NT) + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sb[p * PART + off]);
+    };
+    split::u32x4 fx[3], fb[3];
+    read_b(0, fb);
+#pragma unroll
+    for (int i = 0; i < (KC / 16) * NT; ++i) {
+      const int u = i / NT, t = i % NT;
+      if (t == 0) split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+      split::u32x4 fn[3];
+      if (i + 1 < (KC / 16) * NT) read_b(i + 1, fn);
+      acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < (KC / 16) * NT) {
+        fb[0] = fn[0];
+        fb[1] = fn[1];
+        fb[2] = fn[2];
+      }
+    }
+    __syncthreads();  // vmcnt(0): chunk c + 1 has landed; every wave is done with sB[buf]
+    if (more) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xa[g] = xn[g];
+    }
+  }
+  const int64_t row0 = rb * kPBM + wv * 32;
+  const int n0 = nb * I::BN;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = n0 + 32 * t + r;
@@ -991,7 +1130,23 @@ int gemm_nn_splits(int64_t M, int K, int N) {
   return s;
 }
 
+// the pre-split path (k_nnx_presplit + k_gemm_nnp): large M, split-bf16 family, K % 32 == 0
+static bool nnp_ok(int64_t M, int K, int N) {
+  static const bool off = [] {
+    const char* e = getenv("PPGAT_GEMM_NNP");
+    return e && strcmp(e, "0") == 0;
+  }();
+  return !off && gemm_split_enabled() && M >= 4 * kPBM && K % 32 == 0 && N % 128 == 0 && gemm_nn_splits(M, K, N) == 1;
+}
+
+static size_t nnp_image_bytes(int K, int N) {
+  const int nt = N % 256 == 0 ? 8 : 4;
+  const size_t img = nt == 8 ? (size_t)NnpImg<8>::BYTES : (size_t)NnpImg<4>::BYTES;
+  return (size_t)(N / (32 * nt)) * (size_t)(K / 32) * img;
+}
+
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N) {
+  if (nnp_ok(M, K, N)) return align_up(nnp_image_bytes(K, N));
   const int s = gemm_nn_splits(M, K, N);
   return s > 1 ? align_up((size_t)s * M * N * 4) : 0;
 }
@@ -1002,6 +1157,26 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
   NnArg a{};
   a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.B = B; a.ldb = ldb; a.N = N; a.alpha = alpha; a.bias = bias;
   a.Y = Y; a.ldy = ldy;
+  if (ws != nullptr && nnp_ok(M, K, N)) {  // B pre-split once, then the glds-staged kernel
+    const bool w8 = N % 256 == 0;
+    uint16_t* img = static_cast<uint16_t*>(ws);
+    const int64_t groups = (int64_t)N * (K / 4);
+    const unsigned gp = (unsigned)((groups + 255) / 256);
+    a.row_blocks = (M + kPBM - 1) / kPBM;
+    a.n_blocks = N / (w8 ? 256 : 128);
+    a.splits = 1;
+    const unsigned grid = (unsigned)((a.row_blocks + 7) / 8 * 8 * a.n_blocks);
+    if (w8) {
+      if (bmode == 0) hipLaunchKernelGGL((k_nnx_presplit<8, 0>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+      else hipLaunchKernelGGL((k_nnx_presplit<8, 1>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+      hipLaunchKernelGGL((k_gemm_nnp<8>), dim3(grid), dim3(512), 0, st, a, img);
+    } else {
+      if (bmode == 0) hipLaunchKernelGGL((k_nnx_presplit<4, 0>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+      else hipLaunchKernelGGL((k_nnx_presplit<4, 1>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+      hipLaunchKernelGGL((k_gemm_nnp<4>), dim3(grid), dim3(512), 0, st, a, img);
+    }
+    return hipGetLastError();
+  }
   a.row_blocks = (M + kGBM - 1) / kGBM;
   const int64_t padded = (a.row_blocks + 7) / 8 * 8;
   const bool wide = N % 256 == 0;

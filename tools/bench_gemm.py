@@ -92,6 +92,12 @@ def cfg5(dev, iters):
         y0 = ops.gemm_nn(X, B0, 0, Nc)
         y1 = ops.gemm_nn(X, B1, 1, Nc)
         assert torch.equal(y0, y1), name  # same products, same order
+        # fingerprint of the exact bits (compare runs with PPGAT_GEMM_NNP=0 / 1) and the fp64 error
+        import hashlib
+        res[f"{name}_sha1"] = hashlib.sha1(y0.cpu().numpy().tobytes()).hexdigest()
+        rows = torch.arange(0, M, 997, device=dev)
+        ref = X[rows].double() @ B0.double()
+        res[f"{name}_rel_err_sampled_rows"] = float((y0[rows].double() - ref).abs().max() / ref.abs().max())
         flop = 2.0 * M * K * Nc
         for lay, B in ((0, B0), (1, B1)):
             us = timeit(lambda: ops.gemm_nn(X, B, lay, Nc, out=y0), iters)
