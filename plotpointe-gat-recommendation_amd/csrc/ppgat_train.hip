@@ -376,26 +376,25 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
   }
 }
 
-// Rows no contribution reaches: zero, one subgroup per row, membership by a binary search of
-// the sorted keys (lower bound).  Row-parallel whatever the key distribution -- a rank whose
-// triples are all sentinels, few triples, or a huge Z -- and every row of [0, n_rows) is still
-// written exactly once (by k_bpr_chunks / k_bpr_fixup, or here), so no memset of dZ.
+// Rows no contribution reaches are zeroed by two row-parallel passes over a byte map of the
+// rows (whatever the key distribution: a rank whose triples are all sentinels, few triples, a
+// huge Z): k_bpr_mark sets touched[key] for every sorted key (plain byte stores of one value,
+// no atomics needed), k_bpr_zero_untouched writes zero rows where the byte is clear.  Every
+// row of [0, n_rows) is still written exactly once (k_bpr_chunks / k_bpr_fixup, or here).
+__global__ void __launch_bounds__(256) k_bpr_mark(const int32_t* __restrict__ skey, int64_t total, int64_t n_rows,
+                                                  uint8_t* __restrict__ touched) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < total && (int64_t)skey[p] < n_rows) touched[skey[p]] = 1;
+}
+
 template <int C>
-__global__ void __launch_bounds__(256) k_bpr_zero_untouched(const int32_t* __restrict__ skey, int64_t total,
-                                                            int64_t n_rows, float* __restrict__ dZ) {
+__global__ void __launch_bounds__(256) k_bpr_zero_untouched(const uint8_t* __restrict__ touched, int64_t n_rows,
+                                                            float* __restrict__ dZ) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
-  for (int64_t r = (int64_t)blockIdx.x * SPB + sg; r < n_rows; r += (int64_t)gridDim.x * SPB) {
-    int64_t lo = 0, hi = total;  // first position with skey >= r
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)skey[mid] < r) lo = mid + 1;
-      else hi = mid;
-    }
-    if (lo < total && (int64_t)skey[lo] == r) continue;
-    st4(dZ + r * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
-  }
+  for (int64_t r = (int64_t)blockIdx.x * SPB + sg; r < n_rows; r += (int64_t)gridDim.x * SPB)
+    if (!touched[r]) st4(dZ + r * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
 }
 
 // Fix-up: the chunk in which a chunk-spanning segment starts sums its tail slot and the
@@ -653,7 +652,7 @@ size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
   const int64_t c4 = 4 * S > 0 ? 4 * S : 1;
   const int64_t chunks = (c4 + kChunk - 1) / kChunk;
   return align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4) + 4 * align_up((size_t)c4 * 4) +
-         align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N + 1));
+         align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N + 1)) + align_up((size_t)N + 1);
 }
 
 hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
@@ -692,7 +691,10 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
   int32_t* scid = reinterpret_cast<int32_t*>(p + 3 * e4);
   float* slots = reinterpret_cast<float*>(p + 4 * e4);
   void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
+  uint8_t* touched = static_cast<uint8_t*>(tmp) + rs_workspace_bytes(total, key_bits(N + 1));
   if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
+  err = hipMemsetAsync(touched, 0, (size_t)N, st);
+  if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
                      n_items, row_map, N, keys, vals);
   bool in1 = false;
@@ -708,9 +710,12 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
     hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, skeys, scid, total, u, i, j, n_users, n_items,
                        row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, slots);
     hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, N, dZ);
-    int64_t gz = (N + SPB - 1) / SPB;
-    if (gz > 4096) gz = 4096;
-    if (N > 0) hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, skeys, total, N, dZ);
+    if (N > 0) {
+      hipLaunchKernelGGL(k_bpr_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, skeys, total, N, touched);
+      int64_t gz = (N + SPB - 1) / SPB;
+      if (gz > 4096) gz = 4096;
+      hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, touched, N, dZ);
+    }
   });
   return hipGetLastError();
 }
