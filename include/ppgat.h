@@ -420,6 +420,15 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
                      int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
                      const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
                      void* stream);
+/* The same with a caller workspace (ppgat_fusion_fwd_workspace_bytes, 16-byte aligned): W1 and
+ * W2 are split into their bf16 images once per call and the kernel stages them straight into
+ * LDS (8 waves per workgroup share each staged chunk); bitwise the results of
+ * ppgat_fusion_fwd. */
+int ppgat_fusion_fwd_workspace_bytes(int text_dim, int img_dim, int hidden_dim, int output_dim, size_t* bytes);
+int ppgat_fusion_fwd_ws(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                        int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
+                        const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- fusion MLP training: InfoNCE loss and backward, ReLU + dropout -----------------------
  * Replaces: contrastive_fusion_loss + its autograd backward, embeddings/fuse_modal.py:39-72

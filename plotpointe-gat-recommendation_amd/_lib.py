@@ -94,6 +94,9 @@ SIGNATURES = {
     "ppgat_serve_topk": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_fusion_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_vp, c_vp]),
+    "ppgat_fusion_fwd_workspace_bytes": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_fusion_fwd_ws": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int,
+                                    c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_infonce_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_infonce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_relu_dropout": (c_int, [c_vp, c_i64, c_f, c_u64, c_int, c_vp, c_vp]),

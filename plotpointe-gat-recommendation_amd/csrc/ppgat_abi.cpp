@@ -810,10 +810,9 @@ int ppgat_serve_topk(const float* item_vecs, int64_t n_items, int channels, cons
   return PPGAT_OK;
 }
 
-int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
-                     int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
-                     const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
-                     void* stream) {
+static int fusion_check(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                        int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
+                        const float* w2, const float* b2, int output_dim, float* out) {
   if (!ppgat::fusion_shape_ok(text_dim, img_dim, hidden_dim, output_dim))
     return fail(PPGAT_ERR_UNSUPPORTED, "fusion_fwd: needs hidden 256, output 128, text/img dims % 32 == 0");
   if (n < 0) return fail(PPGAT_ERR_INVALID, "fusion_fwd: n < 0");
@@ -822,11 +821,46 @@ int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_inde
     return fail(PPGAT_ERR_INVALID, "fusion_fwd: null pointer");
   if (img_dim > 0 && img_index != nullptr && !img_fallback)
     return fail(PPGAT_ERR_INVALID, "fusion_fwd: img_index needs img_fallback for rows without an image");
+  return PPGAT_OK;
+}
+
+int ppgat_fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                     int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
+                     const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
+                     void* stream) {
+  const int rc = fusion_check(txt, img, img_index, img_fallback, n, text_dim, img_dim, w1, b1, hidden_dim, w2, b2,
+                              output_dim, out);
+  if (rc != PPGAT_OK) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_FUSION, st);
   hipError_t e = ppgat::fusion_fwd(txt, img, img_index, img_fallback, n, text_dim, img_dim, w1, b1, w2, b2, normalize,
                                    out, z1, st);
   if (e != hipSuccess) return hip_fail(e, "fusion_fwd");
+  return PPGAT_OK;
+}
+
+int ppgat_fusion_fwd_workspace_bytes(int text_dim, int img_dim, int hidden_dim, int output_dim, size_t* bytes) {
+  if (!bytes || !ppgat::fusion_shape_ok(text_dim, img_dim, hidden_dim, output_dim))
+    return fail(PPGAT_ERR_UNSUPPORTED, "fusion_fwd_workspace_bytes: needs hidden 256, output 128, dims % 32 == 0");
+  *bytes = ppgat::fusion_workspace_bytes(text_dim, img_dim);
+  return PPGAT_OK;
+}
+
+int ppgat_fusion_fwd_ws(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
+                        int64_t n, int text_dim, int img_dim, const float* w1, const float* b1, int hidden_dim,
+                        const float* w2, const float* b2, int output_dim, int normalize, float* out, float* z1,
+                        void* workspace, size_t workspace_bytes, void* stream) {
+  const int rc = fusion_check(txt, img, img_index, img_fallback, n, text_dim, img_dim, w1, b1, hidden_dim, w2, b2,
+                              output_dim, out);
+  if (rc != PPGAT_OK) return rc;
+  if (n > 0 && (!workspace || workspace_bytes < ppgat::fusion_workspace_bytes(text_dim, img_dim) ||
+                (reinterpret_cast<uintptr_t>(workspace) & 15)))
+    return fail(PPGAT_ERR_INVALID, "fusion_fwd_ws: workspace too small or not 16-byte aligned");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_FUSION, st);
+  hipError_t e = ppgat::fusion_fwd(txt, img, img_index, img_fallback, n, text_dim, img_dim, w1, b1, w2, b2, normalize,
+                                   out, z1, st, workspace);
+  if (e != hipSuccess) return hip_fail(e, "fusion_fwd_ws");
   return PPGAT_OK;
 }
 

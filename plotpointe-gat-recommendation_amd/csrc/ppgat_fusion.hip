@@ -309,21 +309,19 @@ __global__ void __launch_bounds__(256, 2) k_fusion_fwdx(const float* __restrict_
 #pragma unroll
       for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&lds[p * XP1 + off]);
     };
-    split::u32x4 fx[3], fb[3];
-    read_w(0, fb);
+    // two fragment sets used alternately; each step issues the next step's three LDS reads
+    // before its six MFMAs (see k_gemm_nnp)
+    split::u32x4 fx[3], fb[2][3];
+    read_w(0, fb[0]);
 #pragma unroll
     for (int idx = 0; idx < 16; ++idx) {
       const int u = idx >> 3, t = idx & 7;
       if (t == 0) split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
-      split::u32x4 fn[3];
-      if (idx + 1 < 16) read_w(idx + 1, fn);
-      acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      if (idx + 1 < 16) read_w(idx + 1, fb[(idx + 1) & 1]);
+      acc[t] = split::mfma32_x6(fx, fb[idx & 1], acc[t]);
+      if (idx + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (idx + 1 < 16) {
-        fb[0] = fn[0];
-        fb[1] = fn[1];
-        fb[2] = fn[2];
-      }
     }
     __syncthreads();
     if (more) {
@@ -400,6 +398,167 @@ __global__ void __launch_bounds__(256, 2) k_fusion_fwdx(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same MLP with W1 and W2 pre-split once per call (ppgat::nnx_presplit: the three bf16
+// images per 32-deep chunk in exactly the layout k_fusion_fwdx builds in LDS, so the products
+// and results are bitwise those of k_fusion_fwdx) and staged by global_load_lds_dwordx4:
+// 8 waves = 256 rows per workgroup share every staged chunk, two LDS buffers, one barrier
+// per chunk.  k_fusion_fwdx splits each chunk while staging it (VALU beside the MFMAs) and
+// waits at two barriers per chunk (PMC: MFMA busy 0.51, profiles/r02/v15_fusion_fwdx_pmc.json).
+// LDS: GEMM1 2 x 61,440 B; GEMM2 reuses it: 8 wave patches (36,864 B) + 2 x 30,720 B W2 slices.
+// ---------------------------------------------------------------------------
+constexpr int PBM = 256;                       // rows per k_fusion_fwdp workgroup
+constexpr int kW1Img = 3 * XP1;                // bf16 per W1 chunk image
+constexpr int kW2Img = 3 * XP2;                // bf16 per W2 slice image
+constexpr int kPatchB = 8 * 32 * XLH * 4;      // bytes of the 8 wave patches
+
+// buffer_load ... lds (MUBUF LDS-DMA, tracked on vmcnt only): with global_load_lds the compiler
+// turned every LDS-read wait behind it into lgkmcnt(0), so no fragment read overlapped an MFMA
+__device__ __forceinline__ void glds_copy(const uint16_t* src, uint16_t* dst, int bytes, int wv, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(src), 0, bytes, 0x00020000);
+  char* d = reinterpret_cast<char*>(dst);
+  for (int i = wv; i < bytes / 1024; i += 8)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(d + i * 1024), 16,
+                                             lane * 16 + i * 1024, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(512, 1) k_fusion_fwdp(const float* __restrict__ txt, const float* __restrict__ img,
+                                                        const int32_t* __restrict__ img_index,
+                                                        const float* __restrict__ img_fallback, int64_t B, int Dt,
+                                                        int Di, const uint16_t* __restrict__ w1i,
+                                                        const float* __restrict__ b1, const uint16_t* __restrict__ w2i_g,
+                                                        const float* __restrict__ b2, int normalize,
+                                                        float* __restrict__ out, float* __restrict__ z1_out) {
+  static_assert(kW1Img * 2 % 1024 == 0 && kW2Img * 2 % 1024 == 0, "1-KB wave copies");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kW1Img];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * PBM + 32 * w;
+  const int K = Dt + Di, chunks = K / BK;
+  const int64_t b = row0 + r < B ? row0 + r : B - 1;
+  const float* trow = txt + b * Dt + 4 * hf;
+  const float* irow;
+  if (Di > 0) {
+    const int32_t ii = img_index ? img_index[b] : (int32_t)b;
+    irow = (ii >= 0 ? img + (int64_t)ii * Di : img_fallback) + 4 * hf;
+  } else {
+    irow = trow;
+  }
+  auto load_x = [&](int k0, float4 (&xv)[4]) {
+    const float* src = k0 < Dt ? trow + k0 : irow + (k0 - Dt);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
+  };
+
+  // ---- GEMM1 ----
+  f32x16 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+  float4 xa[4], xn[4];
+  load_x(0, xa);
+  glds_copy(w1i, lds, kW1Img * 2, w, lane);
+  __syncthreads();  // vmcnt(0): chunk 0 and the first x fragments have landed
+  for (int c = 0; c < chunks; ++c) {
+    const uint16_t* sb = lds + (c & 1) * kW1Img;
+    const bool more = c + 1 < chunks;
+    if (more) {
+      glds_copy(w1i + (int64_t)(c + 1) * kW1Img, lds + ((c + 1) & 1) * kW1Img, kW1Img * 2, w, lane);
+      load_x((c + 1) * BK, xn);
+    }
+    auto read_w = [&](int idx, split::u32x4 (&f)[3]) {
+      const int off = (32 * (idx & 7) + r) * XLD + 16 * (idx >> 3) + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sb[p * XP1 + off]);
+    };
+    // two fragment sets used alternately; each step issues the next step's three LDS reads
+    // before its six MFMAs (see k_gemm_nnp)
+    split::u32x4 fx[3], fb[2][3];
+    read_w(0, fb[0]);
+#pragma unroll
+    for (int idx = 0; idx < 16; ++idx) {
+      const int u = idx >> 3, t = idx & 7;
+      if (t == 0) split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
+      if (idx + 1 < 16) read_w(idx + 1, fb[(idx + 1) & 1]);
+      acc[t] = split::mfma32_x6(fx, fb[idx & 1], acc[t]);
+      if (idx + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // chunk c + 1 landed; every wave is done with this buffer
+    if (more) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xa[g] = xn[g];
+    }
+  }
+
+  // ---- GEMM2 over eight 32-column slices of h (W2 slice images double-buffered after the patches) ----
+  float* hp = reinterpret_cast<float*>(lds) + w * 32 * XLH;                   // this wave's patch [32][XLH]
+  uint16_t* w2s = lds + kPatchB / 2;                                           // [2][3][128][XLD]
+  f32x16 acc2[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
+  glds_copy(w2i_g, w2s, kW2Img * 2, w, lane);
+#pragma unroll
+  for (int c = 0; c < H1 / BK; ++c) {
+    const int col = BK * c + r;
+    const float bias = b1[col];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = row_of(q, hf);
+      const float z = acc[c][q] + bias;
+      hp[row * XLH + r] = fmaxf(z, 0.f);
+      if (z1_out != nullptr && row0 + row < B) z1_out[(row0 + row) * H1 + col] = z;
+    }
+    __syncthreads();  // vmcnt(0): slice c landed; the patch is written
+    if (c + 1 < H1 / BK) glds_copy(w2i_g + (int64_t)(c + 1) * kW2Img, w2s + ((c + 1) & 1) * kW2Img, kW2Img * 2, w, lane);
+    const uint16_t* ws2 = w2s + (c & 1) * kW2Img;
+    auto read_w2 = [&](int i, split::u32x4 (&f)[3]) {
+      const int off = (32 * (i & 3) + r) * XLD + 16 * (i >> 2) + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&ws2[p * XP2 + off]);
+    };
+    split::u32x4 fh[3], fb2[2][3];
+    read_w2(0, fb2[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int u = i >> 2, uu = i & 3;
+      if (uu == 0)
+        split::split3(ld4(&hp[r * XLH + 16 * u + 4 * hf]), ld4(&hp[r * XLH + 16 * u + 8 + 4 * hf]), fh[0], fh[1],
+                      fh[2]);
+      if (i + 1 < 8) read_w2(i + 1, fb2[(i + 1) & 1]);
+      acc2[uu] = split::mfma32_x6(fh, fb2[i & 1], acc2[uu]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // the patch and this slice's buffer are free again
+  }
+
+  // ---- bias, row L2 norm (inside the wave), store ----
+  float ss[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) ss[q] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float bias2 = b2[32 * u + r];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc2[u][q] += bias2;
+      ss[q] = fmaf(acc2[u][q], acc2[u][q], ss[q]);
+    }
+  }
+  if (normalize) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ss[q] = 1.f / (sqrtf(group_reduce<Op::Sum, 1, 16>(ss[q])) + 1e-8f);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t row = row0 + row_of(q, hf);
+    if (row >= B) continue;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) out[row * DO + 32 * u + r] = normalize ? acc2[u][q] * ss[q] : acc2[u][q];
+  }
+}
+
 }  // namespace
 
 
@@ -407,10 +566,24 @@ bool fusion_shape_ok(int Dt, int Di, int h1, int d_out) {
   return h1 == H1 && d_out == DO && Dt >= 0 && Di >= 0 && Dt % BK == 0 && Di % BK == 0 && Dt + Di > 0;
 }
 
+size_t fusion_workspace_bytes(int Dt, int Di) {
+  return nnx_image_bytes(Dt + Di, H1, 8) + nnx_image_bytes(H1, DO, 4) + 256;
+}
+
 hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
-                      int normalize, float* out, float* z1_out, hipStream_t st) {
+                      int normalize, float* out, float* z1_out, hipStream_t st, void* ws) {
   if (B == 0) return hipSuccess;
+  if (ws != nullptr && gemm_split_enabled()) {  // W1 / W2 pre-split once, then the glds-staged kernel
+    uint16_t* w1i = static_cast<uint16_t*>(ws);
+    uint16_t* w2i = w1i + nnx_image_bytes(Dt + Di, H1, 8) / 2;
+    hipError_t e = nnx_presplit(W1, Dt + Di, 1, Dt + Di, H1, 8, w1i, st);
+    if (e == hipSuccess) e = nnx_presplit(W2, H1, 1, H1, DO, 4, w2i, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_fusion_fwdp, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img, img_index,
+                       img_fallback, B, Dt, Di, w1i, b1, w2i, b2, normalize, out, z1_out);
+    return hipGetLastError();
+  }
   if (gemm_split_enabled())
     hipLaunchKernelGGL(k_fusion_fwdx, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), 0, st, txt, img, img_index,
                        img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);

@@ -135,9 +135,11 @@ hipError_t sampled_rank(const float* Z, int64_t n_users, int64_t n_items, const 
 
 // fusion MLP (ppgat_fusion.hip)
 bool fusion_shape_ok(int Dt, int Di, int h1, int d_out);
+size_t fusion_workspace_bytes(int Dt, int Di);
 hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_index, const float* img_fallback,
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
-                      int normalize, float* out, float* z1_out, hipStream_t st);
+                      int normalize, float* out, float* z1_out, hipStream_t st,
+                      void* ws = nullptr);
 
 // index-range validation (ppgat_debug.hip)
 hipError_t count_out_of_range(const void* idx, int elem_bytes, int64_t n, int64_t lo, int64_t hi, int64_t* n_bad,
@@ -159,6 +161,9 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
                    float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st,
                    void* ws = nullptr);
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N);
+// the split bf16 images of a GEMM's B operand per (32 nt columns, 32-deep k chunk), once per call
+hipError_t nnx_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, hipStream_t st);
+size_t nnx_image_bytes(int K, int N, int nt);
 // A [2H, K] = [W_h^T att_src[h]; W_h^T att_dst[h]] (any shape) and dx += S A (rank nv <= 16)
 hipError_t att_proj(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
                     hipStream_t st);

@@ -463,13 +463,17 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnp(NnArg a, const uint16_t* __
   const int K = a.K, chunks = K / KC;
   const int64_t m = rb * kPBM + wv * 32 + r;
   const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
-  const char* gimg = reinterpret_cast<const char*>(img + (int64_t)nb * chunks * I::ELEMS);
+  // buffer_load ... lds (MUBUF), not global_load_lds: the compiler counts a FLAT LDS-DMA as a
+  // pending LDS access, and every LDS-read wait behind it became lgkmcnt(0) -- the ds_reads of
+  // step i + 1 could not overlap step i's MFMAs.  A MUBUF LDS-DMA is tracked on vmcnt only.
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(img + (int64_t)nb * chunks * I::ELEMS), 0, chunks * I::BYTES, 0x00020000);
   auto issue = [&](int c, int buf) {  // chunk c's three images -> sB[buf], 1 KB per wave instruction
-    const char* src = gimg + (int64_t)c * I::BYTES + lane * 16;
+    const int src = c * I::BYTES + lane * 16;
     char* dst = reinterpret_cast<char*>(sB[buf]);
     for (int i = wv; i < NI; i += 8)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i * 1024),
-                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                               src + i * 1024, 0, 0, 0);
   };
   float4 xa[4], xn[4];
 #pragma unroll
@@ -493,21 +497,22 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnp(NnArg a, const uint16_t* __
 #pragma unroll
       for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sb[p * PART + off]);
     };
-    split::u32x4 fx[3], fb[3];
-    read_b(0, fb);
+    // B fragments in two register sets used alternately (no copy between them, so the register
+    // allocator cannot merge them): the reads of step i + 1 issue before the six MFMAs of step i
+    // and have those ~190 cycles to land (with one merged set they were scheduled after the
+    // step's fifth MFMA and the next step waited on the LDS latency)
+    split::u32x4 fx[3], fb[2][3];
+    read_b(0, fb[0]);
 #pragma unroll
     for (int i = 0; i < (KC / 16) * NT; ++i) {
       const int u = i / NT, t = i % NT;
       if (t == 0) split::split3(xa[2 * u], xa[2 * u + 1], fx[0], fx[1], fx[2]);
-      split::u32x4 fn[3];
-      if (i + 1 < (KC / 16) * NT) read_b(i + 1, fn);
-      acc[t] = split::mfma32_x6(fx, fb, acc[t]);
+      if (i + 1 < (KC / 16) * NT) read_b(i + 1, fb[(i + 1) & 1]);
+      acc[t] = split::mfma32_x6(fx, fb[i & 1], acc[t]);
+      // order inside the step: the next step's three LDS reads first, then the six MFMAs
+      if (i + 1 < (KC / 16) * NT) __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < (KC / 16) * NT) {
-        fb[0] = fn[0];
-        fb[1] = fn[1];
-        fb[2] = fn[2];
-      }
     }
     __syncthreads();  // vmcnt(0): chunk c + 1 has landed; every wave is done with sB[buf]
     if (more) {
@@ -1130,6 +1135,27 @@ int gemm_nn_splits(int64_t M, int K, int N) {
   return s;
 }
 
+// the three bf16 images of B [K x N] (bmode 0: B[k][n] = B[k ldb + n]; 1: B[n ldb + k]) per
+// (column block of 32 nt columns, 32-deep k chunk), in the LDS layout the split kernels read
+hipError_t nnx_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, hipStream_t st) {
+  const int64_t groups = (int64_t)N * (K / 4);
+  const unsigned gp = (unsigned)((groups + 255) / 256);
+  if (groups <= 0) return hipSuccess;
+  if (nt == 8) {
+    if (bmode == 0) hipLaunchKernelGGL((k_nnx_presplit<8, 0>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+    else hipLaunchKernelGGL((k_nnx_presplit<8, 1>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+  } else {
+    if (bmode == 0) hipLaunchKernelGGL((k_nnx_presplit<4, 0>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+    else hipLaunchKernelGGL((k_nnx_presplit<4, 1>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
+  }
+  return hipGetLastError();
+}
+
+size_t nnx_image_bytes(int K, int N, int nt) {
+  const size_t img = nt == 8 ? (size_t)NnpImg<8>::BYTES : (size_t)NnpImg<4>::BYTES;
+  return (size_t)(N / (32 * nt)) * (size_t)(K / 32) * img;
+}
+
 // the pre-split path (k_nnx_presplit + k_gemm_nnp): large M, split-bf16 family, K % 32 == 0
 static bool nnp_ok(int64_t M, int K, int N) {
   static const bool off = [] {
@@ -1139,11 +1165,7 @@ static bool nnp_ok(int64_t M, int K, int N) {
   return !off && gemm_split_enabled() && M >= 4 * kPBM && K % 32 == 0 && N % 128 == 0 && gemm_nn_splits(M, K, N) == 1;
 }
 
-static size_t nnp_image_bytes(int K, int N) {
-  const int nt = N % 256 == 0 ? 8 : 4;
-  const size_t img = nt == 8 ? (size_t)NnpImg<8>::BYTES : (size_t)NnpImg<4>::BYTES;
-  return (size_t)(N / (32 * nt)) * (size_t)(K / 32) * img;
-}
+static size_t nnp_image_bytes(int K, int N) { return nnx_image_bytes(K, N, N % 256 == 0 ? 8 : 4); }
 
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N) {
   if (nnp_ok(M, K, N)) return align_up(nnp_image_bytes(K, N));
@@ -1160,21 +1182,14 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
   if (ws != nullptr && nnp_ok(M, K, N)) {  // B pre-split once, then the glds-staged kernel
     const bool w8 = N % 256 == 0;
     uint16_t* img = static_cast<uint16_t*>(ws);
-    const int64_t groups = (int64_t)N * (K / 4);
-    const unsigned gp = (unsigned)((groups + 255) / 256);
     a.row_blocks = (M + kPBM - 1) / kPBM;
     a.n_blocks = N / (w8 ? 256 : 128);
     a.splits = 1;
     const unsigned grid = (unsigned)((a.row_blocks + 7) / 8 * 8 * a.n_blocks);
-    if (w8) {
-      if (bmode == 0) hipLaunchKernelGGL((k_nnx_presplit<8, 0>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
-      else hipLaunchKernelGGL((k_nnx_presplit<8, 1>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
-      hipLaunchKernelGGL((k_gemm_nnp<8>), dim3(grid), dim3(512), 0, st, a, img);
-    } else {
-      if (bmode == 0) hipLaunchKernelGGL((k_nnx_presplit<4, 0>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
-      else hipLaunchKernelGGL((k_nnx_presplit<4, 1>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, img);
-      hipLaunchKernelGGL((k_gemm_nnp<4>), dim3(grid), dim3(512), 0, st, a, img);
-    }
+    hipError_t e = nnx_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, st);
+    if (e != hipSuccess) return e;
+    if (w8) hipLaunchKernelGGL((k_gemm_nnp<8>), dim3(grid), dim3(512), 0, st, a, img);
+    else hipLaunchKernelGGL((k_gemm_nnp<4>), dim3(grid), dim3(512), 0, st, a, img);
     return hipGetLastError();
   }
   a.row_blocks = (M + kGBM - 1) / kGBM;

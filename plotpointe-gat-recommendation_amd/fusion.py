@@ -51,9 +51,13 @@ def fusion_forward(txt: torch.Tensor, img: Optional[torch.Tensor], W1, b1, W2, b
     idx32 = img_index.to(torch.int32).contiguous() if img_index is not None else None
     fb = img_fallback.contiguous() if img_fallback is not None else None
     W1c, b1c, W2c, b2c = (t.detach().contiguous() for t in (W1, b1, W2, b2))
-    _lib.check(lib.ppgat_fusion_fwd(ptr(txt), ptr(imgc), ptr(idx32), ptr(fb), n, Dt, Di, W1c.data_ptr(), b1c.data_ptr(),
-                                    H1, W2c.data_ptr(), b2c.data_ptr(), Do, 1 if normalize else 0, out.data_ptr(),
-                                    ptr(z1), _lib.stream_handle(dev)), "fusion_fwd")
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_fusion_fwd_workspace_bytes(Dt, Di, H1, Do, ctypes.byref(nbytes)), "fusion_fwd_workspace")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)  # the pre-split W1 / W2 images
+    _lib.check(lib.ppgat_fusion_fwd_ws(ptr(txt), ptr(imgc), ptr(idx32), ptr(fb), n, Dt, Di, W1c.data_ptr(),
+                                       b1c.data_ptr(), H1, W2c.data_ptr(), b2c.data_ptr(), Do, 1 if normalize else 0,
+                                       out.data_ptr(), ptr(z1), ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)),
+               "fusion_fwd")
     return (out, z1) if want_z1 else out
 
 
