@@ -534,6 +534,155 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnp(NnArg a, const uint16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// NN GEMM on the fp16 matrix cores through the scaled two-term split (ppgat_split.h): three
+// MFMAs per product instead of six.  B is pre-split once per call with a power-of-two scale per
+// column (k_colscale16 + k_nnh_presplit: two fp16 images per (column block, k chunk), the same
+// 80-B rows and permuted reduction order as the bf16 images).  X streams in 32-deep chunks, so a
+// row's scale is set ONLINE: by the first chunk in which the row is nonzero (largest |x| s in
+// [2^9, 2^10)), and lowered only when a later chunk would reach 2^15 (fp16 overflows at 65,520,
+// so 32x headroom) -- then that row's accumulators are multiplied by the exact power of two
+// s_new / s_old (a wave-uniform branch, rare on real data: first-chunk maxima within 32x of the
+// row's).  Elements far below their row's max keep an absolute error <= 2^-34 of that max.
+// ---------------------------------------------------------------------------
+template <int NT>
+struct NnhImg {
+  static constexpr int KC = 32, BN = 32 * NT, LDK = KC + 8, PART = BN * LDK, ELEMS = 2 * PART, BYTES = 2 * ELEMS;
+  static_assert(BYTES % 1024 == 0, "an image is a whole number of 1-KB wave copies");
+};
+
+// per column of B [K x N]: the scale exponent (largest |b| 2^e in [2^9, 2^10); 0 for a zero column)
+template <int BMODE>
+__global__ void __launch_bounds__(256) k_colscale16(const float* __restrict__ B, int64_t ldb, int K, int N,
+                                                    int* __restrict__ ecol) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  float m = 0.f;
+  for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(BMODE == 0 ? B[(int64_t)k * ldb + n] : B[(int64_t)n * ldb + k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) ecol[n] = m > 0.f && m <= 3.4e38f ? split::scale_exp16(m) : 0;
+}
+
+template <int NT, int BMODE>
+__global__ void __launch_bounds__(256) k_nnh_presplit(const float* __restrict__ B, int64_t ldb, int K, int N,
+                                                      const int* __restrict__ ecol, uint16_t* __restrict__ img) {
+  using I = NnhImg<NT>;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * (K / 4)) return;
+  const int ng = (int)(t % N), kq = (int)(t / N);
+  const int k0 = 4 * kq, c = k0 / I::KC, q = (k0 % I::KC) / 4;
+  const int nb = ng / I::BN, n = ng % I::BN;
+  const float s = ldexpf(1.f, ecol[ng]);
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (BMODE == 0 ? B[(int64_t)(k0 + j) * ldb + ng] : B[(int64_t)ng * ldb + k0 + j]) * s;
+  uint2 h, l;
+  uint32_t* ph = &h.x;
+  uint32_t* pl = &l.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const uint32_t hh = split::pk_f16(v[2 * i], v[2 * i + 1]);
+    const split::f32x2e back = __builtin_convertvector(__builtin_bit_cast(split::f16x2, hh), split::f32x2e);
+    ph[i] = hh;
+    pl[i] = split::pk_f16(v[2 * i] - back.x, v[2 * i + 1] - back.y);
+  }
+  const int kk = 16 * (q >> 2) + 8 * (q & 1) + 4 * ((q >> 1) & 1);
+  uint16_t* base = img + ((int64_t)nb * (K / I::KC) + c) * I::ELEMS + n * I::LDK + kk;
+  *reinterpret_cast<uint2*>(base) = h;
+  *reinterpret_cast<uint2*>(base + I::PART) = l;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __restrict__ img,
+                                                     const int* __restrict__ ecol) {
+  using I = NnhImg<NT>;
+  constexpr int KC = I::KC, LDK = I::LDK, PART = I::PART, NI = I::BYTES / 1024;
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][I::ELEMS];
+  __shared__ __attribute__((aligned(16))) float sF[8][32];  // per wave: a factor per row (rescale, epilogue)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int64_t rb = (idx / a.n_blocks) * 8 + (b & 7);  // XCD-aware: a row block's column blocks share an L2
+  const int nb = (int)(idx % a.n_blocks);
+  if (rb >= a.row_blocks) return;
+  const int64_t M = a.M;
+  const int K = a.K, chunks = K / KC;
+  const int64_t m = rb * kPBM + wv * 32 + r;
+  const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(img + (int64_t)nb * chunks * I::ELEMS), 0, chunks * I::BYTES, 0x00020000);
+  auto issue = [&](int c, int buf) {  // chunk c's two images -> sB[buf], 1 KB per wave instruction
+    const int src = c * I::BYTES + lane * 16;
+    char* dst = reinterpret_cast<char*>(sB[buf]);
+    for (int i = wv; i < NI; i += 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                               src + i * 1024, 0, 0, 0);
+  };
+  float4 xa[4], xn[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) xa[g] = ld4(xrow + 8 * g);
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+  int erow = 0;
+  bool set = false;  // the row has had a nonzero element (its scale is fixed until an overflow)
+  issue(0, 0);
+  __syncthreads();  // vmcnt(0): chunk 0 and the first x fragments have landed
+  for (int c = 0; c < chunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < chunks;
+    if (more) {
+      issue(c + 1, buf ^ 1);  // the buffer every wave finished reading before the last barrier
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xn[g] = ld4(xrow + (c + 1) * KC + 8 * g);
+    }
+    const float s = split::row_scale_online<NT>(xa, erow, set, acc, sF[wv], r, hf);  // chunk c's row scales
+    const uint16_t* sb = sB[buf];
+    auto read_b = [&](int i, split::u32x4 (&f)[2]) {
+      const int off = (32 * (i % NT) + r) * LDK + 16 * (i / NT) + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sb[p * PART + off]);
+    };
+    // two fragment sets used alternately; each step issues the next step's two LDS reads before
+    // its three MFMAs (see k_gemm_nnp)
+    split::u32x4 fx[2], fb[2][2];
+    read_b(0, fb[0]);
+#pragma unroll
+    for (int i = 0; i < (KC / 16) * NT; ++i) {
+      const int u = i / NT, t = i % NT;
+      if (t == 0) split::split2h(xa[2 * u], xa[2 * u + 1], s, fx[0], fx[1]);
+      if (i + 1 < (KC / 16) * NT) read_b(i + 1, fb[(i + 1) & 1]);
+      acc[t] = split::mfma32_h3(fx, fb[i & 1], acc[t]);
+      if (i + 1 < (KC / 16) * NT) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x0008, 3, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // vmcnt(0): chunk c + 1 has landed; every wave is done with sB[buf]
+    if (more) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xa[g] = xn[g];
+    }
+  }
+  float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
+  split::row_unscale(erow, sF[wv], r, hf, fr);
+  const int64_t row0 = rb * kPBM + wv * 32;
+  const int n0 = nb * I::BN;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 32 * t + r;
+    const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+    const float ic = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+    }
+  }
+}
+
 // split-K finish: Y = alpha * sum_s part[s] (split order) + bias, float4 per thread
 __global__ void __launch_bounds__(256) k_nn_split_sum(const float* __restrict__ part, int64_t M, int N, int splits,
                                                       float alpha, const float* __restrict__ bias,
@@ -1167,8 +1316,46 @@ static bool nnp_ok(int64_t M, int K, int N) {
 
 static size_t nnp_image_bytes(int K, int N) { return nnx_image_bytes(K, N, N % 256 == 0 ? 8 : 4); }
 
+// the fp16 two-term family (k_gemm_nnh) on the pre-split path; PPGAT_GEMM_F16=0 keeps the bf16 x6 kernel
+static bool nnh_enabled() {
+  static const bool off = [] {
+    const char* e = getenv("PPGAT_GEMM_F16");
+    return e && strcmp(e, "0") == 0;
+  }();
+  return !off;
+}
+
+size_t nnh_image_bytes(int K, int N, int nt) {
+  const size_t img = nt == 8 ? (size_t)NnhImg<8>::BYTES : (size_t)NnhImg<4>::BYTES;
+  return (size_t)(N / (32 * nt)) * (size_t)(K / 32) * img;
+}
+
+// B's column scales and two fp16 images (layout as nnx_presplit's, two parts instead of three)
+hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, int* ecol,
+                        hipStream_t st) {
+  const int64_t groups = (int64_t)N * (K / 4);
+  if (groups <= 0) return hipSuccess;
+  const unsigned gc = (unsigned)((N + 3) / 4), gp = (unsigned)((groups + 255) / 256);
+  if (bmode == 0) hipLaunchKernelGGL((k_colscale16<0>), dim3(gc), dim3(256), 0, st, B, ldb, K, N, ecol);
+  else hipLaunchKernelGGL((k_colscale16<1>), dim3(gc), dim3(256), 0, st, B, ldb, K, N, ecol);
+#define PPGAT_NNH_PRE(NT_, BM_) \
+  hipLaunchKernelGGL((k_nnh_presplit<NT_, BM_>), dim3(gp), dim3(256), 0, st, B, ldb, K, N, ecol, img)
+  if (nt == 8) {
+    if (bmode == 0) PPGAT_NNH_PRE(8, 0); else PPGAT_NNH_PRE(8, 1);
+  } else {
+    if (bmode == 0) PPGAT_NNH_PRE(4, 0); else PPGAT_NNH_PRE(4, 1);
+  }
+#undef PPGAT_NNH_PRE
+  return hipGetLastError();
+}
+
+static size_t nnq_bytes(int K, int N) {  // image + column exponents, either family
+  const int nt = N % 256 == 0 ? 8 : 4;
+  return nnh_enabled() ? align_up(nnh_image_bytes(K, N, nt)) + align_up((size_t)N * 4) : nnp_image_bytes(K, N);
+}
+
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N) {
-  if (nnp_ok(M, K, N)) return align_up(nnp_image_bytes(K, N));
+  if (nnp_ok(M, K, N)) return align_up(nnq_bytes(K, N));
   const int s = gemm_nn_splits(M, K, N);
   return s > 1 ? align_up((size_t)s * M * N * 4) : 0;
 }
@@ -1186,6 +1373,14 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
     a.n_blocks = N / (w8 ? 256 : 128);
     a.splits = 1;
     const unsigned grid = (unsigned)((a.row_blocks + 7) / 8 * 8 * a.n_blocks);
+    if (nnh_enabled()) {  // fp16 two-term split: three MFMAs per product
+      int* ecol = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align_up(nnh_image_bytes(K, N, w8 ? 8 : 4)));
+      hipError_t e = nnh_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, ecol, st);
+      if (e != hipSuccess) return e;
+      if (w8) hipLaunchKernelGGL((k_gemm_nnh<8>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+      else hipLaunchKernelGGL((k_gemm_nnh<4>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+      return hipGetLastError();
+    }
     hipError_t e = nnx_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, st);
     if (e != hipSuccess) return e;
     if (w8) hipLaunchKernelGGL((k_gemm_nnp<8>), dim3(grid), dim3(512), 0, st, a, img);

@@ -185,13 +185,15 @@ def test_gemm_tn_large_shape_deterministic(pkg, cuda):
     assert torch.equal(out, out2) and torch.equal(cs, cs2) and torch.equal(vo, vo2)
 
 
-@pytest.mark.parametrize("family", ["split", "fp32"])
-def test_both_gemm_families(cuda, family):
+@pytest.mark.parametrize("family,f16", [("split", "1"), ("split", "0"), ("fp32", "1")])
+def test_both_gemm_families(cuda, family, f16):
     """Projection (x W^T + scores, + bias), dx and weight-gradient GEMMs at config-2 rows, and
-    the config-5 NN shapes, in a fresh process per family: both within 2e-6 of fp64 (tighter
-    than the suite's 1e-5), bitwise repeatable, the two B layouts of the NN GEMM identical."""
+    the config-5 NN shapes, in a fresh process per family (split: the large-M NN products on the
+    fp16 two-term kernel, or with PPGAT_GEMM_F16=0 on the bf16 x6 one; fp32 MFMA): all within
+    2e-6 of fp64 (tighter than the suite's 1e-5), bitwise repeatable, the two B layouts of the
+    NN GEMM identical."""
     root = Path(__file__).resolve().parents[1]
-    env = dict(os.environ, PPGAT_GEMM=family)
+    env = dict(os.environ, PPGAT_GEMM=family, PPGAT_GEMM_F16=f16)
     res = {}
     for extra in ([], ["--cfg5"]):
         out = subprocess.run([sys.executable, str(root / "tools" / "gemm_split_check.py"), "--iters", "3"] + extra,

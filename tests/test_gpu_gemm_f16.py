@@ -1,0 +1,98 @@
+"""The fp16 two-term NN GEMM (k_gemm_nnh: per-row scales set online, per-column scales on the
+pre-split B) against fp64, on data built to stress the scaling: rows spanning 24 decades, zero
+rows, rows that are zero or tiny in their first chunks and large later (the rescale path), rows
+with one huge late element, columns of B spanning 16 decades.  The bound per row is relative to
+(|x_i| |B|), the scale of fp32 GEMM's own error: <= 4e-6 (2^-21 per product plus fp32
+accumulation); on plain random data the max-abs / max-abs error is <= 2e-6.  Shapes are large
+enough for the pre-split path (>= 128 output tiles, else gemm_nn takes split-K)."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    return importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
+
+
+def _row_bound_err(y, X, B):
+    """max_i ||y_i - (X B)_i|| / ||(|X| |B|)_i|| in fp64 (rows with a zero bound must be exact zeros)."""
+    ref = X @ B
+    bnd = X.abs() @ B.abs()
+    y = y.double().cpu()
+    err = (y - ref).norm(dim=1)
+    nb = bnd.norm(dim=1)
+    nz = nb > 0
+    assert float(y[~nz].abs().max()) == 0.0 if (~nz).any() else True
+    return float((err[nz] / nb[nz]).max())
+
+
+@pytest.mark.parametrize("M,K,N,lay", [(20000, 1024, 256, 0), (5000, 256, 1024, 1), (20000, 896, 128, 1),
+                                       (2049, 64, 256, 0)])
+def test_nnh_random_vs_fp64(pkg, cuda, M, K, N, lay):
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + K + N)
+    X = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N, generator=g, dtype=torch.float64) * 0.05
+    Bd = (B if lay == 0 else B.t().contiguous()).float().to(cuda)
+    y = ops.gemm_nn(X.float().to(cuda), Bd, lay, N)
+    ref = X.float().double() @ B.float().double()
+    assert float((y.double().cpu() - ref).abs().max() / ref.abs().max()) <= 2e-6
+    assert _row_bound_err(y, X.float().double(), B.float().double()) <= 4e-6
+    assert torch.equal(y, ops.gemm_nn(X.float().to(cuda), Bd, lay, N))
+
+
+def test_nnh_dynamic_range_rows_and_columns(pkg, cuda):
+    ops = _ops()
+    rng = np.random.default_rng(11)
+    M, K, N = 16640, 512, 256
+    X = rng.standard_normal((M, K))
+    X *= 10.0 ** rng.uniform(-12, 12, (M, 1))            # rows over 24 decades
+    X[5] = 0.0                                            # a zero row
+    X[6, :64] = 0.0                                       # zero in the first two chunks
+    X[7, :32] *= 1e-6                                     # tiny first chunk: rescaled later
+    X[8, :] *= 1e-3; X[8, 400] = 1e4                      # one huge late element
+    X[9, :32] = 0.0; X[9, 32:64] *= 1e-5                  # set late, small, then rescaled again
+    X[10, 200:] = 0.0                                     # zero tail
+    X[11] = 0.0; X[11, 511] = 3.0                         # a single element in the last chunk
+    X[12] *= 1e-30; X[13] *= 1e25                         # near the ends of fp32's range
+    B = rng.standard_normal((K, N)) * 10.0 ** rng.uniform(-8, 8, (1, N))
+    B[:, 3] = 0.0                                         # a zero column
+    Xf, Bf = torch.from_numpy(X).float(), torch.from_numpy(B).float()
+    y = ops.gemm_nn(Xf.to(cuda), Bf.to(cuda), 0, N)
+    assert torch.isfinite(y).all()
+    assert _row_bound_err(y, Xf.double(), Bf.double()) <= 4e-6
+    # per column too: the error of column j relative to (|X| |B|)_{:, j}
+    ref = Xf.double() @ Bf.double()
+    bnd = Xf.double().abs() @ Bf.double().abs()
+    cerr = ((y.double().cpu() - ref).norm(dim=0) / bnd.norm(dim=0).clamp_min(1e-300))
+    assert float(cerr.max()) <= 4e-6
+    assert float(y[:, 3].abs().max()) == 0.0 and float(y[5].abs().max()) == 0.0
+
+
+def test_nnh_bias_alpha_and_ragged_rows(pkg, cuda):
+    ops = _ops()
+    g = torch.Generator().manual_seed(3)
+    M, K, N = 20003, 128, 128
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    y = ops.gemm_nn(X.to(cuda), W.to(cuda), 1, N, alpha=0.25, bias=b.to(cuda))
+    ref = 0.25 * X.double() @ W.double().t() + b.double()
+    assert float((y.double().cpu() - ref).abs().max() / ref.abs().max()) <= 2e-6
+
+
+def test_large_m_products_run_on_nnh(pkg, cuda):
+    """The config-5 shapes dispatch to the fp16 kernel (and its B pre-split), seen by torch.profiler."""
+    ops = _ops()
+    X = torch.randn(20000, 1024, device=cuda)
+    B = torch.randn(1024, 256, device=cuda)
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        ops.gemm_nn(X, B, 0, 256)
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events()}
+    assert any("k_gemm_nnh" in n for n in names), sorted(names)
+    assert any("k_nnh_presplit" in n for n in names)
