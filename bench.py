@@ -358,8 +358,8 @@ def main():
     # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
     xform_k = C if (H > 1 and H * C > C and pkg.hip_ops.xgat_supported(C, H, C)) else 0
     kern = {k: _lib.profile_read(k) for k in ("scores", "fwd", "bwd_pro", "bwd_src", "bwd_epi", "bwd_red",
-                                               "proj", "gemm_tn", "adam")}
-    fused_ms = sum(ms for k, (ms, _) in kern.items() if k not in ("proj", "gemm_tn", "adam"))
+                                               "proj", "proj_bwd", "gemm_tn", "adam")}
+    fused_ms = sum(ms for k, (ms, _) in kern.items() if k not in ("proj", "proj_bwd", "gemm_tn", "adam"))
     value = E * args.layers * K / el  # the whole job: every edge of the global graph, once per layer
     dom = max(("fwd", "bwd_src", "bwd_epi"), key=lambda k: kern[k][0])
     dom_ms, dom_n = kern[dom]

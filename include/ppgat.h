@@ -271,6 +271,19 @@ int ppgat_project(const float* x0, int64_t ldx0, const float* x1, int64_t ldx1, 
 int ppgat_project_bwd_input(const float* D, int64_t ldd, int64_t n, int k, const float* w, int64_t ldw, int out_cols,
                             const float* att_src, const float* att_dst, const float* S, int64_t lds, float* dx,
                             int64_t lddx, void* stream);
+/* The heads = 1 layer's input gradient AND its weight-gradient products in one pass over D and
+ * x (replaces, with the two calls above: the autograd of GATConv.lin / SimpleGATLayer.lin,
+ * train_gat_pyg.py:77, train_gat_custom.py:77, for the x rows and the weight):
+ *   dx = D W + ds_src (x) (att_src W) + ds_dst (x) (att_dst W)    (dx nullable: skipped)
+ *   G  = D^T x [k, k],   GV = [ds_src^T x ; ds_dst^T x] [2, k]     (for ppgat_weight_grads)
+ * x rows [0, split) from x0, [split, n) from x1 (x1 nullable).  Supported when k == 128 and
+ * the split-bf16 GEMM family is on (ppgat_project_bwd_fused_supported); deterministic. */
+int ppgat_project_bwd_fused_supported(int k);
+int ppgat_project_bwd_fused_workspace_bytes(int64_t n, size_t* bytes);
+int ppgat_project_bwd_fused(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0,
+                            const float* x1, int64_t ldx1, int64_t split, int64_t n, int k, const float* w,
+                            int64_t ldw, const float* att_src, const float* att_dst, float* dx, int64_t lddx,
+                            float* G, float* GV, void* workspace, size_t workspace_bytes, void* stream);
 /* Weight and attention-vector gradients from G = dh_msg^T x [H*C, K] and
  * GV = [ds_src^T x ; ds_dst^T x] [2H, K] (ppgat_gemm_tn with V):
  *   dW = G + att_src (x) GV[:H] + att_dst (x) GV[H:],  datt_src[h] = W_h GV[h],  datt_dst[h] = W_h GV[H + h]. */
@@ -562,7 +575,8 @@ int ppgat_check_index_range(const void* idx, int elem_bytes, int64_t n, int64_t 
 #define PPGAT_K_ADAM 11
 #define PPGAT_K_SAMPLE 12
 #define PPGAT_K_INFONCE 13
-#define PPGAT_K_COUNT 14
+#define PPGAT_K_PROJ_BWD 14
+#define PPGAT_K_COUNT 15
 int ppgat_profile_enable(int on);
 int ppgat_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of kernel k. */

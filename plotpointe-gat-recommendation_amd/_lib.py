@@ -72,6 +72,10 @@ SIGNATURES = {
                               c_vp, c_i64, c_vp, c_vp, c_vp]),
     "ppgat_project_bwd_input": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp,
                                         c_i64, c_vp]),
+    "ppgat_project_bwd_fused_supported": (c_int, [c_int]),
+    "ppgat_project_bwd_fused_workspace_bytes": (c_int, [c_i64, ctypes.POINTER(c_sz)]),
+    "ppgat_project_bwd_fused": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_vp,
+                                        c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_adam_max_tensors": (c_int, []),
     "ppgat_adam_step": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,
@@ -132,7 +136,7 @@ SIGNATURES = {
 
 KERNELS = {"csr": 0, "scores": 1, "fwd": 2, "bwd_pro": 3, "bwd_src": 4, "bwd_epi": 5, "bwd_red": 6, "sched": 7,
            "gemm_tn": 8, "fusion": 9, "proj": 10, "adam": 11,
-           "sample": 12, "infonce": 13}
+           "sample": 12, "infonce": 13, "proj_bwd": 14}
 MODE_PYG, MODE_CUSTOM = 0, 1
 
 _lib = None

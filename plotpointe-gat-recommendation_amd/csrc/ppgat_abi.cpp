@@ -582,6 +582,37 @@ int ppgat_project_bwd_input(const float* D, int64_t ldd, int64_t n, int k, const
   return PPGAT_OK;
 }
 
+int ppgat_project_bwd_fused_supported(int k) { return ppgat::dxw_ok(k, k) ? 1 : 0; }
+
+int ppgat_project_bwd_fused_workspace_bytes(int64_t n, size_t* bytes) {
+  if (n < 0 || !bytes) return fail(PPGAT_ERR_INVALID, "project_bwd_fused_workspace_bytes: bad arguments");
+  *bytes = ppgat::dxw_workspace_bytes(n);
+  return PPGAT_OK;
+}
+
+int ppgat_project_bwd_fused(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0,
+                            const float* x1, int64_t ldx1, int64_t split, int64_t n, int k, const float* w,
+                            int64_t ldw, const float* att_src, const float* att_dst, float* dx, int64_t lddx,
+                            float* G, float* GV, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!ppgat::dxw_ok(k, k)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_fused: needs k == 128 and the split GEMMs");
+  if (n < 0 || split < 0 || split > n) return fail(PPGAT_ERR_INVALID, "project_bwd_fused: bad sizes");
+  if (ldd < k || (ldd % 4) || ldx0 < k || (ldx0 % 4) || (x1 && (ldx1 < k || (ldx1 % 4))) || ldw < k ||
+      (dx && (lddx < k || (lddx % 4))) || lds < 2 || (lds % 2))
+    return fail(PPGAT_ERR_INVALID, "project_bwd_fused: bad leading dimension (>= k and % 4; lds >= 2 and even)");
+  if (!G || !GV || (n > 0 && (!D || !S || !x0 || !w || !att_src || !att_dst)))
+    return fail(PPGAT_ERR_INVALID, "project_bwd_fused: null pointer");
+  if (!al16(D) || !al16(x0) || (x1 && !al16(x1)) || (dx && !al16(dx)) || (reinterpret_cast<uintptr_t>(S) % 8))
+    return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_fused: D/x/dx rows 16-byte, S rows 8-byte aligned");
+  if (!workspace || workspace_bytes < ppgat::dxw_workspace_bytes(n))
+    return fail(PPGAT_ERR_INVALID, "project_bwd_fused: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ_BWD, st);
+  hipError_t e = ppgat::dxw(D, ldd, S, lds, x0, ldx0, x1, ldx1, x1 ? split : n, n, w, ldw, att_src, att_dst, dx, lddx,
+                            G, GV, workspace, st);
+  if (e != hipSuccess) return hip_fail(e, "project_bwd_fused");
+  return PPGAT_OK;
+}
+
 int ppgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src, const float* att_dst,
                        int heads, int channels, int in_channels, float* dW, float* datt_src, float* datt_dst,
                        void* stream) {

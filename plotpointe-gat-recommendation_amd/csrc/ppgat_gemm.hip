@@ -1352,6 +1352,281 @@ __global__ void __launch_bounds__(64 * WV, 1) k_tnx(TnArg a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The heads = 1 layer backward's two GEMMs in ONE pass over D and x (split bf16, §4.3):
+//   dx = D W + ds_src (x) A_src + ds_dst (x) A_dst     (k_projx<1>'s product, A_v = att_v W)
+//   G  = D^T x,   GV = S^T x  (S = [ds_src | ds_dst])   (k_tnx's products)
+// D [n, 128] is read from HBM once instead of twice (k_projx<1> + k_tnx), x once.
+//
+// One workgroup per CU, 8 waves, a contiguous row range per workgroup in 32-row steps; step
+// st + 1's rows are in flight in registers while step st computes.  The staging threads split
+// every D and x element ONCE into its three bf16 terms and store them as row-major images
+// [32 rows][128] (256-B rows, 16-B chunk ch of row r at chunk ch ^ sw(r), sw(r) = (r & 3) << 2
+// | (r >> 2) & 3), so no wave splits an operand itself:
+//  * dx (16x16x32, transposed product as in k_projx): wave w owns output columns 16 w .. +15;
+//    its split W' fragments (A operand) live in 48 registers for the whole kernel; the B
+//    operand is D[row jl][32 kq + 8 s .. +7], one ds_read_b128 per term -- with the swizzle the
+//    kq pairs met by each 16-lane group of a ds_read_b128 sit on complementary bank slots.
+//  * G (32x32x16): wave w owns the 32 x 64 block (channels 32 (w & 3), columns 64 (w >> 2));
+//    both operands are COLUMNS of the images (rows k = 8 h + j of column r), read with the
+//    transposing ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group), conflict-free.
+//  * GV: each staging thread accumulates S^T x over its own rows and 4 columns in fp32.
+// Partials per workgroup (G [128][128] from the accumulators, GV over the 16 row lanes in
+// order) go through the ordered split reduction k_tn_reduce -- deterministic.
+// ---------------------------------------------------------------------------
+constexpr int kDxwWaves = 8;
+constexpr int kDxwRows = 32;                        // rows per step
+constexpr int kDxwImg = kDxwRows * kPT * 2;         // bytes per bf16 term image (8 KB)
+constexpr int kDxwBuf = 6 * kDxwImg;                // D and x, three terms each (48 KB)
+constexpr size_t kDxwLds = 2 * kDxwBuf + (2 * kDxwRows * 2 + 2 * kPT) * sizeof(float);
+
+struct DxwArg {
+  const float* D;   // [n, 128] at ldd
+  int64_t ldd;
+  const float* S;   // [n, 2] at lds: ds_src, ds_dst
+  int64_t lds;
+  const float* x0;  // rows [0, split)
+  int64_t ldx0;
+  const float* x1;  // rows [split, n) (row - split)
+  int64_t ldx1;
+  int64_t split;
+  int64_t n;
+  const float* W;   // [128 (channels), 128] at ldw: dx = D W
+  int64_t ldw;
+  const float* att_src;
+  const float* att_dst;
+  float* dx;        // nullable: [n, 128] at lddx
+  int64_t lddx;
+  int64_t rows_per_wg;
+  float* part;      // [gridDim.x][128][128]
+  float* vpart;     // [gridDim.x][2][128]
+};
+
+struct DxwRegs {
+  float4 d[2];
+  float4 x[2];
+  float2 s[2];
+};
+
+// byte offset of 16-B chunk ch (0..15) of image row r
+__device__ __forceinline__ int dxw_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+// 4 fp32 -> three bf16x4 terms (split3's arithmetic)
+__device__ __forceinline__ void split3_4(const float4& v, uint2& h, uint2& m, uint2& l) {
+  const float e[4] = {v.x, v.y, v.z, v.w};
+  uint32_t hh[2], mm[2], ll[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    hh[i] = split::pk_bf16(e[2 * i], e[2 * i + 1]);
+    const float r0 = e[2 * i] - split::bf_lo(hh[i]), r1 = e[2 * i + 1] - split::bf_hi(hh[i]);
+    mm[i] = split::pk_bf16(r0, r1);
+    ll[i] = split::pk_bf16(r0 - split::bf_lo(mm[i]), r1 - split::bf_hi(mm[i]));
+  }
+  h = make_uint2(hh[0], hh[1]);
+  m = make_uint2(mm[0], mm[1]);
+  l = make_uint2(ll[0], ll[1]);
+}
+
+using s16x4 = __attribute__((ext_vector_type(4))) short;
+__device__ __forceinline__ uint2 ld_tr16(const unsigned char* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dxw_lds[];
+  float* const sS = reinterpret_cast<float*>(dxw_lds + 2 * kDxwBuf);  // [2][32][2]
+  float* const sA = sS + 2 * kDxwRows * 2;                            // [2][128]: A_src, A_dst
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int jl = lane & 15, kq = lane >> 4;  // dx lane roles
+  const int r = lane & 31, hf = lane >> 5;   // G lane roles
+  const int64_t n = a.n, split = a.split;
+  const int64_t rbeg = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t rend = min(n, rbeg + a.rows_per_wg);
+  const int steps = rend > rbeg ? (int)((rend - rbeg + kDxwRows - 1) / kDxwRows) : 0;
+  if (steps == 0) return;  // (no such workgroup: the grid gives every one rows)
+
+  // ---- staging: thread t moves float4 units t and t + 512 of the step's D and x rows (row
+  // lr = t / 32 and lr + 16, columns 4 (t % 32) .. +3).  Bases and strides in scalar
+  // registers; loads unconditional (rows clamped into the workgroup's range, zeroed when
+  // put), so two steps never wait on each other's counts ----
+  gfloat* const Dg = sgpr(a.D);
+  gfloat* const X0 = sgpr(a.x0);
+  gfloat* const X1 = sgpr(a.x1);
+  gfloat* const Sg = sgpr(a.S);
+  const int64_t ldd = sgpr(a.ldd), ldx0 = sgpr(a.ldx0), ldx1 = sgpr(a.ldx1), lds = sgpr(a.lds);
+  const int sc = (tid & 31) * 4, slr = tid >> 5;  // staging column, first staging row
+  auto load = [&](int64_t row0, DxwRegs& R) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int64_t row = min(row0 + slr + 16 * p, rend - 1);
+      R.d[p] = ld4(Dg + row * ldd + sc);
+      gfloat* xs = row < split ? X0 + row * ldx0 : X1 + (row - split) * ldx1;
+      R.x[p] = ld4(xs + sc);
+      using v2 = __attribute__((ext_vector_type(2))) float;
+      const v2 v = *(__attribute__((address_space(1))) const v2*)(Sg + row * lds);
+      R.s[p] = make_float2(v.x, v.y);
+    }
+  };
+  float gv[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // S^T x over this thread's rows
+  auto put = [&](int b, int64_t row0, const DxwRegs& R) {
+    unsigned char* img = dxw_lds + b * kDxwBuf;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lr = slr + 16 * p;
+      const bool ok = row0 + lr < rend;
+      const float4 d = ok ? R.d[p] : z4, x = ok ? R.x[p] : z4;
+      const float2 s = ok ? R.s[p] : make_float2(0.f, 0.f);
+      const int off = dxw_off(lr, sc >> 3) + 8 * ((sc >> 2) & 1);
+      uint2 h, m, l;
+      split3_4(d, h, m, l);
+      *reinterpret_cast<uint2*>(img + off) = h;
+      *reinterpret_cast<uint2*>(img + kDxwImg + off) = m;
+      *reinterpret_cast<uint2*>(img + 2 * kDxwImg + off) = l;
+      split3_4(x, h, m, l);
+      *reinterpret_cast<uint2*>(img + 3 * kDxwImg + off) = h;
+      *reinterpret_cast<uint2*>(img + 4 * kDxwImg + off) = m;
+      *reinterpret_cast<uint2*>(img + 5 * kDxwImg + off) = l;
+      gv[0][0] = fmaf(s.x, x.x, gv[0][0]); gv[0][1] = fmaf(s.x, x.y, gv[0][1]);
+      gv[0][2] = fmaf(s.x, x.z, gv[0][2]); gv[0][3] = fmaf(s.x, x.w, gv[0][3]);
+      gv[1][0] = fmaf(s.y, x.x, gv[1][0]); gv[1][1] = fmaf(s.y, x.y, gv[1][1]);
+      gv[1][2] = fmaf(s.y, x.z, gv[1][2]); gv[1][3] = fmaf(s.y, x.w, gv[1][3]);
+      if (sc == 0) *reinterpret_cast<float2*>(sS + (b * kDxwRows + lr) * 2) = s;
+    }
+  };
+
+  DxwRegs R0;
+  load(rbeg, R0);
+
+  // ---- W' fragments of this wave's 16 output columns, split once (registers): lane (jl, kq),
+  // k step s covers channels 32 kq + 8 s .. +7.  The lane's 32 channels also give its part of
+  // A_v[col] = sum_k att_v[k] W[k][col], summed over the four kq lanes (fixed order) ----
+  const bool want_dx = a.dx != nullptr;
+  u32x4 wh[4], wm[4], wl[4];
+  {
+    const int col = 16 * w + jl;
+    float ps = 0.f, pd = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c0 = 32 * kq + 8 * s;
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = a.W[(int64_t)(c0 + j) * a.ldw + col];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ps = fmaf(a.att_src[c0 + j], t[j], ps);
+        pd = fmaf(a.att_dst[c0 + j], t[j], pd);
+      }
+      split3(make_float4(t[0], t[1], t[2], t[3]), make_float4(t[4], t[5], t[6], t[7]), wh[s], wm[s], wl[s]);
+    }
+    ps += __shfl_xor(ps, 16);
+    pd += __shfl_xor(pd, 16);
+    ps += __shfl_xor(ps, 32);
+    pd += __shfl_xor(pd, 32);
+    if (kq == 0) {
+      sA[col] = ps;
+      sA[kPT + col] = pd;
+    }
+  }
+  put(0, rbeg, R0);
+  __syncthreads();
+
+  f32x16 accg[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) accg[i][q] = 0.f;
+  const int mb = w & 3, nb0 = 2 * (w >> 2);
+  // transposed-read lane address: lane 4 q + p of its 16-lane group g reads row q of the block,
+  // columns 4 p .. +3 of the group's 16 (16 (g & 1) within the 32-column operand block)
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+
+  auto compute = [&](int b, int64_t row0) {
+    const unsigned char* img = dxw_lds + b * kDxwBuf;
+    // ---- dx ----
+    if (want_dx) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int lr = 16 * rb + jl;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int off = dxw_off(lr, 4 * kq + s);
+          const u32x4 bh = *reinterpret_cast<const u32x4*>(img + off);
+          const u32x4 bm = *reinterpret_cast<const u32x4*>(img + kDxwImg + off);
+          const u32x4 bl = *reinterpret_cast<const u32x4*>(img + 2 * kDxwImg + off);
+          acc = mfma_x6(wh[s], wm[s], wl[s], bh, bm, bl, acc);
+        }
+        const int64_t row = row0 + lr;
+        const float2 dv = *reinterpret_cast<const float2*>(sS + (b * kDxwRows + lr) * 2);
+        const int c0 = 16 * w + 4 * kq;
+        const float4 va = *reinterpret_cast<const float4*>(sA + c0);
+        const float4 vb = *reinterpret_cast<const float4*>(sA + kPT + c0);
+        const float4 o = make_float4(fmaf(dv.y, vb.x, fmaf(dv.x, va.x, acc[0])), fmaf(dv.y, vb.y, fmaf(dv.x, va.y, acc[1])),
+                                     fmaf(dv.y, vb.z, fmaf(dv.x, va.z, acc[2])), fmaf(dv.y, vb.w, fmaf(dv.x, va.w, acc[3])));
+        if (row < rend) st4(a.dx + row * a.lddx + c0, o);
+      }
+    }
+    // ---- G = D^T x: columns of both images through the transposing reads ----
+    auto frag = [&](const unsigned char* im, int k0, int col0, u32x4 (&f)[3]) {
+      // rows k0 + 4 t + tq (t = 0, 1), columns col0 + 16 (tg & 1) + 4 tp .. +3
+      const int c = col0 + 16 * (tg & 1) + 4 * tp;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int off = dxw_off(k0 + 4 * t + tq, c >> 3) + 8 * ((c >> 2) & 1);
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          const uint2 v = ld_tr16(im + e * kDxwImg + off);
+          f[e][2 * t] = v.x;
+          f[e][2 * t + 1] = v.y;
+        }
+      }
+    };
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int k0 = 16 * ks + 8 * (tg >> 1);
+      u32x4 fa[3];
+      frag(img, k0, 32 * mb, fa);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        u32x4 fb[3];
+        frag(img + 3 * kDxwImg, k0, 32 * (nb0 + i), fb);
+        accg[i] = mfma32_x6(fa, fb, accg[i]);
+      }
+    }
+  };
+
+  // one register stage: step st + 1's loads are in flight while step st computes
+  for (int st = 0; st < steps; ++st) {
+    const int b = st & 1;
+    load(rbeg + (int64_t)(st + 1) * kDxwRows, R0);
+    compute(b, rbeg + (int64_t)st * kDxwRows);
+    if (st + 1 < steps) put(b ^ 1, rbeg + (int64_t)(st + 1) * kDxwRows, R0);
+    __syncthreads();
+  }
+
+  // ---- partials: G straight from the accumulators, GV through LDS in row-lane order ----
+  float* P = a.part + (int64_t)blockIdx.x * kPT * kPT;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) P[(32 * mb + acc_row(q, hf)) * kPT + 32 * (nb0 + i) + r] = accg[i][q];
+  float* sG = reinterpret_cast<float*>(dxw_lds);  // [16][2][128] (every wave is past the last barrier)
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+    st4(sG + (slr * 2 + v) * kPT + sc, make_float4(gv[v][0], gv[v][1], gv[v][2], gv[v][3]));
+  __syncthreads();
+  if (tid < 2 * kPT) {
+    const int v = tid >> 7, c = tid & 127;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += sG[(q * 2 + v) * kPT + c];
+    a.vpart[((int64_t)blockIdx.x * 2 + v) * kPT + c] = s;
+  }
+}
+
 }  // namespace
 
 // ---- host launchers ----
@@ -1519,6 +1794,56 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
   ra.part = a.part; ra.vpart = a.vpart; ra.cpart = a.cpart; ra.splits = nb; ra.M = M; ra.K = K; ra.nv = nv;
   ra.out = out; ra.vout = vout; ra.colsum = colsum;
   const int64_t elems = kPT * kPT + 2 * kPT + (colsum ? kPT : 0);
+  hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((elems + 63) / 64)), dim3(1024), 0, st, ra);
+  return hipGetLastError();
+}
+
+// ---- fused dx + G + GV (k_dxw) ----
+static int64_t dxw_blocks(int64_t n) {
+  int64_t nb = (n + kDxwRows - 1) / kDxwRows;
+  if (nb > 256) nb = 256;  // one workgroup per CU
+  return nb < 1 ? 1 : nb;
+}
+static int64_t dxw_rows_per_wg(int64_t n) {
+  const int64_t nb = dxw_blocks(n);
+  return (n + nb - 1) / nb;
+}
+
+bool dxw_ok(int hc, int k) { return gemm_split_enabled() && hc == kPT && k == kPT; }
+
+size_t dxw_workspace_bytes(int64_t n) {
+  const int64_t nb = dxw_blocks(n);
+  return align_up((size_t)nb * kPT * kPT * 4) + align_up((size_t)nb * 2 * kPT * 4);
+}
+
+hipError_t dxw(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0, const float* x1,
+               int64_t ldx1, int64_t split, int64_t n, const float* W, int64_t ldw, const float* att_src,
+               const float* att_dst, float* dx, int64_t lddx, float* G, float* GV, void* ws, hipStream_t st) {
+  if (n <= 0) {
+    hipError_t e = hipMemsetAsync(G, 0, (size_t)kPT * kPT * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(GV, 0, (size_t)2 * kPT * 4, st);
+    return e;
+  }
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dxw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kDxwLds) == hipSuccess;
+  }();
+  (void)attr;
+  const int64_t rpw = dxw_rows_per_wg(n);
+  const int64_t nb = (n + rpw - 1) / rpw;  // every workgroup gets rows
+  char* p = static_cast<char*>(ws);
+  DxwArg a{};
+  a.D = D; a.ldd = ldd; a.S = S; a.lds = lds;
+  a.x0 = x0; a.ldx0 = ldx0; a.x1 = x1 ? x1 : x0; a.ldx1 = x1 ? ldx1 : ldx0; a.split = x1 ? split : n; a.n = n;
+  a.W = W; a.ldw = ldw; a.att_src = att_src; a.att_dst = att_dst; a.dx = dx; a.lddx = lddx;
+  a.rows_per_wg = rpw;
+  a.part = reinterpret_cast<float*>(p);
+  a.vpart = reinterpret_cast<float*>(p + align_up((size_t)dxw_blocks(n) * kPT * kPT * 4));
+  hipLaunchKernelGGL(k_dxw, dim3((unsigned)nb), dim3(64 * kDxwWaves), kDxwLds, st, a);
+  TnReduceArg ra{};
+  ra.part = a.part; ra.vpart = a.vpart; ra.cpart = nullptr; ra.splits = nb; ra.M = kPT; ra.K = kPT; ra.nv = 2;
+  ra.out = G; ra.vout = GV; ra.colsum = nullptr;
+  const int64_t elems = kPT * kPT + 2 * kPT;
   hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((elems + 63) / 64)), dim3(1024), 0, st, ra);
   return hipGetLastError();
 }

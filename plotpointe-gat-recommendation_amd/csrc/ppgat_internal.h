@@ -92,6 +92,11 @@ hipError_t tn128(const float* A, int64_t lda, const float* B, int64_t ldb, const
                  void* ws, hipStream_t st);
 hipError_t wgrad_assemble(const float* G, const float* GV, const float* W, const float* att_src, const float* att_dst,
                           int heads, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st);
+bool dxw_ok(int hc, int k);
+size_t dxw_workspace_bytes(int64_t n);
+hipError_t dxw(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0, const float* x1,
+               int64_t ldx1, int64_t split, int64_t n, const float* W, int64_t ldw, const float* att_src,
+               const float* att_dst, float* dx, int64_t lddx, float* G, float* GV, void* ws, hipStream_t st);
 int adam_max_tensors();
 hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st);
 // replicated-item merge (ppgat_dist.hip): phase 0 max, 1 pack, 2 finish

@@ -678,6 +678,28 @@ class GATLayer(torch.autograd.Function):
                 dbias = dbias + db_i
         need_dx = ctx.needs_input_grad[0] or (had_items and ctx.needs_input_grad[12])
         dx = None
+        if (heads == 1 and HC == K and bool(lib.ppgat_project_bwd_fused_supported(K))
+                and not (_async_wgrad_enabled() and _grad_free(ctx.params))):
+            # dx and D^T x, S^T x in one pass over D and x (ppgat_project_bwd_fused)
+            dx = torch.empty(N, K, dtype=torch.float32, device=dev) if need_dx else None
+            G = torch.empty(HC, K, dtype=torch.float32, device=dev)
+            GV = torch.empty(2, K, dtype=torch.float32, device=dev)
+            nbytes = ctypes.c_size_t(0)
+            _lib.check(lib.ppgat_project_bwd_fused_workspace_bytes(N, ctypes.byref(nbytes)), "project_bwd_fused_ws")
+            ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
+            x0, x1, sp = (x, xi, split) if seg else (x, None, N)
+            if seg and split == 0:  # no user rows: every row from the item segment
+                x0, x1, sp = xi, None, N
+            _lib.check(lib.ppgat_project_bwd_fused(D.data_ptr(), HC, S.data_ptr(), 2, x0.data_ptr(), K, _lib.ptr(x1),
+                                                   K, sp, N, K, W.data_ptr(), K, a_s.data_ptr(),
+                                                   a_d.data_ptr(), _lib.ptr(dx), K, G.data_ptr(), GV.data_ptr(),
+                                                   ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)),
+                       "project_bwd_fused")
+            dW, datt_src, datt_dst = weight_grads(G, GV, W, a_s, a_d, heads, C)
+            dx_u = dx[:split] if (dx is not None and had_items) else dx
+            dx_i = dx[split:] if (dx is not None and had_items) else None
+            return (dx_u, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                    None, None, None, None, None, None, None, dx_i, None)
         if need_dx:
             if heads == 1 and project_supported(HC, K):  # reduction over HC, K output columns
                 dx = torch.empty(N, K, dtype=torch.float32, device=dev)

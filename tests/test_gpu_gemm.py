@@ -3,6 +3,7 @@ restatements of the same ops (GATConv.lin + node scores, its input/weight gradie
 torch.optim.Adam).  Tolerance: max-abs error / max-abs reference <= 1e-5.  The default
 GEMM family is the split-bf16 matrix-core one (csrc/ppgat_split.h); test_both_gemm_families
 runs the config-2 and config-5 shapes once per family (PPGAT_GEMM is read once per process)."""
+import ctypes
 import json
 import os
 import subprocess
@@ -76,6 +77,50 @@ def test_project_bwd_input_vs_fp64(pkg, cuda, N):
                                                pkg._lib.stream_handle(cuda)), "project_bwd_input")
     ref = D @ W + S[:, :1] * (a_s @ W)[None] + S[:, 1:2] * (a_d @ W)[None]
     assert rel(dx, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("N,split,with_dx", [(1, 1, True), (31, 31, True), (33, 10, True), (8193, 0, True),
+                                             (20_000, 20_000, False), (255_404, 192_403, True)])
+def test_project_bwd_fused_vs_fp64(pkg, cuda, N, split, with_dx):
+    """ppgat_project_bwd_fused (one pass over D and x): dx, G = D^T x and GV = S^T x against fp64,
+    x in two row segments or one, tail steps, a dx-less call; bitwise reproducible."""
+    lib = pkg._lib.load()
+    if not lib.ppgat_project_bwd_fused_supported(128):
+        pytest.skip("fused dx/dW needs the split GEMM family")
+    g = torch.Generator().manual_seed(N + 7)
+    HC = K = 128
+    D = torch.randn(N, HC, generator=g, dtype=torch.float64)
+    S = torch.randn(N, 2, generator=g, dtype=torch.float64)
+    x = torch.randn(N, K, generator=g, dtype=torch.float64)
+    W = torch.randn(HC, K, generator=g, dtype=torch.float64) / 11
+    a_s = torch.randn(HC, generator=g, dtype=torch.float64)
+    a_d = torch.randn(HC, generator=g, dtype=torch.float64)
+    Dd, Sd, xd, Wd, asd, add = (t.float().to(cuda).contiguous() for t in (D, S, x, W, a_s, a_d))
+    x0, x1, sp = (xd[:split].contiguous(), xd[split:].contiguous(), split) if 0 < split < N else (xd, None, N)
+    nbytes = ctypes.c_size_t(0)
+    pkg._lib.check(lib.ppgat_project_bwd_fused_workspace_bytes(N, ctypes.byref(nbytes)), "ws")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=cuda)
+
+    def run():
+        dx = torch.full((N, K), float("nan"), device=cuda) if with_dx else None
+        G = torch.empty(HC, K, device=cuda)
+        GV = torch.empty(2, K, device=cuda)
+        pkg._lib.check(lib.ppgat_project_bwd_fused(Dd.data_ptr(), HC, Sd.data_ptr(), 2, x0.data_ptr(), K,
+                                                   x1.data_ptr() if x1 is not None else None, K, sp, N, K,
+                                                   Wd.data_ptr(), K, asd.data_ptr(), add.data_ptr(),
+                                                   dx.data_ptr() if dx is not None else None, K, G.data_ptr(),
+                                                   GV.data_ptr(), ws.data_ptr(), nbytes.value,
+                                                   pkg._lib.stream_handle(cuda)), "project_bwd_fused")
+        return dx, G, GV
+
+    dx, G, GV = run()
+    if with_dx:
+        ref = D @ W + S[:, :1] * (a_s @ W)[None] + S[:, 1:2] * (a_d @ W)[None]
+        assert rel(dx, ref) <= 1e-5
+    assert rel(G, D.t() @ x) <= 1e-5
+    assert rel(GV, S.t() @ x) <= 1e-5
+    dx2, G2, GV2 = run()
+    assert torch.equal(G, G2) and torch.equal(GV, GV2) and (dx is None or torch.equal(dx, dx2))
 
 
 def test_gemm_tn_segments(pkg, cuda):

@@ -51,11 +51,24 @@ def main():
     dx = torch.empty(N, 128, device=dev)
     st = pkg._lib.stream_handle(dev)
     res = {}
+    import ctypes
+    nb = ctypes.c_size_t(0)
+    pkg._lib.check(lib.ppgat_project_bwd_fused_workspace_bytes(N, ctypes.byref(nb)), "ws")
+    ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+    G = torch.empty(128, 128, device=dev)
+    GV = torch.empty(2, 128, device=dev)
+
+    def fused_dxw():  # dx + D^T x + S^T x in one pass (ppgat_project_bwd_fused)
+        pkg._lib.check(lib.ppgat_project_bwd_fused(D.data_ptr(), 128, S.data_ptr(), 2, x.data_ptr(), 128, None, 128, N,
+                                                   N, 128, W.data_ptr(), 128, a_s.data_ptr(), a_d.data_ptr(),
+                                                   dx.data_ptr(), 128, G.data_ptr(), GV.data_ptr(), ws.data_ptr(),
+                                                   nb.value, st), "fused")
     cases = {
         "proj_fwd_scores": lambda: ops.project(x, W, att_src=a_s, att_dst=a_d),
         "proj_dx": lambda: pkg._lib.check(lib.ppgat_project_bwd_input(D.data_ptr(), 128, N, 128, W.data_ptr(), 128, 128,
                                                                       a_s.data_ptr(), a_d.data_ptr(), S.data_ptr(), 2,
                                                                       dx.data_ptr(), 128, st), "dx"),
+        "fused_dxw": lambda: fused_dxw(),
         "nn_fwd": lambda: ops.gemm_nn(x, W, 1, 128),
         "nn_dx": lambda: ops.gemm_nn(D, W, 0, 128),
         "tn_dW_V": lambda: ops.gemm_tn(D, x, V=S),
