@@ -1543,67 +1543,111 @@ __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
   // columns 4 p .. +3 of the group's 16 (16 (g & 1) within the 32-column operand block)
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
 
-  auto compute = [&](int b, int64_t row0) {
-    const unsigned char* img = dxw_lds + b * kDxwBuf;
-    // ---- dx ----
-    if (want_dx) {
+  // LDS byte offsets of this lane's fragments (loop invariant): dx B operand per (rb, s), and
+  // the transposed reads of G per (ks, t) for the A block and per (ks, i, t) for the B blocks
+  int odx[8], ota[4], otb[8];
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const int lr = 16 * rb + jl;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < 8; ++g) odx[g] = dxw_off(16 * (g >> 2) + jl, 4 * kq + (g & 3));
+  {
+    const int ca = 32 * mb + 16 * (tg & 1) + 4 * tp;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int off = dxw_off(lr, 4 * kq + s);
-          const u32x4 bh = *reinterpret_cast<const u32x4*>(img + off);
-          const u32x4 bm = *reinterpret_cast<const u32x4*>(img + kDxwImg + off);
-          const u32x4 bl = *reinterpret_cast<const u32x4*>(img + 2 * kDxwImg + off);
-          acc = mfma_x6(wh[s], wm[s], wl[s], bh, bm, bl, acc);
-        }
-        const int64_t row = row0 + lr;
-        const float2 dv = *reinterpret_cast<const float2*>(sS + (b * kDxwRows + lr) * 2);
-        const int c0 = 16 * w + 4 * kq;
-        const float4 va = *reinterpret_cast<const float4*>(sA + c0);
-        const float4 vb = *reinterpret_cast<const float4*>(sA + kPT + c0);
-        const float4 o = make_float4(fmaf(dv.y, vb.x, fmaf(dv.x, va.x, acc[0])), fmaf(dv.y, vb.y, fmaf(dv.x, va.y, acc[1])),
-                                     fmaf(dv.y, vb.z, fmaf(dv.x, va.z, acc[2])), fmaf(dv.y, vb.w, fmaf(dv.x, va.w, acc[3])));
-        if (row < rend) st4(a.dx + row * a.lddx + c0, o);
+    for (int u = 0; u < 4; ++u) {  // u = 2 ks + t
+      const int row = 16 * (u >> 1) + 8 * (tg >> 1) + 4 * (u & 1) + tq;
+      ota[u] = dxw_off(row, ca >> 3) + 8 * ((ca >> 2) & 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int cb = 32 * (nb0 + i) + 16 * (tg & 1) + 4 * tp;
+        otb[2 * u + i] = 3 * kDxwImg + dxw_off(row, cb >> 3) + 8 * ((cb >> 2) & 1);
       }
     }
-    // ---- G = D^T x: columns of both images through the transposing reads ----
-    auto frag = [&](const unsigned char* im, int k0, int col0, u32x4 (&f)[3]) {
-      // rows k0 + 4 t + tq (t = 0, 1), columns col0 + 16 (tg & 1) + 4 tp .. +3
-      const int c = col0 + 16 * (tg & 1) + 4 * tp;
+  }
+
+  // One step's 12 MFMA groups in a fixed order -- dx (rb, s) for 8 groups, then G (ks, i) --
+  // each group's LDS reads issued one group ahead, during the previous group's MFMAs.
+  auto compute = [&](const int b, int64_t row0) {
+    const unsigned char* img = dxw_lds + b * kDxwBuf;
+    auto rd_dx = [&](int g, u32x4 (&f)[3]) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int off = dxw_off(k0 + 4 * t + tq, c >> 3) + 8 * ((c >> 2) & 1);
+      for (int e = 0; e < 3; ++e) f[e] = *reinterpret_cast<const u32x4*>(img + e * kDxwImg + odx[g]);
+    };
+    auto rd_tr = [&](const int (&o)[2], u32x4 (&f)[3]) {  // o[t]: rows 4 t + tq of the k step
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
-          const uint2 v = ld_tr16(im + e * kDxwImg + off);
+          const uint2 v = ld_tr16(img + e * kDxwImg + o[t]);
           f[e][2 * t] = v.x;
           f[e][2 * t + 1] = v.y;
         }
-      }
     };
+    auto rd_ga = [&](int ks, u32x4 (&f)[3]) {
+      const int o[2] = {ota[2 * ks], ota[2 * ks + 1]};
+      rd_tr(o, f);
+    };
+    auto rd_gb = [&](int ks, int i, u32x4 (&f)[3]) {
+      const int o[2] = {otb[4 * ks + i], otb[4 * ks + 2 + i]};
+      rd_tr(o, f);
+    };
+    u32x4 fb[2][3], fa[2][3];
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (want_dx) {
+      rd_dx(0, fb[0]);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int k0 = 16 * ks + 8 * (tg >> 1);
-      u32x4 fa[3];
-      frag(img, k0, 32 * mb, fa);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        u32x4 fb[3];
-        frag(img + 3 * kDxwImg, k0, 32 * (nb0 + i), fb);
-        accg[i] = mfma32_x6(fa, fb, accg[i]);
+      for (int g = 0; g < 8; ++g) {
+        if (g < 7) {
+          rd_dx(g + 1, fb[(g + 1) & 1]);
+        } else {
+          rd_ga(0, fa[0]);
+          rd_gb(0, 0, fb[0]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int s = g & 3;
+        acc = mfma_x6(wh[s], wm[s], wl[s], fb[g & 1][0], fb[g & 1][1], fb[g & 1][2], acc);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == 3) {  // epilogue of row block rb = g / 4
+          const int lr = 16 * (g >> 2) + jl;
+          const int64_t row = row0 + lr;
+          const float2 dv = *reinterpret_cast<const float2*>(sS + (b * kDxwRows + lr) * 2);
+          const int c0 = 16 * w + 4 * kq;
+          const float4 va = *reinterpret_cast<const float4*>(sA + c0);
+          const float4 vb = *reinterpret_cast<const float4*>(sA + kPT + c0);
+          const float4 o = make_float4(fmaf(dv.y, vb.x, fmaf(dv.x, va.x, acc[0])), fmaf(dv.y, vb.y, fmaf(dv.x, va.y, acc[1])),
+                                       fmaf(dv.y, vb.z, fmaf(dv.x, va.z, acc[2])), fmaf(dv.y, vb.w, fmaf(dv.x, va.w, acc[3])));
+          if (row < rend) st4(a.dx + row * a.lddx + c0, o);
+          acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
+    } else {
+      rd_ga(0, fa[0]);
+      rd_gb(0, 0, fb[0]);
     }
+    // ---- G = D^T x: groups (ks, i) = (0, 0), (0, 1), (1, 0), (1, 1) ----
+    rd_gb(0, 1, fb[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    accg[0] = mfma32_x6(fa[0], fb[0], accg[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    rd_ga(1, fa[1]);
+    rd_gb(1, 0, fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    accg[1] = mfma32_x6(fa[0], fb[1], accg[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    rd_gb(1, 1, fb[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    accg[0] = mfma32_x6(fa[1], fb[0], accg[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    accg[1] = mfma32_x6(fa[1], fb[1], accg[1]);
   };
 
-  // one register stage: step st + 1's loads are in flight while step st computes
-  for (int st = 0; st < steps; ++st) {
-    const int b = st & 1;
+  // one register stage, the loop unrolled by two so each half's LDS buffer is a constant
+  for (int st = 0; st < steps; st += 2) {
     load(rbeg + (int64_t)(st + 1) * kDxwRows, R0);
-    compute(b, rbeg + (int64_t)st * kDxwRows);
-    if (st + 1 < steps) put(b ^ 1, rbeg + (int64_t)(st + 1) * kDxwRows, R0);
+    compute(0, rbeg + (int64_t)st * kDxwRows);
+    if (st + 1 < steps) put(1, rbeg + (int64_t)(st + 1) * kDxwRows, R0);
+    __syncthreads();
+    if (st + 1 >= steps) break;
+    load(rbeg + (int64_t)(st + 2) * kDxwRows, R0);
+    compute(1, rbeg + (int64_t)(st + 1) * kDxwRows);
+    if (st + 2 < steps) put(0, rbeg + (int64_t)(st + 2) * kDxwRows, R0);
     __syncthreads();
   }
 
