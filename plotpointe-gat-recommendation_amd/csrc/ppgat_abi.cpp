@@ -519,7 +519,9 @@ int ppgat_gemm_tn_seg(const float* A, int64_t lda, const float* b0, int64_t ldb0
   if (split < 0 || split > n) return fail(PPGAT_ERR_INVALID, "gemm_tn: split outside [0, n]");
   if (lda < m || ldb0 < k || (b1 && ldb1 < k) || (nv > 0 && ldv < nv))
     return fail(PPGAT_ERR_INVALID, "gemm_tn: bad leading dimension");
-  if ((lda % 4) || (ldb0 % 4) || (b1 && (ldb1 % 4)) || !al16(A) || !al16(b0) || (b1 && !al16(b1)))
+  // the skinny kernel reads A by scalars: only B's rows need 16-byte alignment there
+  const bool skinny = m <= 16 && !colsum && nv == 0 && !(b1 && split < n) && (k % 4) == 0 && k <= 1024;
+  if ((!skinny && ((lda % 4) || !al16(A))) || (ldb0 % 4) || (b1 && (ldb1 % 4)) || !al16(b0) || (b1 && !al16(b1)))
     return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: A/B rows must be 16-byte aligned");
   if (!out || (n > 0 && (!A || !b0)) || (nv > 0 && (!V || !vout)))
     return fail(PPGAT_ERR_INVALID, "gemm_tn: null pointer");
@@ -527,7 +529,8 @@ int ppgat_gemm_tn_seg(const float* A, int64_t lda, const float* b0, int64_t ldb0
     return fail(PPGAT_ERR_INVALID, "gemm_tn: workspace too small");
   // the register-accumulator kernel pays a fixed per-wave ramp/epilogue: below ~1e5 rows the
   // LDS-staged split-N kernel is faster (item_proj's 63k rows: 30 vs 46 us)
-  const bool fast = ppgat::tn128_shape_ok(m, k, nv, V, ldv) && (n >= 100000 || (b1 && split < n));
+  // skinny A (m <= 16, plain A^T B): the VALU kernel of ppgat::gemm_tn, not a padded MFMA tile
+  const bool fast = !skinny && ppgat::tn128_shape_ok(m, k, nv, V, ldv) && (n >= 100000 || (b1 && split < n));
   if (!fast && b1 && split < n) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: segmented B needs m, k <= 128, nv <= 2");
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_GEMM_TN, st);

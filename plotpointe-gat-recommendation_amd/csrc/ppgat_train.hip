@@ -720,6 +720,58 @@ hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
   return hipGetLastError();
 }
 
+// ---- skinny A^T B (M <= 16): the multi-head layer's GV = S^T x (S = [ds_src | ds_dst], 2H
+// columns) -- a 128 x 128 MFMA tile would be 94 % padding there.  Thread (row lane, float4
+// column group of B): fp32 FMAs over the block's rows in order, the row lanes summed in lane
+// order, block partials through the ordered split reduction (deterministic). ----
+template <int MV>
+__global__ void __launch_bounds__(256) k_tn_skinny(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+                                                   int64_t ldb, int64_t N, int M, int K, int64_t rows_per_block,
+                                                   float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int T = K >> 2, P = 256 / T, t = threadIdx.x, cg = t % T, rl = t / T;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(N, r0 + rows_per_block);
+  float4 acc[MV];
+#pragma unroll
+  for (int m = 0; m < MV; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rl < P) {
+    for (int64_t r = r0 + rl; r < r1; r += P) {
+      const float4 bv = ld4(B + r * ldb + 4 * cg);
+#pragma unroll
+      for (int m = 0; m < MV; ++m) {
+        if (m < M) {
+          const float av = A[r * lda + m];
+          acc[m] = make_float4(fmaf(av, bv.x, acc[m].x), fmaf(av, bv.y, acc[m].y), fmaf(av, bv.z, acc[m].z),
+                               fmaf(av, bv.w, acc[m].w));
+        }
+      }
+    }
+  }
+  float* out = part + (int64_t)blockIdx.x * M * K;
+#pragma unroll
+  for (int m = 0; m < MV; ++m) {
+    if (m < M) {  // uniform
+      red[t] = acc[m];
+      __syncthreads();
+      if (t < T) {
+        float4 s = red[t];
+        for (int q = 1; q < P; ++q) s = add4(s, red[q * T + t]);
+        st4(out + (int64_t)m * K + 4 * t, s);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+static bool skinny_ok(int M, int K, const float* colsum, const float* V) {
+  return M <= 16 && K % 4 == 0 && K <= 1024 && colsum == nullptr && V == nullptr;
+}
+static int64_t skinny_blocks(int64_t N) {
+  int64_t b = (N + 511) / 512;
+  if (b > 2048) b = 2048;
+  return b < 1 ? 1 : b;
+}
+
 // ---- dW = A^T B ----
 static int64_t gemm_splits(int64_t N, int M, int K) {
   const int64_t tiles = (int64_t)((M + kTN - 1) / kTN) * ((K + kTN - 1) / kTN);
@@ -733,11 +785,32 @@ static int64_t gemm_splits(int64_t N, int M, int K) {
 
 size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv) {
   const int64_t s = gemm_splits(N, M, K);
-  return align_up((size_t)s * M * K * 4) + align_up((size_t)s * M * 4) + align_up((size_t)s * (nv > 0 ? nv : 1) * K * 4);
+  const size_t tiled = align_up((size_t)s * M * K * 4) + align_up((size_t)s * M * 4) +
+                       align_up((size_t)s * (nv > 0 ? nv : 1) * K * 4);
+  const size_t skinny = M <= 16 ? align_up((size_t)skinny_blocks(N) * M * K * 4) : 0;
+  return tiled > skinny ? tiled : skinny;
 }
 
 hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
                    float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st) {
+  if (skinny_ok(M, K, colsum, nv > 0 ? V : nullptr) && N > 0) {
+    int64_t blocks = skinny_blocks(N);
+    const int64_t rpb = (N + blocks - 1) / blocks;
+    blocks = (N + rpb - 1) / rpb;
+    float* part = static_cast<float*>(ws);
+    const int MV = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : M <= 8 ? 8 : 16;
+#define PPGAT_SKINNY(MV_) \
+  hipLaunchKernelGGL((k_tn_skinny<MV_>), dim3((unsigned)blocks), dim3(256), 0, st, A, lda, B, ldb, N, M, K, rpb, part)
+    if (MV == 1) PPGAT_SKINNY(1); else if (MV == 2) PPGAT_SKINNY(2); else if (MV == 4) PPGAT_SKINNY(4);
+    else if (MV == 8) PPGAT_SKINNY(8); else PPGAT_SKINNY(16);
+#undef PPGAT_SKINNY
+    SplitReduceArg ra{};
+    const int64_t elems = (int64_t)M * K;
+    ra.part[0] = part; ra.out[0] = out; ra.elems[0] = elems; ra.blocks[0] = (elems + 63) / 64;
+    for (int q = 1; q < 3; ++q) { ra.part[q] = part; ra.out[q] = out; ra.elems[q] = 0; ra.blocks[q] = ra.blocks[0]; }
+    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)ra.blocks[0]), dim3(1024), 0, st, ra, blocks);
+    return hipGetLastError();
+  }
   const int64_t s = gemm_splits(N, M, K);
   const int64_t rows = ((N + s - 1) / s + kNB - 1) / kNB * kNB;
   char* p = static_cast<char*>(ws);

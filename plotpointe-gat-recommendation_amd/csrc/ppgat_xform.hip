@@ -827,6 +827,243 @@ __global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ par
 }
 
 // ===========================================================================
+// TN GEMM on the fp16 matrix cores: two-term split with per-column power-of-two scales
+// ===========================================================================
+// part[split] = A[rows of split]^T B[rows of split] as in k_gemm_tn, but the reduction runs
+// over rows, so a row-wise online scale (k_gemm_nnh) cannot apply: each column of A and of B
+// gets ONE scale over all M rows -- the power of two that puts the column's largest |v| in
+// [2^9, 2^10) (ppgat_split.h scale_exp16) -- from a max pre-pass (k_colmax_bits: the max of
+// the IEEE bits of |v|, order-free, so deterministic).  Elements far below their column's max
+// keep an absolute error <= 2^-34 of that max; the rest carry 22 bits (2^-21 per product, as
+// k_gemm_nnh).  Workgroup tile 128 (A columns) x 256 (B columns), 8 waves (4 x 2), each wave
+// one 32-column A block against four 32-column B blocks (64 accumulators); the rows of a
+// 32-row chunk are split ONCE by the staging threads into swizzled row-major fp16 images (A:
+// [32][128], B: two [32][128] halves; hi and lo terms) and both operands -- columns over the
+// chunk's rows -- come back through the transposing ds_read_b64_tr_b16 (conflict-free, see
+// k_dxw).  The tiles of one row split run on one XCD, so the rows leave HBM once.
+constexpr int kThImg = kTR * 128 * 2;       // bytes per fp16 image [32][128]
+constexpr int kThBuf = 6 * kThImg;          // A hi/lo, B half 0 hi/lo, B half 1 hi/lo (48 KB)
+constexpr size_t kThLds = 2 * kThBuf + (2 * 128 + 2 * 256) * sizeof(float);
+
+// column maxima of |X| over rows [r0, r1) of a row block, merged into out[] as IEEE bits
+__global__ void __launch_bounds__(256) k_colmax_bits(const float* __restrict__ X, int64_t ldx, int64_t M, int C,
+                                                     int64_t rows_per_block, unsigned* __restrict__ out) {
+  __shared__ float4 red[256];
+  const int T = C >> 2, P = 256 / T, t = threadIdx.x, cg = t % T, rl = t / T;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float4 m = f4(0.f);
+  if (rl < P) {
+    for (int64_t r = r0 + rl; r < r1; r += P) {
+      const float4 v = ld4(X + r * ldx + 4 * cg);
+      m = make_float4(fmaxf(m.x, fabsf(v.x)), fmaxf(m.y, fabsf(v.y)), fmaxf(m.z, fabsf(v.z)), fmaxf(m.w, fabsf(v.w)));
+    }
+  }
+  red[t] = m;
+  __syncthreads();
+  if (t < T) {
+    for (int q = 1; q < P; ++q) {
+      const float4 v = red[q * T + t];
+      m = make_float4(fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w));
+    }
+    atomicMax(out + 4 * t, __float_as_uint(m.x));
+    atomicMax(out + 4 * t + 1, __float_as_uint(m.y));
+    atomicMax(out + 4 * t + 2, __float_as_uint(m.z));
+    atomicMax(out + 4 * t + 3, __float_as_uint(m.w));
+  }
+}
+
+struct TnhArg {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  int64_t M;
+  int Ma, Nb;
+  int tiles_a, tiles_b, splits;
+  int64_t rows_per_split;
+  const unsigned* amax;  // [Ma] column maxima (IEEE bits of |v|)
+  const unsigned* bmax;  // [Nb]
+  float* part;           // [splits, Ma, Nb]
+};
+
+__device__ __forceinline__ int th_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+using th_s16x4 = __attribute__((ext_vector_type(4))) short;
+__device__ __forceinline__ uint2 th_tr16(const unsigned char* p) {
+  const th_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) th_s16x4*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+// 4 values times their column scales -> two fp16x4 terms (split2h's arithmetic)
+__device__ __forceinline__ void split2h_4(const float4& v, const float4& s, uint2& h, uint2& l) {
+  const float e[4] = {v.x * s.x, v.y * s.y, v.z * s.z, v.w * s.w};
+  uint32_t hh[2], ll[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    hh[i] = split::pk_f16(e[2 * i], e[2 * i + 1]);
+    const split::f32x2e back = __builtin_convertvector(__builtin_bit_cast(split::f16x2, hh[i]), split::f32x2e);
+    ll[i] = split::pk_f16(e[2 * i] - back.x, e[2 * i + 1] - back.y);
+  }
+  h = make_uint2(hh[0], hh[1]);
+  l = make_uint2(ll[0], ll[1]);
+}
+
+__global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char th_lds[];
+  float* const sFa = reinterpret_cast<float*>(th_lds + 2 * kThBuf);  // [0,128): 2^e, [128,256): 2^-e
+  float* const sFb = sFa + 2 * 128;                                  // [0,256): 2^e, [256,512): 2^-e
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int wa = w & 3, wb = w >> 2;
+  const int T = a.tiles_a * a.tiles_b;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int tile = (int)(idx % T);
+  const int64_t split = (b & 7) + 8 * (idx / T);  // one split's tiles share an XCD (and its L2)
+  if (split >= a.splits) return;
+  const int ta = tile % a.tiles_a, tb = tile / a.tiles_a;
+  const int64_t r0 = split * a.rows_per_split;
+  const int64_t r1 = min(a.M, r0 + a.rows_per_split);
+  const int steps = r1 > r0 ? (int)((r1 - r0 + kTR - 1) / kTR) : 0;
+  if (tid < 128) {
+    const float m = __uint_as_float(a.amax[ta * 128 + tid]);
+    const int e = (m > 0.f && m <= 3.4e38f) ? split::scale_exp16(m) : 0;
+    sFa[tid] = ldexpf(1.f, e);
+    sFa[128 + tid] = ldexpf(1.f, -e);
+  }
+  if (tid < 256) {
+    const float m = __uint_as_float(a.bmax[tb * 256 + tid]);
+    const int e = (m > 0.f && m <= 3.4e38f) ? split::scale_exp16(m) : 0;
+    sFb[tid] = ldexpf(1.f, e);
+    sFb[256 + tid] = ldexpf(1.f, -e);
+  }
+  __syncthreads();
+
+  // ---- staging: thread t -> rows t / 32 and t / 32 + 16 of the chunk, columns 4 (t % 32) .. +3
+  // of the A tile and of both B halves ----
+  const int sc = (tid & 31) * 4, slr = tid >> 5;
+  const float4 sa = *reinterpret_cast<const float4*>(sFa + sc);
+  const float4 sb0 = *reinterpret_cast<const float4*>(sFb + sc);
+  const float4 sb1 = *reinterpret_cast<const float4*>(sFb + 128 + sc);
+  const float* const Ab = a.A + ta * 128 + sc;
+  const float* const Bb = a.B + tb * 256 + sc;
+  struct Stage {
+    float4 a[2], b0[2], b1[2];
+  };
+  auto load = [&](int64_t row0, Stage& S) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int64_t row = min(row0 + slr + 16 * p, r1 - 1);
+      S.a[p] = ld4(Ab + row * a.lda);
+      S.b0[p] = ld4(Bb + row * a.ldb);
+      S.b1[p] = ld4(Bb + row * a.ldb + 128);
+    }
+  };
+  auto put = [&](int buf, int64_t row0, const Stage& S) {
+    unsigned char* img = th_lds + buf * kThBuf;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lr = slr + 16 * p;
+      const bool ok = row0 + lr < r1;
+      const int off = th_off(lr, sc >> 3) + 8 * ((sc >> 2) & 1);
+      uint2 h, l;
+      split2h_4(ok ? S.a[p] : f4(0.f), sa, h, l);
+      *reinterpret_cast<uint2*>(img + off) = h;
+      *reinterpret_cast<uint2*>(img + kThImg + off) = l;
+      split2h_4(ok ? S.b0[p] : f4(0.f), sb0, h, l);
+      *reinterpret_cast<uint2*>(img + 2 * kThImg + off) = h;
+      *reinterpret_cast<uint2*>(img + 3 * kThImg + off) = l;
+      split2h_4(ok ? S.b1[p] : f4(0.f), sb1, h, l);
+      *reinterpret_cast<uint2*>(img + 4 * kThImg + off) = h;
+      *reinterpret_cast<uint2*>(img + 5 * kThImg + off) = l;
+    }
+  };
+
+  // transposed-read lane address (see k_dxw): lane 4 q + p of 16-lane group g reads row q of a
+  // 4-row block, columns 4 p .. +3 of the group's 16 (16 (g & 1) within a 32-column block)
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  int oa[4], ob[4][4];  // [2 ks + t] for A; [t'][2 ks + t] for B's four blocks (image-relative)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = 16 * (u >> 1) + 8 * (tg >> 1) + 4 * (u & 1) + tq;
+    const int ca = 32 * wa + 16 * (tg & 1) + 4 * tp;
+    oa[u] = th_off(row, ca >> 3) + 8 * ((ca >> 2) & 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int cb = 32 * t + 16 * (tg & 1) + 4 * tp;
+      ob[t][u] = th_off(row, cb >> 3) + 8 * ((cb >> 2) & 1);
+    }
+  }
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x16{};
+
+  auto compute = [&](const int buf) {
+    const unsigned char* img = th_lds + buf * kThBuf;
+    const unsigned char* bimg = img + (2 + 2 * wb) * kThImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      split::u32x4 fa[2], fb[4][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint2 v = th_tr16(img + e * kThImg + oa[2 * ks + t]);
+          fa[e][2 * t] = v.x;
+          fa[e][2 * t + 1] = v.y;
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint2 v = th_tr16(bimg + e * kThImg + ob[q][2 * ks + t]);
+            fb[q][e][2 * t] = v.x;
+            fb[q][e][2 * t + 1] = v.y;
+          }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = split::mfma32_h3(fa, fb[q], acc[q]);
+    }
+  };
+
+  // two register stages (S0 / S1): chunks c + 1 and c + 2 are in flight while chunk c computes
+  // (one stage left the kernel waiting on HBM latency: 48 KB in flight per CU)
+  Stage S0, S1;
+  if (steps > 0) {
+    load(r0, S0);
+    load(r0 + kTR, S1);
+    put(0, r0, S0);
+    __syncthreads();
+  }
+  for (int st = 0; st < steps; st += 2) {
+    load(r0 + (int64_t)(st + 2) * kTR, S0);
+    compute(0);
+    if (st + 1 < steps) put(1, r0 + (int64_t)(st + 1) * kTR, S1);
+    __syncthreads();
+    if (st + 1 >= steps) break;
+    load(r0 + (int64_t)(st + 3) * kTR, S1);
+    compute(1);
+    if (st + 2 < steps) put(0, r0 + (int64_t)(st + 2) * kTR, S0);
+    __syncthreads();
+  }
+  // ---- unscale (exact powers of two) and store this split's partial ----
+  float* P = a.part + (size_t)split * a.Ma * a.Nb;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int nl = 128 * wb + 32 * t + r;
+    const float fb = sFb[256 + nl];
+    const int col = tb * 256 + nl;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ml = 32 * wa + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      P[(size_t)(ta * 128 + ml) * a.Nb + col] = acc[t][q] * sFa[128 + ml] * fb;
+    }
+  }
+}
+
+// ===========================================================================
 // aggregate-then-transform layer pieces
 // ===========================================================================
 // A[v][h][k] = sum_c att_v[h][c] W[h C + c][k]  (v = 0: src, 1: dst) -> [2, H, K]
@@ -1442,13 +1679,76 @@ static int tn_splits(int64_t M, int T) {
 
 bool gemm_tn_big_shape_ok(int Ma, int Nb) { return Ma >= 128 && Ma % 128 == 0 && Nb >= 128 && Nb % 128 == 0; }
 
+// the fp16 two-term TN kernel (k_gemm_tnh): Nb % 256 == 0, with the fp16 family on
+static bool tnh_ok(int Ma, int Nb) { return gemm_split_enabled() && nnh_enabled() && Ma % 128 == 0 && Nb % 256 == 0; }
+static int tnh_splits(int64_t M, int T) {  // one workgroup per CU: splits * tiles <= 256, >= 128 rows per split
+  // two workgroup rounds per CU: the same time as one (3.96 vs 3.98 ms at the config-5 share,
+  // profiles/r03/v16_tnh_*), half the rows per fp32 accumulator chain: 3.3e-6 vs 5.3e-6
+  // max-abs/max-abs on 1.875M-row reductions (fp32 MFMA kernel: 3.5e-6).  PPGAT_TNH_WAVES
+  // overrides (experiments).
+  static const int waves = [] {
+    const char* e = getenv("PPGAT_TNH_WAVES");
+    const int v = e ? atoi(e) : 2;
+    return v >= 1 && v <= 16 ? v : 2;
+  }();
+  int s = 256 * waves / T;
+  if (s < 1) s = 1;
+  while (s > 1 && M / s < 4 * kTR) s /= 2;
+  return s;
+}
+
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb) {
+  if (tnh_ok(Ma, Nb)) {
+    const int T = (Ma / 128) * (Nb / 256);
+    return align_up((size_t)tnh_splits(M, T) * Ma * Nb * 4) + align_up((size_t)(Ma + Nb) * 4);
+  }
   const int T = (Ma / kTA) * (Nb / (Nb % 256 == 0 ? 256 : 128));
   return align_up((size_t)tn_splits(M, T) * Ma * Nb * 4);
 }
 
+static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st) {
+  // C columns in slices of <= 1024 (256 float4 lanes per row pass)
+  for (int c0 = 0; c0 < C; c0 += 1024) {
+    const int c = C - c0 < 1024 ? C - c0 : 1024;
+    int64_t blocks = (M + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    const int64_t rpb = (M + blocks - 1) / blocks;
+    blocks = (M + rpb - 1) / rpb;
+    hipLaunchKernelGGL(k_colmax_bits, dim3((unsigned)blocks), dim3(256), 0, st, X + c0, ldx, M, c, rpb, out + c0);
+  }
+  return hipGetLastError();
+}
+
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
                        void* ws, hipStream_t st) {
+  if (M <= 0) return hipMemsetAsync(out, 0, (size_t)Ma * Nb * 4, st);  // empty sum (no partials)
+  if (tnh_ok(Ma, Nb)) {
+    static const bool attr = [] {
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tnh), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)kThLds) == hipSuccess;
+    }();
+    (void)attr;
+    TnhArg a{};
+    a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.M = M; a.Ma = Ma; a.Nb = Nb;
+    a.tiles_a = Ma / 128;
+    a.tiles_b = Nb / 256;
+    const int T = a.tiles_a * a.tiles_b;
+    a.splits = tnh_splits(M, T);
+    a.rows_per_split = ((M + a.splits - 1) / a.splits + kTR - 1) / kTR * kTR;
+    a.part = static_cast<float*>(ws);
+    unsigned* mx = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + align_up((size_t)a.splits * Ma * Nb * 4));
+    a.amax = mx;
+    a.bmax = mx + Ma;
+    hipError_t e = hipMemsetAsync(mx, 0, (size_t)(Ma + Nb) * 4, st);
+    if (e == hipSuccess) e = colmax_bits(A, lda, M, Ma, mx, st);
+    if (e == hipSuccess) e = colmax_bits(B, ldb, M, Nb, mx + Ma, st);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)(8 * T * ((a.splits + 7) / 8));
+    hipLaunchKernelGGL(k_gemm_tnh, dim3(grid), dim3(512), kThLds, st, a);
+    const int64_t n4 = (int64_t)Ma * Nb / 4;
+    hipLaunchKernelGGL(k_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, n4, a.splits, out);
+    return hipGetLastError();
+  }
   const bool wide = Nb % 256 == 0;
   TnArg a{};
   a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.M = M; a.Ma = Ma; a.Nb = Nb;

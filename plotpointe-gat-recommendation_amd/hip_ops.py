@@ -498,6 +498,13 @@ _SIDE_STREAMS = {}
 _PENDING_JOINS = []
 
 
+def _fused_dxw_enabled() -> bool:
+    """dx and the weight-gradient products in one pass (ppgat_project_bwd_fused); PPGAT_FUSED_DXW=0
+    selects the two-kernel path (ppgat_project_bwd_input + ppgat_gemm_tn), e.g. to compare
+    against the side-stream weight gradients bit for bit."""
+    return os.environ.get("PPGAT_FUSED_DXW", "1") != "0"
+
+
 def _async_wgrad_enabled() -> bool:
     return os.environ.get("PPGAT_ASYNC_WGRAD", "0") == "1"
 
@@ -678,7 +685,7 @@ class GATLayer(torch.autograd.Function):
                 dbias = dbias + db_i
         need_dx = ctx.needs_input_grad[0] or (had_items and ctx.needs_input_grad[12])
         dx = None
-        if (heads == 1 and HC == K and bool(lib.ppgat_project_bwd_fused_supported(K))
+        if (heads == 1 and HC == K and bool(lib.ppgat_project_bwd_fused_supported(K)) and _fused_dxw_enabled()
                 and not (_async_wgrad_enabled() and _grad_free(ctx.params))):
             # dx and D^T x, S^T x in one pass over D and x (ppgat_project_bwd_fused)
             dx = torch.empty(N, K, dtype=torch.float32, device=dev) if need_dx else None

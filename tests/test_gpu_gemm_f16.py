@@ -96,3 +96,63 @@ def test_large_m_products_run_on_nnh(pkg, cuda):
     names = {e.name for e in prof.events()}
     assert any("k_gemm_nnh" in n for n in names), sorted(names)
     assert any("k_nnh_presplit" in n for n in names)
+
+
+# ---------------------------------------------------------------------------------------------
+# The fp16 two-term TN GEMM (k_gemm_tnh, ppgat_gemm_tn_big): per-column scales of A and B from
+# the column-max pre-pass.  Bound per output element relative to (|A|^T |B|), fp32 GEMM's own
+# error scale: <= 4e-6.
+# ---------------------------------------------------------------------------------------------
+def _elem_bound_err(G, A, B):
+    ref = A.t() @ B
+    bnd = A.abs().t() @ B.abs()
+    G = G.double().cpu()
+    nz = bnd > 0
+    if (~nz).any():
+        assert float(G[~nz].abs().max()) == 0.0
+    return float(((G - ref).abs()[nz] / bnd[nz]).max())
+
+
+@pytest.mark.parametrize("M,Ma,Nb", [(200_000, 256, 1024), (33_333, 128, 256), (100, 256, 256), (1, 128, 256)])
+def test_tnh_random_vs_fp64(pkg, cuda, M, Ma, Nb):
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + Ma)
+    A = torch.randn(M, Ma, generator=g, dtype=torch.float64) * 1e-3
+    B = torch.randn(M, Nb, generator=g, dtype=torch.float64) * 7.0
+    G = ops.gemm_tn_big(A.float().to(cuda), B.float().to(cuda))
+    ref = A.t() @ B
+    assert float((G.double().cpu() - ref).abs().max() / ref.abs().max()) <= 2e-6
+    assert _elem_bound_err(G, A, B) <= 4e-6
+    G2 = ops.gemm_tn_big(A.float().to(cuda), B.float().to(cuda))
+    assert torch.equal(G, G2)
+
+
+def test_tnh_dynamic_range_columns(pkg, cuda):
+    """Columns of A and B spanning 30 decades, zero columns, a column whose max sits in its last
+    row, and rows far below their column's max: every element within 4e-6 of (|A|^T |B|)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(5)
+    M, Ma, Nb = 50_000, 128, 256
+    A = torch.randn(M, Ma, generator=g, dtype=torch.float64) * torch.logspace(-15, 15, Ma, dtype=torch.float64)
+    B = torch.randn(M, Nb, generator=g, dtype=torch.float64) * torch.logspace(10, -10, Nb, dtype=torch.float64)
+    A[:, 3] = 0.0
+    B[:, 7] = 0.0
+    A[-1, 5] = 1e3 * A[:, 5].abs().max()
+    B[: M // 2, 11] *= 1e-12  # half the rows far below the column's max
+    G = ops.gemm_tn_big(A.float().to(cuda), B.float().to(cuda))
+    assert torch.isfinite(G).all()
+    assert _elem_bound_err(G, A, B) <= 4e-6
+
+
+@pytest.mark.parametrize("N,M,K", [(1_875_000, 8, 256), (1000, 3, 96), (7, 16, 1024), (300_001, 4, 128)])
+def test_skinny_tn_vs_fp64(pkg, cuda, N, M, K):
+    """gemm_tn with m <= 16 (the multi-head layer's S^T x) on the VALU skinny kernel."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(N + M)
+    A = torch.randn(N, M, generator=g, dtype=torch.float64)
+    B = torch.randn(N, K, generator=g, dtype=torch.float64)
+    out = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda))[0]
+    ref = A.t() @ B
+    assert float((out.double().cpu() - ref).abs().max() / ref.abs().max()) <= 1e-5
+    out2 = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda))[0]
+    assert torch.equal(out, out2)

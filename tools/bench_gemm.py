@@ -36,10 +36,19 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--cfg5", action="store_true", help="config-5 share shapes of ppgat_gemm_nn, both B layouts")
+    ap.add_argument("--tn5", action="store_true", help="config-5 weight gradient G = g^T agg (ppgat_gemm_tn_big)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.cfg5:
         return cfg5(dev, args.iters)
+    if args.tn5:
+        M = 1_875_000
+        g = torch.Generator(device=dev).manual_seed(0)
+        A = torch.randn(M, 256, device=dev, generator=g)
+        B = torch.randn(M, 1024, device=dev, generator=g)
+        us = timeit(lambda: ops.gemm_tn_big(A, B), args.iters)
+        print(json.dumps({"tn_big_us": us, "tflops": 2.0 * M * 256 * 1024 / us / 1e6}))
+        return
     N = args.n
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(N, 128, device=dev, generator=g)
