@@ -169,6 +169,11 @@ size_t gemm_nn_workspace_bytes(int64_t M, int K, int N);
 // the split bf16 images of a GEMM's B operand per (32 nt columns, 32-deep k chunk), once per call
 hipError_t nnx_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, hipStream_t st);
 size_t nnx_image_bytes(int K, int N, int nt);
+// the fp16 two-term family (PPGAT_GEMM_F16=0 turns it off): pre-split images + column exponents
+bool gemm_f16_enabled();
+size_t nnh_image_bytes(int K, int N, int nt);
+hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, int* ecol,
+                        hipStream_t st);
 // A [2H, K] = [W_h^T att_src[h]; W_h^T att_dst[h]] (any shape) and dx += S A (rank nv <= 16)
 hipError_t att_proj(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
                     hipStream_t st);

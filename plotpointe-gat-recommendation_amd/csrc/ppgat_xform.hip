@@ -1562,6 +1562,8 @@ static bool nnh_enabled() {
   return !off;
 }
 
+bool gemm_f16_enabled() { return nnh_enabled(); }
+
 size_t nnh_image_bytes(int K, int N, int nt) {
   const size_t img = nt == 8 ? (size_t)NnhImg<8>::BYTES : (size_t)NnhImg<4>::BYTES;
   return (size_t)(N / (32 * nt)) * (size_t)(K / 32) * img;
@@ -1679,8 +1681,12 @@ static int tn_splits(int64_t M, int T) {
 
 bool gemm_tn_big_shape_ok(int Ma, int Nb) { return Ma >= 128 && Ma % 128 == 0 && Nb >= 128 && Nb % 128 == 0; }
 
-// the fp16 two-term TN kernel (k_gemm_tnh): Nb % 256 == 0, with the fp16 family on
-static bool tnh_ok(int Ma, int Nb) { return gemm_split_enabled() && nnh_enabled() && Ma % 128 == 0 && Nb % 256 == 0; }
+// the fp16 two-term TN kernel (k_gemm_tnh): Nb % 256 == 0, with the fp16 family on, and long
+// reductions only -- below ~64k rows its three extra launches (max buffer clear, two column-max
+// passes) cost more than the fp32 kernel's MFMA time (the FusionMLP training batch of 512 rows)
+static bool tnh_ok(int64_t M, int Ma, int Nb) {
+  return gemm_split_enabled() && nnh_enabled() && M >= 65536 && Ma % 128 == 0 && Nb % 256 == 0;
+}
 static int tnh_splits(int64_t M, int T) {  // one workgroup per CU: splits * tiles <= 256, >= 128 rows per split
   // two workgroup rounds per CU: the same time as one (3.96 vs 3.98 ms at the config-5 share,
   // profiles/r03/v16_tnh_*), half the rows per fp32 accumulator chain: 3.3e-6 vs 5.3e-6
@@ -1698,7 +1704,7 @@ static int tnh_splits(int64_t M, int T) {  // one workgroup per CU: splits * til
 }
 
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb) {
-  if (tnh_ok(Ma, Nb)) {
+  if (tnh_ok(M, Ma, Nb)) {
     const int T = (Ma / 128) * (Nb / 256);
     return align_up((size_t)tnh_splits(M, T) * Ma * Nb * 4) + align_up((size_t)(Ma + Nb) * 4);
   }
@@ -1722,7 +1728,7 @@ static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, uns
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
                        void* ws, hipStream_t st) {
   if (M <= 0) return hipMemsetAsync(out, 0, (size_t)Ma * Nb * 4, st);  // empty sum (no partials)
-  if (tnh_ok(Ma, Nb)) {
+  if (tnh_ok(M, Ma, Nb)) {
     static const bool attr = [] {
       return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tnh), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)kThLds) == hipSuccess;

@@ -99,8 +99,8 @@ def test_large_m_products_run_on_nnh(pkg, cuda):
 
 
 # ---------------------------------------------------------------------------------------------
-# The fp16 two-term TN GEMM (k_gemm_tnh, ppgat_gemm_tn_big): per-column scales of A and B from
-# the column-max pre-pass.  Bound per output element relative to (|A|^T |B|), fp32 GEMM's own
+# The fp16 two-term TN GEMM (k_gemm_tnh, ppgat_gemm_tn_big at >= 65,536 rows; shorter reductions
+# take the fp32 kernel): per-column scales of A and B from the column-max pre-pass.  Bound per output element relative to (|A|^T |B|), fp32 GEMM's own
 # error scale: <= 4e-6.
 # ---------------------------------------------------------------------------------------------
 def _elem_bound_err(G, A, B):
@@ -113,7 +113,8 @@ def _elem_bound_err(G, A, B):
     return float(((G - ref).abs()[nz] / bnd[nz]).max())
 
 
-@pytest.mark.parametrize("M,Ma,Nb", [(200_000, 256, 1024), (33_333, 128, 256), (100, 256, 256), (1, 128, 256)])
+@pytest.mark.parametrize("M,Ma,Nb", [(200_000, 256, 1024), (70_001, 128, 256), (65_536, 256, 512), (33_333, 128, 256),
+                                     (100, 256, 256), (1, 128, 256)])
 def test_tnh_random_vs_fp64(pkg, cuda, M, Ma, Nb):
     ops = _ops()
     g = torch.Generator().manual_seed(M + Ma)
@@ -132,7 +133,7 @@ def test_tnh_dynamic_range_columns(pkg, cuda):
     row, and rows far below their column's max: every element within 4e-6 of (|A|^T |B|)."""
     ops = _ops()
     g = torch.Generator().manual_seed(5)
-    M, Ma, Nb = 50_000, 128, 256
+    M, Ma, Nb = 80_000, 128, 256  # >= 65,536 rows: the fp16 kernel
     A = torch.randn(M, Ma, generator=g, dtype=torch.float64) * torch.logspace(-15, 15, Ma, dtype=torch.float64)
     B = torch.randn(M, Nb, generator=g, dtype=torch.float64) * torch.logspace(10, -10, Nb, dtype=torch.float64)
     A[:, 3] = 0.0

@@ -75,14 +75,17 @@ def main(iters=20):
     ms = a.elapsed_time(b) / iters
     flop = 2.0 * n_items * ((Dt + Di) * 256 + 256 * 128)
     byts = n_items * (Dt + Di + 128) * 4.0
-    # ceiling of the kernel family that ran: the fp32 MFMA peak, or for the split-bf16 kernels
-    # (six bf16 MFMAs per fp32 product, csrc/ppgat_split.h) the dense bf16 peak / 6
+    # ceiling of the kernel family that ran: the fp32 MFMA peak; for the split-bf16 kernels
+    # (six bf16 MFMAs per fp32 product, csrc/ppgat_split.h) the dense bf16 peak / 6; for the
+    # scaled two-term fp16 kernel (three fp16 MFMAs per product, the default) the dense fp16 peak / 3
     import os
     split = os.environ.get("PPGAT_GEMM", "split") != "fp32"
-    peak = 2500.0 / 6 if split else 157.3
+    f16 = split and os.environ.get("PPGAT_GEMM_F16", "1") != "0"
+    peak = (2500.0 / 3 if f16 else 2500.0 / 6) if split else 157.3
+    family = ("fp16 two-term x3" if f16 else "split-bf16 x6") if split else "fp32 MFMA"
     tf = flop / (ms / 1e3) / 1e12
     print(json.dumps({"metric": "fusion MLP inference items/sec (498,196 items, 896->256->128, fp32 result)",
-                      "gemm_family": "split-bf16 x6" if split else "fp32 MFMA",
+                      "gemm_family": family,
                       "items_per_sec": n_items / (ms / 1e3), "ms_per_pass": ms,
                       "tflops_fp32_equiv": tf, "ceiling_tflops": peak, "ceiling_frac": tf / peak,
                       "fp32_mfma_peak_frac": tf / 157.3,
