@@ -485,6 +485,16 @@ int ppgat_gemm_nn_ws(const float* x, int64_t ldx, int64_t m, int k, const float*
 int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes);
 int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb, float* out,
                       void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_gemm_tn_big_bounded: the same product, with the caller's upper bound of |b| per column
+ *   (b_bound_bits[j % bound_period] as IEEE bits, times bound_scale >= 1) in place of the
+ *   column-max pass over b that the fp16 two-term kernel otherwise makes -- e.g. the multi-head
+ *   layer's G = g^T agg with |agg^h_i[k]| <= max_j |x_j[k]| / (1 - p) (train_gat_pyg.py:77 backward).
+ *   Any bound >= the true maxima gives the same accuracy class; the fp32 / bf16 families ignore it.
+ * ppgat_colmax_abs: out_bits[c] = IEEE bits of max_i |x[i, c]| (order-free: deterministic). */
+int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                              const unsigned* b_bound_bits, int bound_period, float bound_scale, float* out,
+                              void* workspace, size_t workspace_bytes, void* stream);
+int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream);
 int ppgat_colsum_workspace_bytes(int64_t n, int c, size_t* bytes);
 int ppgat_colsum(const float* y, int64_t ldy, int64_t n, int c, float* out, void* workspace, size_t workspace_bytes,
                  void* stream);

@@ -1002,6 +1002,38 @@ int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, 
   return PPGAT_OK;
 }
 
+int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                              const unsigned* b_bound_bits, int bound_period, float bound_scale, float* out,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big_bounded: needs ma, nb multiples of 128");
+  if (lda < ma || ldb < nb || (lda % 4) || (ldb % 4))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: bad leading dimension");
+  if (!out || !b_bound_bits || (m > 0 && (!a || !b))) return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: null pointer");
+  if (bound_period < 1 || nb % bound_period || !(bound_scale >= 1.f) || !(bound_scale < 3.4e38f))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: period must divide nb, scale >= 1 and finite");
+  if (!al16(a) || !al16(b)) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big_bounded: 16-byte aligned rows");
+  if (!workspace || workspace_bytes < ppgat::gemm_tn_big_workspace_bytes(m, ma, nb))
+    return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = ppgat::gemm_tn_big(a, lda, b, ldb, m, ma, nb, out, workspace, st, b_bound_bits, bound_period,
+                                    bound_scale);
+  if (e != hipSuccess) return hip_fail(e, "gemm_tn_big_bounded");
+  return PPGAT_OK;
+}
+
+int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream) {
+  if (n < 0 || c < 4 || (c % 4) || ldx < c || (ldx % 4)) return fail(PPGAT_ERR_INVALID, "colmax_abs: bad sizes");
+  if (!out_bits || (n > 0 && !x)) return fail(PPGAT_ERR_INVALID, "colmax_abs: null pointer");
+  if (!al16(x)) return fail(PPGAT_ERR_UNSUPPORTED, "colmax_abs: 16-byte aligned rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = ppgat::colmax_abs(x, ldx, n, c, out_bits, st);
+  if (e != hipSuccess) return hip_fail(e, "colmax_abs");
+  return PPGAT_OK;
+}
+
 int ppgat_colsum_workspace_bytes(int64_t n, int c, size_t* bytes) {
   if (!bytes || n < 0 || (c != 128 && c != 256)) return fail(PPGAT_ERR_UNSUPPORTED, "colsum: c must be 128 or 256");
   *bytes = align_up((size_t)ppgat::colsum_blocks(n) * c * 4);

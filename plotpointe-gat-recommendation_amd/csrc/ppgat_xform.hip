@@ -882,7 +882,9 @@ struct TnhArg {
   int tiles_a, tiles_b, splits;
   int64_t rows_per_split;
   const unsigned* amax;  // [Ma] column maxima (IEEE bits of |v|)
-  const unsigned* bmax;  // [Nb]
+  const unsigned* bmax;  // B column n's bound: bmax[n % bperiod] * bscale
+  int bperiod;
+  float bscale;
   float* part;           // [splits, Ma, Nb]
 };
 
@@ -933,7 +935,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
     sFa[128 + tid] = ldexpf(1.f, -e);
   }
   if (tid < 256) {
-    const float m = __uint_as_float(a.bmax[tb * 256 + tid]);
+    const float m = __uint_as_float(a.bmax[(tb * 256 + tid) % a.bperiod]) * a.bscale;
     const int e = (m > 0.f && m <= 3.4e38f) ? split::scale_exp16(m) : 0;
     sFb[tid] = ldexpf(1.f, e);
     sFb[256 + tid] = ldexpf(1.f, -e);
@@ -1725,8 +1727,14 @@ static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, uns
   return hipGetLastError();
 }
 
+hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(out, 0, (size_t)C * 4, st);
+  if (e == hipSuccess && M > 0) e = colmax_bits(X, ldx, M, C, out, st);
+  return e;
+}
+
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
-                       void* ws, hipStream_t st) {
+                       void* ws, hipStream_t st, const unsigned* b_bound, int b_period, float b_scale) {
   if (M <= 0) return hipMemsetAsync(out, 0, (size_t)Ma * Nb * 4, st);  // empty sum (no partials)
   if (tnh_ok(M, Ma, Nb)) {
     static const bool attr = [] {
@@ -1744,10 +1752,12 @@ hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb,
     a.part = static_cast<float*>(ws);
     unsigned* mx = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + align_up((size_t)a.splits * Ma * Nb * 4));
     a.amax = mx;
-    a.bmax = mx + Ma;
-    hipError_t e = hipMemsetAsync(mx, 0, (size_t)(Ma + Nb) * 4, st);
+    a.bmax = b_bound ? b_bound : mx + Ma;  // a caller's bound of |B| per column skips B's pass
+    a.bperiod = b_bound ? b_period : Nb;
+    a.bscale = b_bound ? b_scale : 1.f;
+    hipError_t e = hipMemsetAsync(mx, 0, (size_t)(b_bound ? Ma : Ma + Nb) * 4, st);
     if (e == hipSuccess) e = colmax_bits(A, lda, M, Ma, mx, st);
-    if (e == hipSuccess) e = colmax_bits(B, ldb, M, Nb, mx + Ma, st);
+    if (e == hipSuccess && !b_bound) e = colmax_bits(B, ldb, M, Nb, mx + Ma, st);
     if (e != hipSuccess) return e;
     const unsigned grid = (unsigned)(8 * T * ((a.splits + 7) / 8));
     hipLaunchKernelGGL(k_gemm_tnh, dim3(grid), dim3(512), kThLds, st, a);

@@ -938,8 +938,22 @@ def gemm_tn_big_supported(ma: int, nb: int) -> bool:
     return ma % 128 == 0 and nb % 128 == 0 and ma >= 128 and nb >= 128
 
 
-def gemm_tn_big(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
-    """A [M, ma]^T B [M, nb] on the matrix cores (ppgat_gemm_tn_big), deterministic."""
+def colmax_abs(X: torch.Tensor) -> torch.Tensor:
+    """IEEE bits (int32 view) of max_i |X[i, c]| per column (ppgat_colmax_abs; deterministic)."""
+    lib = _lib.load()
+    _check_rows("X", X, torch.float32)
+    n, c = X.shape
+    out = torch.empty(c, dtype=torch.int32, device=X.device)
+    _lib.check(lib.ppgat_colmax_abs(X.data_ptr(), X.stride(0) if n > 1 else c, n, c, out.data_ptr(),
+                                    _lib.stream_handle(X.device)), "colmax_abs")
+    return out
+
+
+def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None) -> torch.Tensor:
+    """A [M, ma]^T B [M, nb] on the matrix cores (ppgat_gemm_tn_big), deterministic.  ``b_bound``
+    = (bits [period] from colmax_abs, period, scale >= 1): an upper bound of |B| per column
+    (column j: bits[j % period] * scale) that replaces the fp16 kernel's column-max pass over B
+    (ppgat_gemm_tn_big_bounded)."""
     lib = _lib.load()
     _check_rows("A", A, torch.float32)
     _check_rows("B", B, torch.float32, A.device)
@@ -949,9 +963,17 @@ def gemm_tn_big(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     _lib.check(lib.ppgat_gemm_tn_big_workspace_bytes(M, ma, nb, ctypes.byref(nbytes)), "gemm_tn_big_workspace")
     ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=A.device)
     out = torch.empty(ma, nb, dtype=torch.float32, device=A.device)
-    _lib.check(lib.ppgat_gemm_tn_big(A.data_ptr(), A.stride(0) if M > 1 else ma, B.data_ptr(),
-                                     B.stride(0) if M > 1 else nb, M, ma, nb, out.data_ptr(), ws.data_ptr(),
-                                     nbytes.value, _lib.stream_handle(A.device)), "gemm_tn_big")
+    lda, ldb, st = A.stride(0) if M > 1 else ma, B.stride(0) if M > 1 else nb, _lib.stream_handle(A.device)
+    if b_bound is not None:
+        bits, period, scale = b_bound
+        _require(bits.dtype == torch.int32 and bits.numel() == period and bits.device == A.device,
+                 "gemm_tn_big: b_bound bits must be int32 [period] on A's device")
+        _lib.check(lib.ppgat_gemm_tn_big_bounded(A.data_ptr(), lda, B.data_ptr(), ldb, M, ma, nb, bits.data_ptr(),
+                                                 int(period), float(scale), out.data_ptr(), ws.data_ptr(),
+                                                 nbytes.value, st), "gemm_tn_big_bounded")
+        return out
+    _lib.check(lib.ppgat_gemm_tn_big(A.data_ptr(), lda, B.data_ptr(), ldb, M, ma, nb, out.data_ptr(), ws.data_ptr(),
+                                     nbytes.value, st), "gemm_tn_big")
     return out
 
 
@@ -1115,7 +1137,11 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
                "xgat_bwd_epilogue")
     GV = gemm_tn(S, x)[0]
-    G = gemm_tn_big(g, agg.view(v.n_dst, H * K))
+    # |agg^h_i[k]| = |sum_j beta_ij x_j[k]| <= max_j |x_j[k]| / (1 - p) (the attention weights
+    # sum to 1, the kept ones scaled by 1 / (1 - p)): a column bound of agg from x's column maxima
+    # (x: 1 KB per row) instead of a pass over agg (4 KB per row); 2^-10 margin for fp32 rounding
+    xbound = (colmax_abs(x), K, (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
+    G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound)
     dW = torch.empty_like(W)
     datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)
     datt_dst = torch.empty(H, C, dtype=torch.float32, device=dev)

@@ -157,3 +157,24 @@ def test_skinny_tn_vs_fp64(pkg, cuda, N, M, K):
     assert float((out.double().cpu() - ref).abs().max() / ref.abs().max()) <= 1e-5
     out2 = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda))[0]
     assert torch.equal(out, out2)
+
+
+def test_tnh_bounded_equals_exact_bound(pkg, cuda):
+    """ppgat_gemm_tn_big_bounded: with the exact column maxima as the bound the result is the
+    unbounded call's bit for bit; with a looser bound (x-derived, as the multi-head layer passes
+    for agg) it stays within 4e-6 of (|A|^T |B|).  The bound is periodic over B's columns."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(17)
+    M, Ma, K, H = 120_000, 256, 256, 4
+    A = torch.randn(M, Ma, generator=g, dtype=torch.float64) * 1e-4
+    X = torch.randn(M, K, generator=g, dtype=torch.float64) * torch.logspace(-3, 3, K, dtype=torch.float64)
+    B = torch.cat([X * (0.25 + 0.5 * h) for h in range(H)], 1)  # |B[:, h K + k]| <= 1.75 |X[:, k]|
+    Ad, Bd, Xd = A.float().to(cuda), B.float().to(cuda), X.float().to(cuda)
+    G0 = ops.gemm_tn_big(Ad, Bd)
+    bits_b = ops.colmax_abs(Bd)
+    assert torch.equal(bits_b.view(torch.float32).cpu(), Bd.abs().max(0).values.cpu())
+    G1 = ops.gemm_tn_big(Ad, Bd, b_bound=(bits_b, H * K, 1.0))
+    assert torch.equal(G0, G1)
+    G2 = ops.gemm_tn_big(Ad, Bd, b_bound=(ops.colmax_abs(Xd), K, 1.75 * (1 + 2 ** -10)))
+    assert _elem_bound_err(G2, A, B) <= 4e-6
+    assert torch.equal(G2, ops.gemm_tn_big(Ad, Bd, b_bound=(ops.colmax_abs(Xd), K, 1.75 * (1 + 2 ** -10))))
