@@ -539,6 +539,17 @@ int ppgat_xgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, co
                          float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used, float* dx,
                          int64_t lddx, float* S, int64_t lds, float* dz, void* workspace, size_t workspace_bytes,
                          void* stream);
+/* The same backward edge pass gathering g_i (C floats per edge) instead of gt_i (H * C_in):
+ *   dalpha^h_ij = g_i . hs^h_j with hs^h_j = W_h x_j / heads (caller's GEMM, [n_src, H, C]),
+ *   acc[j][h] = sum_k beta^h g_i [n_src, H, C]; dx = acc W / heads (caller's GEMM, W = lin.weight
+ *   [H*C, C_in]) + the attention terms of S (ppgat_rows_rank_update).  dz, S[:, :H] as
+ *   ppgat_xgat_bwd_edges.  Channels C == 256, heads 2 or 4. */
+int ppgat_xgat_bwd_g_workspace_bytes(int64_t n_hub_items, int channels, int heads, size_t* bytes);
+int ppgat_xgat_bwd_edges_g(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                           const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                           const float* s_src, const float* nstate, const float* g, int64_t ldg, float negative_slope,
+                           float dropout_p, uint64_t seed, const uint64_t* seed_used, float* acc, float* S, int64_t lds,
+                           float* dz, void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_xgat_bwd_epilogue(const float* S, int64_t lds, const float* att_proj, int64_t n_dst, int in_channels,
                             int heads, float* dx, int64_t lddx, void* stream);
 int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src,

@@ -1165,6 +1165,42 @@ int ppgat_xgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, co
   return PPGAT_OK;
 }
 
+int ppgat_xgat_bwd_g_workspace_bytes(int64_t n_hub_items, int channels, int heads, size_t* bytes) {
+  if (!bytes || n_hub_items < 0 || channels != 256 || (heads != 2 && heads != 4))
+    return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_g_workspace_bytes: channels 256, heads 2 or 4");
+  *bytes = partial_bytes(n_hub_items, heads, channels);
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_edges_g(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                           const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                           const float* s_src, const float* nstate, const float* g, int64_t ldg, float negative_slope,
+                           float dropout_p, uint64_t seed, const uint64_t* seed_used, float* acc, float* S, int64_t lds,
+                           float* dz, void* workspace, size_t workspace_bytes, void* stream) {
+  if (channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_edges_g: shape");
+  if (n_edges < 0 || ldg < channels || (ldg % 4) || lds < 2 * heads)
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_g: bad sizes / leading dimensions");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
+  if (int rc = check_sched(src_sched, 0, "xgat_bwd_edges_g")) return rc;
+  if (src_sched->n_items > 0 && (!hs || !s_src || !acc || !S)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_g: null pointer");
+  if (n_edges > 0 && (!row || !nstate || !g || !dz)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_g: null edge pointer");
+  if (dropout_p > 0.f && (!seed_used || (n_edges > 0 && !csc_eid)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_g: dropout needs seed_used and csc_eid");
+  if (src_sched->n_hub_items > 0 && (!workspace || workspace_bytes < partial_bytes(src_sched->n_hub_items, heads, channels)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_g: workspace too small");
+  if (!al16(hs) || !al16(g) || !al16(acc)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_edges_g: 16-byte aligned rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{src_sched->item_row, src_sched->item_beg, src_sched->item_end, src_sched->n_items,
+                           src_sched->n_hub_items, src_sched->n_long_items};
+  Timed t(PPGAT_K_BWD_SRC, st);
+  hipError_t e = ppgat::xgat_bwd_edges_g(it, row, csc_eid, dz_slot, hs, channels, heads, s_src, nstate, g, ldg,
+                                         negative_slope, dropout_p, seed, seed_used, acc, S, lds, dz,
+                                         static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
+                                         src_sched->n_hubs, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_edges_g");
+  return PPGAT_OK;
+}
+
 int ppgat_xgat_bwd_epilogue(const float* S, int64_t lds, const float* att_proj, int64_t n_dst, int in_channels,
                             int heads, float* dx, int64_t lddx, void* stream) {
   if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_epilogue: shape");

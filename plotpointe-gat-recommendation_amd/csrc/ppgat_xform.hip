@@ -1427,6 +1427,163 @@ __global__ void __launch_bounds__(256) k_bwd_x_merge(const int32_t* __restrict__
   if (lane < H) S[j * lds + lane] = ds[lane];
 }
 
+// ---------------------------------------------------------------------------
+// The backward edge pass gathering g_i (C floats per edge) instead of gt_i (H x C_in):
+// dalpha^h_ij = gt^h_i . x_j = g_i . hs^h_j with hs^h_j = W_h x_j / H (one GEMM over the
+// sources, read once per source here), and the message gradient is accumulated per head as
+// acc^h_j = sum_i beta^h_ij g_i (written once per source, [n_src, H, C]); then
+// dx_j = acc_j . W (one NN GEMM, rows h C + c of W = W_h) + the attention terms.  Per edge
+// 1 KB instead of 4 KB of gathers at config 5.  Summation orders as k_bwd_x (edges in CSC
+// order, hub pieces merged in piece order): deterministic.
+// ---------------------------------------------------------------------------
+template <int C, int H>
+__global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restrict__ row,
+                                               const int32_t* __restrict__ csc_eid,
+                                               const int32_t* __restrict__ csc2csr, const float* __restrict__ hs,
+                                               const float* __restrict__ s_src, const float4* __restrict__ nstate,
+                                               const float* __restrict__ g, int64_t ldg, float slope, float p,
+                                               float inv_keep, uint64_t seed, const uint64_t* __restrict__ seed_in,
+                                               float* __restrict__ acc_out, float* __restrict__ S, int64_t lds,
+                                               float* __restrict__ dz, float* __restrict__ partial) {
+  static_assert(C == 256 && H <= 4, "k_bwd_g: C == 256, H <= 4");
+  constexpr int U = 16 / H;  // edges per reduction group (16 partial dots per lane)
+  if (p > 0.f) seed = *seed_in;
+  __shared__ int2 recA[4][64];          // {dst row, dz slot}
+  __shared__ float4 recH[4][H][64];     // per head {beta, c1, c0, -}
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+  if (w >= it.n_items) return;
+  const int64_t j = it.row[w];
+  const int cs = it.beg[w], ce = it.end[w];
+  const bool hub = w < it.n_hub_items;
+  float4 hv[H], acc[H];
+  float ss[H], dsa[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    hv[h] = ld4(hs + (j * H + h) * C + lane * 4);
+    acc[h] = f4(0.f);
+    ss[h] = s_src[j * H + h];
+    dsa[h] = 0.f;
+  }
+  for (int base = cs; base < ce; base += 64) {
+    const int k = base + lane;
+    const bool valid = k < ce;
+    const int i = valid ? row[k] : 0;
+    const int slot = valid ? (csc2csr != nullptr ? csc2csr[k] : k) : 0;  // NULL: dz in CSC order
+    const uint32_t e_id = (valid && p > 0.f) ? (uint32_t)csc_eid[k] : 0u;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float bg = 0.f, c1 = 0.f, c0 = 0.f;
+      if (valid) {
+        const float4 st = nstate[(int64_t)i * H + h];  // {s_dst, m, inv_l, D}
+        const float z = ss[h] + st.x;
+        const float af = expf(lrelu(z, slope) - st.y) * st.z;
+        const float dm = p > 0.f ? drop_scale(seed, e_id, (uint32_t)h, p, inv_keep) : 1.f;
+        bg = af * dm;
+        const float a1 = af * dlrelu(z, slope);
+        c1 = a1 * dm;
+        c0 = a1 * st.w;
+      }
+      recH[wv][h][lane] = make_float4(bg, c1, c0, 0.f);
+    }
+    recA[wv][lane] = make_int2(i, slot);
+    wave_sync();
+    const int n = min(64, ce - base);
+    for (int q0 = 0; q0 < n; q0 += U) {
+      float4 gq[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u;
+        const int64_t ii = recA[wv][min(q, 63)].x;
+        gq[u] = q < n ? ld4(g + ii * ldg + lane * 4) : f4(0.f);
+      }
+      float part[16];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = min(q0 + u, 63);
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const float bq = q0 + u < n ? recH[wv][h][q].x : 0.f;
+          acc[h] = fma4(bq, gq[u], acc[h]);
+          part[u * H + h] = dot4(gq[u], hv[h]);
+        }
+      }
+      int vbase = 0;
+      const int R = tr_reduce<32, 16>(part, lane, vbase);
+      const int t = lane & 7;
+      if (t < R) {
+        float dot = part[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c)
+          if (c == t) dot = part[c];
+        const int vi = vbase + t;
+        const int u = vi / H, h = vi % H;
+        const int q = q0 + u;
+        if (q < n) {
+          const float4 rb = recH[wv][h][q];
+          const float dzv = fmaf(rb.y, dot, -rb.z);
+#pragma unroll
+          for (int c = 0; c < H; ++c)
+            if (c == h) dsa[c] += dzv;
+          dz[(int64_t)recA[wv][q].y * H + h] = dzv;
+        }
+      }
+    }
+    wave_sync();
+  }
+  float ds[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ds[h] = wave_sum(dsa[h]);
+  if (hub) {
+    float* sp = partial + w * (H * C + 4);
+#pragma unroll
+    for (int h = 0; h < H; ++h) st4(sp + h * C + lane * 4, acc[h]);
+    if (lane == 0) {
+      float4 d = f4(0.f);
+      d.x = ds[0];
+      if (H > 1) d.y = ds[1];
+      if (H > 2) d.z = ds[2];
+      if (H > 3) d.w = ds[3];
+      st4(sp + H * C, d);
+    }
+    return;
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) st4(acc_out + (j * H + h) * C + lane * 4, acc[h]);
+  if (lane < H) {
+    float v = ds[0];
+#pragma unroll
+    for (int h = 1; h < H; ++h) v = lane == h ? ds[h] : v;
+    S[j * lds + lane] = v;
+  }
+}
+
+// hub sources of k_bwd_g: pieces summed in piece order
+template <int C, int H>
+__global__ void __launch_bounds__(256) k_bwd_g_merge(const int32_t* __restrict__ hub_row,
+                                                     const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
+                                                     const float* __restrict__ partial, float* __restrict__ acc_out,
+                                                     float* __restrict__ S, int64_t lds) {
+  const int lane = threadIdx.x & 63;
+  const int64_t hb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;
+  const int64_t j = hub_row[hb];
+  float4 acc[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) acc[h] = f4(0.f);
+  float4 d = f4(0.f);
+  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) {
+    const float* sp = partial + (int64_t)q * (H * C + 4);
+#pragma unroll
+    for (int h = 0; h < H; ++h) acc[h] = add4(acc[h], ld4(sp + h * C + lane * 4));
+    d = add4(d, ld4(sp + H * C));
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) st4(acc_out + (j * H + h) * C + lane * 4, acc[h]);
+  const float ds[4] = {d.x, d.y, d.z, d.w};
+  if (lane < H) S[j * lds + lane] = ds[lane];
+}
+
 // dx_i += sum_h ds_dst_i^h A_dst[h] over the destination rows (S[i][H + h] = ds_dst)
 template <int K, int H>
 __global__ void __launch_bounds__(256) k_bwd_x_epi(const float* __restrict__ S, int64_t lds,
@@ -1854,6 +2011,24 @@ hipError_t xgat_bwd_edges(const ItemsArg& it, const int32_t* row, const int32_t*
     PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_x_merge<256, HH>), dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st,
                                    hub_row, hub_ptr, n_hubs, partial, A_src, dx, lddx, S, lds));
   (void)K;
+  return hipGetLastError();
+}
+
+hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
+                            const float* hs, int C, int H, const float* s_src, const float* nstate, const float* g,
+                            int64_t ldg, float slope, float p, uint64_t seed, const uint64_t* seed_in, float* acc,
+                            float* S, int64_t lds, float* dz, float* partial, const int32_t* hub_row,
+                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  if (it.n_items > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
+                                   row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
+                                   slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial));
+  if (n_hubs > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge<256, HH>), dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st,
+                                   hub_row, hub_ptr, n_hubs, partial, acc, S, lds));
+  (void)C;
   return hipGetLastError();
 }
 

@@ -1115,6 +1115,28 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     E = v.n_edges
     S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    if halo_hook is None and _xgat_gather_g(C, H):
+        # gather g_i per edge (C floats) instead of gt_i (H * C_in): hs = x W^T / H per source,
+        # the per-head message gradient acc [n_src, H * C], then dx = acc W / H
+        hs = gemm_nn(x, W, 1, H * C, alpha=1.0 / H)
+        acc = torch.empty(v.n_src, H * C, dtype=torch.float32, device=dev)
+        sched = v.bwd_sched
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = sched.cstruct()
+        _lib.check(lib.ppgat_xgat_bwd_edges_g(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                              _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None,
+                                              E, C, H, hs.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), g.data_ptr(),
+                                              C, float(slope), float(p), int(seed) & (2**64 - 1),
+                                              _lib.ptr(saved["seed_buf"]), acc.data_ptr(), S.data_ptr(), 2 * H,
+                                              dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_g")
+        del hs
+        _xgat_dst_sum(lib, v, dz, S, H, E, st)
+        dx = gemm_nn(acc, W, 0, K, alpha=1.0 / H)
+        del acc
+        rank_update_(dx, S, A.view(2 * H, K))  # + sum_h ds_src^h A_src^h + ds_dst^h A_dst^h
+        return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
     dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
     args = (x, s_src, nstate, gt, A, S, dz, dx, H, K, slope, p, seed, saved["seed_buf"], st)
     if halo_hook is not None and v.bwd_sched_halo is not None:
@@ -1125,6 +1147,21 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
         _xgat_edges_bwd(lib, v.bwd_sched, v, 0, *args)
         if halo_hook is not None:
             halo_hook(dx[v.n_dst:])
+    _xgat_dst_sum(lib, v, dz, S, H, E, st)
+    _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
+               "xgat_bwd_epilogue")
+    return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
+
+
+def _xgat_gather_g(C: int, H: int) -> bool:
+    """The g-gathering backward edge pass (ppgat_xgat_bwd_edges_g) on the single-GPU path;
+    PPGAT_XGAT_GATHER=gt keeps the gt-gathering pass (ppgat_xgat_bwd_edges)."""
+    return C == 256 and H in (2, 4) and os.environ.get("PPGAT_XGAT_GATHER", "g") != "gt"
+
+
+def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st):
+    """ds_dst = per-destination sums of dz into S[:, H:2H] (fixed order)."""
+    dev = dz.device
     fs = v.fwd_sched.cstruct()
     dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
     if v.dz_slot is None:
@@ -1134,8 +1171,12 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     else:
         _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
                                          dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
-    _lib.check(lib.ppgat_xgat_bwd_epilogue(S.data_ptr(), 2 * H, A.data_ptr(), v.n_dst, K, H, dx.data_ptr(), K, st),
-               "xgat_bwd_epilogue")
+
+
+def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st):
+    x, W, a_s, a_d, agg, v = saved["x"], saved["W"], saved["a_s"], saved["a_d"], saved["agg"], saved["v"]
+    H, C, K, slope, p, seed, has_bias = saved["meta"]
+    dev = x.device
     GV = gemm_tn(S, x)[0]
     # |agg^h_i[k]| = |sum_j beta_ij x_j[k]| <= max_j |x_j[k]| / (1 - p) (the attention weights
     # sum to 1, the kept ones scaled by 1 / (1 - p)): a column bound of agg from x's column maxima
