@@ -55,7 +55,7 @@ def parse():
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=None,
                     help="committed PMC summary (default: profiles/r02/cfg2_pmc_traffic.json for config 2, "
-                         "profiles/r02/cfg5_pmc_traffic.json for config 5 at its default scale)")
+                         "profiles/r03/cfg5_pmc_traffic.json for config 5 at its default scale)")
     ap.add_argument("--partition", choices=["auto", "replicated", "halo"], default="auto",
                     help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
                          "'halo' = users and items row-sharded, RCCL all_to_all of the halo rows per layer "
@@ -75,17 +75,21 @@ def parse():
 # algorithmic bytes per launch (DESIGN.md "Kernels and their rooflines")
 # ---------------------------------------------------------------------------
 def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool, xform_k: int = 0,
-               dz_slot: bool = False) -> float:
+               dz_slot: bool = False, gather_g: bool = False) -> float:
     """Algorithmic bytes per launch.  xform_k > 0: the aggregate-then-
     transform kernels (heads > 1, x rows of xform_k floats gathered instead of h rows).
     dz_slot: pass B reads each edge's dz position (the sharded layouts); otherwise dz is stored
-    at the edge's own CSC position (no index read)."""
+    at the edge's own CSC position (no index read).  gather_g: the multi-head pass B gathers
+    g_i (C floats) per edge and reads hs_j / writes acc_j (H * C floats) per source
+    (ppgat_xgat_bwd_edges_g) instead of gathering gt_i (H * xform_k floats)."""
     d = 4 if dropout else 0
     sl = 4 if dz_slot else 0
     if xform_k:
         K = xform_k
         if kernel == "fwd":    # k_fwd_x: col, s_src[H], x_j | sched, s_dst[H], agg[H, K], m, inv_l
             return E * (4 + 4 * H + 4 * K + d) + N * (12 + 4 * H + 4 * H * K + 8 * H)
+        if kernel == "bwd_src" and gather_g:  # k_bwd_g: row, (slot), nstate[H], g_i[C], dz[H] | sched, hs, s_src, acc, S
+            return E * (4 + sl + 16 * H + 4 * C + 4 * H + d) + N * (12 + 4 * H * C + 4 * H + 4 * H * C + 4 * H)
         if kernel == "bwd_src":  # k_bwd_x: row, (slot), nstate[H], gt_i[H, K], dz[H] | sched, x, s_src, dx, S
             return E * (4 + sl + 16 * H + 4 * H * K + 4 * H + d) + N * (12 + 4 * K + 4 * H + 4 * K + 4 * H)
         if kernel == "bwd_pro":  # gt, agg in; s_dst, m, inv_l in; nstate out
@@ -357,6 +361,8 @@ def main():
     H, C = args.heads, args.hidden
     # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
     xform_k = C if (H > 1 and H * C > C and pkg.hip_ops.xgat_supported(C, H, C)) else 0
+    # the g-gathering pass B runs where no halo exchange splits the backward (hip_ops.xgat_backward)
+    gather_g = bool(xform_k) and pkg.hip_ops._xgat_gather_g(C, H)
     kern = {k: _lib.profile_read(k) for k in ("scores", "fwd", "bwd_pro", "bwd_src", "bwd_epi", "bwd_red",
                                                "proj", "proj_bwd", "gemm_tn", "adam")}
     fused_ms = sum(ms for k, (ms, _) in kern.items() if k not in ("proj", "proj_bwd", "gemm_tn", "adam"))
@@ -374,19 +380,21 @@ def main():
         else:
             v = dg.fwd_view if dom == "fwd" else dg.bwd_view
         ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
-                        args.attn_dropout > 0, xform_k, dz_slot=part != "replicated")
+                        args.attn_dropout > 0, xform_k, dz_slot=part != "replicated", gather_g=gather_g)
     else:
-        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k)
+        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k, gather_g=gather_g)
     achieved = ab / avg_s / 1e9
     traffic = None
     try:
         if dist_path:
             raise LookupError("the committed PMC summary is for the unsharded graph")
-        tj_path = args.traffic_json or str(ROOT / "profiles" / "r02" / ("cfg5_pmc_traffic.json" if args.config == 5
-                                                                       else "cfg2_pmc_traffic.json"))
+        tj_path = args.traffic_json or str(ROOT / "profiles" / ("r03/cfg5_pmc_traffic.json" if args.config == 5
+                                                                 else "r02/cfg2_pmc_traffic.json"))
         tj_ = json.loads(Path(tj_path).read_text())
+        # PMC summaries are per workload (config, scale) and per multi-head backward formulation
         if tj_.get("config", 2) == args.config and tj_.get("scale", scale if args.config == 5 else None) == (
-                scale if args.config == 5 else None):  # PMC summaries are per workload
+                scale if args.config == 5 else None) and (
+                not xform_k or tj_.get("bwd_gather", "gt") == ("g" if gather_g else "gt")):
             traffic = tj_.get("per_launch_bytes", {}).get(dom)
     except Exception:
         pass

@@ -482,6 +482,15 @@ int ppgat_gemm_nn_workspace_bytes(int64_t m, int k, int n, size_t* bytes);
 int ppgat_gemm_nn_ws(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
                      float alpha, const float* bias, float* y, int64_t ldy, void* workspace, size_t workspace_bytes,
                      void* stream);
+/* ppgat_gemm_nn_rank: y = alpha x b + bias + s a (s [m, nv] with row stride lds, a [nv, n] with
+ *   row stride lda, nv <= 16, the terms added in v order after alpha and bias: the bits of
+ *   ppgat_gemm_nn_ws followed by ppgat_rows_rank_update).  On the fp16 two-term large-m path
+ *   with nv <= 8 the rank terms are added in the GEMM's epilogue (no second pass over y) --
+ *   the multi-head backward's dx = acc W / H + S A_att (ppgat_xgat_bwd_edges_g).  Same
+ *   workspace as ppgat_gemm_nn_ws. */
+int ppgat_gemm_nn_rank(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
+                       float alpha, const float* bias, const float* s, int64_t lds, int nv, const float* a,
+                       int64_t lda, float* y, int64_t ldy, void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes);
 int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb, float* out,
                       void* workspace, size_t workspace_bytes, void* stream);
@@ -542,7 +551,7 @@ int ppgat_xgat_bwd_edges(const ppgat_schedule* src_sched, const int32_t* row, co
 /* The same backward edge pass gathering g_i (C floats per edge) instead of gt_i (H * C_in):
  *   dalpha^h_ij = g_i . hs^h_j with hs^h_j = W_h x_j / heads (caller's GEMM, [n_src, H, C]),
  *   acc[j][h] = sum_k beta^h g_i [n_src, H, C]; dx = acc W / heads (caller's GEMM, W = lin.weight
- *   [H*C, C_in]) + the attention terms of S (ppgat_rows_rank_update).  dz, S[:, :H] as
+ *   [H*C, C_in]) + the attention terms of S (ppgat_gemm_nn_rank).  dz, S[:, :H] as
  *   ppgat_xgat_bwd_edges.  Channels C == 256, heads 2 or 4. */
 int ppgat_xgat_bwd_g_workspace_bytes(int64_t n_hub_items, int channels, int heads, size_t* bytes);
 int ppgat_xgat_bwd_edges_g(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,

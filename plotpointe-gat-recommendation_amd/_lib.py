@@ -109,6 +109,8 @@ SIGNATURES = {
     "ppgat_gemm_nn_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_gemm_nn_ws": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_int, c_f, c_vp, c_vp, c_i64, c_vp, c_sz,
                                  c_vp]),
+    "ppgat_gemm_nn_rank": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int, c_int, c_f, c_vp, c_vp, c_i64, c_int,
+                                   c_vp, c_i64, c_vp, c_i64, c_vp, c_sz, c_vp]),
     "ppgat_gemm_tn_big_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_gemm_tn_big": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_gemm_tn_big_bounded": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_int, c_f, c_vp, c_vp,

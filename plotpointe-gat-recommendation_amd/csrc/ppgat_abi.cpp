@@ -979,6 +979,29 @@ int ppgat_gemm_nn_ws(const float* x, int64_t ldx, int64_t m, int k, const float*
   return PPGAT_OK;
 }
 
+int ppgat_gemm_nn_rank(const float* x, int64_t ldx, int64_t m, int k, const float* b, int64_t ldb, int b_layout, int n,
+                       float alpha, const float* bias, const float* s, int64_t lds, int nv, const float* a,
+                       int64_t lda, float* y, int64_t ldy, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!ppgat::gemm_nn_shape_ok(m, k, n, b_layout))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn_rank: needs k % 32 == 0, n % 128 == 0, b_layout 0 or 1");
+  if (ldx < k || (ldx % 4) || ldy < n || (ldy % 4) || (b_layout == 0 ? ldb < n : ldb < k) || (ldb % 4))
+    return fail(PPGAT_ERR_INVALID, "gemm_nn_rank: bad leading dimension (>= width, multiple of 4)");
+  if (nv < 0 || nv > 16 || (nv > 0 && (lds < nv || lda < n || (lda % 4))))
+    return fail(PPGAT_ERR_INVALID, "gemm_nn_rank: nv <= 16, lds >= nv, lda >= n and a multiple of 4");
+  if (m > 0 && (!x || !b || !y || (nv > 0 && (!s || !a)))) return fail(PPGAT_ERR_INVALID, "gemm_nn_rank: null pointer");
+  if (!al16(x) || !al16(b) || !al16(y) || (a && !al16(a)))
+    return fail(PPGAT_ERR_UNSUPPORTED, "gemm_nn_rank: 16-byte aligned rows");
+  const size_t need = ppgat::gemm_nn_workspace_bytes(m, k, n);
+  if (need > 0 && (!workspace || workspace_bytes < need))
+    return fail(PPGAT_ERR_INVALID, "gemm_nn_rank: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_PROJ, st);
+  hipError_t e = ppgat::gemm_nn(x, ldx, m, k, b, ldb, b_layout, n, alpha, bias, y, ldy, st,
+                                need > 0 ? workspace : nullptr, s, lds, nv, a, lda);
+  if (e != hipSuccess) return hip_fail(e, "gemm_nn_rank");
+  return PPGAT_OK;
+}
+
 int ppgat_gemm_tn_big_workspace_bytes(int64_t m, int ma, int nb, size_t* bytes) {
   if (!bytes || m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
     return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big: needs ma, nb multiples of 128");

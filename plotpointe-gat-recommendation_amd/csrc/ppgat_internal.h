@@ -164,7 +164,8 @@ bool gemm_nn_shape_ok(int64_t M, int K, int N, int bmode);
 bool gemm_split_enabled();
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
                    float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st,
-                   void* ws = nullptr);
+                   void* ws = nullptr, const float* rS = nullptr, int64_t ldrs = 0, int nv = 0,
+                   const float* rA = nullptr, int64_t ldra = 0);
 size_t gemm_nn_workspace_bytes(int64_t M, int K, int N);
 // the split bf16 images of a GEMM's B operand per (32 nt columns, 32-deep k chunk), once per call
 hipError_t nnx_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, hipStream_t st);

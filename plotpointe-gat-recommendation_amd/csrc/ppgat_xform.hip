@@ -97,6 +97,13 @@ struct NnArg {
   int splits;     // > 1: split-K, raw partial tiles to part[split][M][N] (k_nn_split_sum finishes)
   int k_per;      // reduction length per split (multiple of kGBK)
   float* part;
+  // optional rank update fused into k_gemm_nnh's epilogue: Y += rS[row][:nv] rA[:nv][col]
+  // (v ascending, after alpha and bias -- the order of k_rank_update, so the same bits)
+  const float* rS;
+  int64_t ldrs;
+  int nv;
+  const float* rA;
+  int64_t ldra;
 };
 
 // BMODE 0: B[k][n] = B[k * ldb + n] (image [k][n], b32 reads); 1: B[k][n] = B[n * ldb + k] (X W^T,
@@ -593,7 +600,9 @@ __global__ void __launch_bounds__(256) k_nnh_presplit(const float* __restrict__ 
   *reinterpret_cast<uint2*>(base + I::PART) = l;
 }
 
-template <int NT>
+constexpr int kNnhRank = 8;  // rank terms the fused epilogue keeps in registers
+
+template <int NT, bool RK>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __restrict__ img,
                                                      const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
@@ -670,15 +679,46 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __
   split::row_unscale(erow, sF[wv], r, hf, fr);
   const int64_t row0 = rb * kPBM + wv * 32;
   const int n0 = nb * I::BN;
+  if constexpr (RK) {
+    // + S A (nv <= kNnhRank): this lane's columns of A in registers, each row's S terms loaded
+    // once (broadcast over the 32 lanes of the row), the terms added in v order after alpha, bias
+    const int nv = a.nv;
+    float ra[NT][kNnhRank], bv[NT], ic[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int col = n0 + 32 * t + r;
-    const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
-    const float ic = ldexpf(a.alpha, -ecol[col]);
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      bv[t] = a.bias != nullptr ? a.bias[col] : 0.f;
+      ic[t] = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int v = 0; v < kNnhRank; ++v) ra[t][v] = v < nv ? a.rA[v * a.ldra + col] : 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
-      if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+      const int64_t rr = row < M ? row : M - 1;
+      float sv[kNnhRank];
+#pragma unroll
+      for (int v = 0; v < kNnhRank; ++v) sv[v] = v < nv ? a.rS[rr * a.ldrs + v] : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float y = fmaf(acc[t][q] * fr[q], ic[t], bv[t]);
+#pragma unroll
+        for (int v = 0; v < kNnhRank; ++v)
+          if (v < nv) y = fmaf(sv[v], ra[t][v], y);
+        if (row < M) a.Y[row * a.ldy + n0 + 32 * t + r] = y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+      const float ic = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+      }
     }
   }
 }
@@ -1759,9 +1799,17 @@ size_t gemm_nn_workspace_bytes(int64_t M, int K, int N) {
 }
 
 hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B, int64_t ldb, int bmode, int N,
-                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st, void* ws) {
+                   float alpha, const float* bias, float* Y, int64_t ldy, hipStream_t st, void* ws, const float* rS,
+                   int64_t ldrs, int nv, const float* rA, int64_t ldra) {
   if (M <= 0) return hipSuccess;
+  if (nv > 0 && !(ws != nullptr && nnp_ok(M, K, N) && nnh_enabled() && nv <= kNnhRank)) {
+    // no fused epilogue on this path: the GEMM, then the rank update as its own pass
+    hipError_t e = gemm_nn(X, ldx, M, K, B, ldb, bmode, N, alpha, bias, Y, ldy, st, ws);
+    if (e != hipSuccess) return e;
+    return rank_update(rS, ldrs, nv, rA, ldra, M, N, Y, ldy, st);
+  }
   NnArg a{};
+  a.rS = rS; a.ldrs = ldrs; a.nv = nv; a.rA = rA; a.ldra = ldra;
   a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.B = B; a.ldb = ldb; a.N = N; a.alpha = alpha; a.bias = bias;
   a.Y = Y; a.ldy = ldy;
   if (ws != nullptr && nnp_ok(M, K, N)) {  // B pre-split once, then the glds-staged kernel
@@ -1775,8 +1823,14 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       int* ecol = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align_up(nnh_image_bytes(K, N, w8 ? 8 : 4)));
       hipError_t e = nnh_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, ecol, st);
       if (e != hipSuccess) return e;
-      if (w8) hipLaunchKernelGGL((k_gemm_nnh<8>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-      else hipLaunchKernelGGL((k_gemm_nnh<4>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+      if (nv > 0) {
+        if (w8) hipLaunchKernelGGL((k_gemm_nnh<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        else hipLaunchKernelGGL((k_gemm_nnh<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+      } else if (w8) {
+        hipLaunchKernelGGL((k_gemm_nnh<8, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+      } else {
+        hipLaunchKernelGGL((k_gemm_nnh<4, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+      }
       return hipGetLastError();
     }
     hipError_t e = nnx_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, st);

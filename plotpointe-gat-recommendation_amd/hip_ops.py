@@ -860,8 +860,11 @@ def gemm_nn_supported(m: int, k: int, n: int, b_layout: int) -> bool:
 
 
 def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: float = 1.0,
-            bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """alpha x B (+ bias): B [K, n] row-major (b_layout 0) or [n, K] (b_layout 1: x B^T)."""
+            bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+            rank: Optional[tuple] = None) -> torch.Tensor:
+    """alpha x B (+ bias): B [K, n] row-major (b_layout 0) or [n, K] (b_layout 1: x B^T).
+    rank=(S [M, nv], A [nv, n]): + S A as well (ppgat_gemm_nn_rank; in the GEMM's epilogue on
+    the large-M fp16 path, the same bits as gemm_nn followed by rank_update_)."""
     lib = _lib.load()
     _check_rows("x", x, torch.float32)
     _check_rows("B", B, torch.float32, x.device)
@@ -872,8 +875,19 @@ def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: floa
     if gemm_nn_supported(M, K, n, b_layout):
         _lib.check(lib.ppgat_gemm_nn_workspace_bytes(M, K, n, ctypes.byref(nbytes)), "gemm_nn_workspace_bytes")
     ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=x.device) if nbytes.value else None
-    _lib.check(lib.ppgat_gemm_nn_ws(x.data_ptr(), x.stride(0) if M > 1 else K, M, K, B.data_ptr(), ldb, b_layout, n,
-                                    float(alpha), _lib.ptr(bias), y.data_ptr(), y.stride(0) if M > 1 else n,
+    ldx, ldy = (x.stride(0) if M > 1 else K), (y.stride(0) if M > 1 else n)
+    if rank is not None:
+        S, A = rank
+        nv = S.size(1)
+        _require(S.dim() == 2 and S.size(0) == M and S.stride(1) == 1 and A.is_contiguous() and A.shape == (nv, n),
+                 "gemm_nn: rank=(S [M, nv], A [nv, n] contiguous)")
+        _lib.check(lib.ppgat_gemm_nn_rank(x.data_ptr(), ldx, M, K, B.data_ptr(), ldb, b_layout, n, float(alpha),
+                                          _lib.ptr(bias), S.data_ptr(), S.stride(0) if M > 1 else nv, nv, A.data_ptr(),
+                                          n, y.data_ptr(), ldy, _lib.ptr(ws), nbytes.value,
+                                          _lib.stream_handle(x.device)), "gemm_nn_rank")
+        return y
+    _lib.check(lib.ppgat_gemm_nn_ws(x.data_ptr(), ldx, M, K, B.data_ptr(), ldb, b_layout, n,
+                                    float(alpha), _lib.ptr(bias), y.data_ptr(), ldy,
                                     _lib.ptr(ws), nbytes.value, _lib.stream_handle(x.device)), "gemm_nn")
     return y
 
@@ -1049,6 +1063,24 @@ def _xgat_edges_bwd(lib, sched: Schedule, v: "XViews", base_row: int, x, s_src, 
                                         nbytes.value, st), "xgat_bwd_edges")
 
 
+def _xgat_edges_bwd_g(lib, sched: Schedule, v: "XViews", base_row: int, hs, s_src, nstate, g, acc, S, dz, H, C,
+                      slope, p, seed, seed_buf, st):
+    """ppgat_xgat_bwd_edges_g over one source schedule whose rows start at base_row."""
+    dev = hs.device
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+    cs = sched.cstruct()
+    E = v.n_edges
+    _lib.check(lib.ppgat_xgat_bwd_edges_g(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                          _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None, E, C,
+                                          H, hs.data_ptr() + 4 * base_row * H * C, s_src.data_ptr() + 4 * base_row * H,
+                                          nstate.data_ptr(), g.data_ptr(), C, float(slope), float(p),
+                                          int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                          acc.data_ptr() + 4 * base_row * H * C, S.data_ptr() + 4 * base_row * 2 * H,
+                                          2 * H, dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_g")
+
+
 def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
                  seed: int):
     """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state)."""
@@ -1115,27 +1147,33 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     E = v.n_edges
     S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
-    if halo_hook is None and _xgat_gather_g(C, H):
+    if _xgat_gather_g(C, H):
         # gather g_i per edge (C floats) instead of gt_i (H * C_in): hs = x W^T / H per source,
-        # the per-head message gradient acc [n_src, H * C], then dx = acc W / H
+        # the per-head message gradient acc [n_src, H * C], then dx = acc W / H + S A_att with the
+        # attention terms in the GEMM's epilogue
         hs = gemm_nn(x, W, 1, H * C, alpha=1.0 / H)
         acc = torch.empty(v.n_src, H * C, dtype=torch.float32, device=dev)
-        sched = v.bwd_sched
-        nbytes = ctypes.c_size_t(0)
-        _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
-        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
-        cs = sched.cstruct()
-        _lib.check(lib.ppgat_xgat_bwd_edges_g(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
-                                              _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None,
-                                              E, C, H, hs.data_ptr(), s_src.data_ptr(), nstate.data_ptr(), g.data_ptr(),
-                                              C, float(slope), float(p), int(seed) & (2**64 - 1),
-                                              _lib.ptr(saved["seed_buf"]), acc.data_ptr(), S.data_ptr(), 2 * H,
-                                              dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_g")
-        del hs
-        _xgat_dst_sum(lib, v, dz, S, H, E, st)
-        dx = gemm_nn(acc, W, 0, K, alpha=1.0 / H)
-        del acc
-        rank_update_(dx, S, A.view(2 * H, K))  # + sum_h ds_src^h A_src^h + ds_dst^h A_dst^h
+        dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
+        A2 = A.view(2 * H, K)
+        gargs = (hs, s_src, nstate, g, acc, S, dz, H, C, slope, p, seed, saved["seed_buf"], st)
+        n0 = v.n_dst
+        if halo_hook is not None and v.bwd_sched_halo is not None:
+            # the halo sources first: their rows of dx (no destination terms) go back to their
+            # owners while the own sources' edge pass runs
+            _xgat_edges_bwd_g(lib, v.bwd_sched_halo, v, n0, *gargs)
+            if v.n_src > n0:
+                gemm_nn(acc[n0:], W, 0, K, alpha=1.0 / H, out=dx[n0:], rank=(S[n0:, :H], A2[:H]))
+            halo_hook(dx[n0:])
+            _xgat_edges_bwd_g(lib, v.bwd_sched_own, v, 0, *gargs)
+            _xgat_dst_sum(lib, v, dz, S, H, E, st)
+            gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, out=dx[:n0], rank=(S[:n0], A2))
+        else:
+            _xgat_edges_bwd_g(lib, v.bwd_sched, v, 0, *gargs)
+            _xgat_dst_sum(lib, v, dz, S, H, E, st)
+            gemm_nn(acc, W, 0, K, alpha=1.0 / H, out=dx, rank=(S, A2))  # + sum_h ds_src^h A_src^h + ds_dst^h A_dst^h
+            if halo_hook is not None:
+                halo_hook(dx[n0:])
+        del hs, acc
         return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
     dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
     args = (x, s_src, nstate, gt, A, S, dz, dx, H, K, slope, p, seed, saved["seed_buf"], st)
@@ -1154,7 +1192,7 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
 
 
 def _xgat_gather_g(C: int, H: int) -> bool:
-    """The g-gathering backward edge pass (ppgat_xgat_bwd_edges_g) on the single-GPU path;
+    """The g-gathering backward edge pass (ppgat_xgat_bwd_edges_g), single-GPU and sharded;
     PPGAT_XGAT_GATHER=gt keeps the gt-gathering pass (ppgat_xgat_bwd_edges)."""
     return C == 256 and H in (2, 4) and os.environ.get("PPGAT_XGAT_GATHER", "g") != "gt"
 

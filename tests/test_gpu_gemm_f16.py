@@ -178,3 +178,29 @@ def test_tnh_bounded_equals_exact_bound(pkg, cuda):
     G2 = ops.gemm_tn_big(Ad, Bd, b_bound=(ops.colmax_abs(Xd), K, 1.75 * (1 + 2 ** -10)))
     assert _elem_bound_err(G2, A, B) <= 4e-6
     assert torch.equal(G2, ops.gemm_tn_big(Ad, Bd, b_bound=(ops.colmax_abs(Xd), K, 1.75 * (1 + 2 ** -10))))
+
+
+@pytest.mark.parametrize("M,K,N,nv,lds", [(20001, 1024, 256, 8, 8), (5000, 512, 128, 3, 8), (20001, 1024, 256, 4, 8),
+                                          (3000, 256, 256, 12, 12), (300, 256, 256, 8, 8)])
+def test_gemm_nn_rank_equals_gemm_then_rank_update(pkg, cuda, M, K, N, nv, lds):
+    """ppgat_gemm_nn_rank (the rank terms in k_gemm_nnh's epilogue when nv <= 8 on the large-M
+    path, else a second pass) gives the bits of gemm_nn followed by rows_rank_update, tail rows
+    and a strided S (a column slice of a wider array) included."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + nv)
+    X = torch.randn(M, K, generator=g).to(cuda)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(cuda)
+    Sw = torch.randn(M, lds, generator=g).to(cuda)
+    S = Sw[:, :nv]
+    A = torch.randn(nv, N, generator=g).to(cuda)
+    ref = ops.gemm_nn(X, W, 1, N, alpha=0.25)
+    ops.rank_update_(ref, S, A)
+    y = ops.gemm_nn(X, W, 1, N, alpha=0.25, rank=(S, A))
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    y2 = torch.full((M + 7, N), float("nan"), device=cuda)
+    ops.gemm_nn(X[7:], W, 1, N, alpha=0.25, out=y2[14:], rank=(S[7:], A))
+    ref2 = ops.gemm_nn(X[7:], W, 1, N, alpha=0.25)
+    ops.rank_update_(ref2, S[7:], A)
+    assert torch.equal(y2[14:], ref2)
+    assert torch.isnan(y2[:14]).all()

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON [CONFIG [key=value ...]]
+
+(key=value pairs are copied into the JSON, e.g. scale=0.125 bwd_gather=g for config 5: bench.py
+uses a summary only for the workload it was collected on.)
 
 gfx950 corrections (MI355X_MICROARCH.md "HBM"): counters are in KiB (x1024); FETCH_SIZE
 reports 1/2 of the bytes of a wide (16 B/lane) coalesced read -- all of our kernels read
@@ -18,7 +21,9 @@ from collections import defaultdict
 KERNELS = {"k_fwd<": "fwd_long", "k_fwd_short<": "fwd_short", "k_bwd_src<": "bwd_src_long",
            "k_bwd_src_short<": "bwd_src_short", "k_bwd_epi<": "bwd_epi", "k_bwd_pro<": "bwd_pro",
            "k_scores<": "scores", "k_gemm_tn": "gemm_tn", "k_bpr_chunks<": "bpr_chunks", "k_bpr_fwd<": "bpr_fwd",
-           "k_proj16<0>": "proj_fwd", "k_proj16<1>": "proj_dx", "k_tn128<": "tn128", "k_adam": "adam"}
+           "k_proj16<0>": "proj_fwd", "k_proj16<1>": "proj_dx", "k_tn128<": "tn128", "k_adam": "adam",
+           # the multi-head (aggregate-then-transform) edge passes: one kernel each
+           "k_fwd_x<": "fwd", "k_bwd_x<": "bwd_src", "k_bwd_g<": "bwd_src"}
 # one edge pass = its one-item-per-wave kernel + its four-items-per-wave short-item kernel
 PASSES = {"fwd": ("fwd_long", "fwd_short"), "bwd_src": ("bwd_src_long", "bwd_src_short")}
 
@@ -45,6 +50,12 @@ def main():
     res = {"note": "per-launch HBM-side bytes (L2 fabric requests, Infinity-Cache hits included); "
                    "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes",
            "config": config, "per_launch_bytes": {}, "raw_kib": {}}
+    for kv in sys.argv[5:]:
+        key, val = kv.split("=", 1)
+        try:
+            res[key] = float(val)
+        except ValueError:
+            res[key] = val
     for k in sorted(set(fetch) | set(write)):
         f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1)
         w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1)
