@@ -75,19 +75,22 @@ def parse():
 # algorithmic bytes per launch (DESIGN.md "Kernels and their rooflines")
 # ---------------------------------------------------------------------------
 def algo_bytes(kernel: str, N: int, E: int, H: int, C: int, dropout: bool, xform_k: int = 0,
-               dz_slot: bool = False, gather_g: bool = False) -> float:
+               dz_slot: bool = False, gather_g=False) -> float:
     """Algorithmic bytes per launch.  xform_k > 0: the aggregate-then-
     transform kernels (heads > 1, x rows of xform_k floats gathered instead of h rows).
     dz_slot: pass B reads each edge's dz position (the sharded layouts); otherwise dz is stored
     at the edge's own CSC position (no index read).  gather_g: the multi-head pass B gathers
     g_i (C floats) per edge and reads hs_j / writes acc_j (H * C floats) per source
-    (ppgat_xgat_bwd_edges_g) instead of gathering gt_i (H * xform_k floats)."""
+    (ppgat_xgat_bwd_edges_g) instead of gathering gt_i (H * xform_k floats); "gd" (deferred D,
+    ppgat_xgat_bwd_edges_gd) writes dalpha and beta dalpha per edge and no ds_src."""
     d = 4 if dropout else 0
     sl = 4 if dz_slot else 0
     if xform_k:
         K = xform_k
         if kernel == "fwd":    # k_fwd_x: col, s_src[H], x_j | sched, s_dst[H], agg[H, K], m, inv_l
             return E * (4 + 4 * H + 4 * K + d) + N * (12 + 4 * H + 4 * H * K + 8 * H)
+        if kernel == "bwd_src" and gather_g == "gd":  # deferred D: dalpha and beta dalpha out, no S
+            return E * (4 + sl + 16 * H + 4 * C + 8 * H + d) + N * (12 + 4 * H * C + 4 * H + 4 * H * C)
         if kernel == "bwd_src" and gather_g:  # k_bwd_g: row, (slot), nstate[H], g_i[C], dz[H] | sched, hs, s_src, acc, S
             return E * (4 + sl + 16 * H + 4 * C + 4 * H + d) + N * (12 + 4 * H * C + 4 * H + 4 * H * C + 4 * H)
         if kernel == "bwd_src":  # k_bwd_x: row, (slot), nstate[H], gt_i[H, K], dz[H] | sched, x, s_src, dx, S
@@ -362,7 +365,8 @@ def main():
     # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
     xform_k = C if (H > 1 and H * C > C and pkg.hip_ops.xgat_supported(C, H, C)) else 0
     # the g-gathering pass B runs where no halo exchange splits the backward (hip_ops.xgat_backward)
-    gather_g = bool(xform_k) and pkg.hip_ops._xgat_gather_g(C, H)
+    gather_mode = pkg.hip_ops._xgat_gather_mode(C, H) if xform_k else None
+    gather_g = gather_mode in ("g", "gd")
     kern = {k: _lib.profile_read(k) for k in ("scores", "fwd", "bwd_pro", "bwd_src", "bwd_epi", "bwd_red",
                                                "proj", "proj_bwd", "gemm_tn", "adam")}
     fused_ms = sum(ms for k, (ms, _) in kern.items() if k not in ("proj", "proj_bwd", "gemm_tn", "adam"))
@@ -380,9 +384,9 @@ def main():
         else:
             v = dg.fwd_view if dom == "fwd" else dg.bwd_view
         ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
-                        args.attn_dropout > 0, xform_k, dz_slot=part != "replicated", gather_g=gather_g)
+                        args.attn_dropout > 0, xform_k, dz_slot=part != "replicated", gather_g=gather_mode if gather_g else False)
     else:
-        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k, gather_g=gather_g)
+        ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k, gather_g=gather_mode if gather_g else False)
     achieved = ab / avg_s / 1e9
     traffic = None
     try:
@@ -394,7 +398,7 @@ def main():
         # PMC summaries are per workload (config, scale) and per multi-head backward formulation
         if tj_.get("config", 2) == args.config and tj_.get("scale", scale if args.config == 5 else None) == (
                 scale if args.config == 5 else None) and (
-                not xform_k or tj_.get("bwd_gather", "gt") == ("g" if gather_g else "gt")):
+                not xform_k or tj_.get("bwd_gather", "gt") == (gather_mode if gather_g else "gt")):
             traffic = tj_.get("per_launch_bytes", {}).get(dom)
     except Exception:
         pass

@@ -559,6 +559,28 @@ int ppgat_xgat_bwd_edges_g(const ppgat_schedule* src_sched, const int32_t* row, 
                            const float* s_src, const float* nstate, const float* g, int64_t ldg, float negative_slope,
                            float dropout_p, uint64_t seed, const uint64_t* seed_used, float* acc, float* S, int64_t lds,
                            float* dz, void* workspace, size_t workspace_bytes, void* stream);
+/* Deferred D (the default multi-head backward: no gt GEMM, no gt.agg prologue).  The prologue's
+ * D^h_i = gt^h_i . agg^h_i equals sum_j beta^h_ij dalpha^h_ij with dalpha = g_i . hs^h_j, so:
+ *   ppgat_xgat_nstate: nstate[i][h] = {s_dst, m, inv_l, D or 0 (D NULL)}, D [n_dst, heads];
+ *   ppgat_xgat_bwd_edges_gd: ppgat_xgat_bwd_edges_g's pass with dalpha and pdalpha = beta dalpha
+ *     stored per edge and head (at dz_slot, as dz) instead of dz and ds_src; acc as _g;
+ *   D = the destination sum of pdalpha (ppgat_bwd_dst_sum_csc / ppgat_bwd_dst_sum, heads H);
+ *   ppgat_xgat_bwd_dz: dz = alpha e'(z) (dm dalpha - D_i) in place over dalpha (by source over
+ *     the CSC; nstate with D) and S[j][h] = ds_src_j = sum of the source's dz (fixed order);
+ *   ds_dst = the destination sum of dz, as before.  Heads 2 or 4. */
+int ppgat_xgat_bwd_edges_gd(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                            const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                            const float* s_src, const float* nstate, const float* g, int64_t ldg,
+                            float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
+                            float* acc, float* dalpha, float* pdalpha, void* workspace, size_t workspace_bytes,
+                            void* stream);
+int ppgat_xgat_nstate(const float* s_dst, const float* m, const float* inv_l, const float* D, int64_t n_dst, int heads,
+                      float* nstate, void* stream);
+int ppgat_xgat_bwd_dz_workspace_bytes(int64_t n_hub_items, int heads, size_t* bytes);
+int ppgat_xgat_bwd_dz(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                      const int32_t* dz_slot, int64_t n_edges, int heads, const float* s_src, const float* nstate,
+                      float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used, float* dz,
+                      float* S, int64_t lds, void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_xgat_bwd_epilogue(const float* S, int64_t lds, const float* att_proj, int64_t n_dst, int in_channels,
                             int heads, float* dx, int64_t lddx, void* stream);
 int ppgat_xgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src,

@@ -131,6 +131,12 @@ SIGNATURES = {
     "ppgat_xgat_bwd_g_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_xgat_bwd_edges_g": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64,
                                        c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_bwd_edges_gd": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                        c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_nstate": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
+    "ppgat_xgat_bwd_dz_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
+    "ppgat_xgat_bwd_dz": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_u64, c_vp, c_vp, c_vp,
+                                  c_i64, c_vp, c_sz, c_vp]),
     "ppgat_xgat_bwd_epilogue": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp]),
     "ppgat_att_proj": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     "ppgat_rows_rank_update": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_vp]),

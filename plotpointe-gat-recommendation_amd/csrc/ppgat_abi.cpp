@@ -1224,6 +1224,79 @@ int ppgat_xgat_bwd_edges_g(const ppgat_schedule* src_sched, const int32_t* row, 
   return PPGAT_OK;
 }
 
+int ppgat_xgat_bwd_edges_gd(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                            const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                            const float* s_src, const float* nstate, const float* g, int64_t ldg,
+                            float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
+                            float* acc, float* dalpha, float* pdalpha, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  if (channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_edges_gd: shape");
+  if (n_edges < 0 || ldg < channels || (ldg % 4)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd: bad sizes");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
+  if (int rc = check_sched(src_sched, 0, "xgat_bwd_edges_gd")) return rc;
+  if (src_sched->n_items > 0 && (!hs || !s_src || !acc)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd: null pointer");
+  if (n_edges > 0 && (!row || !nstate || !g || !dalpha || !pdalpha))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd: null edge pointer");
+  if (dropout_p > 0.f && (!seed_used || (n_edges > 0 && !csc_eid)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd: dropout needs seed_used and csc_eid");
+  if (src_sched->n_hub_items > 0 && (!workspace || workspace_bytes < partial_bytes(src_sched->n_hub_items, heads, channels)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd: workspace too small");
+  if (!al16(hs) || !al16(g) || !al16(acc)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_edges_gd: 16-byte aligned rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{src_sched->item_row, src_sched->item_beg, src_sched->item_end, src_sched->n_items,
+                           src_sched->n_hub_items, src_sched->n_long_items};
+  Timed t(PPGAT_K_BWD_SRC, st);
+  hipError_t e = ppgat::xgat_bwd_edges_g(it, row, csc_eid, dz_slot, hs, channels, heads, s_src, nstate, g, ldg,
+                                         negative_slope, dropout_p, seed, seed_used, acc, nullptr, 0, dalpha,
+                                         static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
+                                         src_sched->n_hubs, st, pdalpha);
+  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_edges_gd");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_nstate(const float* s_dst, const float* m, const float* inv_l, const float* D, int64_t n_dst, int heads,
+                      float* nstate, void* stream) {
+  if (n_dst < 0 || heads < 1) return fail(PPGAT_ERR_INVALID, "xgat_nstate: bad sizes");
+  if (n_dst > 0 && (!s_dst || !m || !inv_l || !nstate)) return fail(PPGAT_ERR_INVALID, "xgat_nstate: null pointer");
+  if (!al16(nstate)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_nstate: 16-byte aligned nstate");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_BWD_PRO, st);
+  hipError_t e = ppgat::xgat_nstate(s_dst, m, inv_l, D, n_dst, heads, nstate, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_nstate");
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_dz_workspace_bytes(int64_t n_hub_items, int heads, size_t* bytes) {
+  if (!bytes || n_hub_items < 0 || heads < 1) return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz_workspace_bytes: bad sizes");
+  *bytes = (size_t)n_hub_items * heads * sizeof(float);
+  return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_dz(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                      const int32_t* dz_slot, int64_t n_edges, int heads, const float* s_src, const float* nstate,
+                      float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used, float* dz,
+                      float* S, int64_t lds, void* workspace, size_t workspace_bytes, void* stream) {
+  if (heads != 2 && heads != 4) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_dz: heads 2 or 4");
+  if (n_edges < 0 || lds < heads) return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz: bad sizes / leading dimension");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
+  if (int rc = check_sched(src_sched, 0, "xgat_bwd_dz")) return rc;
+  if (src_sched->n_items > 0 && (!s_src || !S)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz: null pointer");
+  if (n_edges > 0 && (!row || !nstate || !dz)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz: null edge pointer");
+  if (dropout_p > 0.f && (!seed_used || (n_edges > 0 && !csc_eid)))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz: dropout needs seed_used and csc_eid");
+  if (src_sched->n_hub_items > 0 && (!workspace || workspace_bytes < (size_t)src_sched->n_hub_items * heads * 4))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const ppgat::ItemsArg it{src_sched->item_row, src_sched->item_beg, src_sched->item_end, src_sched->n_items,
+                           src_sched->n_hub_items, src_sched->n_long_items};
+  Timed t(PPGAT_K_BWD_EPI, st);
+  hipError_t e = ppgat::xgat_bwd_dz(it, row, csc_eid, dz_slot, heads, s_src, nstate, negative_slope, dropout_p, seed,
+                                    seed_used, dz, S, lds, static_cast<float*>(workspace), src_sched->hub_row,
+                                    src_sched->hub_ptr, src_sched->n_hubs, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_bwd_dz");
+  return PPGAT_OK;
+}
+
 int ppgat_xgat_bwd_epilogue(const float* S, int64_t lds, const float* att_proj, int64_t n_dst, int in_channels,
                             int heads, float* dx, int64_t lddx, void* stream) {
   if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_epilogue: shape");

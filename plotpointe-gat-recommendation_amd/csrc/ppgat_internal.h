@@ -207,7 +207,13 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                             const float* hs, int C, int H, const float* s_src, const float* nstate, const float* g,
                             int64_t ldg, float slope, float p, uint64_t seed, const uint64_t* seed_in, float* acc,
                             float* S, int64_t lds, float* dz, float* partial, const int32_t* hub_row,
-                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
+                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz = nullptr);
+hipError_t xgat_nstate(const float* s_dst, const float* m, const float* invl, const float* D, int64_t n, int H,
+                       float* nstate, hipStream_t st);
+hipError_t xgat_bwd_dz(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr, int H,
+                       const float* s_src, const float* nstate, float slope, float p, uint64_t seed,
+                       const uint64_t* seed_in, float* dz, float* S, int64_t lds, float* partial,
+                       const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
 hipError_t xgat_bwd_epi(const float* S, int64_t lds, const float* A_dst, int64_t n, int K, int H, float* dx,
                         int64_t lddx, hipStream_t st);
 hipError_t xgat_wgrad(const float* G, const float* GV, const float* W, const float* att_src, const float* att_dst,

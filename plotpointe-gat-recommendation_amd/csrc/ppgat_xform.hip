@@ -1484,7 +1484,10 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
                                                const float* __restrict__ g, int64_t ldg, float slope, float p,
                                                float inv_keep, uint64_t seed, const uint64_t* __restrict__ seed_in,
                                                float* __restrict__ acc_out, float* __restrict__ S, int64_t lds,
-                                               float* __restrict__ dz, float* __restrict__ partial) {
+                                               float* __restrict__ dz, float* __restrict__ partial,
+                                               float* __restrict__ pz) {
+  // pz != NULL (deferred D): dz receives dalpha = g_i . hs_j and pz beta * dalpha per edge and
+  // head (D_i = sum_j beta dalpha by a destination sum, dz by k_xgat_dz); no ds_src here
   static_assert(C == 256 && H <= 4, "k_bwd_g: C == 256, H <= 4");
   constexpr int U = 16 / H;  // edges per reduction group (16 partial dots per lane)
   if (p > 0.f) seed = *seed_in;
@@ -1561,11 +1564,17 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
         const int q = q0 + u;
         if (q < n) {
           const float4 rb = recH[wv][h][q];
-          const float dzv = fmaf(rb.y, dot, -rb.z);
+          const int64_t o = (int64_t)recA[wv][q].y * H + h;
+          if (pz != nullptr) {
+            dz[o] = dot;
+            pz[o] = rb.x * dot;
+          } else {
+            const float dzv = fmaf(rb.y, dot, -rb.z);
 #pragma unroll
-          for (int c = 0; c < H; ++c)
-            if (c == h) dsa[c] += dzv;
-          dz[(int64_t)recA[wv][q].y * H + h] = dzv;
+            for (int c = 0; c < H; ++c)
+              if (c == h) dsa[c] += dzv;
+            dz[o] = dzv;
+          }
         }
       }
     }
@@ -1590,12 +1599,89 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) st4(acc_out + (j * H + h) * C + lane * 4, acc[h]);
-  if (lane < H) {
+  if (lane < H && S != nullptr) {  // deferred D: ds_src comes from k_xgat_dz
     float v = ds[0];
 #pragma unroll
     for (int h = 1; h < H; ++h) v = lane == h ? ds[h] : v;
     S[j * lds + lane] = v;
   }
+}
+
+// nstate[i][h] = {s_dst, m, inv_l, D or 0} (the deferred-D backward builds it twice: without D
+// for k_bwd_g, with D for k_xgat_dz)
+__global__ void __launch_bounds__(256) k_xgat_nstate(const float* __restrict__ s_dst, const float* __restrict__ m,
+                                                     const float* __restrict__ invl, const float* __restrict__ D,
+                                                     int64_t n, float4* __restrict__ nstate) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  nstate[t] = make_float4(s_dst[t], m[t], invl[t], D != nullptr ? D[t] : 0.f);
+}
+
+// deferred-D backward, by SOURCE over the CSC: dz = alpha e'(z) (dm dalpha - D_i) per edge and
+// head, in place over dalpha (the formula and rounding of k_bwd_g's dz), and ds_src_j = sum of
+// the source's dz -- 16 lanes per source item, lane sums in edge order, then the 16-lane tree;
+// hub pieces leave a partial that k_xgat_dz_merge adds up in piece order
+template <int H>
+__global__ void __launch_bounds__(256) k_xgat_dz(XItems it, const int32_t* __restrict__ row,
+                                                 const int32_t* __restrict__ csc_eid,
+                                                 const int32_t* __restrict__ csc2csr, const float* __restrict__ s_src,
+                                                 const float4* __restrict__ nstate, float slope, float p,
+                                                 float inv_keep, uint64_t seed, const uint64_t* __restrict__ seed_in,
+                                                 float* __restrict__ dz, float* __restrict__ S, int64_t lds,
+                                                 float* __restrict__ partial) {
+  if (p > 0.f) seed = *seed_in;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t w = t >> 4;
+  const int l = (int)(t & 15);
+  const bool live = w < it.n_items;
+  float ds[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ds[h] = 0.f;
+  int64_t j = 0;
+  if (live) {
+    j = it.row[w];
+    float ss[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) ss[h] = s_src[j * H + h];
+    for (int k = it.beg[w] + l; k < it.end[w]; k += 16) {
+      const int64_t i = row[k];
+      const int64_t slot = csc2csr != nullptr ? (int64_t)csc2csr[k] : (int64_t)k;
+      const uint32_t e_id = p > 0.f ? (uint32_t)csc_eid[k] : 0u;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float4 st = nstate[i * H + h];  // {s_dst, m, inv_l, D}
+        const float z = ss[h] + st.x;
+        const float af = expf(lrelu(z, slope) - st.y) * st.z;
+        const float dm = p > 0.f ? drop_scale(seed, e_id, (uint32_t)h, p, inv_keep) : 1.f;
+        const float a1 = af * dlrelu(z, slope);
+        const float dzv = fmaf(a1 * dm, dz[slot * H + h], -(a1 * st.w));
+        dz[slot * H + h] = dzv;
+        ds[h] += dzv;
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const float x = group_reduce<Op::Sum, 1, 8>(ds[h]);  // the 16 lanes of a DPP row
+    if (live && l == 0) {
+      if (w < it.n_hub_items) partial[w * H + h] = x;
+      else S[j * lds + h] = x;
+    }
+  }
+}
+
+template <int H>
+__global__ void __launch_bounds__(256) k_xgat_dz_merge(const int32_t* __restrict__ hub_row,
+                                                       const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
+                                                       const float* __restrict__ partial, float* __restrict__ S,
+                                                       int64_t lds) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_hubs * H) return;
+  const int64_t hb = t / H;
+  const int h = (int)(t % H);
+  float x = 0.f;
+  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) x += partial[(int64_t)q * H + h];
+  S[(int64_t)hub_row[hb] * lds + h] = x;
 }
 
 // hub sources of k_bwd_g: pieces summed in piece order
@@ -1621,7 +1707,7 @@ __global__ void __launch_bounds__(256) k_bwd_g_merge(const int32_t* __restrict__
 #pragma unroll
   for (int h = 0; h < H; ++h) st4(acc_out + (j * H + h) * C + lane * 4, acc[h]);
   const float ds[4] = {d.x, d.y, d.z, d.w};
-  if (lane < H) S[j * lds + lane] = ds[lane];
+  if (lane < H && S != nullptr) S[j * lds + lane] = ds[lane];
 }
 
 // dx_i += sum_h ds_dst_i^h A_dst[h] over the destination rows (S[i][H + h] = ds_dst)
@@ -2072,17 +2158,42 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                             const float* hs, int C, int H, const float* s_src, const float* nstate, const float* g,
                             int64_t ldg, float slope, float p, uint64_t seed, const uint64_t* seed_in, float* acc,
                             float* S, int64_t lds, float* dz, float* partial, const int32_t* hub_row,
-                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   if (it.n_items > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
                                    row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
-                                   slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial));
+                                   slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz));
   if (n_hubs > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge<256, HH>), dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st,
                                    hub_row, hub_ptr, n_hubs, partial, acc, S, lds));
   (void)C;
+  return hipGetLastError();
+}
+
+hipError_t xgat_nstate(const float* s_dst, const float* m, const float* invl, const float* D, int64_t n, int H,
+                       float* nstate, hipStream_t st) {
+  const int64_t nh = n * H;
+  if (nh > 0)
+    hipLaunchKernelGGL(k_xgat_nstate, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, s_dst, m, invl, D, nh,
+                       reinterpret_cast<float4*>(nstate));
+  return hipGetLastError();
+}
+
+hipError_t xgat_bwd_dz(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr, int H,
+                       const float* s_src, const float* nstate, float slope, float p, uint64_t seed,
+                       const uint64_t* seed_in, float* dz, float* S, int64_t lds, float* partial,
+                       const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+  if (it.n_items > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz<HH>), dim3((unsigned)((it.n_items * 16 + 255) / 256)), dim3(256), 0, st,
+                                   its, row, csc_eid, csc2csr, s_src, reinterpret_cast<const float4*>(nstate), slope, p,
+                                   inv_keep, seed, seed_in, dz, S, lds, partial));
+  if (n_hubs > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz_merge<HH>), dim3((unsigned)((n_hubs * HH + 255) / 256)), dim3(256), 0,
+                                   st, hub_row, hub_ptr, n_hubs, partial, S, lds));
   return hipGetLastError();
 }
 

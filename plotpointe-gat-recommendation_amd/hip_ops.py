@@ -1137,17 +1137,20 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     dev = x.device
     st = _lib.stream_handle(dev)
     g = g.contiguous()
+    E = v.n_edges
+    S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
+    dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
+    mode = _xgat_gather_mode(C, H)
+    if mode == "gd":
+        return _xgat_backward_deferred_d(lib, saved, g, S, dz, nstate, want_bias_grad, halo_hook, st)
     Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
                "xgat_weights")
     gt = gemm_nn(g, Wg, 0, H * K)
-    nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_bwd_prologue(gt.data_ptr(), agg.data_ptr(), s_dst.data_ptr(), m.data_ptr(),
                                            inv_l.data_ptr(), v.n_dst, K, H, nstate.data_ptr(), st), "xgat_bwd_prologue")
-    E = v.n_edges
-    S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
-    dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
-    if _xgat_gather_g(C, H):
+    if mode == "g":
         # gather g_i per edge (C floats) instead of gt_i (H * C_in): hs = x W^T / H per source,
         # the per-head message gradient acc [n_src, H * C], then dx = acc W / H + S A_att with the
         # attention terms in the GEMM's epilogue
@@ -1191,23 +1194,106 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
 
 
+def _xgat_gather_mode(C: int, H: int) -> str:
+    """Which multi-head backward runs (read per call): "gd" (default) gathers g_i per edge and
+    defers D (no gt GEMM: ppgat_xgat_bwd_edges_gd + D by a destination sum + ppgat_xgat_bwd_dz);
+    PPGAT_XGAT_GATHER=g gathers g_i with D from the gt GEMM's prologue (ppgat_xgat_bwd_edges_g);
+    PPGAT_XGAT_GATHER=gt gathers gt_i (ppgat_xgat_bwd_edges, round 2's pass).  DESIGN.md §4.2."""
+    mode = os.environ.get("PPGAT_XGAT_GATHER", "gd")
+    if C != 256 or H not in (2, 4):
+        return "gt"
+    return mode if mode in ("g", "gt") else "gd"
+
+
 def _xgat_gather_g(C: int, H: int) -> bool:
-    """The g-gathering backward edge pass (ppgat_xgat_bwd_edges_g), single-GPU and sharded;
-    PPGAT_XGAT_GATHER=gt keeps the gt-gathering pass (ppgat_xgat_bwd_edges)."""
-    return C == 256 and H in (2, 4) and os.environ.get("PPGAT_XGAT_GATHER", "g") != "gt"
+    """True when the backward edge pass gathers g_i (either "g" or the default "gd")."""
+    return _xgat_gather_mode(C, H) != "gt"
 
 
-def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st):
-    """ds_dst = per-destination sums of dz into S[:, H:2H] (fixed order)."""
+def _xgat_backward_deferred_d(lib, saved: dict, g, S, dz, nstate, want_bias_grad: bool, halo_hook, st):
+    """The default multi-head backward: D^h_i = sum_j beta dalpha from the edge
+    pass itself instead of gt^h_i . agg^h_i, so neither gt = g W_grad nor its prologue runs."""
+    x, W, A = saved["x"], saved["W"], saved["A"]
+    s_src, s_dst, m, inv_l, v = saved["s_src"], saved["s_dst"], saved["m"], saved["inv_l"], saved["v"]
+    H, C, K, slope, p, seed, has_bias = saved["meta"]
+    dev = x.device
+    E = v.n_edges
+    n0 = v.n_dst
+    seed_buf = saved["seed_buf"]
+    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H,
+                                     nstate.data_ptr(), st), "xgat_nstate")
+    hs = gemm_nn(x, W, 1, H * C, alpha=1.0 / H)
+    acc = torch.empty(v.n_src, H * C, dtype=torch.float32, device=dev)
+    pdal = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    split = halo_hook is not None and v.bwd_sched_halo is not None
+    scheds = [(v.bwd_sched_halo, n0), (v.bwd_sched_own, 0)] if split else [(v.bwd_sched, 0)]
+    for sched, base in scheds:  # dalpha (into dz) and beta dalpha per edge, acc per source
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = sched.cstruct()
+        _lib.check(lib.ppgat_xgat_bwd_edges_gd(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                               _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None,
+                                               E, C, H, hs.data_ptr() + 4 * base * H * C,
+                                               s_src.data_ptr() + 4 * base * H, nstate.data_ptr(), g.data_ptr(), C,
+                                               float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                               acc.data_ptr() + 4 * base * H * C, dz.data_ptr(), pdal.data_ptr(),
+                                               ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_gd")
+    del hs
+    D = torch.empty(max(n0, 1), H, dtype=torch.float32, device=dev)
+    _xgat_dst_sum(lib, v, pdal, D, H, E, st, col0=0, ld=H)  # D_i = sum_j beta dalpha
+    del pdal
+    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), D.data_ptr(), n0, H,
+                                     nstate.data_ptr(), st), "xgat_nstate")
+
+    def dz_pass(sched, base):  # dz in place over dalpha, ds_src into S[:, :H]
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_bwd_dz_workspace_bytes(sched.n_hub_items, H, ctypes.byref(nbytes)), "xgat_dz_ws")
+        ws = torch.empty(max(int(nbytes.value), 4), dtype=torch.uint8, device=dev)
+        cs = sched.cstruct()
+        _lib.check(lib.ppgat_xgat_bwd_dz(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                         _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None, E, H,
+                                         s_src.data_ptr() + 4 * base * H, nstate.data_ptr(), float(slope), float(p),
+                                         int(seed) & (2**64 - 1), _lib.ptr(seed_buf), dz.data_ptr(),
+                                         S.data_ptr() + 4 * base * 2 * H, 2 * H, ws.data_ptr(), nbytes.value, st),
+                   "xgat_bwd_dz")
+
+    dx = torch.empty(v.n_src, K, dtype=torch.float32, device=dev)
+    A2 = A.view(2 * H, K)
+    if split:
+        # the halo sources first: their rows of dx (no destination terms) go back to their owners
+        # while the own sources' dz pass, the destination sums and the GEMMs run
+        dz_pass(v.bwd_sched_halo, n0)
+        if v.n_src > n0:
+            gemm_nn(acc[n0:], W, 0, K, alpha=1.0 / H, out=dx[n0:], rank=(S[n0:, :H], A2[:H]))
+        halo_hook(dx[n0:])
+        dz_pass(v.bwd_sched_own, 0)
+        _xgat_dst_sum(lib, v, dz, S, H, E, st)
+        gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, out=dx[:n0], rank=(S[:n0], A2))
+    else:
+        dz_pass(v.bwd_sched, 0)
+        _xgat_dst_sum(lib, v, dz, S, H, E, st)
+        gemm_nn(acc, W, 0, K, alpha=1.0 / H, out=dx, rank=(S, A2))
+        if halo_hook is not None:
+            halo_hook(dx[n0:])
+    del acc
+    return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
+
+
+def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[int] = None, ld: Optional[int] = None):
+    """Per-destination sums of dz (per edge and head) into S[:, col0:col0 + H] with row stride
+    ld (default: ds_dst into S[:, H:2H], ld 2H), fixed order."""
     dev = dz.device
+    col0 = H if col0 is None else col0
+    ld = 2 * H if ld is None else ld
     fs = v.fwd_sched.cstruct()
     dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
     if v.dz_slot is None:
         _lib.check(lib.ppgat_bwd_dst_sum_csc(ctypes.byref(fs), v.n_dst, E, H, dz.data_ptr(),
-                                             _lib.ptr(v.csr2csc) if E else None, S.data_ptr() + 4 * H, 2 * H,
+                                             _lib.ptr(v.csr2csc) if E else None, S.data_ptr() + 4 * col0, ld,
                                              dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum_csc")
     else:
-        _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * H, 2 * H,
+        _lib.check(lib.ppgat_bwd_dst_sum(ctypes.byref(fs), v.n_dst, H, dz.data_ptr(), S.data_ptr() + 4 * col0, ld,
                                          dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 

@@ -97,7 +97,7 @@ def _graph(rng, n, e, hub_rows=0):
     return np.stack([src, dst]).astype(np.int64)
 
 
-@pytest.mark.parametrize("gather", ["g", "gt"])
+@pytest.mark.parametrize("gather", ["gd", "g", "gt"])
 @pytest.mark.parametrize("n,e,C,heads,p,hubs", [(2000, 20_000, 256, 4, 0.0, 0), (1500, 30_000, 256, 4, 0.2, 3),
                                                 (1200, 12_000, 128, 2, 0.1, 0), (900, 25_000, 256, 2, 0.0, 2)])
 def test_gatconv_aggregate_then_transform_vs_oracle(pkg, oracle, cuda, monkeypatch, n, e, C, heads, p, hubs, gather):

@@ -37,7 +37,7 @@ for s in $STEPS; do
     prof5)  (cd /tmp && run rocprof_cfg5 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof5" -o run --output-format csv -- python "$R/bench.py" --config 5 --steps 5 --warmup 2) ;;
     pmc5)  (cd /tmp && run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc5_fetch" -o fetch -- python "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
            (cd /tmp && run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc5_write" -o write -- python "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
-           python "$R/tools/pmc_summary.py" "$OUT/pmc5_fetch" "$OUT/pmc5_write" "$OUT/cfg5_pmc_traffic.json" 5 scale=0.125 bwd_gather=g > "$OUT/pmc5_summary.log" 2>&1 ;;
+           python "$R/tools/pmc_summary.py" "$OUT/pmc5_fetch" "$OUT/pmc5_write" "$OUT/cfg5_pmc_traffic.json" 5 scale=0.125 bwd_gather=gd > "$OUT/pmc5_summary.log" 2>&1 ;;
     fusion) run bench_fusion 300 python tools/bench_fusion.py ;;
     prof)  (cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --steps 10 --warmup 3 --cpu-baseline-seconds 0) ;;
     pmc)   (cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o fetch -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \
