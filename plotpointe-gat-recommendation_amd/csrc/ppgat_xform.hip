@@ -1619,10 +1619,13 @@ __global__ void __launch_bounds__(256) k_xgat_nstate(const float* __restrict__ s
 
 // deferred-D backward, by SOURCE over the CSC: dz = alpha e'(z) (dm dalpha - D_i) per edge and
 // head, in place over dalpha (the formula and rounding of k_bwd_g's dz), and ds_src_j = sum of
-// the source's dz -- 16 lanes per source item, lane sums in edge order, then the 16-lane tree;
-// hub pieces leave a partial that k_xgat_dz_merge adds up in piece order
-template <int H>
-__global__ void __launch_bounds__(256) k_xgat_dz(XItems it, const int32_t* __restrict__ row,
+// the source's dz.  LPI lanes per source item over items [w0, w1): 16 for the hub and long items,
+// 4 for the short ones (<= 16 edges: four rows per lane group keep four times as many items in
+// flight).  Each lane takes every LPI-th edge, four at a time with all their loads issued
+// first, summed in edge order, then the LPI-lane tree; hub pieces leave a partial that
+// k_xgat_dz_merge adds up in piece order.
+template <int H, int LPI>
+__global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t w1, const int32_t* __restrict__ row,
                                                  const int32_t* __restrict__ csc_eid,
                                                  const int32_t* __restrict__ csc2csr, const float* __restrict__ s_src,
                                                  const float4* __restrict__ nstate, float slope, float p,
@@ -1631,9 +1634,9 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, const int32_t* __res
                                                  float* __restrict__ partial) {
   if (p > 0.f) seed = *seed_in;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t w = t >> 4;
-  const int l = (int)(t & 15);
-  const bool live = w < it.n_items;
+  const int64_t w = w0 + t / LPI;
+  const int l = (int)(t % LPI);
+  const bool live = w < w1;
   float ds[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) ds[h] = 0.f;
@@ -1643,26 +1646,46 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, const int32_t* __res
     float ss[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) ss[h] = s_src[j * H + h];
-    for (int k = it.beg[w] + l; k < it.end[w]; k += 16) {
-      const int64_t i = row[k];
-      const int64_t slot = csc2csr != nullptr ? (int64_t)csc2csr[k] : (int64_t)k;
-      const uint32_t e_id = p > 0.f ? (uint32_t)csc_eid[k] : 0u;
+    const int ce = it.end[w];
+    for (int k0 = it.beg[w] + l; k0 < ce; k0 += 4 * LPI) {
+      int64_t ii[4], sl[4];
+      uint32_t e_id[4];
 #pragma unroll
-      for (int h = 0; h < H; ++h) {
-        const float4 st = nstate[i * H + h];  // {s_dst, m, inv_l, D}
-        const float z = ss[h] + st.x;
-        const float af = expf(lrelu(z, slope) - st.y) * st.z;
-        const float dm = p > 0.f ? drop_scale(seed, e_id, (uint32_t)h, p, inv_keep) : 1.f;
-        const float a1 = af * dlrelu(z, slope);
-        const float dzv = fmaf(a1 * dm, dz[slot * H + h], -(a1 * st.w));
-        dz[slot * H + h] = dzv;
-        ds[h] += dzv;
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * LPI < ce ? k0 + u * LPI : k0;
+        ii[u] = row[k];
+        sl[u] = csc2csr != nullptr ? (int64_t)csc2csr[k] : (int64_t)k;
+        e_id[u] = p > 0.f ? (uint32_t)csc_eid[k] : 0u;
+      }
+      float4 st[4][H];
+      float dv[4][H];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          st[u][h] = nstate[ii[u] * H + h];  // {s_dst, m, inv_l, D}
+          dv[u][h] = dz[sl[u] * H + h];
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u * LPI < ce) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            const float z = ss[h] + st[u][h].x;
+            const float af = expf(lrelu(z, slope) - st[u][h].y) * st[u][h].z;
+            const float dm = p > 0.f ? drop_scale(seed, e_id[u], (uint32_t)h, p, inv_keep) : 1.f;
+            const float a1 = af * dlrelu(z, slope);
+            const float dzv = fmaf(a1 * dm, dv[u][h], -(a1 * st[u][h].w));
+            dz[sl[u] * H + h] = dzv;
+            ds[h] += dzv;
+          }
+        }
       }
     }
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) {
-    const float x = group_reduce<Op::Sum, 1, 8>(ds[h]);  // the 16 lanes of a DPP row
+    const float x = group_reduce<Op::Sum, 1, LPI / 2>(ds[h]);  // the LPI lanes of the item
     if (live && l == 0) {
       if (w < it.n_hub_items) partial[w * H + h] = x;
       else S[j * lds + h] = x;
@@ -2187,10 +2210,19 @@ hipError_t xgat_bwd_dz(const ItemsArg& it, const int32_t* row, const int32_t* cs
                        const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-  if (it.n_items > 0)
-    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz<HH>), dim3((unsigned)((it.n_items * 16 + 255) / 256)), dim3(256), 0, st,
-                                   its, row, csc_eid, csc2csr, s_src, reinterpret_cast<const float4*>(nstate), slope, p,
-                                   inv_keep, seed, seed_in, dz, S, lds, partial));
+  // [0, wl): hub pieces and long items, 16 lanes each; [wl, n_items): short items, 4 lanes each
+  const int64_t wl = it.n_long_items >= it.n_hub_items && it.n_long_items <= it.n_items ? it.n_long_items
+                                                                                         : it.n_items;
+  if (wl > 0)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz<HH, 16>), dim3((unsigned)((wl * 16 + 255) / 256)), dim3(256), 0, st,
+                                   its, (int64_t)0, wl, row, csc_eid, csc2csr, s_src,
+                                   reinterpret_cast<const float4*>(nstate), slope, p, inv_keep, seed, seed_in, dz, S,
+                                   lds, partial));
+  if (it.n_items > wl)
+    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz<HH, 4>), dim3((unsigned)(((it.n_items - wl) * 4 + 255) / 256)),
+                                   dim3(256), 0, st, its, wl, it.n_items, row, csc_eid, csc2csr, s_src,
+                                   reinterpret_cast<const float4*>(nstate), slope, p, inv_keep, seed, seed_in, dz, S,
+                                   lds, partial));
   if (n_hubs > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz_merge<HH>), dim3((unsigned)((n_hubs * HH + 255) / 256)), dim3(256), 0,
                                    st, hub_row, hub_ptr, n_hubs, partial, S, lds));
