@@ -519,8 +519,9 @@ int ppgat_gemm_tn_seg(const float* A, int64_t lda, const float* b0, int64_t ldb0
   if (split < 0 || split > n) return fail(PPGAT_ERR_INVALID, "gemm_tn: split outside [0, n]");
   if (lda < m || ldb0 < k || (b1 && ldb1 < k) || (nv > 0 && ldv < nv))
     return fail(PPGAT_ERR_INVALID, "gemm_tn: bad leading dimension");
-  // the skinny kernel reads A by scalars: only B's rows need 16-byte alignment there
-  const bool skinny = m <= 16 && !colsum && nv == 0 && !(b1 && split < n) && (k % 4) == 0 && k <= 1024;
+  // the skinny kernel reads A (and V) by scalars: only B's rows need 16-byte alignment there;
+  // it takes every m <= 16 product, with or without the extras (path-independent bits)
+  const bool skinny = m <= 16 && nv <= 16 && !(b1 && split < n) && (k % 4) == 0 && k <= 1024;
   if ((!skinny && ((lda % 4) || !al16(A))) || (ldb0 % 4) || (b1 && (ldb1 % 4)) || !al16(b0) || (b1 && !al16(b1)))
     return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn: A/B rows must be 16-byte aligned");
   if (!out || (n > 0 && (!A || !b0)) || (nv > 0 && (!V || !vout)))

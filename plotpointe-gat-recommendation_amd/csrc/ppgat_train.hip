@@ -763,13 +763,18 @@ __global__ void __launch_bounds__(256) k_tn_skinny(const float* __restrict__ A, 
   }
 }
 
-static bool skinny_ok(int M, int K, const float* colsum, const float* V) {
-  return M <= 16 && K % 4 == 0 && K <= 1024 && colsum == nullptr && V == nullptr;
-}
+// A^T B with M <= 16 always takes the skinny kernel, extras or not, so the product's bits do
+// not depend on whether colsum(A) / V^T B are requested: V^T B is a second skinny product
+// (nv <= 16) and colsum(A) = A^T 1 a third one against a broadcast row of ones (ldb = 0)
+static bool skinny_ok(int M, int K, int nv) { return M <= 16 && K % 4 == 0 && K <= 1024 && nv <= 16; }
 static int64_t skinny_blocks(int64_t N) {
   int64_t b = (N + 511) / 512;
   if (b > 2048) b = 2048;
   return b < 1 ? 1 : b;
+}
+static size_t skinny_ws(int64_t N, int K) {
+  const int Kp = K < 4 ? 4 : K;
+  return align_up((size_t)skinny_blocks(N) * 16 * Kp * 4) + align_up(16 + 16 * 4 * 4);
 }
 
 // ---- dW = A^T B ----
@@ -787,29 +792,47 @@ size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv) {
   const int64_t s = gemm_splits(N, M, K);
   const size_t tiled = align_up((size_t)s * M * K * 4) + align_up((size_t)s * M * 4) +
                        align_up((size_t)s * (nv > 0 ? nv : 1) * K * 4);
-  const size_t skinny = M <= 16 ? align_up((size_t)skinny_blocks(N) * M * K * 4) : 0;
+  const size_t skinny = skinny_ok(M, K, nv) ? skinny_ws(N, K) : 0;
   return tiled > skinny ? tiled : skinny;
+}
+
+// out [M, K] = A^T B through k_tn_skinny + the ordered split reduction (part: workspace)
+static hipError_t skinny_product(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K,
+                                 float* out, float* part, hipStream_t st) {
+  int64_t blocks = skinny_blocks(N);
+  const int64_t rpb = (N + blocks - 1) / blocks;
+  blocks = (N + rpb - 1) / rpb;
+  const int MV = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : M <= 8 ? 8 : 16;
+#define PPGAT_SKINNY(MV_) \
+  hipLaunchKernelGGL((k_tn_skinny<MV_>), dim3((unsigned)blocks), dim3(256), 0, st, A, lda, B, ldb, N, M, K, rpb, part)
+  if (MV == 1) PPGAT_SKINNY(1); else if (MV == 2) PPGAT_SKINNY(2); else if (MV == 4) PPGAT_SKINNY(4);
+  else if (MV == 8) PPGAT_SKINNY(8); else PPGAT_SKINNY(16);
+#undef PPGAT_SKINNY
+  SplitReduceArg ra{};
+  const int64_t elems = (int64_t)M * K;
+  ra.part[0] = part; ra.out[0] = out; ra.elems[0] = elems; ra.blocks[0] = (elems + 63) / 64;
+  for (int q = 1; q < 3; ++q) { ra.part[q] = part; ra.out[q] = out; ra.elems[q] = 0; ra.blocks[q] = ra.blocks[0]; }
+  hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)ra.blocks[0]), dim3(1024), 0, st, ra, blocks);
+  return hipGetLastError();
 }
 
 hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
                    float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st) {
-  if (skinny_ok(M, K, colsum, nv > 0 ? V : nullptr) && N > 0) {
-    int64_t blocks = skinny_blocks(N);
-    const int64_t rpb = (N + blocks - 1) / blocks;
-    blocks = (N + rpb - 1) / rpb;
-    float* part = static_cast<float*>(ws);
-    const int MV = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : M <= 8 ? 8 : 16;
-#define PPGAT_SKINNY(MV_) \
-  hipLaunchKernelGGL((k_tn_skinny<MV_>), dim3((unsigned)blocks), dim3(256), 0, st, A, lda, B, ldb, N, M, K, rpb, part)
-    if (MV == 1) PPGAT_SKINNY(1); else if (MV == 2) PPGAT_SKINNY(2); else if (MV == 4) PPGAT_SKINNY(4);
-    else if (MV == 8) PPGAT_SKINNY(8); else PPGAT_SKINNY(16);
-#undef PPGAT_SKINNY
-    SplitReduceArg ra{};
-    const int64_t elems = (int64_t)M * K;
-    ra.part[0] = part; ra.out[0] = out; ra.elems[0] = elems; ra.blocks[0] = (elems + 63) / 64;
-    for (int q = 1; q < 3; ++q) { ra.part[q] = part; ra.out[q] = out; ra.elems[q] = 0; ra.blocks[q] = ra.blocks[0]; }
-    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)ra.blocks[0]), dim3(1024), 0, st, ra, blocks);
-    return hipGetLastError();
+  if (skinny_ok(M, K, (V && nv > 0) ? nv : 0) && N > 0) {
+    // workspace: [split partials | ones float4 | colsum staging M x 4] (skinny_ws)
+    char* p = static_cast<char*>(ws);
+    float* part = reinterpret_cast<float*>(p);
+    float* ones = reinterpret_cast<float*>(p + align_up((size_t)skinny_blocks(N) * 16 * K * 4));
+    float* cs4 = ones + 4;
+    hipError_t e = skinny_product(A, lda, B, ldb, N, M, K, out, part, st);
+    if (e == hipSuccess && V && nv > 0) e = skinny_product(V, ldv, B, ldb, N, nv, K, vout, part, st);
+    if (e == hipSuccess && colsum) {
+      e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ones), 0x3f800000, 4, st);
+      if (e == hipSuccess) e = skinny_product(A, lda, ones, 0, N, M, 4, cs4, part, st);
+      if (e == hipSuccess)
+        e = hipMemcpy2DAsync(colsum, sizeof(float), cs4, 4 * sizeof(float), sizeof(float), M, hipMemcpyDeviceToDevice, st);
+    }
+    return e;
   }
   const int64_t s = gemm_splits(N, M, K);
   const int64_t rows = ((N + s - 1) / s + kNB - 1) / kNB * kNB;

@@ -771,6 +771,15 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     split = B.size(0)
     nb = split + (B_items.size(0) if B_items is not None else 0)
     _require(A.size(0) == nb, "gemm_tn: A [N,M], B [N,K]")
+    if not all(_aligned_rows(t) for t in (A, B) + ((B_items,) if B_items is not None else ())):
+        # the kernels read 16-byte row segments: zero-pad the columns of any operand whose rows
+        # are not 16-byte aligned (e.g. the [B, B] logit gradient of a ragged InfoNCE batch);
+        # the zero columns only add output rows / columns that are dropped here
+        M0, K0 = A.size(1), B.size(1)
+        out, cs, vout = gemm_tn(_pad_cols4(A), _pad_cols4(B), want_colsum, V,
+                                _pad_cols4(B_items) if B_items is not None else None)
+        return (out[:M0, :K0].contiguous(), cs[:M0].contiguous() if cs is not None else None,
+                vout[:, :K0].contiguous() if vout is not None else None)
     N, M, K = A.size(0), A.size(1), B.size(1)
     nv = 0 if V is None else V.size(1)
     if B_items is None and M * K > 128 * 128 and gemm_tn_big_supported(M, K):
@@ -894,6 +903,17 @@ def gemm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: floa
 
 def _aligned_rows(t: torch.Tensor) -> bool:
     return t.dim() == 2 and t.stride(1) == 1 and (t.size(0) <= 1 or t.stride(0) % 4 == 0) and t.data_ptr() % 16 == 0
+
+
+def _pad_cols4(t: torch.Tensor) -> torch.Tensor:
+    """``t`` itself when its rows are 16-byte aligned, else a copy with its columns zero-padded
+    to a multiple of 4."""
+    if _aligned_rows(t):
+        return t
+    n, c = t.shape
+    tp = torch.zeros(n, c + (-c) % 4, dtype=t.dtype, device=t.device)
+    tp[:, :c] = t
+    return tp
 
 
 def mm_nn(x: torch.Tensor, B: torch.Tensor, b_layout: int, n: int, alpha: float = 1.0,

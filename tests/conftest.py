@@ -88,3 +88,35 @@ def _seeded():
     random.seed(1234)
     np.random.seed(1234)
     torch.manual_seed(1234)
+
+
+def kink_report(kst):
+    """oracle kink_stats entries -> report rows."""
+    return [{"edges": n, "max_abs_z_rel": r, "max_abs_z_over_fp32_bound": rb} for n, r, rb in kst]
+
+
+def assert_kink_ties(kst):
+    """The LeakyReLU kink: where the fp64 logit z = a_src + a_dst is within fp32 resolution of 0,
+    an fp32 implementation (ours, and the reference's own fp32 CPU path) may land on either side,
+    and the logit gradient takes slope 1 or 0.2 accordingly (tools/diag_parity.py found such
+    single edges behind the only large gradient differences at configs 4 and 5).  The oracle
+    takes the side the kernels took (hip_ops.KINK_TAP); every edge where that side differs from
+    the fp64 sign must be an fp32 tie: |z| <= B_e, the worst-case fp32 error of that edge's logit
+    (oracle.pyg_gat_conv: u ((C + K + 4)(U_src + U_dst) + |z|))."""
+    for n, _, rb in kst:
+        assert rb <= 1.0, (n, rb)
+
+
+def check_att_dst(err_abs, ref, ref_src, tol):
+    """datt_dst against the oracle.  datt_src and datt_dst are sums of the same per-edge logit
+    gradients (over a source's out-edges / a destination's in-edges); where every in-edge of a
+    destination sits on one side of the LeakyReLU the destination sum cancels exactly and
+    datt_dst is rounding only (1.4e-18 in the fp64 oracle at config 3, layer 2).  Only in that
+    cancellation regime (|ref| below 1e-6 of the pair's scale) is the error judged on the pair's
+    scale; otherwise on its own, like every other gradient."""
+    own = float(ref.abs().max())
+    pair = max(own, float(ref_src.abs().max()))
+    if own < 1e-6 * pair:
+        assert err_abs <= tol * pair, (err_abs, own, pair)
+    else:
+        assert err_abs <= tol * own, (err_abs, own)

@@ -21,8 +21,9 @@ reference's outputs), written as .npz / .json next to this script:
                      step with attn dropout 0, eval_sampled (:184-210) metrics.
   trajectory_cfg1.*  the reference's main() (:227-400) for 20 epochs on the config-1
                      inputs (attn dropout 0, --eval-neg-k 100): the best checkpoint's
-                     export forward, per-epoch loss / val metrics, test metrics; run twice
-                     (default and 1 torch thread) to record the reference's own spread.
+                     export forward, per-epoch loss / val metrics, test metrics; run with
+                     the default torch thread count and 1, 2, 4 threads to record the
+                     reference's own run-to-run envelope (per-epoch drift, top-20 agreement).
 
     python tests/golden/make_golden.py trajectory    # only the trajectory fixture
 """
@@ -352,7 +353,7 @@ def trajectory_case(ref, epochs: int = 20):
         def bucket(self, name):
             return _Bucket()
 
-    rec = {"val": [], "loss": [], "triples": None}
+    rec = {"val": [], "loss": [], "triples": None, "items": []}
     base_gat, base_eval, base_sample = ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch
 
     class _NoDropGAT(base_gat):
@@ -367,6 +368,7 @@ def trajectory_case(ref, epochs: int = 20):
                 u, i, j = (torch.from_numpy(a).long() for a in rec["triples"])
                 with torch.no_grad():
                     U, I = Z[:self.n_users], Z[self.n_users:]
+                    rec["items"].append(I.detach().numpy().astype(np.float32).copy())
                     pos = (U[u] * I[i]).sum(dim=-1)
                     neg = (U[u] * I[j]).sum(dim=-1)
                     rec["loss"].append(float(-torch.log(torch.sigmoid(pos - neg) + 1e-8).mean()))
@@ -427,38 +429,100 @@ def trajectory_case(ref, epochs: int = 20):
     print(f"trajectory ({torch.get_num_threads()} threads): {epochs} epochs, best epoch {best_epoch}, "
           f"loss {rec['loss'][0]:.6f} -> {rec['loss'][-1]:.6f}, test {metrics['test']}")
     arrays = dict(item_embeddings=I, user_embeddings=U, loss=np.array(rec["loss"], np.float64),
+                  epoch_items=np.stack(rec["items"][:epochs]),
                   **{"best__" + k: v.numpy() for k, v in ckpt["state_dict"].items()})
     return arrays, metrics
 
 
+TRAJ_THREADS = (1, 2, 4)                       # extra reference runs besides the default count
+TRAJ_EPOCHS_KEPT = (1, 2, 3, 5, 8, 12, 16, 20)  # training-forward item rows stored per epoch
+NEAR_TIE = 1e-6                                 # a top-K swap within 1e-6 of max|score|
+
+
+def row_rel_np(a, b):
+    """max over the rows of ``b`` with a nonzero norm of |a_i - b_i| / |b_i| (fp64)."""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    nb = np.linalg.norm(b, axis=1)
+    nz = nb > 0
+    return float((np.linalg.norm(a - b, axis=1)[nz] / nb[nz]).max()) if nz.any() else 0.0
+
+
+def top20_gaps(Ia, Ua, Ib, Ub, k=20):
+    """Per user, 0 when the two top-k lists (descending fp64 score, ties by index) are equal,
+    else the largest score gap on ``b``'s scores between the items at the differing positions,
+    relative to ``b``'s max |score| (the rule tests/test_gpu_trajectory.py applies)."""
+    Sa = np.asarray(Ua, np.float64) @ np.asarray(Ia, np.float64).T
+    Sb = np.asarray(Ub, np.float64) @ np.asarray(Ib, np.float64).T
+    out = np.zeros(len(Sa))
+    ar = np.arange(Sa.shape[1])
+    for u in range(len(Sa)):
+        a = np.lexsort((ar, -Sa[u]))[:k]
+        b = np.lexsort((ar, -Sb[u]))[:k]
+        d = a != b
+        if d.any():
+            out[u] = np.abs(Sb[u, a[d]] - Sb[u, b[d]]).max() / np.abs(Sb[u]).max()
+    return out
+
+
 def trajectory_fixture(ref, epochs: int = 20):
-    """Two runs of the reference trainer that differ only in torch's CPU thread count (the
-    default, then 1): the reference's own run-to-run spread.  Its float reductions
-    (``index_add_`` / ``scatter_add_`` / GEMM) change order with the thread count, and Adam
-    turns the resulting sign noise of near-zero gradients into lr-sized steps, so two runs of
-    the REFERENCE differ after 20 epochs; the GPU test measures our trainer against this
-    envelope.  The default-thread run is the primary fixture, the 1-thread run is ``t1__*``."""
+    """Runs of the reference trainer that differ only in torch's CPU thread count (the
+    default, then each of ``TRAJ_THREADS``): the reference's own run-to-run envelope.  Its
+    float reductions (``index_add_`` / ``scatter_add_`` / GEMM) change order with the thread
+    count, and Adam turns the resulting sign noise of near-zero gradients into lr-sized steps,
+    so runs of the REFERENCE differ after 20 epochs; the GPU test measures our trainer against
+    this envelope.  The default-thread run is the primary fixture (its per-epoch training-
+    forward item rows at ``TRAJ_EPOCHS_KEPT`` are ``epoch_items``), the other runs' final
+    item / user rows are ``t<threads>__*``; every pair's final item-row spread, per-epoch drift and top-20 agreement go to
+    the JSON."""
     threads = torch.get_num_threads()
-    arr, met = trajectory_case(ref, epochs)
-    torch.set_num_threads(1)
+    runs = {f"t{threads}": trajectory_case(ref, epochs)}
     try:
-        arr1, met1 = trajectory_case(ref, epochs)
+        for t in TRAJ_THREADS:
+            if t != threads:
+                torch.set_num_threads(t)
+                runs[f"t{t}"] = trajectory_case(ref, epochs)
     finally:
         torch.set_num_threads(threads)
-    nz = np.linalg.norm(arr["item_embeddings"], axis=1) > 0
-    d = arr["item_embeddings"].astype(np.float64) - arr1["item_embeddings"]
-    spread = float((np.linalg.norm(d, axis=1)[nz] / np.linalg.norm(arr["item_embeddings"], axis=1)[nz]).max())
+    names = list(runs)
+    arr, met = runs[names[0]]
+    arr1, met1 = runs["t1"]
+    pair, top = {}, {}
+    for x in range(len(names)):
+        for y in range(x + 1, len(names)):
+            a, b = runs[names[x]][0], runs[names[y]][0]
+            key = f"{names[x]}~{names[y]}"
+            pair[key] = max(row_rel_np(a["item_embeddings"], b["item_embeddings"]),
+                            row_rel_np(b["item_embeddings"], a["item_embeddings"]))
+            gaps = top20_gaps(a["item_embeddings"], a["user_embeddings"], b["item_embeddings"], b["user_embeddings"])
+            top[key] = {"exact": int((gaps == 0).sum()), "differing": int((gaps > 0).sum()),
+                        "beyond_near_tie_1e-6": int((gaps >= NEAR_TIE).sum()), "worst_gap_rel": float(gaps.max())}
+    per_epoch = {n: [row_rel_np(runs[n][0]["epoch_items"][e], arr["epoch_items"][e]) for e in range(epochs)]
+                 for n in names[1:]}
     met["reference_self_spread"] = {
         "what": "max over nonzero final item rows of |Z_a - Z_b| / |Z_a|, reference run with the default "
                 "torch thread count vs 1 thread",
-        "item_row_rel": spread,
+        "item_row_rel": row_rel_np(arr1["item_embeddings"], arr["item_embeddings"]),
+        "threads": names,
+        "envelope_item_row_rel": max(pair.values()),
+        "pairwise_item_row_rel": pair,
+        "pairwise_top20": top,
+        "per_epoch_item_row_rel_vs_primary": per_epoch,
+        "epochs_kept": list(TRAJ_EPOCHS_KEPT),
         "t1_val_per_epoch": met1["val_per_epoch"], "t1_test": met1["test"], "t1_best_epoch": met1["best_epoch"]}
-    np.savez_compressed(HERE / "trajectory_cfg1.npz", **arr,
-                        t1__item_embeddings=arr1["item_embeddings"], t1__user_embeddings=arr1["user_embeddings"],
-                        t1__loss=arr1["loss"])
+    met["reference_runs"] = {n: {"best_epoch": runs[n][1]["best_epoch"], "test": runs[n][1]["test"],
+                                 "val_per_epoch": runs[n][1]["val_per_epoch"]} for n in names}
+    keep = [e - 1 for e in TRAJ_EPOCHS_KEPT if e <= epochs]
+    prim = {k: v for k, v in arr.items() if k != "epoch_items"}
+    others = {}
+    for n in names[1:]:
+        others[f"{n}__item_embeddings"] = runs[n][0]["item_embeddings"]
+        others[f"{n}__user_embeddings"] = runs[n][0]["user_embeddings"]
+        others[f"{n}__loss"] = runs[n][0]["loss"]
+    np.savez_compressed(HERE / "trajectory_cfg1.npz", **prim, epoch_items=arr["epoch_items"][keep], **others)
     with open(HERE / "trajectory_cfg1.json", "w") as f:
         json.dump(met, f, indent=2)
-    print(f"trajectory: reference self-spread (threads {threads} vs 1) {spread:.3e} per item row")
+    print(f"trajectory: reference envelope over threads {names}: {max(pair.values()):.3e} per item row; "
+          f"pairs {pair}; top-20 {top}")
 
 
 def pd_read(path):

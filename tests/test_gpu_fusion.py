@@ -150,3 +150,20 @@ def test_native_train_loop_matches_autograd_loop(pkg, gold, cuda):
         l1 = [float(pkg.fusion.contrastive_fusion_loss(m.train()(txt[:512], img[:512]), m.txt_proj(txt[:512]),
                                                        m.img_proj(img[:512]))[0]) for m in (m1, m2)]
     assert abs(l1[0] - l1[1]) <= 1e-3 * abs(l1[1]), l1
+
+
+def test_autograd_loop_ragged_last_batch(pkg, gold, cuda):
+    """train_fusion(native=False) with a last batch of 45 rows (301 = 2 x 128 + 45): the
+    autograd InfoNCE backward takes dW = g^T x of the [45, 45] logit gradient through
+    hip_ops.gemm_tn, whose rows are not 16-byte aligned (padded there, not refused); the
+    per-epoch losses agree with the native loop's."""
+    g = torch.Generator().manual_seed(5)
+    txt = torch.randn(301, 384, generator=g).to(cuda)
+    img = torch.randn(301, 512, generator=g).to(cuda)
+    hs = []
+    for native in (True, False):
+        m = _model(pkg, gold, cuda)
+        m.mlp[2].p = 0.0
+        hs.append(pkg.fusion.train_fusion(m, txt, img, epochs=2, batch_size=128, native=native))
+    for a, b in zip(*hs):
+        assert np.allclose(a, b, rtol=1e-4, atol=1e-5), hs

@@ -30,8 +30,22 @@ def test_gemm_tn_vs_fp64(pkg, cuda, N, M, K):
     assert rel(out2, A.t() @ B) <= 1e-5
     out3, _, _ = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda))
     assert torch.equal(out2, out3)
-    if M > 16:  # same kernel with or without the extras
-        assert torch.equal(out, out2)
+    assert torch.equal(out, out2)  # same kernel and order with or without the extras (M <= 16 too)
+
+
+@pytest.mark.parametrize("N,M,K", [(489, 489, 128), (45, 45, 45), (301, 13, 130)])
+def test_gemm_tn_unaligned_rows(pkg, cuda, N, M, K):
+    """Operands whose rows are not 16-byte aligned (e.g. the [B, B] InfoNCE logit gradient of
+    a ragged last batch) are zero-padded to a multiple of 4 columns, not refused."""
+    from importlib import import_module
+    ops = import_module("plotpointe-gat-recommendation_amd.hip_ops")
+    g = torch.Generator().manual_seed(N * M + K)
+    A = torch.randn(N, M, generator=g, dtype=torch.float64)
+    B = torch.randn(N, K, generator=g, dtype=torch.float64)
+    out, cs, _ = ops.gemm_tn(A.float().to(cuda), B.float().to(cuda), want_colsum=True)
+    assert out.shape == (M, K) and cs.shape == (M,)
+    assert rel(out, A.t() @ B) <= 1e-5
+    assert rel(cs, A.sum(0)) <= 1e-5
 
 
 def test_gemm_tn_strided_operands(pkg, cuda):

@@ -19,18 +19,24 @@ tool (export.py), everything on the HIP kernels.  Checked:
 The trajectory bound is set by the reference itself: its CPU reductions (``index_add_``,
 ``scatter_add_``, the GEMMs) change order with the thread count and are not even repeatable
 at a fixed count, and Adam turns the sign noise of near-zero gradients into lr-sized steps,
-so two runs of the REFERENCE end 4-6e-5 apart per item row after 20 epochs (the fixture
-records its default-vs-1-thread spread).  Our run is held to 4x that spread, and the
-figures go to ``gpurun_out/parity/trajectory_cfg1.json`` (committed under profiles/).
+so runs of the REFERENCE end apart per item row after 20 epochs.  The fixture holds four
+reference runs (torch threads 8, 1, 2, 4): the largest pairwise final item-row spread is the
+envelope our run is held to (no multiplier), and every user whose top-20 differs must differ
+by less than that envelope in score.  The count of users whose top-20 differ beyond SURVEY.md
+8(d)'s 1e-6 near-tie rule is reported next to the same count between reference runs (up to 1
+of 1,500 there; it is not asserted: it follows the chaotic final drift).  Per-epoch drift (ours and each reference run against the primary run) and
+both top-20 rules go to ``gpurun_out/parity/trajectory_cfg1<tag>.json`` (committed under
+profiles/); ``PPGAT_REPORT_TAG`` names a variant run (e.g. ``PPGAT_GEMM=fp32``).
 """
 import importlib
 import json
+import os
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, row_rel, write_report
+from conftest import GOLDEN, ROOT, row_rel, write_report
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
@@ -72,17 +78,26 @@ def _top20_compare(oracle, Ia, Ua, Ib, Ub, tau):
     return exact, near, mism, worst
 
 
-def test_reference_trajectory_cfg1(pkg, oracle, cuda, tmp_path, capsys):
+NEAR_TIE = 1e-6
+
+
+def test_reference_trajectory_cfg1(pkg, oracle, cuda, tmp_path, capsys, monkeypatch):
     g = dict(np.load(GOLDEN / "trajectory_cfg1.npz"))
     meta = json.loads((GOLDEN / "trajectory_cfg1.json").read_text())
-    spread = meta["reference_self_spread"]["item_row_rel"]
+    env = meta["reference_self_spread"]
+    spread = env["item_row_rel"]
+    envelope = env["envelope_item_row_rel"]
+    ref_beyond = max(v["beyond_near_tie_1e-6"] for v in env["pairwise_top20"].values())
     train = importlib.import_module("plotpointe-gat-recommendation_amd.train")
     export = importlib.import_module("plotpointe-gat-recommendation_amd.export")
     maps, feats = _inputs(pkg, tmp_path)
     nu, ni = int(maps["n_users"]), int(maps["n_items"])
     common = ["--staging-prefix", str(tmp_path / "staging"), "--graphs-prefix", str(tmp_path / "graphs"),
               "--embeddings-prefix", str(tmp_path / "emb")]
-    rep = {"epochs": 20, "reference_self_spread_item_row_rel": spread}
+    rep = {"epochs": 20, "variant": {k: v for k, v in os.environ.items() if k.startswith("PPGAT_")},
+           "reference_self_spread_item_row_rel": spread, "reference_envelope_item_row_rel": envelope,
+           "reference_pairwise_item_row_rel": env["pairwise_item_row_rel"],
+           "reference_pairwise_top20": env["pairwise_top20"]}
 
     # 1. the reference's best checkpoint through our export forward (identical state)
     ck = tmp_path / "ref_best.pt"
@@ -93,7 +108,16 @@ def test_reference_trajectory_cfg1(pkg, oracle, cuda, tmp_path, capsys):
     r_fwd, row_fwd, z_fwd = row_rel(I_fwd, g["item_embeddings"])
     rep["forward_same_state"] = {"item_row_rel_max": r_fwd, "worst_row": row_fwd, "zero_rows_max_abs": z_fwd}
 
-    # 2. the whole run through our trainer
+    # 2. the whole run through our trainer; the training forward's item rows of every epoch
+    # are captured where the loss reads them (the reference fixture records the same rows)
+    epoch_items = []
+    base_loss = train.model_mod.bpr_loss
+
+    def _loss(Z, n_users, *a, **k):
+        epoch_items.append(Z[n_users:].detach().float().cpu().numpy().copy())
+        return base_loss(Z, n_users, *a, **k)
+
+    monkeypatch.setattr(train.model_mod, "bpr_loss", _loss)
     capsys.readouterr()
     out = train.main(common + ["--models-prefix", str(tmp_path / "models"), "--model-family", "gat_custom",
                                "--attn-dropout", "0", "--epochs", "20", "--samples-per-epoch", "200000",
@@ -121,23 +145,39 @@ def test_reference_trajectory_cfg1(pkg, oracle, cuda, tmp_path, capsys):
     val_equal = [ours_val[k] == ref_val[k] for k in range(20)]
     val_maxdiff = max(abs(ours_val[k][q] - ref_val[k][q]) for k in range(20) for q in ref_val[k])
     test_maxdiff = max(abs(out["test"][q] - meta["test"][q]) for q in meta["test"])
-    tau = 4.0 * spread
-    exact, near, mism, worst_gap = _top20_compare(oracle, I, U, g["item_embeddings"], g["user_embeddings"], tau)
-    # the reference against itself (default vs 1 thread), same rule: what a near-tie looks like
-    r_exact, r_near, r_mism, _ = _top20_compare(oracle, g["t1__item_embeddings"], g["t1__user_embeddings"],
-                                                g["item_embeddings"], g["user_embeddings"], tau)
+    kept = env["epochs_kept"]
+    drift = {e: row_rel(epoch_items[e - 1], g["epoch_items"][k])[0] for k, e in enumerate(kept)}
+    ref_drift = {n: {e: c[e - 1] for e in kept} for n, c in env["per_epoch_item_row_rel_vs_primary"].items()}
+    exact, near, beyond, worst_gap = _top20_compare(oracle, I, U, g["item_embeddings"], g["user_embeddings"],
+                                                    NEAR_TIE)
+    tau = envelope
+    _, near_env, mism_env, _ = _top20_compare(oracle, I, U, g["item_embeddings"], g["user_embeddings"], tau)
     rep.update({
         "loss_rel_max": float(loss_rel.max()), "loss_rel_epoch1": float(loss_rel[0]),
         "best_epoch": {"ours": ours_best, "reference": meta["best_epoch"]},
         "val_epochs_equal": int(sum(val_equal)), "val_max_abs_diff": val_maxdiff,
         "test": {"ours": out["test"], "reference": meta["test"], "max_abs_diff": test_maxdiff},
         "item_row_rel_max": r_items, "item_worst_row": row_items, "item_zero_rows_max_abs": z_items,
-        "item_row_rel_over_reference_spread": r_items / spread, "user_row_rel_max": r_users,
-        "top20": {"users": nu, "exact": exact, "near_tie": near, "mismatched": mism, "tau": tau,
-                  "worst_gap_rel": worst_gap,
-                  "reference_vs_itself": {"exact": r_exact, "near_tie": r_near, "mismatched": r_mism}},
+        "item_row_rel_over_reference_spread": r_items / spread,
+        "item_row_rel_over_reference_envelope": r_items / envelope, "user_row_rel_max": r_users,
+        "per_epoch_item_row_rel_vs_reference": {"ours": drift, **ref_drift},
+        "top20": {"users": nu, "exact": exact, "worst_gap_rel": worst_gap,
+                  "rule_1e-6": {"near_tie": near, "beyond": beyond,
+                                "reference_pairs_max_beyond": ref_beyond},
+                  "rule_envelope": {"tau": tau, "near_tie": near_env, "mismatched": mism_env}},
     })
-    write_report("trajectory_cfg1", rep)
+    # our top-20 against every reference run (same 1e-6 rule): is our run one more draw from
+    # the reference's own run-to-run distribution?
+    rep["top20"]["rule_1e-6"]["vs_each_reference_run"] = {
+        n: _top20_compare(oracle, I, U, g[f"{n}__item_embeddings"], g[f"{n}__user_embeddings"], NEAR_TIE)[2]
+        for n in env["threads"][1:]}
+    rep["item_row_rel_vs_each_reference_run"] = {
+        n: row_rel(I, g[f"{n}__item_embeddings"])[0] for n in env["threads"][1:]}
+    tag = os.environ.get("PPGAT_REPORT_TAG", "")
+    name = "trajectory_cfg1" + (f"_{tag}" if tag else "")
+    write_report(name, rep)
+    np.savez_compressed(ROOT / "gpurun_out" / "parity" / f"{name}_rows.npz", items=I, users=U,
+                        epoch_items=np.stack(epoch_items))
     assert r_fwd <= 1e-5 and z_fwd == 0.0, rep["forward_same_state"]
     assert loss_rel[0] <= 1e-6, loss_rel[0]          # identical initial state
     assert loss_rel.max() <= 1e-5, loss_rel
@@ -145,5 +185,8 @@ def test_reference_trajectory_cfg1(pkg, oracle, cuda, tmp_path, capsys):
     # one rank flip of one of the 1,500 validation users moves recall@K by 1/1500 and ndcg by less
     assert val_maxdiff <= 1.0 / 1500 + 1e-12 and test_maxdiff <= 1.0 / 1500 + 1e-12, rep
     assert z_items == 0.0
-    assert r_items <= 4.0 * spread, (r_items, spread)
-    assert mism == 0, rep["top20"]
+    assert r_items <= envelope, (r_items, envelope)
+    # every user whose top-20 differs does so by less than the reference's own run-to-run
+    # spread; the 1e-6 rule (reported above, next to the reference pairs' counts) is not
+    # asserted: after 20 chaotic Adam epochs the reference runs themselves differ beyond it
+    assert mism_env == 0, rep["top20"]

@@ -161,7 +161,7 @@ def test_kink_sides_option(oracle):
     base = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1)
     st = []
     same = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_pos=(z > 0).view(-1, 1), kink_stats=st)
-    assert torch.equal(base, same) and st == [(0, 0.0)]
+    assert torch.equal(base, same) and st == [(0, 0.0, 0.0)]
     lin = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_pos=torch.ones(ei.size(1), 1, dtype=torch.bool))
     ref = oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, negative_slope=1.0)
     assert torch.allclose(lin, ref, rtol=0, atol=1e-12)
@@ -169,4 +169,4 @@ def test_kink_sides_option(oracle):
     flip = (z > 0).view(-1, 1).clone()
     flip[:3] = ~flip[:3]
     oracle.pyg_gat_conv(x, ei, W, a_s, a_d, b, 1, kink_pos=flip, kink_stats=st)
-    assert st[0][0] == 3 and st[0][1] > 0
+    assert st[0][0] == 3 and st[0][1] > 0 and st[0][2] > 1.0  # real flips, far beyond an fp32 tie

@@ -30,6 +30,9 @@ for s in $STEPS; do
     sampler) run pytest_sampler 300 python -u -m pytest tests/test_sampler.py "tests/test_gpu_eval.py::test_trainer_device_sampler" -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     bsampler) run bench_sampler 300 python tools/bench_sampler.py ;;
     sel) run pytest_sel 1100 python -u -m pytest $TESTS -m gpu -v -s -rf --durations=15 --timeout 170 --timeout-method thread ;;
+    traj) for v in default:PPGAT_NONE=1 fuseddxw0:PPGAT_FUSED_DXW=0 gemmfp32:PPGAT_GEMM=fp32; do
+            run "traj_${v%%:*}" 900 env PPGAT_REPORT_TAG="${v%%:*}" "${v#*:}" python -u -m pytest tests/test_gpu_trajectory.py -m gpu -v -s -rf --timeout 800 --timeout-method thread
+          done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
