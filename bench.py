@@ -364,8 +364,11 @@ def main():
     H, C = args.heads, args.hidden
     # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
     xform_k = C if (H > 1 and H * C > C and pkg.hip_ops.xgat_supported(C, H, C)) else 0
-    # the g-gathering pass B runs where no halo exchange splits the backward (hip_ops.xgat_backward)
-    gather_mode = pkg.hip_ops._xgat_gather_mode(C, H) if xform_k else None
+    # the backward formulation hip_ops.xgat_backward picks for these layer sizes
+    if xform_k and dist_path and part == "halo":  # the formulation the local layer sizes select
+        gather_mode = pkg.hip_ops._xgat_gather_mode(C, H, dg.R, dg.n_own, dg.bwd_view.n_bwd_edges, C)
+    else:
+        gather_mode = pkg.hip_ops._xgat_gather_mode(C, H) if xform_k else None
     gather_g = gather_mode in ("g", "gd")
     kern = {k: _lib.profile_read(k) for k in ("scores", "fwd", "bwd_pro", "bwd_src", "bwd_epi", "bwd_red",
                                                "proj", "proj_bwd", "gemm_tn", "adam")}

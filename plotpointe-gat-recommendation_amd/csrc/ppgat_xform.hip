@@ -723,6 +723,178 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_gemm_nnh2: k_gemm_nnh's arithmetic (the same products in the same order: bitwise equal
+// results) with a deeper pipeline.  In k_gemm_nnh the compiler waits for the whole vector-memory
+// queue twice per 32-deep chunk -- before the first LDS read after an LDS-DMA issue (it cannot
+// tell the DMA target from the buffer being read) and at every __syncthreads (its workgroup
+// fence) -- so the next chunk's X rows, streamed from HBM one chunk ahead, had only part of a
+// chunk to arrive (MFMA busy 0.41, 46 % of the wave cycles waiting; profiles/r03/v27_nnh_pmc.json).
+// Here:
+//  * B chunks go to LDS by LDS-DMA issued in inline asm (the compiler sees no memory access, so
+//    it adds no wait before LDS reads), three buffers, issued two chunks ahead;
+//  * X rows stream two chunks ahead in two register sets; a chunk's rows are scaled and split
+//    into their fp16 fragments at the top of the chunk, which frees the set for chunk c + 2;
+//  * the chunk barrier is a bare s_barrier after an explicit vmcnt wait for exactly this
+//    wave's DMA of chunk c + 1 (the only operation the barrier must cover: everything issued
+//    after it -- X of c + 1, DMA and X of c + 2 -- stays in flight).
+// Global issue order per wave: DMA(0) X(0) DMA(1) X(1) | chunk c: DMA(c+2) X(c+2) ...
+// ---------------------------------------------------------------------------
+using i32x4 = __attribute__((ext_vector_type(4))) int;
+
+// one buffer_load_dwordx4 ... lds: 16 B per lane from rsrc at voff + soff into LDS at m0 = lds
+__device__ __forceinline__ void dma_lds16(const i32x4& rsrc, uint32_t lds, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
+               : "memory", "m0");
+}
+
+// s_waitcnt vmcnt(n) (gfx9 encoding; expcnt / lgkmcnt left open)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int NT, bool RK>
+__global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* __restrict__ img,
+                                                      const int* __restrict__ ecol) {
+  using I = NnhImg<NT>;
+  constexpr int KC = I::KC, LDK = I::LDK, PART = I::PART, NI = I::BYTES / 1024;
+  __shared__ __attribute__((aligned(16))) uint16_t sB[3][I::ELEMS];
+  __shared__ __attribute__((aligned(16))) float sF[8][32];  // per wave: a factor per row (rescale, epilogue)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int64_t rb = (idx / a.n_blocks) * 8 + (b & 7);  // XCD-aware: a row block's column blocks share an L2
+  const int nb = (int)(idx % a.n_blocks);
+  if (rb >= a.row_blocks) return;
+  const int64_t M = a.M;
+  const int K = a.K, chunks = K / KC;
+  const int64_t m = rb * kPBM + wv * 32 + r;
+  const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
+  // buffer resource of this column block's images (stride 0, raw bytes), wave-uniform
+  const uint64_t base = reinterpret_cast<uint64_t>(img + (int64_t)nb * chunks * I::ELEMS);
+  const i32x4 rsrc = {__builtin_amdgcn_readfirstlane((int)(uint32_t)base),
+                      __builtin_amdgcn_readfirstlane((int)((base >> 32) & 0xffff)),
+                      __builtin_amdgcn_readfirstlane(chunks * I::BYTES), 0x00020000};
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(&sB[0][0]);
+  const uint32_t voff = (uint32_t)lane * 16u;
+  constexpr int ND = (NI + 7) / 8;  // DMA instructions of waves 0 .. (NI % 8) - 1 (one fewer for the rest)
+  const bool full = (NI % 8 == 0) || wv < NI % 8;
+  auto issue = [&](int c) {  // chunk c's two images -> sB[c % 3], 1 KB per wave instruction
+    const uint32_t dst = lds0 + (uint32_t)((c % 3) * I::ELEMS * 2);
+    for (int i = wv; i < NI; i += 8) dma_lds16(rsrc, dst + i * 1024, voff, (uint32_t)(c * I::BYTES + i * 1024));
+  };
+  auto loadx = [&](int c, float4 (&x)[4]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) x[g] = ld4(xrow + c * KC + 8 * g);
+  };
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+  int erow = 0;
+  bool set = false;  // the row has had a nonzero element (its scale is fixed until an overflow)
+  // chunks is even (>= 2; the launcher checks): the loop below runs chunk pairs (xA, xB) and
+  // every chunk loads an X set, the last two re-reading chunk chunks - 1, so the compiler sees
+  // the same four loads per chunk on every path and waits for exactly the set it reads
+  float4 xA[4], xB[4];
+  issue(0);
+  loadx(0, xA);
+  issue(1);
+  loadx(1, xB);
+  if (full) wait_vm<4 + ND + 4>(); else wait_vm<4 + ND - 1 + 4>();  // DMA(0) has landed
+  __builtin_amdgcn_s_barrier();
+
+  auto body = [&](const int c, float4 (&xc)[4]) {
+    // X(c): this chunk's row scales and fp16 fragments (both k steps), then the set is free
+    const float s = split::row_scale_online<NT>(xc, erow, set, acc, sF[wv], r, hf);
+    split::u32x4 fx[2][2];
+    split::split2h(xc[0], xc[1], s, fx[0][0], fx[0][1]);
+    split::split2h(xc[2], xc[3], s, fx[1][0], fx[1][1]);
+    const bool ahead = c + 2 < chunks;
+    if (ahead) issue(c + 2);
+    loadx(ahead ? c + 2 : chunks - 1, xc);
+    const uint16_t* sb = sB[c % 3];
+    auto read_b = [&](int i, split::u32x4 (&f)[2]) {
+      const int off = (32 * (i % NT) + r) * LDK + 16 * (i / NT) + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sb[p * PART + off]);
+    };
+    split::u32x4 fb[2][2];
+    read_b(0, fb[0]);
+#pragma unroll
+    for (int i = 0; i < (KC / 16) * NT; ++i) {
+      const int u = i / NT, t = i % NT;
+      if (i + 1 < (KC / 16) * NT) read_b(i + 1, fb[(i + 1) & 1]);
+      acc[t] = split::mfma32_h3(fx[u], fb[i & 1], acc[t]);
+      if (i + 1 < (KC / 16) * NT) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x0008, 3, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // DMA(c + 1) must have landed before any wave reads it, and every wave must be done with
+    // sB[c % 3] before chunk c + 3's DMA (issued in chunk c + 1) overwrites it.  Issued after
+    // DMA(c + 1): X(c + 1), and in this chunk DMA(c + 2) (if any) and an X set.
+    if (ahead) {
+      if (full) wait_vm<4 + ND + 4>(); else wait_vm<4 + ND - 1 + 4>();
+    } else {
+      wait_vm<4 + 4>();
+    }
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int c = 0; c < chunks; c += 2) {
+    body(c, xA);
+    body(c + 1, xB);
+  }
+  float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
+  split::row_unscale(erow, sF[wv], r, hf, fr);
+  const int64_t row0 = rb * kPBM + wv * 32;
+  const int n0 = nb * I::BN;
+  if constexpr (RK) {
+    const int nv = a.nv;
+    float ra[NT][kNnhRank], bv[NT], ic[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      bv[t] = a.bias != nullptr ? a.bias[col] : 0.f;
+      ic[t] = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int v = 0; v < kNnhRank; ++v) ra[t][v] = v < nv ? a.rA[v * a.ldra + col] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      const int64_t rr = row < M ? row : M - 1;
+      float sv[kNnhRank];
+#pragma unroll
+      for (int v = 0; v < kNnhRank; ++v) sv[v] = v < nv ? a.rS[rr * a.ldrs + v] : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float y = fmaf(acc[t][q] * fr[q], ic[t], bv[t]);
+#pragma unroll
+        for (int v = 0; v < kNnhRank; ++v)
+          if (v < nv) y = fmaf(sv[v], ra[t][v], y);
+        if (row < M) a.Y[row * a.ldy + n0 + 32 * t + r] = y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+      const float ic = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+      }
+    }
+  }
+}
+
 // split-K finish: Y = alpha * sum_s part[s] (split order) + bias, float4 per thread
 __global__ void __launch_bounds__(256) k_nn_split_sum(const float* __restrict__ part, int64_t M, int N, int splits,
                                                       float alpha, const float* __restrict__ bias,
@@ -1896,6 +2068,15 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
   return hipGetLastError();
 }
 
+// k_gemm_nnh2 (the pipelined variant) unless PPGAT_NNH2=0; read once per process
+static bool nnh2_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PPGAT_NNH2");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 static size_t nnq_bytes(int K, int N) {  // image + column exponents, either family
   const int nt = N % 256 == 0 ? 8 : 4;
   return nnh_enabled() ? align_up(nnh_image_bytes(K, N, nt)) + align_up((size_t)N * 4) : nnp_image_bytes(K, N);
@@ -1932,6 +2113,17 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       int* ecol = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align_up(nnh_image_bytes(K, N, w8 ? 8 : 4)));
       hipError_t e = nnh_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, ecol, st);
       if (e != hipSuccess) return e;
+      if (nnh2_enabled() && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
+        if (nv > 0) {
+          if (w8) hipLaunchKernelGGL((k_gemm_nnh2<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          else hipLaunchKernelGGL((k_gemm_nnh2<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        } else if (w8) {
+          hipLaunchKernelGGL((k_gemm_nnh2<8, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        } else {
+          hipLaunchKernelGGL((k_gemm_nnh2<4, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        }
+        return hipGetLastError();
+      }
       if (nv > 0) {
         if (w8) hipLaunchKernelGGL((k_gemm_nnh<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
         else hipLaunchKernelGGL((k_gemm_nnh<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);

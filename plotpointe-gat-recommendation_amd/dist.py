@@ -3,8 +3,9 @@
 Two partitions of the node rows, both exact (every result equals the single-device layer):
 
 Halo partition (``build_halo_graph`` / ``HaloPyGGAT``, any graph; configs 4 and 5).
-  Users and items are two segments, each cut into `world` contiguous ranges balanced by
-  degree, so every rank owns a slice of both: its "own" rows, users first then items.
+  Users and items are two segments: users cut into `world` contiguous ranges balanced by
+  degree, items dealt to the ranks by degree (``halo_owner``), so every rank owns a slice of
+  both: its "own" rows, users first then items.
   Every edge_index column lives on the rank that owns its DESTINATION, so a rank holds the
   complete in-edge list (CSR) of each own row.  The sources those edges read that belong to
   other ranks are its halo rows; the local row space is [own rows | halo rows], the halo
@@ -312,8 +313,8 @@ class HaloGraph:
     n_nodes: int
     n_edges: int
     n_users: int
-    seg_bounds: list            # [user bounds [world+1], item bounds [world+1]] (node ids)
-    n_own: int                  # own rows: users [u0, u1) then items [i0, i1)
+    user_bounds: np.ndarray     # [world + 1]: rank r owns the users [b_r, b_{r+1}) (node ids)
+    n_own: int                  # own rows: users [u0, u1), then the own items by id (halo_owner)
     n_halo: int                 # halo rows: users (by owner) then items (by owner)
     plan_u: ExchangePlan        # the layer halo exchange of user rows
     plan_i: ExchangePlan        # ... of item rows
@@ -325,6 +326,12 @@ class HaloGraph:
     halo_items: torch.Tensor = None  # [n_halo_i] int64 item indices (node id - n_users) of the halo items
     bwd_sched_own: object = None   # backward schedule over the own source rows
     bwd_sched_halo: object = None  # ... over the halo source rows (row ids relative to n_own)
+    n_own_u: int = 0               # own rows [0, n_own_u) are users, [n_own_u, n_own) items
+    bipartite: bool = False        # every edge joins a user and an item (the U-I graph)
+    fwd_sched_u: object = None     # forward schedule over the own user destinations
+    fwd_sched_i: object = None     # ... over the own item destinations (rows relative to n_own_u)
+    own_items: torch.Tensor = None # [n_own - n_own_u] int64 item indices (node id - n_users), ascending
+    item_partition: str = "dealt"
 
     @property
     def R(self) -> int:
@@ -340,16 +347,18 @@ class HaloGraph:
 
     @property
     def bounds(self) -> np.ndarray:
-        return self.seg_bounds[0]
+        return self.user_bounds
 
-    def owned(self, rank: Optional[int] = None):
-        """((u0, u1), (i0, i1)): the node-id ranges of a rank's users and items."""
+    def owned_users(self, n_users: int = 0, rank: Optional[int] = None):
+        """(u0, u1): the node-id range of a rank's users."""
         r = self.rank if rank is None else rank
-        ub, ib = self.seg_bounds
-        return (int(ub[r]), int(ub[r + 1])), (int(ib[r]), int(ib[r + 1]))
+        return int(self.user_bounds[r]), int(self.user_bounds[r + 1])
 
-    def owned_users(self, n_users: int, rank: Optional[int] = None):
-        return self.owned(rank)[0]
+    def own_node_ids(self, rank: Optional[int] = None) -> np.ndarray:
+        """A rank's own rows as global node ids, in its own-local row order (host)."""
+        r = self.rank if rank is None else rank
+        u0, u1 = self.owned_users(rank=r)
+        return np.concatenate([np.arange(u0, u1), self.n_users + np.flatnonzero(self.owner[self.n_users:] == r)])
 
     def xviews(self):
         """The local edge lists as hip_ops.XViews (aggregate-then-transform layer): CSR over the
@@ -360,30 +369,57 @@ class HaloGraph:
                       b.bwd_sched, self.bwd_sched_own, self.bwd_sched_halo, rowptr=f.rowptr)
 
 
+def halo_owner(deg: np.ndarray, n_users: int, world: int, item_partition: str = "dealt"):
+    """Row ownership of the halo partition -> (owner [N] int32, user bounds [world + 1]).
+
+    Users: contiguous id ranges with equal degree sums (users are uniform: each rank sends
+    about the same number of user rows).  Items (``item_partition``):
+      "dealt"      -- items sorted by degree (descending, ties by id) and dealt to the ranks in
+                      snake order 0..W-1, W-1..0, ...: every rank gets the same mix of hub and
+                      tail items, so the degree sums, the row counts AND the halo sends (a hub
+                      goes to every peer, a tail item to few) are balanced together;
+      "contiguous" -- contiguous id ranges with equal degree sums (with popularity-ordered
+                      ids, e.g. config 5's Zipf items, one rank then owns all the hubs and
+                      another the long tail: equal edges but 2x the sends of the mean).
+    Deterministic: every rank computes the same owner array."""
+    N, nu = len(deg), int(n_users)
+    owner = np.empty(N, np.int32)
+    ub = partition_bounds(deg[:nu], world)
+    owner[:nu] = np.repeat(np.arange(world, dtype=np.int32), np.diff(ub))
+    if item_partition == "dealt":
+        order = np.argsort(-deg[nu:], kind="stable")
+        pos = np.arange(N - nu)
+        k, cyc = pos % world, pos // world
+        owner[nu + order] = np.where(cyc % 2 == 0, k, world - 1 - k).astype(np.int32)
+    elif item_partition == "contiguous":
+        ib = partition_bounds(deg[nu:], world)
+        owner[nu:] = np.repeat(np.arange(world, dtype=np.int32), np.diff(ib))
+    else:
+        raise ValueError(f"item_partition must be 'dealt' or 'contiguous', not {item_partition!r}")
+    return owner, ub
+
+
 def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,
                      csr_builder: Callable = _hip_csr, sched_builder: Optional[Callable] = _hip_sched,
-                     node_weight: float = 4.0) -> HaloGraph:
+                     node_weight: float = 4.0, item_partition: Optional[str] = None) -> HaloGraph:
     """Every rank calls this with the same global edge_index (LongTensor [2, E], users
     [0, n_users), items [n_users, N)) and gets its own slices; deterministic, so all ranks
-    agree on the plan without exchanging it."""
+    agree on the plan without exchanging it.  ``item_partition``: halo_owner's (default
+    "dealt", or $PPGAT_ITEM_PARTITION)."""
     dev = edge_index.device
     N, nu = int(n_nodes), int(n_users)
     E = int(edge_index.size(1))
     ei = edge_index.cpu().numpy()
     src, dst = ei[0], ei[1]
     deg = (np.bincount(dst, minlength=N) + np.bincount(src, minlength=N)).astype(np.float64) + node_weight
-    seg_bounds = []
-    owner = np.empty(N, np.int32)
-    for a, b in ((0, nu), (nu, N)):
-        bnd = a + partition_bounds(deg[a:b], world)
-        seg_bounds.append(bnd)
-        owner[a:b] = np.repeat(np.arange(world, dtype=np.int32), np.diff(bnd))
-    u0, u1 = int(seg_bounds[0][rank]), int(seg_bounds[0][rank + 1])
-    i0, i1 = int(seg_bounds[1][rank]), int(seg_bounds[1][rank + 1])
-    n_own = (u1 - u0) + (i1 - i0)
+    item_partition = item_partition or os.environ.get("PPGAT_ITEM_PARTITION", "dealt")
+    owner, ub = halo_owner(deg, nu, world, item_partition)
+    u0, u1 = int(ub[rank]), int(ub[rank + 1])
+    own_items = nu + np.flatnonzero(owner[nu:] == rank)   # ascending node ids
+    n_own = (u1 - u0) + len(own_items)
     local_of = np.full(N, -1, np.int64)
     local_of[u0:u1] = np.arange(u1 - u0)
-    local_of[i0:i1] = (u1 - u0) + np.arange(i1 - i0)
+    local_of[own_items] = (u1 - u0) + np.arange(len(own_items))
     od, osrc = owner[dst], owner[src]
     loc = np.flatnonzero(od == rank)                       # edges homed here (destination owned)
     lsrc = src[loc]
@@ -415,8 +451,12 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     row, csc_eid, slot = G.row[:El].contiguous(), orig(G.csc_eid[:El]), G.csc2csr[:El].contiguous()
     fwd_view = LocalView(n_own, rowptr_own, col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
     bwd_view = LocalView(R, G.rowptr.contiguous(), col, csr_eid, El, G.colptr.contiguous(), row, csc_eid, slot, El)
-    hg = HaloGraph(world, rank, N, E, nu, seg_bounds, n_own, len(halo), plan_u, plan_i, fwd_view, bwd_view, local_of,
+    hg = HaloGraph(world, rank, N, E, nu, ub, n_own, len(halo), plan_u, plan_i, fwd_view, bwd_view, local_of,
                    owner, {}, torch.from_numpy(halo_i - nu).to(dev))
+    hg.own_items = torch.from_numpy(own_items - nu).to(dev)
+    hg.item_partition = item_partition
+    hg.n_own_u = u1 - u0
+    hg.bipartite = bool(np.all((src < nu) != (dst < nu)))  # the same decision on every rank
     if dev.type == "cuda" and _lib.debug_build():  # debug build: plans and views within bounds
         for pname, plan in (("plan_u", plan_u), ("plan_i", plan_i)):
             _lib.check_index_range(plan.send_idx, 0, n_own, f"halo.{pname}.send_idx")
@@ -433,6 +473,10 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
         # gradients go back to their owners while the own sources are processed)
         hg.bwd_sched_own = sched_builder(bwd_view.colptr[:n_own + 1].contiguous(), El)
         hg.bwd_sched_halo = sched_builder(bwd_view.colptr[n_own:].contiguous(), El)
+        # the forward split by destination class (bipartite graphs: a class's sources are the
+        # other class, so a phase needs only that class's halo rows; _HaloLayerX)
+        hg.fwd_sched_u = sched_builder(rowptr_own[:hg.n_own_u + 1].contiguous(), El)
+        hg.fwd_sched_i = sched_builder(rowptr_own[hg.n_own_u:].contiguous(), El)
     return hg
 
 
@@ -493,34 +537,125 @@ def _comm_stream(dev) -> torch.cuda.Stream:
     return s
 
 
+class HaloRows:
+    """The input rows [own | halo users | halo items] of one multi-head halo layer and the state
+    of its two halo classes ("u", "i").  A class's rows are either received -- ``start(cls,
+    src)`` gathers the owner's rows of ``src`` each peer needs and runs the all_to_all, on the
+    communication stream under RCCL, as soon as the owner has them (for layer l+1 right after
+    the phase of layer l that produced them) -- or computed locally (``set_local``: the first
+    layer's halo items).  ``wait(cls)`` orders the current stream after that class's rows."""
+
+    def __init__(self, hg: "HaloGraph", comm: "Comm", stages, width: int, like: torch.Tensor):
+        self.hg, self.comm, self.stages = hg, comm, stages
+        self.x = torch.empty((hg.R, width), dtype=like.dtype, device=like.device)
+        self.events = {}
+        self.local = set()
+        self.started = []   # exchanged classes, in start order
+
+    def span(self, cls):
+        hg = self.hg
+        return (hg.n_own, hg.n_own + hg.n_halo_u) if cls == "u" else (hg.n_own + hg.n_halo_u, hg.R)
+
+    def plan(self, cls) -> ExchangePlan:
+        return self.hg.plan_u if cls == "u" else self.hg.plan_i
+
+    def set_local(self, cls, rows: torch.Tensor):
+        a, b = self.span(cls)
+        if b > a:
+            self.x[a:b].copy_(rows)
+        self.local.add(cls)
+
+    def start(self, cls, src: torch.Tensor):
+        """Send the own rows of ``src`` (own-local row order) of class ``cls`` to the peers."""
+        plan, (a, b) = self.plan(cls), self.span(cls)
+        self.started.append(cls)
+        comm, st = self.comm, self.stages
+        if comm.backend != "nccl" or not comm.active:
+            comm.all_to_all_rows(st.gather_rows(src, plan.send_idx), plan.send_counts, plan.recv_counts,
+                                 out=self.x[a:b])
+            return
+        dev = self.x.device
+        main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
+        cs.wait_stream(main)
+        src.record_stream(cs)
+        self.x.record_stream(cs)
+        with torch.cuda.stream(cs):
+            comm.all_to_all_rows(st.gather_rows(src, plan.send_idx), plan.send_counts, plan.recv_counts,
+                                 out=self.x[a:b])
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        self.events[cls] = ev
+
+    def wait(self, cls):
+        ev = self.events.pop(cls, None)
+        if ev is not None:
+            torch.cuda.current_stream(self.x.device).wait_event(ev)
+
+    def wait_all(self):
+        for cls in list(self.events):
+            self.wait(cls)
+
+
+def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows]):
+    """The phases of a halo layer's forward (hip_ops.XPhase).  On a bipartite graph the user
+    destinations read item sources only and the item destinations user sources only, so each
+    phase waits for one halo class: the phase whose class is local or arrives first runs first,
+    and right after it the rows it produced start towards the next layer's peers (its output
+    rows of that destination class).  Otherwise one phase after both classes."""
+    from .hip_ops import XPhase
+    send = (lambda cls: (lambda out: rows_out.start(cls, out))) if rows_out is not None else (lambda cls: None)
+    if not (hg.bipartite and hg.fwd_sched_u is not None and hg.fwd_sched_i is not None):
+        def after_all(out):
+            if rows_out is not None:
+                rows_out.start("u", out)
+                rows_out.start("i", out)
+        return [XPhase(0, hg.n_own, hg.fwd_view.fwd_sched, (rows_in.span("u"), rows_in.span("i")), rows_in.wait_all,
+                       after_all)]
+    # destination class -> (rows, schedule, the source class it reads)
+    ph = {"u": (0, hg.n_own_u, hg.fwd_sched_u, "i"), "i": (hg.n_own_u, hg.n_own, hg.fwd_sched_i, "u")}
+    order = sorted(ph, key=lambda d: (ph[d][3] not in rows_in.local,
+                                      rows_in.started.index(ph[d][3]) if ph[d][3] in rows_in.started else 0))
+    return [XPhase(ph[d][0], ph[d][1], ph[d][2], (rows_in.span(ph[d][3]),),
+                   (lambda c: (lambda: rows_in.wait(c)))(ph[d][3]), send(d)) for d in order]
+
+
 class _HaloLayerX(torch.autograd.Function):
     """One multi-head layer on the halo partition, aggregate-then-transform (hip_ops.xgat_*):
-    forward = all_to_all of the halo rows of x (users, then items -- or, first layer, the
-    halo items' rows computed locally: ``x_halo_items``), then the layer over
-    [own | halo] sources; backward = the halo sources' edge pass first, their input gradients
-    sent back to the owners on a communication stream (RCCL all_to_all) while the own
-    sources' edge pass and the weight-gradient GEMMs run, then the owners add the returned
-    rows in peer order."""
+    forward = the layer over [own | halo] sources, its halo rows of x received by all_to_all
+    (users, then items -- or, first layer, the halo items' rows computed locally:
+    ``x_halo_items``), in phases by destination class that each wait only for the halo class
+    they read (``HaloRows``, ``_halo_phases``); with ``rows_out`` the layer starts sending its
+    own output rows to the next layer's peers as each phase finishes, so that exchange runs
+    beside this layer's remaining work.  Backward = the halo sources' edge pass first, their
+    input gradients sent back to the owners on a communication stream (RCCL all_to_all) while
+    the own sources' edge pass and the weight-gradient GEMMs run, then the owners add the
+    returned rows in peer order."""
 
     @staticmethod
     def forward(ctx, x_own, x_halo_items, weight, att_src, att_dst, bias, hg: "HaloGraph", comm: "Comm", stages,
-                heads: int, C: int, slope: float, p: float, seed: int):
+                heads: int, C: int, slope: float, p: float, seed: int, rows_in: Optional[HaloRows] = None,
+                rows_out: Optional[HaloRows] = None):
         from .hip_ops import xgat_forward
-        plans = [hg.plan_u] if x_halo_items is not None else [hg.plan_u, hg.plan_i]
         x_own = x_own.contiguous()
-        x_loc = torch.empty((hg.R, x_own.size(1)), dtype=x_own.dtype, device=x_own.device)
-        x_loc[:hg.n_own].copy_(x_own)
-        off = hg.n_own
-        for plan in plans:
-            comm.all_to_all_rows(stages.gather_rows(x_own, plan.send_idx), plan.send_counts, plan.recv_counts,
-                                 out=x_loc[off:off + plan.n_recv])
-            off += plan.n_recv
-        if x_halo_items is not None and x_halo_items.size(0):
-            x_loc[off:].copy_(x_halo_items)
-        out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed)
-        ctx.hg, ctx.comm, ctx.stages, ctx.plans = hg, comm, stages, plans
+        if rows_in is None:
+            rows_in = HaloRows(hg, comm, stages, x_own.size(1), x_own)
+            if x_halo_items is not None:
+                rows_in.set_local("i", x_halo_items)
+            for cls in ("u", "i"):
+                if cls not in rows_in.local:
+                    rows_in.start(cls, x_own)
+        elif x_halo_items is not None:
+            rows_in.set_local("i", x_halo_items)
+        x_loc = rows_in.x
+        if x_loc.data_ptr() != x_own.data_ptr():
+            x_loc[:hg.n_own].copy_(x_own)
+        out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed,
+                                      phases=_halo_phases(hg, rows_in, rows_out))
+        rows_in.wait_all()
+        ctx.hg, ctx.comm, ctx.stages = hg, comm, stages
+        ctx.plans = [rows_in.plan(c) for c in ("u", "i") if c not in rows_in.local]
         ctx.att_shapes = (att_src.shape, att_dst.shape)
-        ctx.local_items = x_halo_items is not None
+        ctx.local_items = "i" in rows_in.local
         return out
 
     @staticmethod
@@ -560,7 +695,7 @@ class _HaloLayerX(torch.autograd.Function):
             st.return_add(dx_own, ret, plan.ret_ptr, plan.ret_pos)
         d_items = dx[hg.n_own + hg.n_halo_u:] if ctx.local_items else None
         return (dx_own, d_items, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 class _ShardedBase(torch.nn.Module):
@@ -630,10 +765,8 @@ class HaloPyGGAT(_ShardedBase):
     ``forward`` returns the own rows [n_own, C]: own users, then own items."""
 
     def node_features(self, item_feats):
-        (i0, i1) = self.dg.owned()[1]
-        nu = self.n_users
-        x_items = self.stages.linear(item_feats[i0 - nu:i1 - nu].contiguous(), self.item_proj.weight,
-                                     self.item_proj.bias)
+        f = self.stages.gather_rows(item_feats, self.dg.own_items)
+        x_items = self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
         return torch.cat([self.user_emb_local, x_items], 0)
 
     @staticmethod
@@ -649,8 +782,18 @@ class HaloPyGGAT(_ShardedBase):
         f = self.stages.gather_rows(item_feats, hg.halo_items)
         return self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
 
+    def _x_path(self, li: int) -> bool:
+        conv = self.convs[li]
+        return self.exchanges_input(conv) and getattr(self.stages, "supports_x", lambda c: False)(conv)
+
     def forward(self, item_feats):
         hg = self.dg
+        rows = None
+        if self._x_path(0):
+            # the first layer's halo user rows are parameters: their exchange starts before
+            # the item projections (the own and the halo items' rows) are computed
+            rows = HaloRows(hg, self.comm, self.stages, self.user_emb_local.size(1), self.user_emb_local)
+            rows.start("u", self.user_emb_local.detach())
         x = self.node_features(item_feats)
         for li, conv in enumerate(self.convs):
             p = float(conv.dropout) if self.training else 0.0
@@ -659,12 +802,17 @@ class HaloPyGGAT(_ShardedBase):
             if li == 0 and xh is None:
                 xh = x.new_zeros(0, x.size(1))
             if self.exchanges_input(conv):
-                if getattr(self.stages, "supports_x", lambda c: False)(conv):
-                    # aggregate-then-transform on the local rows: no halo projection, the
-                    # return of the halo gradients overlapped with the own rows' backward
+                if self._x_path(li):
+                    # aggregate-then-transform on the local rows: no halo projection; the next
+                    # layer's halo rows start moving as this layer's phases finish, and the
+                    # return of the halo gradients overlaps the own rows' backward
+                    nxt = None
+                    if li + 1 < len(self.convs) and self._x_path(li + 1):
+                        nxt = HaloRows(hg, self.comm, self.stages, conv.out_channels, x)
                     x = _HaloLayerX.apply(x, xh, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg,
                                           self.comm, self.stages, conv.heads, conv.out_channels,
-                                          float(conv.negative_slope), p, seed)
+                                          float(conv.negative_slope), p, seed, rows, nxt)
+                    rows = nxt
                     continue
                 h = self.stages.linear(halo_exchange(x, hg, self.comm, self.stages, xh), conv.lin.weight, None)
             else:
@@ -690,7 +838,7 @@ def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j, plan_key=None):
         if hit is not None:
             return hit
     nu, N = hg.n_users, hg.n_nodes
-    (u0, u1), _ = hg.owned()
+    u0, u1 = hg.owned_users()
     un, inn, jn = (t.detach().cpu().numpy().astype(np.int64) for t in (u, i, j))
     mine = (un >= u0) & (un < u1)
     items = np.unique(np.concatenate([inn[mine], jn[mine]])) + nu if mine.any() else np.zeros(0, np.int64)
@@ -731,17 +879,14 @@ def halo_bpr_loss(Z_own, hg: HaloGraph, comm: "Comm", u, i, j, n_users: int, n_i
 def halo_rows_to_global(Z_own, hg: HaloGraph, comm: "Comm") -> torch.Tensor:
     """[n_own, C] own rows -> [N, C] in node-id order on every rank (all_gather; export and
     test helper, not on the training path)."""
-    pad = max(int(hg.seg_bounds[0][r + 1] - hg.seg_bounds[0][r] + hg.seg_bounds[1][r + 1] - hg.seg_bounds[1][r])
-              for r in range(hg.world))
+    ids = [hg.own_node_ids(r) for r in range(hg.world)]
+    pad = max(len(a) for a in ids)
     blk = Z_own.new_zeros(max(pad, 1), Z_own.size(1))
     blk[:hg.n_own] = Z_own
     allb = comm.all_gather_rows(blk)
     idx = np.empty(hg.n_nodes, np.int64)
-    ub, ib = hg.seg_bounds
     for r in range(hg.world):
-        nur = int(ub[r + 1] - ub[r])
-        idx[ub[r]:ub[r + 1]] = r * pad + np.arange(nur)
-        idx[ib[r]:ib[r + 1]] = r * pad + nur + np.arange(int(ib[r + 1] - ib[r]))
+        idx[ids[r]] = r * max(pad, 1) + np.arange(len(ids[r]))
     return allb.index_select(0, torch.from_numpy(idx).to(allb.device))
 
 

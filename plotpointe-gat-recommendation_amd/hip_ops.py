@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Callable, Optional
 
 import torch
 
@@ -1101,9 +1101,29 @@ def _xgat_edges_bwd_g(lib, sched: Schedule, v: "XViews", base_row: int, hs, s_sr
                                           2 * H, dz.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_g")
 
 
+@dataclass
+class XPhase:
+    """One step of a phased aggregate-then-transform forward (dist._HaloLayerX): the destination
+    rows [d0, d1) with their schedule (rows relative to d0), the source row ranges whose node
+    scores this phase computes first (rows outside the own destination rows, e.g. halo rows that
+    have just arrived), ``before()`` (e.g. make the stream wait for those rows' exchange) and
+    ``after(out)`` (e.g. start sending the phase's output rows to the peers)."""
+    d0: int
+    d1: int
+    sched: Schedule
+    src_ranges: tuple = ()
+    before: Optional[Callable] = None
+    after: Optional[Callable] = None
+
+
 def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
-                 seed: int):
-    """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state)."""
+                 seed: int, phases: Optional[list] = None):
+    """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state).
+
+    ``phases`` (a list of XPhase partitioning [0, n_dst) in order): the node scores of the
+    destination rows first, then per phase its sources' scores, the edge pass over its
+    destination rows and their rows of the output GEMM.  Per destination the result is the
+    same as the one-phase forward (same per-row kernels and order): bitwise equal."""
     lib = _lib.load()
     x = x.contiguous()
     dev = x.device
@@ -1121,24 +1141,40 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
                                       Wt.data_ptr(), None, st), "xgat_weights")
     s_src = torch.empty(v.n_src, H, dtype=torch.float32, device=dev)
     s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_src, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
+    if phases is None:
+        phases = [XPhase(0, v.n_dst, v.fwd_sched, ((v.n_dst, v.n_src),) if v.n_src > v.n_dst else ())]
+    # the destination rows' scores (s_src and s_dst), then each phase's other sources
+    _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_dst, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
                                      s_dst.data_ptr(), st), "xgat_scores")
-    _tap_kinks(v.rowptr, v.col, v.csr_eid, s_src, s_dst, H)
     agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
     m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
     inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
+    out = torch.empty(v.n_dst, C, dtype=torch.float32, device=dev)
     seed_buf = seed_buffer(p, dev)
-    nbytes = ctypes.c_size_t(0)
-    _lib.check(lib.ppgat_xgat_fwd_workspace_bytes(v.fwd_sched.n_hub_items, H, K, ctypes.byref(nbytes)), "xgat_ws")
-    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
-    cs = v.fwd_sched.cstruct()
     E = v.n_edges
-    _lib.check(lib.ppgat_xgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
-                                  _lib.ptr(v.csr_eid) if E else None, v.n_dst, E, K, H, x.data_ptr(), K,
-                                  s_src.data_ptr(), s_dst.data_ptr(), float(slope), float(p),
-                                  int(seed) & (2**64 - 1), _lib.ptr(seed_buf), agg.data_ptr(), m.data_ptr(),
-                                  inv_l.data_ptr(), ws.data_ptr(), nbytes.value, st), "xgat_fwd")
-    out = gemm_nn(agg.view(v.n_dst, H * K), Wt, 0, C, alpha=1.0 / H, bias=b)
+    for ph in phases:
+        if ph.before is not None:
+            ph.before()
+        for r0, r1 in ph.src_ranges:
+            if r1 > r0:
+                _lib.check(lib.ppgat_xgat_scores(x.data_ptr() + 4 * r0 * K, K, r1 - r0, 0, K, H, A.data_ptr(),
+                                                 s_src.data_ptr() + 4 * r0 * H, None, st), "xgat_scores")
+        nd = ph.d1 - ph.d0
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_fwd_workspace_bytes(ph.sched.n_hub_items, H, K, ctypes.byref(nbytes)), "xgat_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = ph.sched.cstruct()
+        _lib.check(lib.ppgat_xgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
+                                      _lib.ptr(v.csr_eid) if E else None, nd, E, K, H, x.data_ptr(), K,
+                                      s_src.data_ptr(), s_dst.data_ptr() + 4 * ph.d0 * H, float(slope), float(p),
+                                      int(seed) & (2**64 - 1), _lib.ptr(seed_buf), agg.data_ptr() + 4 * ph.d0 * H * K,
+                                      m.data_ptr() + 4 * ph.d0 * H, inv_l.data_ptr() + 4 * ph.d0 * H, ws.data_ptr(),
+                                      nbytes.value, st), "xgat_fwd")
+        if nd > 0:
+            gemm_nn(agg[ph.d0:ph.d1].view(nd, H * K), Wt, 0, C, alpha=1.0 / H, bias=b, out=out[ph.d0:ph.d1])
+        if ph.after is not None:
+            ph.after(out)
+    _tap_kinks(v.rowptr, v.col, v.csr_eid, s_src, s_dst, H)
     saved = dict(x=x, W=W, a_s=a_s, a_d=a_d, A=A, s_src=s_src, s_dst=s_dst, agg=agg, m=m, inv_l=inv_l,
                  seed_buf=seed_buf, v=v, meta=(H, C, K, slope, p, seed, bias is not None))
     return out, saved
@@ -1161,7 +1197,7 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     S = torch.zeros(v.n_src, 2 * H, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
     nstate = torch.empty(max(v.n_dst, 1), H, 4, dtype=torch.float32, device=dev)
-    mode = _xgat_gather_mode(C, H)
+    mode = _xgat_gather_mode(C, H, v.n_src, v.n_dst, E, K)
     if mode == "gd":
         return _xgat_backward_deferred_d(lib, saved, g, S, dz, nstate, want_bias_grad, halo_hook, st)
     Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
@@ -1214,20 +1250,34 @@ def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=
     return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
 
 
-def _xgat_gather_mode(C: int, H: int) -> str:
-    """Which multi-head backward runs (read per call): "gd" (default) gathers g_i per edge and
-    defers D (no gt GEMM: ppgat_xgat_bwd_edges_gd + D by a destination sum + ppgat_xgat_bwd_dz);
-    PPGAT_XGAT_GATHER=g gathers g_i with D from the gt GEMM's prologue (ppgat_xgat_bwd_edges_g);
-    PPGAT_XGAT_GATHER=gt gathers gt_i (ppgat_xgat_bwd_edges, round 2's pass).  DESIGN.md §4.2."""
-    mode = os.environ.get("PPGAT_XGAT_GATHER", "gd")
+def _xgat_bytes(mode: str, n_src: int, n_dst: int, n_edges: int, C: int, H: int, K: int) -> float:
+    """HBM bytes of one multi-head layer backward per formulation: per edge the
+    gathered row (g_i: 4C, or gt_i: 4HK) and the per-edge terms; per source the hs and acc rows
+    of the g-gathering passes (written, read back: 4 x 4HC) and x / dx (2 x 4K), or x / dx only;
+    per destination the gt GEMM and its prologue (3 x 4HK) in the gt-gathering pass."""
+    if mode == "gt":
+        return n_edges * (4 + 24 * H + 4 * H * K) + n_dst * 12 * H * K + n_src * 8 * K
+    return n_edges * (4 + 24 * H + 4 * C) + n_src * (8 * K + 16 * H * C)
+
+
+def _xgat_gather_mode(C: int, H: int, n_src: Optional[int] = None, n_dst: Optional[int] = None,
+                      n_edges: Optional[int] = None, K: Optional[int] = None) -> str:
+    """Which multi-head backward runs (read per call): "gd" gathers g_i per edge and defers D (no
+    gt GEMM: ppgat_xgat_bwd_edges_gd + D by a destination sum + ppgat_xgat_bwd_dz); "g" gathers
+    g_i with D from the gt GEMM's prologue (ppgat_xgat_bwd_edges_g); "gt" gathers gt_i
+    (ppgat_xgat_bwd_edges, round 2's pass).  DESIGN.md §4.2.  PPGAT_XGAT_GATHER picks one; by
+    default "gd", except where the layer's sources far outnumber its destinations (the halo
+    partition at 8 ranks: 11M local rows for 1.9M own) and the g-gathering passes' per-source
+    GEMMs would move more bytes than gathering gt_i per edge (_xgat_bytes)."""
     if C != 256 or H not in (2, 4):
         return "gt"
-    return mode if mode in ("g", "gt") else "gd"
-
-
-def _xgat_gather_g(C: int, H: int) -> bool:
-    """True when the backward edge pass gathers g_i (either "g" or the default "gd")."""
-    return _xgat_gather_mode(C, H) != "gt"
+    mode = os.environ.get("PPGAT_XGAT_GATHER")
+    if mode in ("g", "gt", "gd"):
+        return mode
+    if n_src is not None and n_src > n_dst and \
+            _xgat_bytes("gt", n_src, n_dst, n_edges, C, H, K) < _xgat_bytes("gd", n_src, n_dst, n_edges, C, H, K):
+        return "gt"
+    return "gd"
 
 
 def _xgat_backward_deferred_d(lib, saved: dict, g, S, dz, nstate, want_bias_grad: bool, halo_hook, st):

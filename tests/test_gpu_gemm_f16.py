@@ -204,3 +204,46 @@ def test_gemm_nn_rank_equals_gemm_then_rank_update(pkg, cuda, M, K, N, nv, lds):
     ops.rank_update_(ref2, S[7:], A)
     assert torch.equal(y2[14:], ref2)
     assert torch.isnan(y2[:14]).all()
+
+
+_NNH2_CHECK = r"""
+import hashlib, importlib, json, sys, torch
+sys.path.insert(0, sys.argv[1])
+ops = importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(3)
+out = {}
+for M, K, N, lay in ((70000, 1024, 256, 0), (9000, 256, 1024, 1), (30001, 896, 128, 1)):
+    X = torch.randn(M, K, device=dev, generator=g)
+    X[::7] *= 1e-3                                   # rows with different scales
+    X[5, K // 2:] *= 1e6                             # a row whose scale drops mid-way (rescale path)
+    B = torch.randn(K, N, device=dev, generator=g) * 0.05
+    Bl = B if lay == 0 else B.t().contiguous()
+    y = ops.gemm_nn(X, Bl, lay, N, alpha=0.25)
+    S = torch.randn(M, 8, device=dev, generator=g)
+    A = torch.randn(8, N, device=dev, generator=g)
+    yr = ops.gemm_nn(X, Bl, lay, N, rank=(S, A))
+    torch.cuda.synchronize()
+    out[f"{M}x{K}x{N}"] = [hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest() for t in (y, yr)]
+print(json.dumps(out))
+"""
+
+
+def test_nnh2_bitwise_equals_nnh(cuda):
+    """The pipelined NN kernel (k_gemm_nnh2, the default) and k_gemm_nnh (PPGAT_NNH2=0) compute
+    the same products in the same order: bitwise equal outputs, with and without the fused rank
+    epilogue, on both B layouts, a ragged row count, an odd chunk count (K = 896: k_gemm_nnh
+    runs it) and a row that takes the rescale path."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    res = []
+    for v in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", _NNH2_CHECK, str(root)], env=dict(os.environ, PPGAT_NNH2=v),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1]

@@ -33,6 +33,9 @@ for s in $STEPS; do
     traj) for v in default:PPGAT_NONE=1 fuseddxw0:PPGAT_FUSED_DXW=0 gemmfp32:PPGAT_GEMM=fp32; do
             run "traj_${v%%:*}" 900 env PPGAT_REPORT_TAG="${v%%:*}" "${v#*:}" python -u -m pytest tests/test_gpu_trajectory.py -m gpu -v -s -rf --timeout 800 --timeout-method thread
           done ;;
+    probe5) for a in "0 0" "7 0" "7 640"; do set -- $a
+              run "probe5_r$1_a$2" 900 python -u tools/scale_probe.py --config 5 --world 8 --rank $1 --streams --a2a-gbs $2 --steps 5 --warmup 2
+            done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;

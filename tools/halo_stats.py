@@ -4,6 +4,7 @@ computed on the host with the partition code itself (no GPU):
 
     python tools/halo_stats.py --config 5 --world 8      # 200M-edge synthetic, d=256, heads=4
     python tools/halo_stats.py --config 2 --world 8      # config 4 (config-2 graph)
+    python tools/halo_stats.py --config 5 --item-partition contiguous   # the round-3 ownership
 
 Per rank: own rows, halo rows received, rows sent, local (destination-owned) edges; bytes per
 layer and direction for the exchanged operand (x: C_in floats when H*C > C_in, else h)."""
@@ -24,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=5)
     ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--item-partition", choices=["dealt", "contiguous"], default="dealt")
     args = ap.parse_args()
     d = pkg.data
     if args.config == 5:
@@ -37,10 +39,7 @@ def main():
     items = g.user_items.astype(np.int64) + nu
     # the U-I columns come in (u -> i, i -> u) pairs: each interaction is a message both ways
     deg = np.bincount(users, minlength=N) * 2 + np.bincount(items, minlength=N) * 2 + 4.0
-    owner = np.empty(N, np.int32)
-    for a, b in ((0, nu), (nu, N)):
-        bnd = a + pkg.dist.partition_bounds(deg[a:b].astype(np.float64), W)
-        owner[a:b] = np.repeat(np.arange(W, dtype=np.int32), np.diff(bnd))
+    owner, _ = pkg.dist.halo_owner(deg.astype(np.float64), nu, W, args.item_partition)  # the partition code itself
     ou, oi = owner[users], owner[items]
     out = []
     for r in range(W):
@@ -65,7 +64,10 @@ def main():
     l1 = max(max(o["halo_users"], o["sent_users"]) for o in out) * row_bytes / 1e9
     l2 = max(max(o["halo_rows"], o["sent_rows"]) for o in out) * row_bytes / 1e9
     print(json.dumps({"layer1_GB_busiest_rank": l1, "layer2_GB_busiest_rank": l2, "step_GB_busiest_rank": 2 * (l1 + l2)}))
-    print(json.dumps({"config": args.config, "world": W, "nodes": N, "edges": 2 * len(users), "row_bytes": row_bytes,
+    sends = [o["send_GB_per_layer_dir"] for o in out]
+    print(json.dumps({"config": args.config, "world": W, "item_partition": args.item_partition, "nodes": N,
+                      "edges": 2 * len(users), "row_bytes": row_bytes,
+                      "max_send_over_mean": max(sends) / (sum(sends) / W),
                       "max_recv_GB": max(o["recv_GB_per_layer_dir"] for o in out),
                       "max_send_GB": max(o["send_GB_per_layer_dir"] for o in out),
                       "max_local_edges": max(o["local_edges"] for o in out)}))

@@ -1,12 +1,19 @@
 #!/usr/bin/env python3
-"""One rank's share of an N-GPU config-2 step, on one GPU, collectives stubbed out.
+"""One rank's share of an N-GPU step, on one GPU, collectives stubbed out.
 
     python tools/scale_probe.py --world 8 --rank 0 [--partition replicated|halo]
+    python tools/scale_probe.py --config 5 --world 8 --rank 7 --streams --a2a-gbs 640
 
-Builds the same per-rank graph and model as `bench.py --gpus N` and times the step with
-every collective replaced by a no-op (results are NOT the job's; only the compute and the
-host enqueue time of one rank are measured).  Shows what is left per rank once the
-exchange is overlapped or free: the floor under N-GPU ms/step."""
+Builds the same per-rank graph and model as `bench.py --gpus N` (config 2, or --config 5: the
+200M-edge synthetic, d=256, heads=4, halo partition) and times the step with every collective
+replaced by a stub (results are NOT the job's; only the compute and the host enqueue time of
+one rank are measured).  Without --a2a-gbs the stub is free: the floor under N-GPU ms/step.
+With --a2a-gbs B the stub holds the stream it runs on for this rank's exchange time at B GB/s
+(max(bytes sent, bytes received) / B per all_to_all, 2 (N-1)/N x bytes / B per all_reduce;
+a GPU-side sleep of one wave, calibrated at start): with --streams the exchanges run on the
+communication stream as RCCL's would, so the step time shows how much of the modelled
+exchange the overlaps hide.  A model, not a measurement of RCCL over xGMI: the real
+all_to_all also reads and writes HBM beside the compute."""
 import argparse
 import importlib
 import json
@@ -27,8 +34,18 @@ data = pkg.data
 
 
 class NullComm:
-    def __init__(self, world, rank):
+    def __init__(self, world, rank, gbs=0.0, cycles_per_ms=0.0):
         self.world, self.rank, self.backend, self.group, self.active = world, rank, "null", None, True
+        self.gbs, self.cycles_per_ms = gbs, cycles_per_ms
+        self.modelled_ms = 0.0   # exchange time modelled per step (host-side tally)
+
+    def _hold(self, nbytes):
+        """Hold the current stream for nbytes at self.gbs (the modelled exchange)."""
+        if self.gbs <= 0 or nbytes <= 0:
+            return
+        ms = nbytes / (self.gbs * 1e9) * 1e3
+        self.modelled_ms += ms
+        torch.cuda._sleep(int(ms * self.cycles_per_ms))
 
     def all_gather_rows(self, t):
         return t.contiguous().repeat((self.world,) + (1,) * (t.dim() - 1))
@@ -37,6 +54,7 @@ class NullComm:
         return t.contiguous()[: t.size(0) // self.world].contiguous()
 
     def all_reduce_(self, t, op=None):
+        self._hold(2 * (self.world - 1) / self.world * t.numel() * t.element_size())
         return t
 
     own_id = 0  # a node id this rank owns (set after the graph is built): the stubbed id exchange
@@ -45,6 +63,9 @@ class NullComm:
         # stub: received rows are zeros, received ids are an id this rank owns (so the loss
         # plan's requests resolve to local rows); timing only
         n = int(sum(recv_counts))
+        row = t[0].numel() * t.element_size() if t.dim() and t.size(0) else 0
+        row = row or (int(np.prod(t.shape[1:])) * t.element_size() if t.dim() > 1 else t.element_size())
+        self._hold(max(int(sum(send_counts)), n) * row)
         if out is None:
             fill = self.own_id if not t.is_floating_point() else 0
             out = torch.full((n,) + tuple(t.shape[1:]), fill, dtype=t.dtype, device=t.device)
@@ -67,17 +88,35 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph (as bench.py for N>1)")
     ap.add_argument("--streams", action="store_true",
                     help="report the stub as RCCL so the comm-stream overlaps (fwd_split / bwd_split) run as at N>1")
+    ap.add_argument("--config", type=int, choices=[2, 5], default=2)
+    ap.add_argument("--a2a-gbs", type=float, default=0.0,
+                    help="model each exchange as this rank's bytes at this rate (GB/s); 0: free")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    g = data.synthetic_ui_graph(seed=42)
-    feats = torch.from_numpy(data.synthetic_item_features(g.n_items, 128, seed=42)).to(dev)
+    if args.config == 5:
+        args.partition = "halo"
+        g = data.synthetic_scaling_graph(1.0, seed=42)
+        fdim, hidden, heads = 256, 256, 4
+    else:
+        g = data.synthetic_ui_graph(seed=42)
+        fdim, hidden, heads = 128, 128, 1
+    feats = torch.from_numpy(data.synthetic_item_features(g.n_items, fdim, seed=42)).to(dev)
     ei = torch.from_numpy(g.edge_index_numpy()).to(dev)
     u, i, j = data.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items, 200_000, seed=42)
     tu, ti, tj = (torch.from_numpy(a).to(dev) for a in (u, i, j))
     torch.manual_seed(42)
-    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=128, hidden=128, layers=2, heads=1,
+    full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=fdim, hidden=hidden, layers=2, heads=heads,
                       attn_dropout=0.1).to(dev)
-    comm = NullComm(args.world, args.rank)
+    cyc = 0.0
+    if args.a2a_gbs > 0:  # calibrate the GPU sleep: cycles per millisecond
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1_000_000)
+        a.record()
+        torch.cuda._sleep(50_000_000)
+        b.record()
+        torch.cuda.synchronize()
+        cyc = 50_000_000 / a.elapsed_time(b)
+    comm = NullComm(args.world, args.rank, args.a2a_gbs, cyc)
     if args.streams:
         comm.backend = "nccl"
     D = pkg.dist
@@ -88,7 +127,10 @@ def main():
         n_edges = dg.view.n_fwd_edges
     else:
         dg = D.build_halo_graph(ei, g.n_nodes, g.n_users, args.world, args.rank)
-        comm.own_id = int(dg.owned()[1][0])  # first own item
+        del ei
+        ei = None
+        torch.cuda.empty_cache()
+        comm.own_id = int(dg.own_node_ids()[dg.n_own_u]) if dg.n_own > dg.n_own_u else 0  # first own item
         model = D.HaloPyGGAT(full, dg, comm)
         loss_fn = D.halo_bpr_loss
         n_edges = dg.fwd_view.n_fwd_edges
@@ -99,7 +141,7 @@ def main():
         if args.graph:
             _lib.dropout_advance(dev)
         Z = model(feats)
-        loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items)
+        loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items, plan_key="probe")  # fixed triples
         opt.zero_grad(set_to_none=True)
         loss.backward()
         model.allreduce_grads()
@@ -121,6 +163,7 @@ def main():
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
+    comm.modelled_ms = 0.0
     _lib.profile_reset()
     _lib.profile_enable(not args.graph)
     t0 = time.perf_counter()
@@ -132,8 +175,10 @@ def main():
     _lib.profile_enable(False)
     kern = {k: _lib.profile_read(k)[0] / args.steps for k in ("fwd", "bwd_pro", "bwd_src", "bwd_epi", "proj",
                                                                "gemm_tn", "adam")}
-    print(json.dumps({"partition": args.partition, "graph": args.graph, "world": args.world, "rank": args.rank,
-                      "rows": int(dg.R), "local_edges": int(n_edges), "global_edges": int(ei.size(1)),
+    print(json.dumps({"config": args.config, "partition": args.partition, "graph": args.graph, "world": args.world,
+                      "rank": args.rank, "streams": args.streams, "a2a_gbs": args.a2a_gbs,
+                      "modelled_exchange_ms_per_step": comm.modelled_ms / args.steps if not args.graph else None,
+                      "rows": int(dg.R), "local_edges": int(n_edges), "global_edges": int(2 * g.n_interactions),
                       "ms_per_step": el / args.steps * 1e3, "host_enqueue_ms_per_step": th / args.steps * 1e3,
                       "kernel_ms_per_step": kern}), flush=True)
 
