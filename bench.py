@@ -443,8 +443,15 @@ def main():
         "hip_graph": graph is not None,
         "formulation": ("aggregate-then-transform (x_j gathered once per edge for all heads)" if xform_k else
                         "transform-then-aggregate (h_j gathered per edge)"),
-        "gemm": ("fp32 MFMA (PPGAT_GEMM=fp32)" if os.environ.get("PPGAT_GEMM") == "fp32" else
-                 "fp32 results on bf16 MFMA, three-term split, 6 products (DESIGN.md 4.3)"),
+        "gemm": ("fp32 MFMA, exact fp32 FMA chains (PPGAT_GEMM=fp32)" if os.environ.get("PPGAT_GEMM") == "fp32" else
+                 "fp32 operands and results on the matrix cores through operand splits (DESIGN.md 4.3): "
+                 "fp16 two-term split with power-of-two row/column scales, 3 MFMAs per product, <= 2^-21 "
+                 "relative per product, for the large-M NN and TN products (k_gemm_nnh2, k_gemm_tnh); bf16 "
+                 "three-term split, 6 MFMAs, <= 2^-24, for the rest"
+                 if args.config == 5 and os.environ.get("PPGAT_GEMM_F16", "1") != "0" else
+                 "fp32 operands and results on the matrix cores through the bf16 three-term split (6 MFMAs "
+                 "per product, <= 2^-24 relative per product: k_projx, k_dxw; DESIGN.md 4.3), fp32 MFMA "
+                 "for the small weight-gradient products"),
         "kernel_timing": kern_src,
         "fused_kernel_edges_per_sec": E * args.layers * K / (fused_ms / 1e3) if fused_ms else None,
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},

@@ -498,12 +498,20 @@ int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, 
  *   (b_bound_bits[j % bound_period] as IEEE bits, times bound_scale >= 1) in place of the
  *   column-max pass over b that the fp16 two-term kernel otherwise makes -- e.g. the multi-head
  *   layer's G = g^T agg with |agg^h_i[k]| <= max_j |x_j[k]| / (1 - p) (train_gat_pyg.py:77 backward).
- *   Any bound >= the true maxima gives the same accuracy class; the fp32 / bf16 families ignore it.
- * ppgat_colmax_abs: out_bits[c] = IEEE bits of max_i |x[i, c]| (order-free: deterministic). */
+ *   The fp16 split's error is relative to the bound, not to b's own column maxima: a column
+ *   whose bound is 2^k above its true maximum loses about k bits (22 - k significant bits per
+ *   product), so the bound should be tight -- for agg, the column maxima over the rows that are
+ *   the SOURCE of an edge (ppgat_colmax_abs_sources), not over all rows of x.  The fp32 / bf16
+ *   families ignore it.
+ * ppgat_colmax_abs: out_bits[c] = IEEE bits of max_i |x[i, c]| (order-free: deterministic).
+ * ppgat_colmax_abs_sources: the same over the rows i with src_ptr[i + 1] > src_ptr[i] (src_ptr:
+ *   the CSC pointers [n + 1] of the edge list; rows with no out-edge never enter an aggregate). */
 int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
                               const unsigned* b_bound_bits, int bound_period, float bound_scale, float* out,
                               void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream);
+int ppgat_colmax_abs_sources(const float* x, int64_t ldx, int64_t n, int c, const int32_t* src_ptr,
+                             unsigned* out_bits, void* stream);
 int ppgat_colsum_workspace_bytes(int64_t n, int c, size_t* bytes);
 int ppgat_colsum(const float* y, int64_t ldy, int64_t n, int c, float* out, void* workspace, size_t workspace_bytes,
                  void* stream);

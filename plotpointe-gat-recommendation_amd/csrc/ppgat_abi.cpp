@@ -1058,6 +1058,18 @@ int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* ou
   return PPGAT_OK;
 }
 
+int ppgat_colmax_abs_sources(const float* x, int64_t ldx, int64_t n, int c, const int32_t* src_ptr,
+                             unsigned* out_bits, void* stream) {
+  if (n < 0 || c < 4 || (c % 4) || ldx < c || (ldx % 4)) return fail(PPGAT_ERR_INVALID, "colmax_abs_sources: bad sizes");
+  if (!out_bits || (n > 0 && (!x || !src_ptr))) return fail(PPGAT_ERR_INVALID, "colmax_abs_sources: null pointer");
+  if (!al16(x)) return fail(PPGAT_ERR_UNSUPPORTED, "colmax_abs_sources: 16-byte aligned rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_GEMM_TN, st);
+  hipError_t e = ppgat::colmax_abs(x, ldx, n, c, out_bits, st, src_ptr);
+  if (e != hipSuccess) return hip_fail(e, "colmax_abs_sources");
+  return PPGAT_OK;
+}
+
 int ppgat_colsum_workspace_bytes(int64_t n, int c, size_t* bytes) {
   if (!bytes || n < 0 || (c != 128 && c != 256)) return fail(PPGAT_ERR_UNSUPPORTED, "colsum: c must be 128 or 256");
   *bytes = align_up((size_t)ppgat::colsum_blocks(n) * c * 4);

@@ -185,7 +185,8 @@ size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
                        void* ws, hipStream_t st, const unsigned* b_bound = nullptr, int b_period = 0,
                        float b_scale = 1.f);
-hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st);
+hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st,
+                      const int32_t* src_ptr = nullptr);
 bool xgat_shape_ok(int K, int H, int C);
 hipError_t xgat_weights(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
                         float* Wt, float* Wg, hipStream_t st);

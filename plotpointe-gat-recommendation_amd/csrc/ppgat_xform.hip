@@ -757,7 +757,9 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int NT, bool RK>
+// LAB (diagnostics only, PPGAT_NNH2_LAB; results wrong): 1 = no X loads after the first two
+// chunks (registers reused), 2 = no B DMA after the first two chunks (LDS reused), 3 = both
+template <int NT, bool RK, int LAB = 0>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
@@ -816,8 +818,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
     split::split2h(xc[0], xc[1], s, fx[0][0], fx[0][1]);
     split::split2h(xc[2], xc[3], s, fx[1][0], fx[1][1]);
     const bool ahead = c + 2 < chunks;
-    if (ahead) issue(c + 2);
-    loadx(ahead ? c + 2 : chunks - 1, xc);
+    if (ahead && !(LAB & 2)) issue(c + 2);
+    if (!(LAB & 1)) loadx(ahead ? c + 2 : chunks - 1, xc);
     const uint16_t* sb = sB[c % 3];
     auto read_b = [&](int i, split::u32x4 (&f)[2]) {
       const int off = (32 * (i % NT) + r) * LDK + 16 * (i / NT) + 8 * hf;
@@ -838,7 +840,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
     // DMA(c + 1) must have landed before any wave reads it, and every wave must be done with
     // sB[c % 3] before chunk c + 3's DMA (issued in chunk c + 1) overwrites it.  Issued after
     // DMA(c + 1): X(c + 1), and in this chunk DMA(c + 2) (if any) and an X set.
-    if (ahead) {
+    if (LAB) {
+      wait_vm<0>();
+    } else if (ahead) {
       if (full) wait_vm<4 + ND + 4>(); else wait_vm<4 + ND - 1 + 4>();
     } else {
       wait_vm<4 + 4>();
@@ -1057,15 +1061,18 @@ constexpr int kThImg = kTR * 128 * 2;       // bytes per fp16 image [32][128]
 constexpr int kThBuf = 6 * kThImg;          // A hi/lo, B half 0 hi/lo, B half 1 hi/lo (48 KB)
 constexpr size_t kThLds = 2 * kThBuf + (2 * 128 + 2 * 256) * sizeof(float);
 
-// column maxima of |X| over rows [r0, r1) of a row block, merged into out[] as IEEE bits
+// column maxima of |X| over rows [r0, r1) of a row block, merged into out[] as IEEE bits;
+// with rp (CSC pointers [M + 1]) only over the rows that are the source of an edge
 __global__ void __launch_bounds__(256) k_colmax_bits(const float* __restrict__ X, int64_t ldx, int64_t M, int C,
-                                                     int64_t rows_per_block, unsigned* __restrict__ out) {
+                                                     int64_t rows_per_block, const int32_t* __restrict__ rp,
+                                                     unsigned* __restrict__ out) {
   __shared__ float4 red[256];
   const int T = C >> 2, P = 256 / T, t = threadIdx.x, cg = t % T, rl = t / T;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   float4 m = f4(0.f);
   if (rl < P) {
     for (int64_t r = r0 + rl; r < r1; r += P) {
+      if (rp != nullptr && rp[r + 1] == rp[r]) continue;
       const float4 v = ld4(X + r * ldx + 4 * cg);
       m = make_float4(fmaxf(m.x, fabsf(v.x)), fmaxf(m.y, fabsf(v.y)), fmaxf(m.z, fabsf(v.z)), fmaxf(m.w, fabsf(v.w)));
     }
@@ -2077,6 +2084,14 @@ static bool nnh2_enabled() {
   return on;
 }
 
+static int nnh2_lab() {
+  static const int lab = [] {
+    const char* e = getenv("PPGAT_NNH2_LAB");
+    return e ? atoi(e) : 0;
+  }();
+  return lab;
+}
+
 static size_t nnq_bytes(int K, int N) {  // image + column exponents, either family
   const int nt = N % 256 == 0 ? 8 : 4;
   return nnh_enabled() ? align_up(nnh_image_bytes(K, N, nt)) + align_up((size_t)N * 4) : nnp_image_bytes(K, N);
@@ -2114,6 +2129,12 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       hipError_t e = nnh_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, ecol, st);
       if (e != hipSuccess) return e;
       if (nnh2_enabled() && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
+        if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {
+          if (lab == 1) hipLaunchKernelGGL((k_gemm_nnh2<8, false, 1>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          else if (lab == 2) hipLaunchKernelGGL((k_gemm_nnh2<8, false, 2>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          else hipLaunchKernelGGL((k_gemm_nnh2<8, false, 3>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          return hipGetLastError();
+        }
         if (nv > 0) {
           if (w8) hipLaunchKernelGGL((k_gemm_nnh2<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
           else hipLaunchKernelGGL((k_gemm_nnh2<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
@@ -2226,7 +2247,8 @@ size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb) {
   return align_up((size_t)tn_splits(M, T) * Ma * Nb * 4);
 }
 
-static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st) {
+static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st,
+                              const int32_t* rp = nullptr) {
   // C columns in slices of <= 1024 (256 float4 lanes per row pass)
   for (int c0 = 0; c0 < C; c0 += 1024) {
     const int c = C - c0 < 1024 ? C - c0 : 1024;
@@ -2234,14 +2256,15 @@ static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, uns
     if (blocks > 1024) blocks = 1024;
     const int64_t rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
-    hipLaunchKernelGGL(k_colmax_bits, dim3((unsigned)blocks), dim3(256), 0, st, X + c0, ldx, M, c, rpb, out + c0);
+    hipLaunchKernelGGL(k_colmax_bits, dim3((unsigned)blocks), dim3(256), 0, st, X + c0, ldx, M, c, rpb, rp, out + c0);
   }
   return hipGetLastError();
 }
 
-hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st) {
+hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st,
+                      const int32_t* src_ptr) {
   hipError_t e = hipMemsetAsync(out, 0, (size_t)C * 4, st);
-  if (e == hipSuccess && M > 0) e = colmax_bits(X, ldx, M, C, out, st);
+  if (e == hipSuccess && M > 0) e = colmax_bits(X, ldx, M, C, out, st, src_ptr);
   return e;
 }
 

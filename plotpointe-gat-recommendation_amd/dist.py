@@ -332,6 +332,14 @@ class HaloGraph:
     fwd_sched_i: object = None     # ... over the own item destinations (rows relative to n_own_u)
     own_items: torch.Tensor = None # [n_own - n_own_u] int64 item indices (node id - n_users), ascending
     item_partition: str = "dealt"
+    # symmetric edge list (every column j -> i has its i -> j, as build_edge_index's U-I graph):
+    # the rows a rank needs as sources (forward) are exactly the rows it needs as destinations of
+    # its own rows' out-edges, so the backward can run at the SOURCE's owner (_halo_xgat_backward)
+    symmetric: bool = False
+    src_views: object = None       # hip_ops.XViews of the edges whose source is own (CSC over own rows,
+                                   # CSR over the [own | halo] destination table)
+    src_sched_u: object = None     # their schedule over the own user sources
+    src_sched_i: object = None     # ... over the own item sources (rows relative to n_own_u)
 
     @property
     def R(self) -> int:
@@ -366,7 +374,7 @@ class HaloGraph:
         from .hip_ops import XViews
         f, b = self.fwd_view, self.bwd_view
         return XViews(self.n_own, self.R, f.n_fwd_edges, f.col, f.csr_eid, f.fwd_sched, b.row, b.csc_eid, b.dz_slot,
-                      b.bwd_sched, self.bwd_sched_own, self.bwd_sched_halo, rowptr=f.rowptr)
+                      b.bwd_sched, self.bwd_sched_own, self.bwd_sched_halo, rowptr=f.rowptr, colptr=b.colptr)
 
 
 def halo_owner(deg: np.ndarray, n_users: int, world: int, item_partition: str = "dealt"):
@@ -397,6 +405,27 @@ def halo_owner(deg: np.ndarray, n_users: int, world: int, item_partition: str = 
     else:
         raise ValueError(f"item_partition must be 'dealt' or 'contiguous', not {item_partition!r}")
     return owner, ub
+
+
+def _mix64(k: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser over uint64 keys (wrapping arithmetic)."""
+    k = k.astype(np.uint64)
+    k = (k ^ (k >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    k = (k ^ (k >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return k ^ (k >> np.uint64(31))
+
+
+def edges_symmetric(src: np.ndarray, dst: np.ndarray, n: int) -> bool:
+    """Whether the multiset of columns (src, dst) equals that of (dst, src): equal in- and
+    out-degrees and equal sums of a 64-bit hash of the ordered pair (a multiset hash; a false
+    positive needs a 2^-64 collision).  build_edge_index's U-I graph (u -> i and i -> u per
+    interaction) is symmetric."""
+    with np.errstate(over="ignore"):
+        if not np.array_equal(np.bincount(src, minlength=n), np.bincount(dst, minlength=n)):
+            return False
+        a = _mix64(src.astype(np.uint64) * np.uint64(n) + dst.astype(np.uint64)).sum(dtype=np.uint64)
+        b = _mix64(dst.astype(np.uint64) * np.uint64(n) + src.astype(np.uint64)).sum(dtype=np.uint64)
+    return bool(a == b)
 
 
 def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,
@@ -457,6 +486,18 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     hg.item_partition = item_partition
     hg.n_own_u = u1 - u0
     hg.bipartite = bool(np.all((src < nu) != (dst < nu)))  # the same decision on every rank
+    hg.symmetric = edges_symmetric(src, dst, N)
+    if hg.symmetric:
+        # the edges whose SOURCE this rank owns: source rows own-local, destinations in the
+        # [own | halo] table (by symmetry every such destination is own or a halo row)
+        sh = np.flatnonzero(osrc == rank)
+        dl = lidx[dst[sh]]
+        assert (dl >= 0).all(), "symmetric graph: every out-neighbour of an own row is own or halo"
+        Gb = csr_builder(torch.from_numpy(np.stack([local_of[src[sh]], dl])).to(dev), R)
+        Eb = len(sh)
+        gidb = torch.from_numpy(sh.astype(np.int32)).to(dev)
+        origb = (lambda t: gidb[t.long()].contiguous()) if Eb else (lambda t: t[:0].contiguous())
+        hg.src_views = _src_views(n_own, R, Eb, Gb, origb)
     if dev.type == "cuda" and _lib.debug_build():  # debug build: plans and views within bounds
         for pname, plan in (("plan_u", plan_u), ("plan_i", plan_i)):
             _lib.check_index_range(plan.send_idx, 0, n_own, f"halo.{pname}.send_idx")
@@ -477,7 +518,23 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
         # other class, so a phase needs only that class's halo rows; _HaloLayerX)
         hg.fwd_sched_u = sched_builder(rowptr_own[:hg.n_own_u + 1].contiguous(), El)
         hg.fwd_sched_i = sched_builder(rowptr_own[hg.n_own_u:].contiguous(), El)
+        if hg.src_views is not None:
+            sv = hg.src_views
+            sv.fwd_sched = sched_builder(sv.rowptr, sv.n_edges)   # destination sums over the R table rows
+            hg.src_sched_u = sched_builder(sv.colptr[:hg.n_own_u + 1].contiguous(), sv.n_edges)
+            hg.src_sched_i = sched_builder(sv.colptr[hg.n_own_u:].contiguous(), sv.n_edges)
+            sv.bwd_sched = sched_builder(sv.colptr, sv.n_edges)
     return hg
+
+
+def _src_views(n_own: int, R: int, Eb: int, Gb, orig):
+    """hip_ops.XViews of the edges whose source is own: CSC over the own source rows (row = the
+    destination's row in the [own | halo] table, dz in CSC order), CSR over the table rows (the
+    per-destination partial sums, read through csr2csc); edge ids mapped to edge_index columns."""
+    from .hip_ops import XViews
+    return XViews(R, n_own, Eb, Gb.col[:Eb].contiguous(), orig(Gb.csr_eid[:Eb]), None, Gb.row[:Eb].contiguous(),
+                  orig(Gb.csc_eid[:Eb]), None, None, csr2csc=Gb.csc2csr[:Eb].contiguous(),
+                  rowptr=Gb.rowptr.contiguous(), colptr=Gb.colptr[:n_own + 1].contiguous())
 
 
 # ---------------------------------------------------------------------------
@@ -663,6 +720,15 @@ class _HaloLayerX(torch.autograd.Function):
         from .hip_ops import xgat_backward
         hg, comm, st, plans = ctx.hg, ctx.comm, ctx.stages, ctx.plans
         dev = g.device
+        if source_homed_backward(hg):
+            dx, dW, datt_src, datt_dst, dbias = _halo_xgat_backward(ctx.saved, g, hg, comm, st,
+                                                                    ctx.needs_input_grad[5])
+            ctx.saved = None
+            # every input gradient of an own row is complete here (its out-edges live on this
+            # rank); the halo rows' -- incl. the first layer's locally computed halo items -- are
+            # their owners' business
+            return (dx, None, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
+                    None, None, None, None, None, None, None, None, None, None)
         pending = {}
 
         def a2a_back(dx_halo):
@@ -696,6 +762,101 @@ class _HaloLayerX(torch.autograd.Function):
         d_items = dx[hg.n_own + hg.n_halo_u:] if ctx.local_items else None
         return (dx_own, d_items, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
                 None, None, None, None, None, None, None, None, None, None)
+
+
+def source_homed_backward(hg: "HaloGraph") -> bool:
+    """The multi-head halo layer's backward runs at the source rows' owners (_halo_xgat_backward)
+    on a symmetric edge list unless PPGAT_HALO_BWD=dst (the round-3 backward: edges at their
+    destination's owner, halo sources' input gradients returned)."""
+    return hg.src_views is not None and os.environ.get("PPGAT_HALO_BWD", "src") != "dst"
+
+
+def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Comm", stages,
+                        want_bias_grad: bool):
+    """Backward of the multi-head halo layer with every edge processed at its SOURCE's owner.
+
+    The forward ran each edge at its destination's owner (the aggregation needs a destination's
+    whole in-edge list).  The backward's edge pass is by source (pass B), and on the round-3 path
+    it also ran at the destination's owner: every rank then computed hs = x W^T / H and
+    dx = acc W / H for all of its local rows -- own AND halo, 11M rows against 1.9M own at 8 ranks
+    on config 5 -- and returned the halo rows' dx.  On a symmetric edge list the destinations of
+    an own row's out-edges are exactly the rows the rank already holds as [own | halo], so here:
+      1. the own rows' destination state: gt = g W_g, nstate {s_dst, m, inv_l, D = gt . agg}
+         (the g-gathering formulation; D needs agg, which only the destination's owner has);
+      2. g and nstate of the halo rows arrive by the forward's plans (the same rows; g starts
+         at once, beside the gt GEMM, the prologue and the hs GEMM; nstate after the prologue);
+      3. hs = x W^T / H over the OWN rows only; the edge pass over the own sources' out-edges in
+         two phases by source class (item sources read user rows and vice versa), each waiting
+         only for its class of halo rows: dz per edge, ds_src and acc per own source;
+      4. ds_dst: per destination row of the table, this rank's partial sum; the halo rows'
+         partials go back to their owners (H floats per row), added after the own partial in
+         peer order (ppgat_rows_return_add: deterministic);
+      5. dx = acc W / H + ds_src A_src + ds_dst A_dst over the own rows (rank terms in the
+         GEMM's epilogue) -- the complete input gradient, nothing returned;
+      6. dW from G = g^T agg (own destinations) and GV = S^T x (own rows), datt, dbias.
+    Exchanges per layer: g + nstate of the halo rows (the forward's x volume) and the partial
+    ds_dst return, instead of the halo rows' dx; per-rank GEMMs over own rows only."""
+    from . import hip_ops as O
+    lib = _lib.load()
+    x, W, A = saved["x"], saved["W"], saved["A"]
+    s_src, s_dst, agg, m, inv_l = saved["s_src"], saved["s_dst"], saved["agg"], saved["m"], saved["inv_l"]
+    H, C, K, slope, p, seed, has_bias = saved["meta"]
+    dev = x.device
+    st = _lib.stream_handle(dev)
+    n0, R, sv = hg.n_own, hg.R, hg.src_views
+    E = sv.n_edges
+    g = g.contiguous()
+    gtab = HaloRows(hg, comm, stages, C, g)
+    gtab.x[:n0].copy_(g)
+    for cls in ("u", "i"):
+        gtab.start(cls, g)
+    # 1. destination state of the own rows
+    Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
+               "xgat_weights")
+    gt = O.gemm_nn(g, Wg, 0, H * K)
+    nst = torch.empty(max(n0, 1), 4 * H, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_bwd_prologue(gt.data_ptr(), agg.data_ptr(), s_dst.data_ptr(), m.data_ptr(),
+                                           inv_l.data_ptr(), n0, K, H, nst.data_ptr(), st), "xgat_bwd_prologue")
+    del gt, Wg
+    nst = nst[:n0]
+    ntab = HaloRows(hg, comm, stages, 4 * H, nst)
+    ntab.x[:n0].copy_(nst)
+    for cls in ("u", "i"):
+        ntab.start(cls, nst)
+    # 3. own sources
+    hs = O.gemm_nn(x[:n0], W, 1, H * C, alpha=1.0 / H)
+    acc = torch.empty(n0, H * C, dtype=torch.float32, device=dev)
+    S = torch.zeros(max(n0, 1), 2 * H, dtype=torch.float32, device=dev)
+    dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    phases = ([("i", hg.src_sched_i, hg.n_own_u, "u"), ("u", hg.src_sched_u, 0, "i")] if hg.bipartite else
+              [("all", sv.bwd_sched, 0, None)])
+    for _, sched, base, need in phases:
+        for tab in (gtab, ntab):
+            tab.wait_all() if need is None else tab.wait(need)
+        O._xgat_edges_bwd_g(lib, sched, sv, base, hs, s_src, ntab.x, gtab.x, acc, S, dz, H, C, slope, p, seed,
+                            saved["seed_buf"], st)
+    gtab.wait_all()
+    ntab.wait_all()
+    del hs
+    # 4. ds_dst: partial sums over the table rows, the halo rows' back to their owners
+    dsd = torch.zeros(max(R, 1), H, dtype=torch.float32, device=dev)
+    O._xgat_dst_sum(lib, sv, dz, dsd, H, E, st, col0=0, ld=H)
+    del dz
+    own = dsd[:n0]
+    off = n0
+    for plan in (hg.plan_u, hg.plan_i):
+        ret = comm.all_to_all_rows(dsd[off:off + plan.n_recv], plan.recv_counts, plan.send_counts)
+        stages.return_add(own, ret, plan.ret_ptr, plan.ret_pos)
+        off += plan.n_recv
+    S = S[:n0]
+    S[:, H:].copy_(own)
+    # 5. the complete input gradient of the own rows
+    dx = O.gemm_nn(acc, W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
+        torch.zeros(0, K, dtype=torch.float32, device=dev)
+    del acc
+    # 6. weight gradients (the sums over ranks: the dense all-reduce)
+    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0])
 
 
 class _ShardedBase(torch.nn.Module):

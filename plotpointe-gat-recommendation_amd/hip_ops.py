@@ -972,14 +972,23 @@ def gemm_tn_big_supported(ma: int, nb: int) -> bool:
     return ma % 128 == 0 and nb % 128 == 0 and ma >= 128 and nb >= 128
 
 
-def colmax_abs(X: torch.Tensor) -> torch.Tensor:
-    """IEEE bits (int32 view) of max_i |X[i, c]| per column (ppgat_colmax_abs; deterministic)."""
+def colmax_abs(X: torch.Tensor, src_ptr: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """IEEE bits (int32 view) of max_i |X[i, c]| per column (ppgat_colmax_abs; deterministic);
+    with ``src_ptr`` (CSC pointers [n + 1]) over the rows that are an edge's source only
+    (ppgat_colmax_abs_sources)."""
     lib = _lib.load()
     _check_rows("X", X, torch.float32)
     n, c = X.shape
     out = torch.empty(c, dtype=torch.int32, device=X.device)
-    _lib.check(lib.ppgat_colmax_abs(X.data_ptr(), X.stride(0) if n > 1 else c, n, c, out.data_ptr(),
-                                    _lib.stream_handle(X.device)), "colmax_abs")
+    ld = X.stride(0) if n > 1 else c
+    if src_ptr is not None:
+        _check_dev("src_ptr", src_ptr, torch.int32, X.device)
+        _require(src_ptr.numel() == n + 1, "colmax_abs: src_ptr must hold n + 1 CSC pointers")
+        _lib.check(lib.ppgat_colmax_abs_sources(X.data_ptr(), ld, n, c, src_ptr.data_ptr(), out.data_ptr(),
+                                                _lib.stream_handle(X.device)), "colmax_abs_sources")
+        return out
+    _lib.check(lib.ppgat_colmax_abs(X.data_ptr(), ld, n, c, out.data_ptr(), _lib.stream_handle(X.device)),
+               "colmax_abs")
     return out
 
 
@@ -1054,11 +1063,12 @@ class XViews:
     # dz_slot None: dz in CSC order, summed per destination through csr2csc
     csr2csc: Optional[torch.Tensor] = None
     rowptr: Optional[torch.Tensor] = None  # CSR row pointers over the destinations (KINK_TAP only)
+    colptr: Optional[torch.Tensor] = None  # CSC pointers over the sources [n_src + 1] (agg's column bound)
 
     @staticmethod
     def of_graph(g: "CSRGraph") -> "XViews":
         return XViews(g.n_nodes, g.n_nodes, g.n_edges, g.col, g.csr_eid, g.fwd_sched, g.row, g.csc_eid, None,
-                      g.bwd_sched, csr2csc=_csr2csc(g), rowptr=g.rowptr)
+                      g.bwd_sched, csr2csc=_csr2csc(g), rowptr=g.rowptr, colptr=g.colptr)
 
 
 def xgat_supported(in_channels: int, heads: int, channels: int) -> bool:
@@ -1367,15 +1377,19 @@ def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[in
                                          dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
-def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st):
+def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None):
+    """dW, datt, dbias from G = g^T agg and GV = S^T x (``x_rows``: the rows of x that S covers,
+    default all of the layer's source rows)."""
     x, W, a_s, a_d, agg, v = saved["x"], saved["W"], saved["a_s"], saved["a_d"], saved["agg"], saved["v"]
     H, C, K, slope, p, seed, has_bias = saved["meta"]
     dev = x.device
-    GV = gemm_tn(S, x)[0]
-    # |agg^h_i[k]| = |sum_j beta_ij x_j[k]| <= max_j |x_j[k]| / (1 - p) (the attention weights
-    # sum to 1, the kept ones scaled by 1 / (1 - p)): a column bound of agg from x's column maxima
-    # (x: 1 KB per row) instead of a pass over agg (4 KB per row); 2^-10 margin for fp32 rounding
-    xbound = (colmax_abs(x), K, (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
+    GV = gemm_tn(S, x if x_rows is None else x_rows)[0]
+    # |agg^h_i[k]| = |sum_j beta_ij x_j[k]| <= max_j |x_j[k]| / (1 - p) over i's sources j (the
+    # attention weights sum to 1, the kept ones scaled by 1 / (1 - p)): a column bound of agg from
+    # the column maxima of the SOURCE rows of x (1 KB per row; a row with no out-edge -- however
+    # large -- never enters an aggregate and must not loosen the bound: the fp16 split's error is
+    # relative to it) instead of a pass over agg (4 KB per row); 2^-10 margin for fp32 rounding
+    xbound = (colmax_abs(x, v.colptr), K, (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
     G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound)
     dW = torch.empty_like(W)
     datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)

@@ -7,10 +7,17 @@ and ``save_npz`` exactly as build_ii_knn.py:104-116 writes it.
 
 Steps (build_ii_knn.py line refs): rows normalised as e / (||e|| + 1e-8) (:57-59) and again
 by sklearn's cosine_similarity (:76); per block of query rows the similarity block
-E_q E^T is one ``ppgat_gemm_nn`` launch (fp32 results on the matrix cores; the rows are
-zero-padded once to the kernel's widths, exact zeros); the selection -- self excluded, top-k,
-sorted, thresholded (:79-95) -- is libppgat's ``ppgat_knn_topk`` kernel.  The full n x n
-matrix is never materialised (block_rows x n at a time).
+E_q E^T is one ``ppgat_gemm_nn`` launch on the matrix cores through an operand split -- the
+bf16 three-term split (<= 2^-24 relative per product) or, for blocks of >= 1,024 rows, the
+fp16 two-term split with per-row / per-column power-of-two scales (<= 2^-21 per product;
+DESIGN.md §4.3) -- NOT bitwise sklearn's fp32 dot products: where two candidates'
+similarities, or a similarity and ``min_similarity``, are within ~1e-6 the order or the
+membership can differ from the reference's (tests/test_knn.py pins the lists against the
+reference script's own output with a 1e-5 near-tie / threshold rule).  The rows are copied
+once into a zero-padded [n_p, d_p] buffer (exact zeros; the kernel's widths), so the
+embeddings are held twice during the build; the selection -- self excluded, top-k, sorted,
+thresholded (:79-95) -- is libppgat's ``ppgat_knn_topk`` kernel.  The full n x n matrix is
+never materialised (block_rows x n at a time).
 """
 from __future__ import annotations
 

@@ -191,3 +191,34 @@ def test_replicated_items_refuses_user_user_columns():
     ei = torch.tensor([[0, 1], [1, 2]])
     with pytest.raises(NotImplementedError):
         pkg.dist.build_replicated_graph(ei, 4, 2, 1, 0, csr_builder=csr_builder, sched_builder=None)
+
+
+def test_edges_symmetric_and_source_homed_views():
+    """dist.edges_symmetric on build_edge_index's U-I graph (u -> i and i -> u per interaction)
+    and on it with one column dropped; on the symmetric graph every rank's source-homed edge set
+    (the edges whose source it owns, dist._halo_xgat_backward) has its destinations in the rank's
+    [own | halo] table, and the ranks' sets partition the edge list."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _cpu_stages import csr_builder
+    pkg, g, ei, feats, full, _ = _setup()
+    D = pkg.dist
+    src, dst = ei[0].numpy(), ei[1].numpy()
+    assert D.edges_symmetric(src, dst, g.n_nodes)
+    assert not D.edges_symmetric(src[1:], dst[1:], g.n_nodes)
+    assert not D.edges_symmetric(np.array([0, 1, 2]), np.array([1, 2, 0]), 3)  # equal degrees, not symmetric
+    seen = []
+    for world in (1, 3):
+        ids = []
+        for r in range(world):
+            hg = D.build_halo_graph(ei, g.n_nodes, g.n_users, world, r, csr_builder=csr_builder, sched_builder=None)
+            assert hg.symmetric and hg.src_views is not None
+            sv = hg.src_views
+            assert sv.n_src == hg.n_own and sv.n_dst == hg.R
+            assert int(sv.row.max()) < hg.R and int(sv.colptr[-1]) == sv.n_edges
+            e = sv.csc_eid.long().numpy()
+            assert (hg.owner[src[e]] == r).all()
+            ids.append(e)
+        allids = np.sort(np.concatenate(ids))
+        assert np.array_equal(allids, np.arange(ei.size(1)))
+        seen.append(len(allids))
+    assert seen[0] == seen[1]

@@ -157,3 +157,31 @@ def test_linear_256_on_matrix_cores(pkg, cuda):
     assert rel(xd.grad, xr.grad) <= 1e-5
     assert rel(Wd.grad, Wr.grad) <= 1e-5
     assert rel(bd.grad, br.grad) <= 1e-5
+
+
+def test_weight_grad_bound_ignores_rows_without_out_edges(pkg, oracle, cuda):
+    """the fp16 weight-gradient G = g^T agg takes agg's column bound from the column
+    maxima of x; the fp16 split's error is relative to that bound.  Ten rows of x 1e4 times
+    larger than the rest that are nobody's source (no out-edge) never enter an aggregate: the
+    bound comes from the source rows only (ppgat_colmax_abs_sources), so dW stays within 1e-5 of
+    the fp64 oracle.  70,000 rows: the fp16 TN kernel's range (>= 64k rows)."""
+    rng = np.random.default_rng(11)
+    n, e, heads, C = 70_000, 500_000, 4, 256
+    out_rows = np.arange(n - 10, n)
+    ei = np.stack([rng.integers(0, n - 10, e), rng.integers(0, n, e)]).astype(np.int64)  # n-10.. are never sources
+    torch.manual_seed(5)
+    conv = pkg.GATConv(256, C, heads=heads, dropout=0.0, add_self_loops=False, concat=False).to(cuda)
+    x64 = torch.from_numpy(rng.standard_normal((n, 256)))
+    x64[out_rows] *= 1e4
+    G64 = torch.from_numpy(rng.standard_normal((n, C)))
+    x = x64.float().to(cuda).requires_grad_(True)
+    out = conv(x, torch.from_numpy(ei).to(cuda))
+    (out * G64.float().to(cuda)).sum().backward()
+    P = {k: v.detach().double().requires_grad_(True) for k, v in conv.named_parameters()}
+    xr = x64.to(cuda).requires_grad_(True)
+    ref = oracle.pyg_gat_conv(xr, torch.from_numpy(ei).to(cuda), P["lin.weight"], P["att_src"], P["att_dst"],
+                              P["bias"], heads)
+    (ref * G64.to(cuda)).sum().backward()
+    assert rel(out, ref) <= 1e-5
+    assert rel(conv.lin.weight.grad, P["lin.weight"].grad) <= 1e-5, rel(conv.lin.weight.grad, P["lin.weight"].grad)
+    assert rel(x.grad, xr.grad) <= 1e-5

@@ -33,9 +33,16 @@ for s in $STEPS; do
     traj) for v in default:PPGAT_NONE=1 fuseddxw0:PPGAT_FUSED_DXW=0 gemmfp32:PPGAT_GEMM=fp32; do
             run "traj_${v%%:*}" 900 env PPGAT_REPORT_TAG="${v%%:*}" "${v#*:}" python -u -m pytest tests/test_gpu_trajectory.py -m gpu -v -s -rf --timeout 800 --timeout-method thread
           done ;;
-    probe5) for a in "0 0" "7 0" "7 640"; do set -- $a
-              run "probe5_r$1_a$2" 900 python -u tools/scale_probe.py --config 5 --world 8 --rank $1 --streams --a2a-gbs $2 --steps 5 --warmup 2
+    probe5) for a in ${PROBES:-0:0 7:0 7:640}; do set -- ${a%%:*} ${a#*:}
+              run "probe5_r$1_a$2" 900 python -u tools/scale_probe.py --config 5 --world 8 --rank $1 --streams --a2a-gbs $2 --steps 5 --warmup 2 ${PROBE_ARGS:-}
             done ;;
+    gemm5) run gemm5_nnh 300 env PPGAT_NNH2=0 python tools/bench_gemm.py --cfg5 --iters 10 && \
+           run gemm5_nnh2 300 env PPGAT_NNH2=1 python tools/bench_gemm.py --cfg5 --iters 10 ;;
+    pmcdst) (cd /tmp && run pmcdst_a 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_a" -o a -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
+            (cd /tmp && run pmcdst_b 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_b" -o b -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
+            python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
+            python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
+    nnhlab) for l in 0 1 2 3; do run "nnhlab$l" 300 env PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;

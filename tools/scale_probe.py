@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--config", type=int, choices=[2, 5], default=2)
     ap.add_argument("--a2a-gbs", type=float, default=0.0,
                     help="model each exchange as this rank's bytes at this rate (GB/s); 0: free")
+    ap.add_argument("--host-profile", action="store_true", help="cProfile one eager step after the timed ones")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.config == 5:
@@ -175,6 +176,18 @@ def main():
     _lib.profile_enable(False)
     kern = {k: _lib.profile_read(k)[0] / args.steps for k in ("fwd", "bwd_pro", "bwd_src", "bwd_epi", "proj",
                                                                "gemm_tn", "adam")}
+    if args.host_profile:
+        import cProfile
+        import io
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+        step()
+        torch.cuda.synchronize()
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(30)
+        print(buf.getvalue(), flush=True)
     print(json.dumps({"config": args.config, "partition": args.partition, "graph": args.graph, "world": args.world,
                       "rank": args.rank, "streams": args.streams, "a2a_gbs": args.a2a_gbs,
                       "modelled_exchange_ms_per_step": comm.modelled_ms / args.steps if not args.graph else None,
