@@ -365,7 +365,10 @@ def main():
     # the multi-head layers run aggregate-then-transform when H*C exceeds the input width
     xform_k = C if (H > 1 and H * C > C and pkg.hip_ops.xgat_supported(C, H, C)) else 0
     # the backward formulation hip_ops.xgat_backward picks for these layer sizes
-    if xform_k and dist_path and part == "halo":  # the formulation the local layer sizes select
+    src_homed = dist_path and part == "halo" and xform_k and pkg.dist.source_homed_backward(dg)
+    if src_homed:  # the source-homed backward (dist._halo_xgat_backward): deferred D unless PPGAT_XGAT_GATHER=g
+        gather_mode = "g" if os.environ.get("PPGAT_XGAT_GATHER") == "g" else "gd"
+    elif xform_k and dist_path and part == "halo":  # the formulation the local layer sizes select
         gather_mode = pkg.hip_ops._xgat_gather_mode(C, H, dg.R, dg.n_own, dg.bwd_view.n_bwd_edges, C)
     else:
         gather_mode = pkg.hip_ops._xgat_gather_mode(C, H) if xform_k else None
@@ -386,8 +389,13 @@ def main():
             v = dg.view
         else:
             v = dg.fwd_view if dom == "fwd" else dg.bwd_view
-        ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
-                        args.attn_dropout > 0, xform_k, dz_slot=part != "replicated", gather_g=gather_mode if gather_g else False)
+        if src_homed and dom != "fwd":  # the backward passes run over the own sources' out-edges
+            ab = algo_bytes(dom, dg.n_own, dg.src_views.n_edges, H, C, args.attn_dropout > 0, xform_k,
+                            dz_slot=False, gather_g=gather_mode)
+        else:
+            ab = algo_bytes(dom, v.n_rows, v.n_fwd_edges if dom == "fwd" else v.n_bwd_edges, H, C,
+                            args.attn_dropout > 0, xform_k, dz_slot=part != "replicated",
+                            gather_g=gather_mode if gather_g else False)
     else:
         ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k, gather_g=gather_mode if gather_g else False)
     achieved = ab / avg_s / 1e9

@@ -142,6 +142,40 @@ __global__ void __launch_bounds__(256) k_rows_return_add(float* __restrict__ dst
   }
 }
 
+// narrow rows (cols <= 16, 16-B aligned): L = cols / 4 lanes per row (rounded up to a power of
+// two), 64 / L rows per wave -- the halo layer's nstate rows (4 H floats) and partial sums (H)
+template <int L>
+__global__ void __launch_bounds__(256) k_rows_gather_narrow(const float* __restrict__ src, int64_t lds,
+                                                            const int64_t* __restrict__ idx, int64_t n, int cols,
+                                                            float* __restrict__ dst, int64_t ldd) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = t / L;
+  const int c = 4 * (int)(t % L);
+  if (r >= n || c >= cols) return;
+  *reinterpret_cast<float4*>(dst + r * ldd + c) = *reinterpret_cast<const float4*>(src + idx[r] * lds + c);
+}
+
+// one thread per row, the row's float4 columns in a loop; copies added in k order
+__global__ void __launch_bounds__(256) k_rows_return_add_narrow(float* __restrict__ dst, int64_t ldd,
+                                                                const float* __restrict__ ret, int64_t ldr,
+                                                                const int32_t* __restrict__ ptr,
+                                                                const int32_t* __restrict__ pos, int64_t n,
+                                                                int cols) {
+  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= n) return;
+  const int k0 = ptr[o], k1 = ptr[o + 1];
+  if (k0 == k1) return;
+  float* d = dst + o * ldd;
+  for (int c = 0; c < cols; c += 4) {
+    float4 a = *reinterpret_cast<const float4*>(d + c);
+    for (int k = k0; k < k1; ++k) {
+      const float4 b = *reinterpret_cast<const float4*>(ret + (int64_t)pos[k] * ldr + c);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    *reinterpret_cast<float4*>(d + c) = a;
+  }
+}
+
 }  // namespace
 
 static bool vec_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int cols) {
@@ -152,6 +186,14 @@ static bool vec_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int c
 hipError_t rows_gather(const float* src, int64_t lds, const int64_t* idx, int64_t n, int cols, float* dst,
                        int64_t ldd, hipStream_t st) {
   if (n <= 0 || cols <= 0) return hipSuccess;
+  if (cols <= 16 && vec_ok(src, lds, dst, ldd, cols)) {  // narrow rows: several rows per wave
+    const int L = cols <= 4 ? 1 : cols <= 8 ? 2 : 4;
+    const unsigned g = (unsigned)((n * L + 255) / 256);
+    if (L == 1) hipLaunchKernelGGL(k_rows_gather_narrow<1>, dim3(g), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd);
+    else if (L == 2) hipLaunchKernelGGL(k_rows_gather_narrow<2>, dim3(g), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd);
+    else hipLaunchKernelGGL(k_rows_gather_narrow<4>, dim3(g), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_rows_gather, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd,
                      vec_ok(src, lds, dst, ldd, cols) ? 1 : 0);
   return hipGetLastError();
@@ -160,6 +202,11 @@ hipError_t rows_gather(const float* src, int64_t lds, const int64_t* idx, int64_
 hipError_t rows_return_add(float* dst, int64_t ldd, const float* ret, int64_t ldr, const int32_t* ptr,
                            const int32_t* pos, int64_t n, int cols, hipStream_t st) {
   if (n <= 0 || cols <= 0) return hipSuccess;
+  if (cols <= 16 && vec_ok(dst, ldd, ret, ldr, cols)) {  // narrow rows: one thread per row
+    hipLaunchKernelGGL(k_rows_return_add_narrow, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dst, ldd, ret,
+                       ldr, ptr, pos, n, cols);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_rows_return_add, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, dst, ldd, ret, ldr, ptr, pos,
                      n, cols, vec_ok(dst, ldd, ret, ldr, cols) ? 1 : 0);
   return hipGetLastError();

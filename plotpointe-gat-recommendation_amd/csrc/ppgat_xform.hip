@@ -757,8 +757,9 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// LAB (diagnostics only, PPGAT_NNH2_LAB; results wrong): 1 = no X loads after the first two
-// chunks (registers reused), 2 = no B DMA after the first two chunks (LDS reused), 3 = both
+// LAB (diagnostics only, PPGAT_NNH2_LAB; results wrong), bits: 1 = no X loads after the first
+// two chunks (registers reused), 2 = no B DMA after the first two chunks (LDS reused), 4 = no
+// epilogue stores (a row is stored only if its first accumulator is NaN), 8 = no chunk barrier
 template <int NT, bool RK, int LAB = 0>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
@@ -847,7 +848,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
     } else {
       wait_vm<4 + 4>();
     }
-    __builtin_amdgcn_s_barrier();
+    if (!(LAB & 8)) __builtin_amdgcn_s_barrier();
   };
   for (int c = 0; c < chunks; c += 2) {
     body(c, xA);
@@ -893,7 +894,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
-        if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+        if (row < M && (!(LAB & 4) || acc[0][q] != acc[0][q])) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
       }
     }
   }
@@ -2130,9 +2131,10 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       if (e != hipSuccess) return e;
       if (nnh2_enabled() && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
         if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {
-          if (lab == 1) hipLaunchKernelGGL((k_gemm_nnh2<8, false, 1>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-          else if (lab == 2) hipLaunchKernelGGL((k_gemm_nnh2<8, false, 2>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-          else hipLaunchKernelGGL((k_gemm_nnh2<8, false, 3>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+#define PPGAT_LAB(L) \
+  if (lab == L) hipLaunchKernelGGL((k_gemm_nnh2<8, false, L>), dim3(grid), dim3(512), 0, st, a, img, ecol)
+          PPGAT_LAB(1); PPGAT_LAB(2); PPGAT_LAB(3); PPGAT_LAB(7); PPGAT_LAB(15);
+#undef PPGAT_LAB
           return hipGetLastError();
         }
         if (nv > 0) {

@@ -36,6 +36,7 @@ the ranks' own RNG states.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 from types import SimpleNamespace
@@ -532,8 +533,11 @@ def _src_views(n_own: int, R: int, Eb: int, Gb, orig):
     destination's row in the [own | halo] table, dz in CSC order), CSR over the table rows (the
     per-destination partial sums, read through csr2csc); edge ids mapped to edge_index columns."""
     from .hip_ops import XViews
+    c2r = Gb.csc2csr[:Eb].long()
+    csr2csc = torch.empty(Eb, dtype=torch.int32, device=c2r.device)  # CSR slot -> CSC position
+    csr2csc[c2r] = torch.arange(Eb, dtype=torch.int32, device=c2r.device)
     return XViews(R, n_own, Eb, Gb.col[:Eb].contiguous(), orig(Gb.csr_eid[:Eb]), None, Gb.row[:Eb].contiguous(),
-                  orig(Gb.csc_eid[:Eb]), None, None, csr2csc=Gb.csc2csr[:Eb].contiguous(),
+                  orig(Gb.csc_eid[:Eb]), None, None, csr2csc=csr2csc,
                   rowptr=Gb.rowptr.contiguous(), colptr=Gb.colptr[:n_own + 1].contiguous())
 
 
@@ -706,8 +710,10 @@ class _HaloLayerX(torch.autograd.Function):
         x_loc = rows_in.x
         if x_loc.data_ptr() != x_own.data_ptr():
             x_loc[:hg.n_own].copy_(x_own)
+        # the output rows go straight into the next layer's table (its own rows)
+        dest = rows_out.x[:hg.n_own] if rows_out is not None and rows_out.x.size(1) == C else None
         out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed,
-                                      phases=_halo_phases(hg, rows_in, rows_out))
+                                      phases=_halo_phases(hg, rows_in, rows_out), out=dest)
         rows_in.wait_all()
         ctx.hg, ctx.comm, ctx.stages = hg, comm, stages
         ctx.plans = [rows_in.plan(c) for c in ("u", "i") if c not in rows_in.local]
@@ -795,7 +801,9 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
          GEMM's epilogue) -- the complete input gradient, nothing returned;
       6. dW from G = g^T agg (own destinations) and GV = S^T x (own rows), datt, dbias.
     Exchanges per layer: g + nstate of the halo rows (the forward's x volume) and the partial
-    ds_dst return, instead of the halo rows' dx; per-rank GEMMs over own rows only."""
+    ds_dst return, instead of the halo rows' dx; per-rank GEMMs over own rows only.
+    This is the PPGAT_XGAT_GATHER=g variant; by default D is deferred instead
+    (_halo_xgat_backward_deferred_d: no gt GEMM, D's partials go home and back out)."""
     from . import hip_ops as O
     lib = _lib.load()
     x, W, A = saved["x"], saved["W"], saved["A"]
@@ -810,6 +818,8 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
     gtab.x[:n0].copy_(g)
     for cls in ("u", "i"):
         gtab.start(cls, g)
+    if os.environ.get("PPGAT_XGAT_GATHER") != "g":
+        return _halo_xgat_backward_deferred_d(saved, g, hg, comm, stages, want_bias_grad, gtab)
     # 1. destination state of the own rows
     Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
@@ -843,19 +853,112 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
     dsd = torch.zeros(max(R, 1), H, dtype=torch.float32, device=dev)
     O._xgat_dst_sum(lib, sv, dz, dsd, H, E, st, col0=0, ld=H)
     del dz
-    own = dsd[:n0]
-    off = n0
-    for plan in (hg.plan_u, hg.plan_i):
-        ret = comm.all_to_all_rows(dsd[off:off + plan.n_recv], plan.recv_counts, plan.send_counts)
-        stages.return_add(own, ret, plan.ret_ptr, plan.ret_pos)
-        off += plan.n_recv
     S = S[:n0]
-    S[:, H:].copy_(own)
+    S[:, H:].copy_(_partials_home(hg, comm, stages, dsd))
     # 5. the complete input gradient of the own rows
     dx = O.gemm_nn(acc, W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
         torch.zeros(0, K, dtype=torch.float32, device=dev)
     del acc
     # 6. weight gradients (the sums over ranks: the dense all-reduce)
+    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0])
+
+
+def _partials_home(hg: "HaloGraph", comm: "Comm", stages, part: torch.Tensor) -> torch.Tensor:
+    """part [R, w]: this rank's partial sums per table row -> the own rows' complete sums (the
+    halo rows' partials returned to their owners by the reverse plans, each own row adding its
+    copies after its own partial, in peer order: deterministic)."""
+    own = part[:hg.n_own]
+    off = hg.n_own
+    for plan in (hg.plan_u, hg.plan_i):
+        ret = comm.all_to_all_rows(part[off:off + plan.n_recv], plan.recv_counts, plan.send_counts)
+        stages.return_add(own, ret, plan.ret_ptr, plan.ret_pos)
+        off += plan.n_recv
+    return own
+
+
+def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm", stages, want_bias_grad: bool,
+                                   gtab: "HaloRows"):
+    """_halo_xgat_backward with D deferred (the single-GPU default): no gt GEMM
+    and no prologue.  nstate {s_dst, m, inv_l, .} of the own rows goes out with g at once; the
+    edge pass writes dalpha and beta dalpha per edge; D_i = sum_j beta dalpha is summed per table
+    row, the halo rows' partials go home and the completed D of the own rows back out (H floats
+    per row each way); then the dz pass, ds_dst (partials home again) and the own rows' GEMMs."""
+    from . import hip_ops as O
+    lib = _lib.load()
+    x, W, A = saved["x"], saved["W"], saved["A"]
+    s_src, s_dst, m, inv_l = saved["s_src"], saved["s_dst"], saved["m"], saved["inv_l"]
+    H, C, K, slope, p, seed, has_bias = saved["meta"]
+    dev = x.device
+    st = _lib.stream_handle(dev)
+    n0, R, sv = hg.n_own, hg.R, hg.src_views
+    E = sv.n_edges
+    seed_buf = saved["seed_buf"]
+    nst = torch.empty(max(n0, 1), 4 * H, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H, nst.data_ptr(),
+                                     st), "xgat_nstate")
+    nst = nst[:n0]
+    ntab = HaloRows(hg, comm, stages, 4 * H, nst)
+    ntab.x[:n0].copy_(nst)
+    for cls in ("u", "i"):
+        ntab.start(cls, nst)
+    hs = O.gemm_nn(x[:n0], W, 1, H * C, alpha=1.0 / H)
+    acc = torch.empty(max(n0, 1), H * C, dtype=torch.float32, device=dev)
+    dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    pdal = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    phases = ([(hg.src_sched_i, hg.n_own_u, "u"), (hg.src_sched_u, 0, "i")] if hg.bipartite else
+              [(sv.bwd_sched, 0, None)])
+    for sched, base, need in phases:  # dalpha (into dz) and beta dalpha per edge, acc per own source
+        for tab in (gtab, ntab):
+            tab.wait_all() if need is None else tab.wait(need)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        cs = sched.cstruct()
+        _lib.check(lib.ppgat_xgat_bwd_edges_gd(ctypes.byref(cs), _lib.ptr(sv.row) if E else None,
+                                               _lib.ptr(sv.csc_eid) if E else None, None, E, C, H,
+                                               hs.data_ptr() + 4 * base * H * C, s_src.data_ptr() + 4 * base * H,
+                                               ntab.x.data_ptr(), gtab.x.data_ptr(), C, float(slope), float(p),
+                                               int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                               acc.data_ptr() + 4 * base * H * C, dz.data_ptr(), pdal.data_ptr(),
+                                               ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_gd")
+    gtab.wait_all()
+    ntab.wait_all()
+    del hs
+    # D: per table row partial sums of beta dalpha, completed at the owner, sent back out
+    Dp = torch.zeros(max(R, 1), H, dtype=torch.float32, device=dev)
+    O._xgat_dst_sum(lib, sv, pdal, Dp, H, E, st, col0=0, ld=H)
+    del pdal
+    Dtab = HaloRows(hg, comm, stages, H, Dp)
+    Dtab.x[:n0].copy_(_partials_home(hg, comm, stages, Dp))
+    del Dp
+    for cls in ("u", "i"):
+        Dtab.start(cls, Dtab.x[:n0])
+    Dtab.wait_all()
+    ntab.x.view(R, H, 4)[:, :, 3].copy_(Dtab.x)  # nstate {s_dst, m, inv_l, D} of every table row
+    del Dtab
+    # dz in place over dalpha, ds_src per own source
+    S = torch.zeros(max(n0, 1), 2 * H, dtype=torch.float32, device=dev)
+    for sched, base, _ in phases:
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_xgat_bwd_dz_workspace_bytes(sched.n_hub_items, H, ctypes.byref(nbytes)), "xgat_dz_ws")
+        ws = torch.empty(max(int(nbytes.value), 4), dtype=torch.uint8, device=dev)
+        cs = sched.cstruct()
+        _lib.check(lib.ppgat_xgat_bwd_dz(ctypes.byref(cs), _lib.ptr(sv.row) if E else None,
+                                         _lib.ptr(sv.csc_eid) if E else None, None, E, H,
+                                         s_src.data_ptr() + 4 * base * H, ntab.x.data_ptr(), float(slope), float(p),
+                                         int(seed) & (2**64 - 1), _lib.ptr(seed_buf), dz.data_ptr(),
+                                         S.data_ptr() + 4 * base * 2 * H, 2 * H, ws.data_ptr(), nbytes.value, st),
+                   "xgat_bwd_dz")
+    # ds_dst: partials per table row, completed at the owner
+    dsd = torch.zeros(max(R, 1), H, dtype=torch.float32, device=dev)
+    O._xgat_dst_sum(lib, sv, dz, dsd, H, E, st, col0=0, ld=H)
+    del dz
+    S = S[:n0]
+    S[:, H:].copy_(_partials_home(hg, comm, stages, dsd))
+    del dsd
+    dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
+        torch.zeros(0, K, dtype=torch.float32, device=dev)
+    del acc
     return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0])
 
 

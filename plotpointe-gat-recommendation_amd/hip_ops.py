@@ -1127,13 +1127,14 @@ class XPhase:
 
 
 def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
-                 seed: int, phases: Optional[list] = None):
+                 seed: int, phases: Optional[list] = None, out: Optional[torch.Tensor] = None):
     """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state).
 
     ``phases`` (a list of XPhase partitioning [0, n_dst) in order): the node scores of the
     destination rows first, then per phase its sources' scores, the edge pass over its
     destination rows and their rows of the output GEMM.  Per destination the result is the
-    same as the one-phase forward (same per-row kernels and order): bitwise equal."""
+    same as the one-phase forward (same per-row kernels and order): bitwise equal.  ``out``: a
+    contiguous [n_dst, C] destination (the next halo layer's own rows: no copy there)."""
     lib = _lib.load()
     x = x.contiguous()
     dev = x.device
@@ -1159,7 +1160,9 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
     m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
     inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
-    out = torch.empty(v.n_dst, C, dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty(v.n_dst, C, dtype=torch.float32, device=dev)
+    _require(out.shape == (v.n_dst, C) and out.is_contiguous(), "xgat_forward: out must be contiguous [n_dst, C]")
     seed_buf = seed_buffer(p, dev)
     E = v.n_edges
     for ph in phases:

@@ -217,6 +217,8 @@ def test_edges_symmetric_and_source_homed_views():
             assert int(sv.row.max()) < hg.R and int(sv.colptr[-1]) == sv.n_edges
             e = sv.csc_eid.long().numpy()
             assert (hg.owner[src[e]] == r).all()
+            # csr2csc: CSR slot -> CSC position of the same edge
+            assert torch.equal(sv.csc_eid[sv.csr2csc.long()], sv.csr_eid)
             ids.append(e)
         allids = np.sort(np.concatenate(ids))
         assert np.array_equal(allids, np.arange(ei.size(1)))

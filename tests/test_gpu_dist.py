@@ -69,6 +69,12 @@ def _setup(dev, heads=1, size="toy"):
 
 def _run(rank, world, out_dir, heads, part, size="toy"):
     dev = torch.device("cuda", 0)
+    if part == "halo-dstbwd":  # the round-3 multi-head halo backward (edges at the destination's owner)
+        os.environ["PPGAT_HALO_BWD"] = "dst"
+        part = "halo"
+    elif part == "halo-srcg":  # the source-homed backward with D from the gt GEMM's prologue
+        os.environ["PPGAT_XGAT_GATHER"] = "g"
+        part = "halo"
     pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads, size)
     D = pkg.dist
     comm = D.Comm()
@@ -172,8 +178,9 @@ def test_sharded_world1_rccl(cuda, tmp_path, monkeypatch, heads, part):
     _check(torch.load(tmp_path / "sharded_1.pt", weights_only=False), _oracle(heads))
 
 
-@pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (4, "halo"), (1, "replicated"), (2, "replicated"),
-                                        (1, "replicated-staged")])
+@pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (4, "halo"), (4, "halo-dstbwd"), (4, "halo-srcg"),
+                                        (1, "replicated"),
+                                        (2, "replicated"), (1, "replicated-staged")])
 def test_sharded_world2_shared_gpu(cuda, tmp_path, heads, part):
     store = _master_store()
     mp.start_processes(_worker, args=(2, store.port, str(tmp_path), heads, part), nprocs=2, join=True,

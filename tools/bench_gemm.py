@@ -113,7 +113,9 @@ def cfg5(dev, iters):
         B1 = B0.t().contiguous()
         y0 = ops.gemm_nn(X, B0, 0, Nc)
         y1 = ops.gemm_nn(X, B1, 1, Nc)
-        assert torch.equal(y0, y1), name  # same products, same order
+        import os
+        if not os.environ.get("PPGAT_NNH2_LAB"):  # the lab variants' outputs are not the product
+            assert torch.equal(y0, y1), name  # same products, same order
         # fingerprint of the exact bits (compare runs with PPGAT_GEMM_NNP=0 / 1) and the fp64 error
         import hashlib
         res[f"{name}_sha1"] = hashlib.sha1(y0.cpu().numpy().tobytes()).hexdigest()

@@ -42,7 +42,8 @@ for s in $STEPS; do
             (cd /tmp && run pmcdst_b 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_b" -o b -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
             python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
-    nnhlab) for l in 0 1 2 3; do run "nnhlab$l" 300 env PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
+    nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
+    profprobe) (cd /tmp && run rocprof_probe5 900 rocprofv3 --kernel-trace --stats -d "$OUT/profprobe" -o run --output-format csv -- python "$R/tools/scale_probe.py" --config 5 --world 8 --rank ${PROBE_RANK:-7} --streams --steps 3 --warmup 1) ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
