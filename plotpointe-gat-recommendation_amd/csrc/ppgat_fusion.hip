@@ -31,6 +31,7 @@
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
 #include "ppgat_split.h"
+#include "ppgat_nnh_pipe.h"
 
 namespace ppgat {
 namespace {
@@ -743,6 +744,144 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_fusion_fwdh with GEMM1 on the pipelined loop of k_gemm_nnh3 (ppgat_nnh_pipe.h: W1 chunks by
+// LDS-DMA into three buffers two chunks ahead, x two chunks ahead, the next chunk's row scale
+// and fp16 split inside the current chunk's MFMA sequence, one bare barrier per chunk) -- the
+// same products in the same order (bitwise equal outputs); GEMM2 and the epilogue unchanged.
+// Even chunk counts (the reference's 384 + 512 = 28 chunks); LDS 3 x 40,960 B.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict__ txt, const float* __restrict__ img,
+                                                        const int32_t* __restrict__ img_index,
+                                                        const float* __restrict__ img_fallback, int64_t B, int Dt,
+                                                        int Di, const uint16_t* __restrict__ w1i,
+                                                        const int* __restrict__ e1, const float* __restrict__ b1,
+                                                        const uint16_t* __restrict__ w2i_g, const int* __restrict__ e2,
+                                                        const float* __restrict__ b2, int normalize,
+                                                        float* __restrict__ out, float* __restrict__ z1_out) {
+  static_assert(kH1Img * 2 % 1024 == 0 && kH2Img * 2 % 1024 == 0, "1-KB wave copies");
+  static_assert(kPatchB + 2 * kH2Img * 2 <= 3 * kH1Img * 2, "GEMM2 fits GEMM1's LDS");
+  static_assert(kH1Img == NnhImg<8>::ELEMS, "W1 chunks are k_gemm_nnh's 256-column images");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[3 * kH1Img];
+  __shared__ __attribute__((aligned(16))) float sF[8][32];  // per wave: a factor per row
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * PBM + 32 * w;
+  const int K = Dt + Di, chunks = K / BK;
+  const int64_t b = row0 + r < B ? row0 + r : B - 1;
+  const float* trow = txt + b * Dt + 4 * hf;
+  const float* irow;
+  if (Di > 0) {
+    const int32_t ii = img_index ? img_index[b] : (int32_t)b;
+    irow = (ii >= 0 ? img + (int64_t)ii * Di : img_fallback) + 4 * hf;
+  } else {
+    irow = trow;
+  }
+  auto load_x_chunk = [&](int c, float4 (&xv)[4]) {  // a chunk never straddles txt | img (Dt % 32 == 0)
+    const int k0 = c * BK;
+    const float* src = k0 < Dt ? trow + k0 : irow + (k0 - Dt);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
+  };
+
+  // ---- GEMM1: the pipelined fp16 two-term loop (ppgat_nnh_pipe.h), rows scaled online ----
+  f32x16 acc[8];
+  int erow = 0;
+  nnh3_loop<8>(w1i, lds, chunks, load_x_chunk, acc, erow, sF[w], w, lane);
+
+  // ---- h = relu(z), z = acc / (s_row s_col) + b1 (exact unscale); h's row maxima ----
+  float fr[16];
+  split::row_unscale(erow, sF[w], r, hf, fr);
+  float hm[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) hm[q] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int col = BK * t + r;
+    const float fc = ldexpf(1.f, -e1[col]), bias = b1[col];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float z = fmaf(acc[t][q] * fr[q], fc, bias);
+      const int row = row_of(q, hf);
+      if (z1_out != nullptr && row0 + row < B) z1_out[(row0 + row) * H1 + col] = z;
+      const float h = fmaxf(z, 0.f);
+      acc[t][q] = h;
+      hm[q] = fmaxf(hm[q], h);
+    }
+  }
+  float fr2[16];  // 1 / s_h of this lane's accumulator rows (GEMM2 epilogue)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float m = group_reduce<Op::Max, 1, 16>(hm[q]);
+    const int e = (m > 0.f && m <= 3.4e38f) ? split::scale_exp16(m) : 0;
+    fr2[q] = ldexpf(1.f, -e);
+    if (r == q) sF[w][row_of(q, hf)] = ldexpf(1.f, e);  // s_h for the A-operand lanes
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const float sh = sF[w][r];  // this lane's GEMM2 A-operand row is row r
+
+  // ---- GEMM2 over eight 32-column slices of h ----
+  float* hp = reinterpret_cast<float*>(lds) + w * 32 * XLH;   // this wave's patch [32][XLH]
+  uint16_t* w2s = lds + kPatchB / 2;                           // [2][kH2Img]
+  f32x16 acc2[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
+  glds_copy(w2i_g, w2s, kH2Img * 2, w, lane);
+#pragma unroll
+  for (int c = 0; c < H1 / BK; ++c) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) hp[row_of(q, hf) * XLH + r] = acc[c][q];
+    __syncthreads();  // vmcnt(0): slice c landed; the patch is written
+    if (c + 1 < H1 / BK) glds_copy(w2i_g + (int64_t)(c + 1) * kH2Img, w2s + ((c + 1) & 1) * kH2Img, kH2Img * 2, w, lane);
+    const uint16_t* ws2 = w2s + (c & 1) * kH2Img;
+    auto read_w2 = [&](int i, split::u32x4 (&f)[2]) {
+      const int off = (32 * (i & 3) + r) * HLDK + 16 * (i >> 2) + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&ws2[p * kH2Part + off]);
+    };
+    split::u32x4 fh[2], fb2[2][2];
+    read_w2(0, fb2[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int u = i >> 2, uu = i & 3;
+      if (uu == 0) split::split2h(ld4(&hp[r * XLH + 16 * u + 4 * hf]), ld4(&hp[r * XLH + 16 * u + 8 + 4 * hf]), sh, fh[0], fh[1]);
+      if (i + 1 < 8) read_w2(i + 1, fb2[(i + 1) & 1]);
+      acc2[uu] = split::mfma32_h3(fh, fb2[i & 1], acc2[uu]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // the patch and this slice's buffer are free again
+  }
+
+  // ---- unscale, bias, row L2 norm (inside the wave), store ----
+  float ss[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) ss[q] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int col = 32 * u + r;
+    const float fc = ldexpf(1.f, -e2[col]), bias2 = b2[col];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc2[u][q] = fmaf(acc2[u][q] * fr2[q], fc, bias2);
+      ss[q] = fmaf(acc2[u][q], acc2[u][q], ss[q]);
+    }
+  }
+  if (normalize) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ss[q] = 1.f / (sqrtf(group_reduce<Op::Sum, 1, 16>(ss[q])) + 1e-8f);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t row = row0 + row_of(q, hf);
+    if (row >= B) continue;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) out[row * DO + 32 * u + r] = normalize ? acc2[u][q] * ss[q] : acc2[u][q];
+  }
+}
+
 }  // namespace
 
 
@@ -771,8 +910,12 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
     hipError_t e = nnh_presplit(W1, Dt + Di, 1, Dt + Di, H1, 8, w1i, e1, st);
     if (e == hipSuccess) e = nnh_presplit(W2, H1, 1, H1, DO, 4, w2i, e2, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_fusion_fwdh, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img, img_index,
-                       img_fallback, B, Dt, Di, w1i, e1, b1, w2i, e2, b2, normalize, out, z1_out);
+    if (nnh_pipeline_variant() == 3 && ((Dt + Di) / BK) % 2 == 0)
+      hipLaunchKernelGGL(k_fusion_fwdh3, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
+                         img_index, img_fallback, B, Dt, Di, w1i, e1, b1, w2i, e2, b2, normalize, out, z1_out);
+    else
+      hipLaunchKernelGGL(k_fusion_fwdh, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
+                         img_index, img_fallback, B, Dt, Di, w1i, e1, b1, w2i, e2, b2, normalize, out, z1_out);
     return hipGetLastError();
   }
   if (ws != nullptr && gemm_split_enabled()) {  // W1 / W2 pre-split once, then the glds-staged kernel

@@ -147,6 +147,55 @@ __device__ __forceinline__ float row_scale_online(const float4 (&xa)[4], int& er
   return __builtin_ldexpf(1.f, erow);
 }
 
+// row_scale_online in two halves, for a caller that prepares chunk c + 1 while chunk c's
+// products run: absmax4 folds (the same expression and order as row_scale_online), row_scale_plan
+// gives the chunk's per-lane exponent and whether its row rescales, and row_rescale applies the
+// rescale to the accumulators once chunk c's products are in them (bitwise the same arithmetic)
+__device__ __forceinline__ float absmax4(const float4& v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+__device__ __forceinline__ bool row_scale_plan(float mx, int erow, bool set, int& enew) {
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  // branch-free (the caller interleaves this with MFMAs): every term evaluated, combined bitwise
+  const bool over = mx * __builtin_ldexpf(1.f, erow) >= 32768.f, pos = mx > 0.f, fin = mx <= 3.4e38f;
+  const bool need = fin & ((set & over) | (!set & pos));
+  enew = need ? scale_exp16(mx) : erow;
+  return need;
+}
+template <int NT>
+__device__ __forceinline__ void row_rescale(int erow, int enew, bool set, f32x16 (&acc)[NT], float* sFw, int r,
+                                            int hf) {
+  if (hf == 0) sFw[r] = set ? __builtin_ldexpf(1.f, enew - erow) : 1.f;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float f[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 v = *reinterpret_cast<const float4*>(&sFw[8 * j + 4 * hf]);
+    f[4 * j] = v.x; f[4 * j + 1] = v.y; f[4 * j + 2] = v.z; f[4 * j + 3] = v.w;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[t][q] *= f[q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// half of split2h: the 4 values of p -> terms [2 j0, 2 j0 + 1] of h and l
+__device__ __forceinline__ void split2h_half(const float4& p, float s, u32x4& h, u32x4& l, int j0) {
+  const float v[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float a = v[2 * i] * s, b = v[2 * i + 1] * s;
+    const uint32_t hh = pk_f16(a, b);
+    const f32x2e back = __builtin_convertvector(__builtin_bit_cast(f16x2, hh), f32x2e);
+    h[j0 + i] = hh;
+    l[j0 + i] = pk_f16(a - back.x, b - back.y);
+  }
+}
+
 // the per-row unscale factors 2^-erow of this lane's 16 accumulator rows (through sFw)
 __device__ __forceinline__ void row_unscale(int erow, float* sFw, int r, int hf, float (&f)[16]) {
   if (hf == 0) sFw[r] = __builtin_ldexpf(1.f, -erow);

@@ -33,9 +33,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "ppgat_internal.h"
 #include "ppgat_lanes.h"
 #include "ppgat_split.h"
+#include "ppgat_nnh_pipe.h"
 
 namespace ppgat {
 namespace {
@@ -552,11 +555,6 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnp(NnArg a, const uint16_t* __
 // s_new / s_old (a wave-uniform branch, rare on real data: first-chunk maxima within 32x of the
 // row's).  Elements far below their row's max keep an absolute error <= 2^-34 of that max.
 // ---------------------------------------------------------------------------
-template <int NT>
-struct NnhImg {
-  static constexpr int KC = 32, BN = 32 * NT, LDK = KC + 8, PART = BN * LDK, ELEMS = 2 * PART, BYTES = 2 * ELEMS;
-  static_assert(BYTES % 1024 == 0, "an image is a whole number of 1-KB wave copies");
-};
 
 // per column of B [K x N]: the scale exponent (largest |b| 2^e in [2^9, 2^10); 0 for a zero column)
 template <int BMODE>
@@ -740,22 +738,6 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __
 //    after it -- X of c + 1, DMA and X of c + 2 -- stays in flight).
 // Global issue order per wave: DMA(0) X(0) DMA(1) X(1) | chunk c: DMA(c+2) X(c+2) ...
 // ---------------------------------------------------------------------------
-using i32x4 = __attribute__((ext_vector_type(4))) int;
-
-// one buffer_load_dwordx4 ... lds: 16 B per lane from rsrc at voff + soff into LDS at m0 = lds
-__device__ __forceinline__ void dma_lds16(const i32x4& rsrc, uint32_t lds, uint32_t voff, uint32_t soff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               :
-               : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
-               : "memory", "m0");
-}
-
-// s_waitcnt vmcnt(n) (gfx9 encoding; expcnt / lgkmcnt left open)
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
 
 // LAB (diagnostics only, PPGAT_NNH2_LAB; results wrong), bits: 1 = no X loads after the first
 // two chunks (registers reused), 2 = no B DMA after the first two chunks (LDS reused), 4 = no
@@ -895,6 +877,82 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
       for (int q = 0; q < 16; ++q) {
         const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
         if (row < M && (!(LAB & 4) || acc[0][q] != acc[0][q])) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_gemm_nnh3: k_gemm_nnh2's pipeline with the next chunk prepared inside the current chunk's
+// MFMA sequence (ppgat_nnh_pipe.h: nnh3_loop), same products in the same order as k_gemm_nnh.
+// ---------------------------------------------------------------------------
+template <int NT, bool RK>
+__global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
+                                                      const int* __restrict__ ecol) {
+  using I = NnhImg<NT>;
+  constexpr int KC = I::KC;
+  __shared__ __attribute__((aligned(16))) uint16_t sB[3 * I::ELEMS];
+  __shared__ __attribute__((aligned(16))) float sF[8][32];  // per wave: a factor per row (rescale, epilogue)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int64_t rb = (idx / a.n_blocks) * 8 + (b & 7);  // XCD-aware: a row block's column blocks share an L2
+  const int nb = (int)(idx % a.n_blocks);
+  if (rb >= a.row_blocks) return;
+  const int64_t M = a.M;
+  const int chunks = a.K / KC;
+  const int64_t m = rb * kPBM + wv * 32 + r;
+  const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
+  auto loadx = [&](int c, float4 (&x)[4]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) x[g] = ld4(xrow + c * KC + 8 * g);
+  };
+  f32x16 acc[NT];
+  int erow = 0;
+  nnh3_loop<NT>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv, lane);
+  float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
+  split::row_unscale(erow, sF[wv], r, hf, fr);
+  const int64_t row0 = rb * kPBM + wv * 32;
+  const int n0 = nb * I::BN;
+  if constexpr (RK) {
+    const int nv = a.nv;
+    float ra[NT][kNnhRank], bv[NT], ic[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      bv[t] = a.bias != nullptr ? a.bias[col] : 0.f;
+      ic[t] = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int v = 0; v < kNnhRank; ++v) ra[t][v] = v < nv ? a.rA[v * a.ldra + col] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      const int64_t rr = row < M ? row : M - 1;
+      float sv[kNnhRank];
+#pragma unroll
+      for (int v = 0; v < kNnhRank; ++v) sv[v] = v < nv ? a.rS[rr * a.ldrs + v] : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float y = fmaf(acc[t][q] * fr[q], ic[t], bv[t]);
+#pragma unroll
+        for (int v = 0; v < kNnhRank; ++v)
+          if (v < nv) y = fmaf(sv[v], ra[t][v], y);
+        if (row < M) a.Y[row * a.ldy + n0 + 32 * t + r] = y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+      const float ic = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
       }
     }
   }
@@ -2076,13 +2134,16 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
   return hipGetLastError();
 }
 
-// k_gemm_nnh2 (the pipelined variant) unless PPGAT_NNH2=0; read once per process
-static bool nnh2_enabled() {
-  static const bool on = [] {
+// the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =3 k_gemm_nnh3 (and k_fusion_fwdh3), else
+// k_gemm_nnh2; read once per process
+int nnh_pipeline_variant() {
+  static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
-    return !(e && strcmp(e, "0") == 0);
+    if (e && strcmp(e, "0") == 0) return 1;
+    if (e && strcmp(e, "3") == 0) return 3;
+    return 2;
   }();
-  return on;
+  return v;
 }
 
 static int nnh2_lab() {
@@ -2129,7 +2190,18 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       int* ecol = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align_up(nnh_image_bytes(K, N, w8 ? 8 : 4)));
       hipError_t e = nnh_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, ecol, st);
       if (e != hipSuccess) return e;
-      if (nnh2_enabled() && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
+      if (nnh_pipeline_variant() == 3 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh3 runs chunk pairs
+        if (nv > 0) {
+          if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          else hipLaunchKernelGGL((k_gemm_nnh3<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        } else if (w8) {
+          hipLaunchKernelGGL((k_gemm_nnh3<8, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        } else {
+          hipLaunchKernelGGL((k_gemm_nnh3<4, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+        }
+        return hipGetLastError();
+      }
+      if (nnh_pipeline_variant() == 2 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
         if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {
 #define PPGAT_LAB(L) \
   if (lab == L) hipLaunchKernelGGL((k_gemm_nnh2<8, false, L>), dim3(grid), dim3(512), 0, st, a, img, ecol)

@@ -612,6 +612,23 @@ class HaloRows:
         self.events = {}
         self.local = set()
         self.started = []   # exchanged classes, in start order
+        self.s = self.s_dst = self.A = None  # the consuming layer's node scores (enable_scores)
+
+    def enable_scores(self, A: torch.Tensor):
+        """The rows' node scores under the consuming multi-head layer's A [2, H, K] travel with
+        them: the owner computes s_src / s_dst of its own rows (score_rows, as each producing
+        phase finishes) and start() sends s_src beside the rows (H floats per row), so the
+        consuming layer runs no score pass over its 11M table rows (hip_ops.xgat_forward
+        ``scores``; the same kernel on the same rows: the same values)."""
+        H = A.size(1)
+        self.A = A
+        self.s = torch.empty((self.hg.R, H), dtype=torch.float32, device=self.x.device)
+        self.s_dst = torch.empty((max(self.hg.n_own, 1), H), dtype=torch.float32, device=self.x.device)
+
+    def score_rows(self, out: torch.Tensor, d0: int, d1: int):
+        """Scores of the own rows [d0, d1) of ``out`` (the producing layer's output)."""
+        from .hip_ops import xgat_scores_rows
+        xgat_scores_rows(out[d0:d1], self.A, self.s[d0:d1], self.s_dst[d0:d1])
 
     def span(self, cls):
         hg = self.hg
@@ -631,18 +648,26 @@ class HaloRows:
         plan, (a, b) = self.plan(cls), self.span(cls)
         self.started.append(cls)
         comm, st = self.comm, self.stages
-        if comm.backend != "nccl" or not comm.active:
+        n0 = self.hg.n_own
+
+        def send():
             comm.all_to_all_rows(st.gather_rows(src, plan.send_idx), plan.send_counts, plan.recv_counts,
                                  out=self.x[a:b])
+            if self.s is not None:
+                comm.all_to_all_rows(st.gather_rows(self.s[:n0], plan.send_idx), plan.send_counts,
+                                     plan.recv_counts, out=self.s[a:b])
+        if comm.backend != "nccl" or not comm.active:
+            send()
             return
         dev = self.x.device
         main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
         cs.wait_stream(main)
         src.record_stream(cs)
         self.x.record_stream(cs)
+        if self.s is not None:
+            self.s.record_stream(cs)
         with torch.cuda.stream(cs):
-            comm.all_to_all_rows(st.gather_rows(src, plan.send_idx), plan.send_counts, plan.recv_counts,
-                                 out=self.x[a:b])
+            send()
             ev = torch.cuda.Event()
             ev.record(cs)
         self.events[cls] = ev
@@ -664,10 +689,21 @@ def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows
     and right after it the rows it produced start towards the next layer's peers (its output
     rows of that destination class).  Otherwise one phase after both classes."""
     from .hip_ops import XPhase
-    send = (lambda cls: (lambda out: rows_out.start(cls, out))) if rows_out is not None else (lambda cls: None)
+
+    def send(cls, d0=0, d1=0):
+        if rows_out is None:
+            return lambda out: None
+
+        def go(out):
+            if rows_out.s is not None:  # the next layer's scores of the rows this phase produced
+                rows_out.score_rows(out, d0, d1)
+            rows_out.start(cls, out)
+        return go
     if not (hg.bipartite and hg.fwd_sched_u is not None and hg.fwd_sched_i is not None):
         def after_all(out):
             if rows_out is not None:
+                if rows_out.s is not None:
+                    rows_out.score_rows(out, 0, hg.n_own)
                 rows_out.start("u", out)
                 rows_out.start("i", out)
         return [XPhase(0, hg.n_own, hg.fwd_view.fwd_sched, (rows_in.span("u"), rows_in.span("i")), rows_in.wait_all,
@@ -677,7 +713,7 @@ def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows
     order = sorted(ph, key=lambda d: (ph[d][3] not in rows_in.local,
                                       rows_in.started.index(ph[d][3]) if ph[d][3] in rows_in.started else 0))
     return [XPhase(ph[d][0], ph[d][1], ph[d][2], (rows_in.span(ph[d][3]),),
-                   (lambda c: (lambda: rows_in.wait(c)))(ph[d][3]), send(d)) for d in order]
+                   (lambda c: (lambda: rows_in.wait(c)))(ph[d][3]), send(d, ph[d][0], ph[d][1])) for d in order]
 
 
 class _HaloLayerX(torch.autograd.Function):
@@ -712,8 +748,9 @@ class _HaloLayerX(torch.autograd.Function):
             x_loc[:hg.n_own].copy_(x_own)
         # the output rows go straight into the next layer's table (its own rows)
         dest = rows_out.x[:hg.n_own] if rows_out is not None and rows_out.x.size(1) == C else None
+        scores = (rows_in.s, rows_in.s_dst) if rows_in.s is not None else None
         out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed,
-                                      phases=_halo_phases(hg, rows_in, rows_out), out=dest)
+                                      phases=_halo_phases(hg, rows_in, rows_out), out=dest, scores=scores)
         rows_in.wait_all()
         ctx.hg, ctx.comm, ctx.stages = hg, comm, stages
         ctx.plans = [rows_in.plan(c) for c in ("u", "i") if c not in rows_in.local]
@@ -860,7 +897,22 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
         torch.zeros(0, K, dtype=torch.float32, device=dev)
     del acc
     # 6. weight gradients (the sums over ranks: the dense all-reduce)
-    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0])
+    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0],
+                                xbits=_source_colmax_bits(x[:n0], hg, comm))
+
+
+def _source_colmax_bits(x_own: torch.Tensor, hg: "HaloGraph", comm: "Comm") -> torch.Tensor:
+    """The column bound of the weight-gradient GEMM's aggregate operand (hip_ops._xgat_weight_grads):
+    |agg_i[k]| <= max |x_j[k]| over i's sources j.  The exact set -- every table row with an edge
+    into an own destination -- is 11M rows (11 GB) per rank at world 8 on config 5; instead each
+    rank takes its OWN rows with an out-edge (src_views.colptr: on the symmetric edge list the
+    table rows' out-edges are their owners' own out-edges) and the ranks' maxima are combined by
+    an all_reduce(MAX) of K int32 (IEEE bits of non-negative floats order as the floats): the
+    maximum over every row with an out-edge anywhere, a superset of the sources, never a
+    row without one.  At world 1 it is the exact set."""
+    from . import hip_ops as O
+    bits = O.colmax_abs(x_own, hg.src_views.colptr)
+    return comm.all_reduce_(bits, op=dist.ReduceOp.MAX)
 
 
 def _partials_home(hg: "HaloGraph", comm: "Comm", stages, part: torch.Tensor) -> torch.Tensor:
@@ -959,7 +1011,8 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
         torch.zeros(0, K, dtype=torch.float32, device=dev)
     del acc
-    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0])
+    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0],
+                                xbits=_source_colmax_bits(x[:n0], hg, comm))
 
 
 class _ShardedBase(torch.nn.Module):
@@ -1051,6 +1104,7 @@ class HaloPyGGAT(_ShardedBase):
         return self.exchanges_input(conv) and getattr(self.stages, "supports_x", lambda c: False)(conv)
 
     def forward(self, item_feats):
+        from .hip_ops import xgat_att_proj
         hg = self.dg
         rows = None
         if self._x_path(0):
@@ -1073,6 +1127,9 @@ class HaloPyGGAT(_ShardedBase):
                     nxt = None
                     if li + 1 < len(self.convs) and self._x_path(li + 1):
                         nxt = HaloRows(hg, self.comm, self.stages, conv.out_channels, x)
+                        cn = self.convs[li + 1]
+                        nxt.enable_scores(xgat_att_proj(cn.lin.weight, cn.att_src, cn.att_dst, cn.heads,
+                                                        cn.out_channels))
                     x = _HaloLayerX.apply(x, xh, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg,
                                           self.comm, self.stages, conv.heads, conv.out_channels,
                                           float(conv.negative_slope), p, seed, rows, nxt)

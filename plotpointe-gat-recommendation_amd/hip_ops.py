@@ -1126,15 +1126,43 @@ class XPhase:
     after: Optional[Callable] = None
 
 
+def xgat_att_proj(weight, att_src, att_dst, heads: int, C: int) -> torch.Tensor:
+    """A [2, H, K]: A_v[h] = W_h^T att_v[h] (ppgat_xgat_weights) -- the node scores are x . A."""
+    lib = _lib.load()
+    W = weight.detach().contiguous()
+    K = W.size(1)
+    a_s = att_src.detach().reshape(heads, C).contiguous()
+    a_d = att_dst.detach().reshape(heads, C).contiguous()
+    A = torch.empty(2, heads, K, dtype=torch.float32, device=W.device)
+    _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), heads, C, K, A.data_ptr(), None,
+                                      None, _lib.stream_handle(W.device)), "xgat_weights")
+    return A
+
+
+def xgat_scores_rows(x_rows, A, s_src, s_dst):
+    """s_src / s_dst [n, H] of the rows x_rows [n, K] (row stride x_rows.stride(0)) under A
+    [2, H, K] (ppgat_xgat_scores; per row the same arithmetic whatever the launch)."""
+    lib = _lib.load()
+    n, K = x_rows.shape
+    H = A.size(1)
+    if n:
+        _lib.check(lib.ppgat_xgat_scores(x_rows.data_ptr(), x_rows.stride(0), n, n, K, H, A.data_ptr(),
+                                         s_src.data_ptr(), s_dst.data_ptr(), _lib.stream_handle(x_rows.device)),
+                   "xgat_scores")
+
+
 def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
-                 seed: int, phases: Optional[list] = None, out: Optional[torch.Tensor] = None):
+                 seed: int, phases: Optional[list] = None, out: Optional[torch.Tensor] = None, scores=None):
     """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state).
 
     ``phases`` (a list of XPhase partitioning [0, n_dst) in order): the node scores of the
     destination rows first, then per phase its sources' scores, the edge pass over its
     destination rows and their rows of the output GEMM.  Per destination the result is the
     same as the one-phase forward (same per-row kernels and order): bitwise equal.  ``out``: a
-    contiguous [n_dst, C] destination (the next halo layer's own rows: no copy there)."""
+    contiguous [n_dst, C] destination (the next halo layer's own rows: no copy there).
+    ``scores`` = (s_src [n_src, H], s_dst [>= n_dst, H]): the node scores, already computed
+    (the halo partition: the owners computed them with the rows and sent them along, ready by
+    each phase's ``before``) -- no score pass here."""
     lib = _lib.load()
     x = x.contiguous()
     dev = x.device
@@ -1150,13 +1178,18 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     Wt = torch.empty(H * K, C, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), H, C, K, A.data_ptr(),
                                       Wt.data_ptr(), None, st), "xgat_weights")
-    s_src = torch.empty(v.n_src, H, dtype=torch.float32, device=dev)
-    s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
     if phases is None:
         phases = [XPhase(0, v.n_dst, v.fwd_sched, ((v.n_dst, v.n_src),) if v.n_src > v.n_dst else ())]
-    # the destination rows' scores (s_src and s_dst), then each phase's other sources
-    _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_dst, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
-                                     s_dst.data_ptr(), st), "xgat_scores")
+    if scores is not None:
+        s_src, s_dst = scores
+        _require(s_src.shape == (v.n_src, H) and s_dst.size(0) >= max(v.n_dst, 1) and s_dst.size(1) == H
+                 and s_src.is_contiguous() and s_dst.is_contiguous(), "xgat_forward: scores must be [n_src, H], [n_dst, H]")
+    else:
+        s_src = torch.empty(v.n_src, H, dtype=torch.float32, device=dev)
+        s_dst = torch.empty(max(v.n_dst, 1), H, dtype=torch.float32, device=dev)
+        # the destination rows' scores (s_src and s_dst), then each phase's other sources
+        _lib.check(lib.ppgat_xgat_scores(x.data_ptr(), K, v.n_dst, v.n_dst, K, H, A.data_ptr(), s_src.data_ptr(),
+                                         s_dst.data_ptr(), st), "xgat_scores")
     agg = torch.empty(v.n_dst, H, K, dtype=torch.float32, device=dev)
     m = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
     inv_l = torch.empty(v.n_dst, H, dtype=torch.float32, device=dev)
@@ -1168,7 +1201,7 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     for ph in phases:
         if ph.before is not None:
             ph.before()
-        for r0, r1 in ph.src_ranges:
+        for r0, r1 in (ph.src_ranges if scores is None else ()):
             if r1 > r0:
                 _lib.check(lib.ppgat_xgat_scores(x.data_ptr() + 4 * r0 * K, K, r1 - r0, 0, K, H, A.data_ptr(),
                                                  s_src.data_ptr() + 4 * r0 * H, None, st), "xgat_scores")
@@ -1380,9 +1413,10 @@ def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[in
                                          dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
-def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None):
+def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None, xbits=None):
     """dW, datt, dbias from G = g^T agg and GV = S^T x (``x_rows``: the rows of x that S covers,
-    default all of the layer's source rows)."""
+    default all of the layer's source rows; ``xbits``: a precomputed column bound of the source
+    rows of x, colmax_abs bits, e.g. the maximum over the ranks of their own rows')."""
     x, W, a_s, a_d, agg, v = saved["x"], saved["W"], saved["a_s"], saved["a_d"], saved["agg"], saved["v"]
     H, C, K, slope, p, seed, has_bias = saved["meta"]
     dev = x.device
@@ -1392,7 +1426,8 @@ def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_r
     # the column maxima of the SOURCE rows of x (1 KB per row; a row with no out-edge -- however
     # large -- never enters an aggregate and must not loosen the bound: the fp16 split's error is
     # relative to it) instead of a pass over agg (4 KB per row); 2^-10 margin for fp32 rounding
-    xbound = (colmax_abs(x, v.colptr), K, (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
+    xbound = (colmax_abs(x, v.colptr) if xbits is None else xbits, K,
+              (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
     G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound)
     dW = torch.empty_like(W)
     datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)

@@ -351,7 +351,9 @@ class _StubComm:
 
     def all_reduce_(self, t, op=dist.ReduceOp.SUM):
         torch.cuda._sleep(2_000_000)
-        t.add_(1.0 if op == dist.ReduceOp.SUM else 0.5)
+        if t.dtype.is_floating_point:
+            t.add_(1.0 if op == dist.ReduceOp.SUM else 0.5)
+        # integer MAX (the weight-gradient column bound's IEEE bits): one rank's maximum is itself
         return t
 
     def all_gather_rows(self, t):

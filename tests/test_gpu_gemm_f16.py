@@ -213,10 +213,13 @@ ops = importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(3)
 out = {}
-for M, K, N, lay in ((70000, 1024, 256, 0), (9000, 256, 1024, 1), (30001, 896, 128, 1)):
+for M, K, N, lay in ((70000, 1024, 256, 0), (9000, 256, 1024, 1), (30001, 896, 128, 1), (5000, 64, 256, 0),
+                     (4100, 864, 256, 1)):
     X = torch.randn(M, K, device=dev, generator=g)
     X[::7] *= 1e-3                                   # rows with different scales
     X[5, K // 2:] *= 1e6                             # a row whose scale drops mid-way (rescale path)
+    X[9, :K // 2] = 0                                # a row whose scale is set late (zero first chunks)
+    X[11, 32:64] *= 1e5                              # a rescale in the second chunk
     B = torch.randn(K, N, device=dev, generator=g) * 0.05
     Bl = B if lay == 0 else B.t().contiguous()
     y = ops.gemm_nn(X, Bl, lay, N, alpha=0.25)
@@ -225,15 +228,29 @@ for M, K, N, lay in ((70000, 1024, 256, 0), (9000, 256, 1024, 1), (30001, 896, 1
     yr = ops.gemm_nn(X, Bl, lay, N, rank=(S, A))
     torch.cuda.synchronize()
     out[f"{M}x{K}x{N}"] = [hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest() for t in (y, yr)]
+fus = importlib.import_module("plotpointe-gat-recommendation_amd.fusion")
+for Bn, Dt, Di in ((20000, 384, 512), (3001, 64, 0)):   # k_fusion_fwdh / k_fusion_fwdh3 (28 and 2 chunks)
+    txt = torch.randn(Bn, Dt, device=dev, generator=g)
+    txt[4, 200:] *= 1e5 if Dt > 200 else 1.0
+    img = torch.randn(Bn, Di, device=dev, generator=g) if Di else None
+    W1 = torch.randn(256, Dt + Di, device=dev, generator=g) * 0.05
+    W2 = torch.randn(128, 256, device=dev, generator=g) * 0.05
+    b1, b2 = torch.randn(256, device=dev, generator=g), torch.randn(128, device=dev, generator=g)
+    kw = dict(normalize=True, img_index=torch.arange(Bn, dtype=torch.int32, device=dev), img_fallback=img.mean(0)) if Di else dict(normalize=True)
+    o = fus.fusion_forward(txt, img, W1, b1, W2, b2, **kw)
+    torch.cuda.synchronize()
+    out[f"fusion{Bn}x{Dt}+{Di}"] = hashlib.sha1(o.cpu().numpy().tobytes()).hexdigest()
 print(json.dumps(out))
 """
 
 
 def test_nnh2_bitwise_equals_nnh(cuda):
-    """The pipelined NN kernel (k_gemm_nnh2, the default) and k_gemm_nnh (PPGAT_NNH2=0) compute
-    the same products in the same order: bitwise equal outputs, with and without the fused rank
-    epilogue, on both B layouts, a ragged row count, an odd chunk count (K = 896: k_gemm_nnh
-    runs it) and a row that takes the rescale path."""
+    """The pipelined NN kernels (k_gemm_nnh2, k_gemm_nnh3: PPGAT_NNH2=3) and k_gemm_nnh
+    (PPGAT_NNH2=0) compute the same products in the same order: bitwise equal outputs, with and
+    without the fused rank epilogue, on both B layouts, a ragged row count, the shortest
+    pipelined K (two chunks), an odd chunk count (K = 864: k_gemm_nnh runs it for every variant),
+    rows that take the rescale path (in the second chunk, mid-way) and a row whose scale is set
+    only by its first nonzero chunk."""
     import json
     import os
     import subprocess
@@ -241,9 +258,10 @@ def test_nnh2_bitwise_equals_nnh(cuda):
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
     res = []
-    for v in ("1", "0"):
+    for v in ("2", "0", "3"):
         r = subprocess.run([sys.executable, "-c", _NNH2_CHECK, str(root)], env=dict(os.environ, PPGAT_NNH2=v),
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append(json.loads(r.stdout.strip().splitlines()[-1]))
     assert res[0] == res[1]
+    assert res[2] == res[0]

@@ -3,7 +3,7 @@
 # tools/bench_fusion.py (one rocprofv3 run per counter group).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-R=$(pwd); OUT=$R/gpurun_out/fusion; mkdir -p "$OUT"; export TMPDIR=/tmp
+R=$(pwd); OUT=$R/gpurun_out/fusion${FUSION_TAG:-}; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fusion.py tests/test_gpu_eval.py -m gpu -v -rf --timeout 150 --timeout-method thread > "$OUT/pytest.log" 2>&1
 rc=$?; tail -5 "$OUT/pytest.log"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 180 python -u tools/bench_fusion.py --train > "$OUT/bench.json" 2>&1 || exit $?

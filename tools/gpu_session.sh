@@ -37,11 +37,13 @@ for s in $STEPS; do
               run "probe5_r$1_a$2" 900 python -u tools/scale_probe.py --config 5 --world 8 --rank $1 --streams --a2a-gbs $2 --steps 5 --warmup 2 ${PROBE_ARGS:-}
             done ;;
     gemm5) run gemm5_nnh 300 env PPGAT_NNH2=0 python tools/bench_gemm.py --cfg5 --iters 10 && \
-           run gemm5_nnh2 300 env PPGAT_NNH2=1 python tools/bench_gemm.py --cfg5 --iters 10 ;;
+           run gemm5_nnh2 300 env PPGAT_NNH2=2 python tools/bench_gemm.py --cfg5 --iters 10 && \
+           run gemm5_nnh3 300 env PPGAT_NNH2=3 python tools/bench_gemm.py --cfg5 --iters 10 ;;
     pmcdst) (cd /tmp && run pmcdst_a 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_a" -o a -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             (cd /tmp && run pmcdst_b 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_b" -o b -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
             python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
+    nnhpmc) run "nnhpmc${NNHV:-3}" 500 env GEMM_ARGS=--cfg5 GEMM_TAG="_nnh${NNHV:-3}" PPGAT_NNH2="${NNHV:-3}" bash tools/gemm_pmc.sh ;;
     nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
     profprobe) (cd /tmp && run rocprof_probe5 900 rocprofv3 --kernel-trace --stats -d "$OUT/profprobe" -o run --output-format csv -- python "$R/tools/scale_probe.py" --config 5 --world 8 --rank ${PROBE_RANK:-7} --streams --steps 3 --warmup 1) ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -52,7 +54,9 @@ for s in $STEPS; do
     pmc5)  (cd /tmp && run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc5_fetch" -o fetch -- python "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
            (cd /tmp && run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc5_write" -o write -- python "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
            python "$R/tools/pmc_summary.py" "$OUT/pmc5_fetch" "$OUT/pmc5_write" "$OUT/cfg5_pmc_traffic.json" 5 scale=0.125 bwd_gather=gd > "$OUT/pmc5_summary.log" 2>&1 ;;
-    fusion) run bench_fusion 300 python tools/bench_fusion.py ;;
+    fusion) run bench_fusion 300 python tools/bench_fusion.py && \
+            run bench_fusion3 300 env PPGAT_NNH2=3 python tools/bench_fusion.py ;;
+    fusionpmc) run "fusionpmc${NNHV:-3}" 500 env PPGAT_NNH2="${NNHV:-3}" FUSION_TAG="_nnh${NNHV:-3}" bash tools/fusion_pmc.sh ;;
     prof)  (cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --steps 10 --warmup 3 --cpu-baseline-seconds 0) ;;
     pmc)   (cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o fetch -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \
            (cd /tmp && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o write -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \
