@@ -746,6 +746,14 @@ class _HaloLayerX(torch.autograd.Function):
         x_loc = rows_in.x
         if x_loc.data_ptr() != x_own.data_ptr():
             x_loc[:hg.n_own].copy_(x_own)
+        if rows_in.s is not None and x_halo_items is not None:
+            # the first layer: the own users' scores went out with their rows; the own items'
+            # and the locally computed halo items' are computed here
+            from .hip_ops import xgat_scores_rows
+            nu, n0 = hg.n_own_u, hg.n_own
+            xgat_scores_rows(x_loc[nu:n0], rows_in.A, rows_in.s[nu:n0], rows_in.s_dst[nu:n0])
+            a, b = rows_in.span("i")
+            xgat_scores_rows(x_halo_items, rows_in.A, rows_in.s[a:b])
         # the output rows go straight into the next layer's table (its own rows)
         dest = rows_out.x[:hg.n_own] if rows_out is not None and rows_out.x.size(1) == C else None
         scores = (rows_in.s, rows_in.s_dst) if rows_in.s is not None else None
@@ -1111,6 +1119,9 @@ class HaloPyGGAT(_ShardedBase):
             # the first layer's halo user rows are parameters: their exchange starts before
             # the item projections (the own and the halo items' rows) are computed
             rows = HaloRows(hg, self.comm, self.stages, self.user_emb_local.size(1), self.user_emb_local)
+            c0 = self.convs[0]
+            rows.enable_scores(xgat_att_proj(c0.lin.weight, c0.att_src, c0.att_dst, c0.heads, c0.out_channels))
+            rows.score_rows(self.user_emb_local.detach(), 0, hg.n_own_u)  # sent beside the user rows
             rows.start("u", self.user_emb_local.detach())
         x = self.node_features(item_feats)
         for li, conv in enumerate(self.convs):

@@ -1139,16 +1139,17 @@ def xgat_att_proj(weight, att_src, att_dst, heads: int, C: int) -> torch.Tensor:
     return A
 
 
-def xgat_scores_rows(x_rows, A, s_src, s_dst):
-    """s_src / s_dst [n, H] of the rows x_rows [n, K] (row stride x_rows.stride(0)) under A
-    [2, H, K] (ppgat_xgat_scores; per row the same arithmetic whatever the launch)."""
+def xgat_scores_rows(x_rows, A, s_src, s_dst=None):
+    """s_src (and, given, s_dst) [n, H] of the rows x_rows [n, K] (row stride x_rows.stride(0))
+    under A [2, H, K] (ppgat_xgat_scores; per row the same arithmetic whatever the launch)."""
     lib = _lib.load()
     n, K = x_rows.shape
     H = A.size(1)
     if n:
-        _lib.check(lib.ppgat_xgat_scores(x_rows.data_ptr(), x_rows.stride(0), n, n, K, H, A.data_ptr(),
-                                         s_src.data_ptr(), s_dst.data_ptr(), _lib.stream_handle(x_rows.device)),
-                   "xgat_scores")
+        _lib.check(lib.ppgat_xgat_scores(x_rows.data_ptr(), x_rows.stride(0), n, n if s_dst is not None else 0, K, H,
+                                         A.data_ptr(), s_src.data_ptr(),
+                                         s_dst.data_ptr() if s_dst is not None else None,
+                                         _lib.stream_handle(x_rows.device)), "xgat_scores")
 
 
 def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
