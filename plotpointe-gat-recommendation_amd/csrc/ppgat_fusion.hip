@@ -910,7 +910,7 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
     hipError_t e = nnh_presplit(W1, Dt + Di, 1, Dt + Di, H1, 8, w1i, e1, st);
     if (e == hipSuccess) e = nnh_presplit(W2, H1, 1, H1, DO, 4, w2i, e2, st);
     if (e != hipSuccess) return e;
-    if (nnh_pipeline_variant() == 3 && ((Dt + Di) / BK) % 2 == 0)
+    if (nnh_pipeline_variant() >= 3 && ((Dt + Di) / BK) % 2 == 0)
       hipLaunchKernelGGL(k_fusion_fwdh3, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
                          img_index, img_fallback, B, Dt, Di, w1i, e1, b1, w2i, e2, b2, normalize, out, z1_out);
     else

@@ -54,9 +54,13 @@ __device__ __forceinline__ void wait_vm() {
 // column block's chunk images (chunks x NnhImg<NT>::ELEMS); sB: LDS, 3 x ELEMS; sFw: this wave's
 // 32-float LDS scratch; loadx(c, x): this lane's 16 values of chunk c (4 float4, the fragment
 // order of split2h: x[g] = row[32 c + 8 g + 4 hf .. + 3]).
-template <int NT, class LoadX>
+// BD: B fragments read BD MFMA steps ahead (1: the step before, as k_gemm_nnh2; 2: two steps,
+// eight more VGPRs, for LDS latency under eight waves of reads).  PRIO: waves 4-7 (the second-
+// dispatched half, the issue-arbitration loser) at s_setprio 1 for the whole loop.
+template <int NT, int BD = 1, bool PRIO = false, class LoadX>
 __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int chunks, const LoadX& loadx,
                                           split::f32x16 (&acc)[NT], int& erow, float* sFw, int wv, int lane) {
+  static_assert(BD == 1 || BD == 2, "B read depth");
   using I = NnhImg<NT>;
   constexpr int LDK = I::LDK, PART = I::PART, NI = I::BYTES / 1024;
   constexpr int STEPS = (I::KC / 16) * NT;  // MFMA steps (three products each) per chunk
@@ -115,6 +119,7 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
     erow = pen;
     set = set || pneed;
   };
+  if (PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
   float4 xA[4], xB[4];
   split::u32x4 fxA[2][2], fxB[2][2];
   issue(0);
@@ -140,20 +145,21 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
 #pragma unroll
       for (int p = 0; p < 2; ++p) f[p] = *reinterpret_cast<const split::u32x4*>(&sb[p * PART + off]);
     };
-    split::u32x4 fb[2][2];
-    read_b(0, fb[0]);
+    split::u32x4 fb[BD + 1][2];
+#pragma unroll
+    for (int i = 0; i < BD; ++i) read_b(i, fb[i]);
 #pragma unroll
     for (int i = 0; i < STEPS; ++i) {
       const int u = i / NT, t = i % NT;
-      if (i + 1 < STEPS) read_b(i + 1, fb[(i + 1) & 1]);
-      acc[t] = split::mfma32_h3(fxc[u], fb[i & 1], acc[t]);
+      if (i + BD < STEPS) read_b(i + BD, fb[(i + BD) % (BD + 1)]);
+      acc[t] = split::mfma32_h3(fxc[u], fb[i % (BD + 1)], acc[t]);
       if constexpr (NEXT) {
         if (i >= STEPS / 2) {
 #pragma unroll
           for (int k = 0; k < PPS; ++k) prep((i - STEPS / 2) * PPS + k, xn, fxn);
         }
       }
-      if (i + 1 < STEPS) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);
+      if (i + BD < STEPS) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x0002, 6, 0);
       __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
@@ -179,6 +185,7 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
   }
   body(chunks - 2, xA, xB, fxA, fxB, yes{});
   body(chunks - 1, xB, xA, fxB, fxA, no{});
+  if (PRIO && wv >= 4) __builtin_amdgcn_s_setprio(0);
 }
 
 }  // namespace ppgat

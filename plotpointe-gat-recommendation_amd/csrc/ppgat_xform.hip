@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
 // k_gemm_nnh3: k_gemm_nnh2's pipeline with the next chunk prepared inside the current chunk's
 // MFMA sequence (ppgat_nnh_pipe.h: nnh3_loop), same products in the same order as k_gemm_nnh.
 // ---------------------------------------------------------------------------
-template <int NT, bool RK>
+template <int NT, bool RK, int BD = 1, bool PRIO = false>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
@@ -911,7 +911,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* _
   };
   f32x16 acc[NT];
   int erow = 0;
-  nnh3_loop<NT>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv, lane);
+  nnh3_loop<NT, BD, PRIO>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv, lane);
   float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
   split::row_unscale(erow, sF[wv], r, hf, fr);
   const int64_t row0 = rb * kPBM + wv * 32;
@@ -2134,13 +2134,15 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
   return hipGetLastError();
 }
 
-// the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =3 k_gemm_nnh3 (and k_fusion_fwdh3), else
-// k_gemm_nnh2; read once per process
+// the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2, =3 k_gemm_nnh3 (and
+// k_fusion_fwdh3), =4 k_gemm_nnh3 with B read two steps ahead, =5 that with the second half of
+// the waves at s_setprio 1 (experiments; the fusion kernel runs its variant-3 loop for 3..5);
+// default 2.  Read once per process.
 int nnh_pipeline_variant() {
   static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
     if (e && strcmp(e, "0") == 0) return 1;
-    if (e && strcmp(e, "3") == 0) return 3;
+    if (e && (strcmp(e, "3") == 0 || strcmp(e, "4") == 0 || strcmp(e, "5") == 0)) return e[0] - '0';
     return 2;
   }();
   return v;
@@ -2190,15 +2192,23 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       int* ecol = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align_up(nnh_image_bytes(K, N, w8 ? 8 : 4)));
       hipError_t e = nnh_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, ecol, st);
       if (e != hipSuccess) return e;
-      if (nnh_pipeline_variant() == 3 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh3 runs chunk pairs
-        if (nv > 0) {
-          if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-          else hipLaunchKernelGGL((k_gemm_nnh3<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-        } else if (w8) {
-          hipLaunchKernelGGL((k_gemm_nnh3<8, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-        } else {
-          hipLaunchKernelGGL((k_gemm_nnh3<4, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
-        }
+      if (nnh_pipeline_variant() >= 3 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh3 runs chunk pairs
+        const int v = nnh_pipeline_variant();
+#define PPGAT_NNH3(BD, PR)                                                                              \
+  do {                                                                                                  \
+    if (nv > 0) {                                                                                       \
+      if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, true, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol); \
+      else hipLaunchKernelGGL((k_gemm_nnh3<4, true, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol);    \
+    } else if (w8) {                                                                                    \
+      hipLaunchKernelGGL((k_gemm_nnh3<8, false, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
+    } else {                                                                                            \
+      hipLaunchKernelGGL((k_gemm_nnh3<4, false, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
+    }                                                                                                   \
+  } while (0)
+        if (v == 3) PPGAT_NNH3(1, false);
+        else if (v == 4) PPGAT_NNH3(2, false);
+        else PPGAT_NNH3(2, true);
+#undef PPGAT_NNH3
         return hipGetLastError();
       }
       if (nnh_pipeline_variant() == 2 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs

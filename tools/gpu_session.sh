@@ -38,7 +38,7 @@ for s in $STEPS; do
             done ;;
     gemm5) run gemm5_nnh 300 env PPGAT_NNH2=0 python tools/bench_gemm.py --cfg5 --iters 10 && \
            run gemm5_nnh2 300 env PPGAT_NNH2=2 python tools/bench_gemm.py --cfg5 --iters 10 && \
-           run gemm5_nnh3 300 env PPGAT_NNH2=3 python tools/bench_gemm.py --cfg5 --iters 10 ;;
+           for v in ${NNHVS:-3}; do run "gemm5_nnh$v" 300 env PPGAT_NNH2=$v python tools/bench_gemm.py --cfg5 --iters 10; done ;;
     pmcdst) (cd /tmp && run pmcdst_a 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_a" -o a -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             (cd /tmp && run pmcdst_b 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_b" -o b -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
