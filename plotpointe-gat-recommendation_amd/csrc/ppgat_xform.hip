@@ -2135,15 +2135,16 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
 }
 
 // the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2, =3 k_gemm_nnh3 (and
-// k_fusion_fwdh3), =4 k_gemm_nnh3 with B read two steps ahead, =5 that with the second half of
-// the waves at s_setprio 1 (experiments; the fusion kernel runs its variant-3 loop for 3..5);
-// default 2.  Read once per process.
+// k_fusion_fwdh3; the default: 2-3 % faster than k_gemm_nnh2 at config-5 shapes, bitwise equal,
+// profiles/r04/v8_gemm5_nnh*.log), =4 k_gemm_nnh3 with B read two steps ahead, =5 that with the
+// second half of the waves at s_setprio 1 (both within 1 % of 3: kept as measured negatives;
+// the fusion kernel runs its variant-3 loop for 3..5).  Read once per process.
 int nnh_pipeline_variant() {
   static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
     if (e && strcmp(e, "0") == 0) return 1;
-    if (e && (strcmp(e, "3") == 0 || strcmp(e, "4") == 0 || strcmp(e, "5") == 0)) return e[0] - '0';
-    return 2;
+    if (e && (strcmp(e, "2") == 0 || strcmp(e, "4") == 0 || strcmp(e, "5") == 0)) return e[0] - '0';
+    return 3;
   }();
   return v;
 }

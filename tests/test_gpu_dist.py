@@ -450,3 +450,30 @@ def test_halo_forward_overlap_ordering(cuda):
     assert len(res["nccl"]) == len(res["inline"]) > 4
     for a, b in zip(res["nccl"], res["inline"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cols", [4, 12, 16, 130, 256, 512])
+def test_rows_gather_and_return_add_bitwise(cuda, cols):
+    """ppgat_rows_gather (narrow, one-wave-per-row and the 4-rows-per-wave 1-KB kernel) equals
+    torch indexing, and ppgat_rows_return_add equals the same adds done in peer (k) order --
+    bitwise, with rows getting 0 to 11 copies (more than one 8-load batch) and a ragged tail."""
+    pkg = importlib.import_module("plotpointe-gat-recommendation_amd")
+    st = pkg.hip_ops.HipStages()
+    g = torch.Generator(device=cuda).manual_seed(cols)
+    n_src, n = 5003, 4097
+    src = torch.randn(n_src, cols, device=cuda, generator=g)
+    idx = torch.randint(0, n_src, (n,), device=cuda, generator=g)
+    assert torch.equal(st.gather_rows(src, idx), src[idx])
+    cnt = torch.randint(0, 12, (n,), device=cuda, generator=g)
+    ptr = torch.zeros(n + 1, dtype=torch.int32, device=cuda)
+    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    tot = int(ptr[-1])
+    ret = torch.randn(tot + 7, cols, device=cuda, generator=g)
+    pos = torch.randperm(tot + 7, device=cuda, generator=g)[:tot].to(torch.int32)
+    dst = torch.randn(n, cols, device=cuda, generator=g)
+    ref = dst.clone()
+    for j in range(int(cnt.max())):  # the j-th copy of every row that has one, in k order
+        rows = torch.nonzero(cnt > j).squeeze(1)
+        ref[rows] += ret[pos[(ptr[rows] + j).long()].long()]
+    st.return_add(dst, ret, ptr, pos)
+    assert torch.equal(dst, ref)

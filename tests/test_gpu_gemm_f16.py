@@ -245,7 +245,8 @@ print(json.dumps(out))
 
 
 def test_nnh2_bitwise_equals_nnh(cuda):
-    """The pipelined NN kernels (k_gemm_nnh2, k_gemm_nnh3: PPGAT_NNH2=3) and k_gemm_nnh
+    """The pipelined NN kernels (k_gemm_nnh3, the default; k_gemm_nnh2 and the nnh3 variants:
+    PPGAT_NNH2=2 / 4 / 5; the FusionMLP's k_fusion_fwdh3 beside k_fusion_fwdh) and k_gemm_nnh
     (PPGAT_NNH2=0) compute the same products in the same order: bitwise equal outputs, with and
     without the fused rank epilogue, on both B layouts, a ragged row count, the shortest
     pipelined K (two chunks), an odd chunk count (K = 864: k_gemm_nnh runs it for every variant),
@@ -258,7 +259,7 @@ def test_nnh2_bitwise_equals_nnh(cuda):
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
     res = []
-    for v in ("2", "0", "3", "4", "5"):
+    for v in ("3", "0", "2", "4", "5"):
         r = subprocess.run([sys.executable, "-c", _NNH2_CHECK, str(root)], env=dict(os.environ, PPGAT_NNH2=v),
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
