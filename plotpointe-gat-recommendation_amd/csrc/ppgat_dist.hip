@@ -112,27 +112,6 @@ __global__ void __launch_bounds__(256) k_rows_gather(const float* __restrict__ s
   }
 }
 
-// 1-KB rows (cols == 256, 16-B aligned: the halo layers' x and g rows): a wave moves RPW rows,
-// all their loads issued before the first store, so each wave keeps RPW KB in flight instead of
-// one (a one-row wave spends its life waiting for one HBM round trip)
-template <int RPW>
-__global__ void __launch_bounds__(256) k_rows_gather_1k(const float* __restrict__ src, int64_t lds,
-                                                        const int64_t* __restrict__ idx, int64_t n,
-                                                        float* __restrict__ dst, int64_t ldd) {
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  if (r0 >= n) return;
-  const int c = (threadIdx.x & 63) * 4;
-  float4 v[RPW];
-#pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    const int64_t r = r0 + j < n ? r0 + j : n - 1;
-    v[j] = *reinterpret_cast<const float4*>(src + idx[r] * lds + c);
-  }
-#pragma unroll
-  for (int j = 0; j < RPW; ++j)
-    if (r0 + j < n) *reinterpret_cast<float4*>(dst + (r0 + j) * ldd + c) = v[j];
-}
-
 // dst[o, :] += sum_{k in [ptr[o], ptr[o+1])} ret[pos[k], :], k ascending (peer order)
 __global__ void __launch_bounds__(256) k_rows_return_add(float* __restrict__ dst, int64_t ldd,
                                                          const float* __restrict__ ret, int64_t ldr,
@@ -222,12 +201,6 @@ hipError_t rows_gather(const float* src, int64_t lds, const int64_t* idx, int64_
     if (L == 1) hipLaunchKernelGGL(k_rows_gather_narrow<1>, dim3(g), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd);
     else if (L == 2) hipLaunchKernelGGL(k_rows_gather_narrow<2>, dim3(g), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd);
     else hipLaunchKernelGGL(k_rows_gather_narrow<4>, dim3(g), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd);
-    return hipGetLastError();
-  }
-  if (cols == 256 && vec_ok(src, lds, dst, ldd, cols)) {
-    constexpr int RPW = 4;
-    hipLaunchKernelGGL(k_rows_gather_1k<RPW>, dim3((unsigned)((n + 4 * RPW - 1) / (4 * RPW))), dim3(256), 0, st, src,
-                       lds, idx, n, dst, ldd);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_rows_gather, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, lds, idx, n, cols, dst, ldd,

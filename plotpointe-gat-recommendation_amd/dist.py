@@ -861,10 +861,10 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
     g = g.contiguous()
     gtab = HaloRows(hg, comm, stages, C, g)
     gtab.x[:n0].copy_(g)
-    for cls in ("u", "i"):
-        gtab.start(cls, g)
     if os.environ.get("PPGAT_XGAT_GATHER") != "g":
         return _halo_xgat_backward_deferred_d(saved, g, hg, comm, stages, want_bias_grad, gtab)
+    for cls in ("u", "i"):
+        gtab.start(cls, g)
     # 1. destination state of the own rows
     Wg = torch.empty(C, H * K, dtype=torch.float32, device=dev)
     _lib.check(lib.ppgat_xgat_weights(W.data_ptr(), None, None, H, C, K, None, None, Wg.data_ptr(), st),
@@ -923,6 +923,14 @@ def _source_colmax_bits(x_own: torch.Tensor, hg: "HaloGraph", comm: "Comm") -> t
     return comm.all_reduce_(bits, op=dist.ReduceOp.MAX)
 
 
+def _small_class_first(hg: "HaloGraph") -> tuple:
+    """The halo classes in exchange order: the one with fewer nodes in the whole graph first
+    (every rank computes the same order -- the all_to_alls must match -- and on a bipartite
+    graph a class's halo rows scale with its node count)."""
+    n_items = hg.n_nodes - hg.n_users
+    return ("i", "u") if n_items <= hg.n_users else ("u", "i")
+
+
 def _partials_home(hg: "HaloGraph", comm: "Comm", stages, part: torch.Tensor) -> torch.Tensor:
     """part [R, w]: this rank's partial sums per table row -> the own rows' complete sums (the
     halo rows' partials returned to their owners by the reverse plans, each own row adding its
@@ -959,14 +967,19 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     nst = nst[:n0]
     ntab = HaloRows(hg, comm, stages, 4 * H, nst)
     ntab.x[:n0].copy_(nst)
-    for cls in ("u", "i"):
+    # both tables of the smaller halo class first (the same order on every rank: it is decided
+    # from the global segment sizes), so the phase that reads it starts while the other class
+    # is still on the wire
+    order = _small_class_first(hg)
+    for cls in order:
         ntab.start(cls, nst)
+        gtab.start(cls, g)
     hs = O.gemm_nn(x[:n0], W, 1, H * C, alpha=1.0 / H)
     acc = torch.empty(max(n0, 1), H * C, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
     pdal = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
-    phases = ([(hg.src_sched_i, hg.n_own_u, "u"), (hg.src_sched_u, 0, "i")] if hg.bipartite else
-              [(sv.bwd_sched, 0, None)])
+    by_need = {"i": (hg.src_sched_u, 0, "i"), "u": (hg.src_sched_i, hg.n_own_u, "u")}  # user sources read items
+    phases = [by_need[c] for c in order] if hg.bipartite else [(sv.bwd_sched, 0, None)]
     for sched, base, need in phases:  # dalpha (into dz) and beta dalpha per edge, acc per own source
         for tab in (gtab, ntab):
             tab.wait_all() if need is None else tab.wait(need)

@@ -454,7 +454,7 @@ def test_halo_forward_overlap_ordering(cuda):
 
 @pytest.mark.parametrize("cols", [4, 12, 16, 130, 256, 512])
 def test_rows_gather_and_return_add_bitwise(cuda, cols):
-    """ppgat_rows_gather (narrow, one-wave-per-row and the 4-rows-per-wave 1-KB kernel) equals
+    """ppgat_rows_gather (the narrow and the one-wave-per-row kernels) equals
     torch indexing, and ppgat_rows_return_add equals the same adds done in peer (k) order --
     bitwise, with rows getting 0 to 11 copies (more than one 8-load batch) and a ragged tail."""
     pkg = importlib.import_module("plotpointe-gat-recommendation_amd")

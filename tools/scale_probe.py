@@ -57,18 +57,22 @@ class NullComm:
         self._hold(2 * (self.world - 1) / self.world * t.numel() * t.element_size())
         return t
 
-    own_id = 0  # a node id this rank owns (set after the graph is built): the stubbed id exchange
+    own_ids = None  # node ids of this rank's own items (set after the graph is built): the stubbed id exchange
 
     def all_to_all_rows(self, t, send_counts, recv_counts, out=None):
-        # stub: received rows are zeros, received ids are an id this rank owns (so the loss
-        # plan's requests resolve to local rows); timing only
+        # stub: received rows are zeros; received ids (the loss plan's requests from the peers)
+        # are this rank's own items in turn -- each own item then gets about as many returned
+        # copies as at world 8 (at most a few), not all of them one row; timing only
         n = int(sum(recv_counts))
         row = t[0].numel() * t.element_size() if t.dim() and t.size(0) else 0
         row = row or (int(np.prod(t.shape[1:])) * t.element_size() if t.dim() > 1 else t.element_size())
         self._hold(max(int(sum(send_counts)), n) * row)
         if out is None:
-            fill = self.own_id if not t.is_floating_point() else 0
-            out = torch.full((n,) + tuple(t.shape[1:]), fill, dtype=t.dtype, device=t.device)
+            if not t.is_floating_point() and self.own_ids is not None and len(self.own_ids):
+                ids = self.own_ids.to(t.device)
+                out = ids[torch.arange(n, device=t.device) % len(ids)].to(t.dtype)
+            else:
+                out = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return out
 
     def all_to_all_counts(self, counts):
@@ -131,7 +135,7 @@ def main():
         del ei
         ei = None
         torch.cuda.empty_cache()
-        comm.own_id = int(dg.own_node_ids()[dg.n_own_u]) if dg.n_own > dg.n_own_u else 0  # first own item
+        comm.own_ids = torch.from_numpy(dg.own_node_ids()[dg.n_own_u:].astype(np.int64))  # own items
         model = D.HaloPyGGAT(full, dg, comm)
         loss_fn = D.halo_bpr_loss
         n_edges = dg.fwd_view.n_fwd_edges
