@@ -454,7 +454,7 @@ def main():
         "gemm": ("fp32 MFMA, exact fp32 FMA chains (PPGAT_GEMM=fp32)" if os.environ.get("PPGAT_GEMM") == "fp32" else
                  "fp32 operands and results on the matrix cores through operand splits (DESIGN.md 4.3): "
                  "fp16 two-term split with power-of-two row/column scales, 3 MFMAs per product, <= 2^-21 "
-                 "relative per product, for the large-M NN and TN products (k_gemm_nnh2, k_gemm_tnh); bf16 "
+                 "relative per product, for the large-M NN and TN products (k_gemm_nnh3, k_gemm_tnh); bf16 "
                  "three-term split, 6 MFMAs, <= 2^-24, for the rest"
                  if args.config == 5 and os.environ.get("PPGAT_GEMM_F16", "1") != "0" else
                  "fp32 operands and results on the matrix cores through the bf16 three-term split (6 MFMAs "

@@ -113,14 +113,17 @@ def main():
     full = pkg.PyGGAT(g.n_users, g.n_items, item_feat_dim=fdim, hidden=hidden, layers=2, heads=heads,
                       attn_dropout=0.1).to(dev)
     cyc = 0.0
-    if args.a2a_gbs > 0:  # calibrate the GPU sleep: cycles per millisecond
+    cal = []
+    if args.a2a_gbs > 0:  # calibrate the GPU sleep: cycles per millisecond (median of 6 timings)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda._sleep(1_000_000)
-        a.record()
-        torch.cuda._sleep(50_000_000)
-        b.record()
-        torch.cuda.synchronize()
-        cyc = 50_000_000 / a.elapsed_time(b)
+        for n in (20_000_000, 40_000_000) * 3:
+            a.record()
+            torch.cuda._sleep(n)
+            b.record()
+            torch.cuda.synchronize()
+            cal.append(n / a.elapsed_time(b))
+        cyc = float(np.median(cal))
     comm = NullComm(args.world, args.rank, args.a2a_gbs, cyc)
     if args.streams:
         comm.backend = "nccl"
@@ -192,8 +195,18 @@ def main():
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(30)
         print(buf.getvalue(), flush=True)
+    sleep_check = None
+    if cyc > 0:  # the calibration re-checked after the run: one sleep of the modelled per-step exchange
+        want = comm.modelled_ms / args.steps
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        torch.cuda._sleep(int(want * cyc))
+        b.record()
+        torch.cuda.synchronize()
+        sleep_check = {"intended_ms": want, "measured_ms": a.elapsed_time(b)}
     print(json.dumps({"config": args.config, "partition": args.partition, "graph": args.graph, "world": args.world,
                       "rank": args.rank, "streams": args.streams, "a2a_gbs": args.a2a_gbs,
+                      "sleep_cycles_per_ms": cyc, "sleep_calibration": cal, "sleep_check": sleep_check,
                       "modelled_exchange_ms_per_step": comm.modelled_ms / args.steps if not args.graph else None,
                       "rows": int(dg.R), "local_edges": int(n_edges), "global_edges": int(2 * g.n_interactions),
                       "ms_per_step": el / args.steps * 1e3, "host_enqueue_ms_per_step": th / args.steps * 1e3,
