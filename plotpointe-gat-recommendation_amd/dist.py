@@ -612,6 +612,7 @@ class HaloRows:
         self.events = {}
         self.local = set()
         self.started = []   # exchanged classes, in start order
+        self.keep = {}      # class -> the source tensors of its exchange in flight
         self.s = self.s_dst = self.A = None  # the consuming layer's node scores (enable_scores)
 
     def enable_scores(self, A: torch.Tensor):
@@ -662,20 +663,23 @@ class HaloRows:
         dev = self.x.device
         main, cs = torch.cuda.current_stream(dev), _comm_stream(dev)
         cs.wait_stream(main)
-        src.record_stream(cs)
-        self.x.record_stream(cs)
-        if self.s is not None:
-            self.s.record_stream(cs)
+        # no record_stream: the tables are this object's and ``src`` is held here until the
+        # current stream has waited for the exchange (wait / wait_all), so every block the comm
+        # stream reads or writes is released in stream order after that wait.  (record_stream
+        # defers each freed block to an event query; with 11-GB tables and steps enqueued ahead
+        # the caching allocator then ran short and synchronised the host on the comm stream.)
         with torch.cuda.stream(cs):
             send()
             ev = torch.cuda.Event()
             ev.record(cs)
         self.events[cls] = ev
+        self.keep.setdefault(cls, []).append(src)
 
     def wait(self, cls):
         ev = self.events.pop(cls, None)
         if ev is not None:
             torch.cuda.current_stream(self.x.device).wait_event(ev)
+        self.keep.pop(cls, None)
 
     def wait_all(self):
         for cls in list(self.events):
