@@ -1861,7 +1861,7 @@ __global__ void __launch_bounds__(256) k_xgat_nstate(const float* __restrict__ s
 // 4 for the short ones (<= 16 edges: four rows per lane group keep four times as many items in
 // flight).  Each lane takes every LPI-th edge, four at a time with all their loads issued
 // first, summed in edge order, then the LPI-lane tree; hub pieces leave a partial that
-// k_xgat_dz_merge adds up in piece order.
+// k_xgat_dz_merge_wg adds up (pieces dealt to the waves, combined in wave order).
 template <int H, int LPI>
 __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t w1, const int32_t* __restrict__ row,
                                                  const int32_t* __restrict__ csc_eid,
@@ -1931,44 +1931,164 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t 
   }
 }
 
-template <int H>
-__global__ void __launch_bounds__(256) k_xgat_dz_merge(const int32_t* __restrict__ hub_row,
-                                                       const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
-                                                       const float* __restrict__ partial, float* __restrict__ S,
-                                                       int64_t lds) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= n_hubs * H) return;
-  const int64_t hb = t / H;
-  const int h = (int)(t % H);
-  float x = 0.f;
-  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) x += partial[(int64_t)q * H + h];
-  S[(int64_t)hub_row[hb] * lds + h] = x;
+// ---------------------------------------------------------------------------
+// Hub merges with a whole workgroup on each hub: the pieces are dealt to the kMW waves in
+// turn (each wave keeps several partial rows in flight), and the waves' sums are combined in
+// wave order through LDS -- a fixed order, deterministic.  One wave per hub (k_fwd_merge,
+// k_bwd_g_merge, k_xgat_dz_merge: pieces in a single wave's loop) left config 5's top item --
+// 1M edges = 3,900 pieces of 256 edges, on the rank that owns it -- merging for 4 ms per call,
+// 10 ms per step of that rank (profiles/r04/v16_probe5_r0_kernel_stats.csv).
+// ---------------------------------------------------------------------------
+constexpr int kMW = 8;  // waves per hub
+
+// aggregate-then-transform forward: agg[i,h] = sum_q e^(m_q - M) ax_q / sum_q e^(m_q - M) l_q
+__global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __restrict__ hub_row,
+                                                           const int32_t* __restrict__ hub_ptr, int heads,
+                                                           const float* __restrict__ partial, float eps,
+                                                           float* __restrict__ m_out, float* __restrict__ invl_out,
+                                                           float* __restrict__ agg_out) {
+  constexpr int C = 256;
+  __shared__ float4 red[kMW][64];
+  __shared__ float sr[kMW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t hb = blockIdx.x;
+  const int64_t i = hub_row[hb];
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  auto slot = [&](int q, int hd) { return partial + ((int64_t)q * heads + hd) * (C + 4); };
+  for (int hd = 0; hd < heads; ++hd) {
+    float M = -INFINITY;
+    for (int q = p0 + tid; q < p1; q += 64 * kMW) M = fmaxf(M, slot(q, hd)[C]);
+    M = wave_max(M);
+    if (lane == 0) sr[w] = M;
+    __syncthreads();
+    M = sr[0];
+    for (int k = 1; k < kMW; ++k) M = fmaxf(M, sr[k]);
+    __syncthreads();
+    float t = 0.f;
+    for (int q = p0 + tid; q < p1; q += 64 * kMW) t += slot(q, hd)[C + 1] * expf(slot(q, hd)[C] - M);
+    t = wave_sum(t);
+    if (lane == 0) sr[w] = t;
+    float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
+    int q = p0 + w;
+    for (; q + 3 * kMW < p1; q += 4 * kMW) {
+      const float* s0 = slot(q, hd);
+      const float* s1 = slot(q + kMW, hd);
+      const float* s2 = slot(q + 2 * kMW, hd);
+      const float* s3 = slot(q + 3 * kMW, hd);
+      const float4 v0 = ld4(s0 + lane * 4), v1 = ld4(s1 + lane * 4), v2 = ld4(s2 + lane * 4), v3 = ld4(s3 + lane * 4);
+      a0 = fma4(expf(s0[C] - M), v0, a0);
+      a1 = fma4(expf(s1[C] - M), v1, a1);
+      a2 = fma4(expf(s2[C] - M), v2, a2);
+      a3 = fma4(expf(s3[C] - M), v3, a3);
+    }
+    for (; q < p1; q += kMW) a0 = fma4(expf(slot(q, hd)[C] - M), ld4(slot(q, hd) + lane * 4), a0);
+    red[w][lane] = add4(add4(a0, a1), add4(a2, a3));
+    __syncthreads();
+    if (w == 0) {
+      float l = 0.f;
+      for (int k = 0; k < kMW; ++k) l += sr[k];
+      float4 acc = red[0][lane];
+      for (int k = 1; k < kMW; ++k) acc = add4(acc, red[k][lane]);
+      const float invl = 1.f / (l + eps);
+      st4(agg_out + (i * heads + hd) * C + lane * 4, mul4(acc, invl));
+      if (lane == 0) {
+        m_out[i * heads + hd] = M;
+        invl_out[i * heads + hd] = invl;
+      }
+    }
+    __syncthreads();  // sr / red are the next head's
+  }
 }
 
-// hub sources of k_bwd_g: pieces summed in piece order
+// hub sources of k_bwd_g: the pieces' [acc^h (C) x H | ds] summed, waves in order
 template <int C, int H>
-__global__ void __launch_bounds__(256) k_bwd_g_merge(const int32_t* __restrict__ hub_row,
-                                                     const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
-                                                     const float* __restrict__ partial, float* __restrict__ acc_out,
-                                                     float* __restrict__ S, int64_t lds) {
-  const int lane = threadIdx.x & 63;
-  const int64_t hb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (hb >= n_hubs) return;
+__global__ void __launch_bounds__(64 * kMW) k_bwd_g_merge_wg(const int32_t* __restrict__ hub_row,
+                                                             const int32_t* __restrict__ hub_ptr,
+                                                             const float* __restrict__ partial,
+                                                             float* __restrict__ acc_out, float* __restrict__ S,
+                                                             int64_t lds) {
+  static_assert(C == 256, "one float4 per lane");
+  __shared__ float4 red[kMW][H + 1][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t hb = blockIdx.x;
   const int64_t j = hub_row[hb];
-  float4 acc[H];
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  float4 a[H], b[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) acc[h] = f4(0.f);
-  float4 d = f4(0.f);
-  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) {
-    const float* sp = partial + (int64_t)q * (H * C + 4);
+  for (int h = 0; h < H; ++h) a[h] = b[h] = f4(0.f);
+  float4 da = f4(0.f), db = f4(0.f);
+  int q = p0 + w;
+  for (; q + kMW < p1; q += 2 * kMW) {
+    const float* s0 = partial + (int64_t)q * (H * C + 4);
+    const float* s1 = partial + (int64_t)(q + kMW) * (H * C + 4);
+    float4 v0[H], v1[H];
 #pragma unroll
-    for (int h = 0; h < H; ++h) acc[h] = add4(acc[h], ld4(sp + h * C + lane * 4));
-    d = add4(d, ld4(sp + H * C));
+    for (int h = 0; h < H; ++h) {
+      v0[h] = ld4(s0 + h * C + lane * 4);
+      v1[h] = ld4(s1 + h * C + lane * 4);
+    }
+    const float4 d0 = ld4(s0 + H * C), d1 = ld4(s1 + H * C);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      a[h] = add4(a[h], v0[h]);
+      b[h] = add4(b[h], v1[h]);
+    }
+    da = add4(da, d0);
+    db = add4(db, d1);
+  }
+  if (q < p1) {
+    const float* s0 = partial + (int64_t)q * (H * C + 4);
+#pragma unroll
+    for (int h = 0; h < H; ++h) a[h] = add4(a[h], ld4(s0 + h * C + lane * 4));
+    da = add4(da, ld4(s0 + H * C));
   }
 #pragma unroll
-  for (int h = 0; h < H; ++h) st4(acc_out + (j * H + h) * C + lane * 4, acc[h]);
-  const float ds[4] = {d.x, d.y, d.z, d.w};
-  if (lane < H && S != nullptr) S[j * lds + lane] = ds[lane];
+  for (int h = 0; h < H; ++h) red[w][h][lane] = add4(a[h], b[h]);
+  red[w][H][lane] = add4(da, db);
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int h = 0; h <= H; ++h) {
+    float4 acc = red[0][h][lane];
+    for (int k = 1; k < kMW; ++k) acc = add4(acc, red[k][h][lane]);
+    if (h < H) {
+      st4(acc_out + (j * H + h) * C + lane * 4, acc);
+    } else if (S != nullptr && lane < H) {
+      const float ds[4] = {acc.x, acc.y, acc.z, acc.w};
+      S[j * lds + lane] = ds[lane];
+    }
+  }
+}
+
+// hub sources of k_xgat_dz: ds_src = the pieces' partial sums, threads over pieces, then the
+// lanes (tree) and the waves (in order)
+template <int H>
+__global__ void __launch_bounds__(64 * kMW) k_xgat_dz_merge_wg(const int32_t* __restrict__ hub_row,
+                                                               const int32_t* __restrict__ hub_ptr,
+                                                               const float* __restrict__ partial, float* __restrict__ S,
+                                                               int64_t lds) {
+  __shared__ float sr[kMW][H];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t hb = blockIdx.x;
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  float x[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) x[h] = 0.f;
+  for (int q = p0 + tid; q < p1; q += 64 * kMW) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) x[h] += partial[(int64_t)q * H + h];
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    x[h] = wave_sum(x[h]);
+    if (lane == 0) sr[w][h] = x[h];
+  }
+  __syncthreads();
+  if (tid < H) {
+    float v = 0.f;
+    for (int k = 0; k < kMW; ++k) v += sr[k][tid];
+    S[(int64_t)hub_row[hb] * lds + tid] = v;
+  }
 }
 
 // dx_i += sum_h ds_dst_i^h A_dst[h] over the destination rows (S[i][H + h] = ds_dst)
@@ -2444,7 +2564,10 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)K;
-  return launch_fwd_merge(256, hub_row, hub_ptr, n_hubs, H, partial, 1e-16f, m, invl, agg, st);
+  if (n_hubs > 0)
+    hipLaunchKernelGGL(k_fwd_merge_wg, dim3((unsigned)n_hubs), dim3(64 * kMW), 0, st, hub_row, hub_ptr, H, partial,
+                       1e-16f, m, invl, agg);
+  return hipGetLastError();
 }
 
 hipError_t xgat_bwd_pro(const float* gt, const float* agg, const float* s_dst, const float* m, const float* invl,
@@ -2489,8 +2612,8 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                                    row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
                                    slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz));
   if (n_hubs > 0)
-    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge<256, HH>), dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st,
-                                   hub_row, hub_ptr, n_hubs, partial, acc, S, lds));
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs), dim3(64 * kMW), 0, st, hub_row,
+                                   hub_ptr, partial, acc, S, lds));
   (void)C;
   return hipGetLastError();
 }
@@ -2524,8 +2647,8 @@ hipError_t xgat_bwd_dz(const ItemsArg& it, const int32_t* row, const int32_t* cs
                                    reinterpret_cast<const float4*>(nstate), slope, p, inv_keep, seed, seed_in, dz, S,
                                    lds, partial));
   if (n_hubs > 0)
-    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz_merge<HH>), dim3((unsigned)((n_hubs * HH + 255) / 256)), dim3(256), 0,
-                                   st, hub_row, hub_ptr, n_hubs, partial, S, lds));
+    PPGAT_XH(H, hipLaunchKernelGGL((k_xgat_dz_merge_wg<HH>), dim3((unsigned)n_hubs), dim3(64 * kMW), 0, st, hub_row,
+                                   hub_ptr, partial, S, lds));
   return hipGetLastError();
 }
 

@@ -36,17 +36,18 @@ def build_ii_knn(embeddings: torch.Tensor, k: int = 20, min_similarity: float = 
     e = embeddings.to(torch.float32).contiguous()
     n = e.size(0)
     dev = e.device
+    d = e.size(1)
+    n_p, d_p = -(-n // 128) * 128, -(-max(d, 1) // 32) * 32
+    exp = torch.zeros(n_p, d_p, dtype=torch.float32, device=dev)  # padded rows/columns are exact zeros
     en = e / (torch.linalg.vector_norm(e, dim=1, keepdim=True) + 1e-8)
     n2 = torch.linalg.vector_norm(en, dim=1, keepdim=True)
-    ex = en / torch.where(n2 == 0, torch.ones_like(n2), n2)  # sklearn.preprocessing.normalize
+    # sklearn.preprocessing.normalize, written straight into the padded operand (no third copy)
+    torch.div(en, torch.where(n2 == 0, torch.ones_like(n2), n2), out=exp[:n, :d])
+    del en, n2
     idx = torch.empty(n, k, dtype=torch.int32, device=dev)
     sim = torch.empty(n, k, dtype=torch.float32, device=dev)
     cnt = torch.empty(n, dtype=torch.int32, device=dev)
     st = _lib.stream_handle(dev)
-    d = ex.size(1)
-    n_p, d_p = -(-n // 128) * 128, -(-max(d, 1) // 32) * 32
-    exp = torch.zeros(n_p, d_p, dtype=torch.float32, device=dev)  # padded rows/columns are exact zeros
-    exp[:n, :d] = ex
     for q0 in range(0, n, block_rows):
         q1 = min(q0 + block_rows, n)
         S = hip_ops.gemm_nn(exp[q0:q1], exp, 1, n_p)  # [q, n_p]: the similarity block, columns >= n unused
