@@ -735,7 +735,8 @@ class _HaloLayerX(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_own, x_halo_items, weight, att_src, att_dst, bias, hg: "HaloGraph", comm: "Comm", stages,
                 heads: int, C: int, slope: float, p: float, seed: int, rows_in: Optional[HaloRows] = None,
-                rows_out: Optional[HaloRows] = None):
+                rows_out: Optional[HaloRows] = None, link_in: Optional[dict] = None,
+                link_out: Optional[dict] = None):
         from .hip_ops import xgat_forward
         x_own = x_own.contiguous()
         if rows_in is None:
@@ -764,6 +765,11 @@ class _HaloLayerX(torch.autograd.Function):
         out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed,
                                       phases=_halo_phases(hg, rows_in, rows_out), out=dest, scores=scores)
         rows_in.wait_all()
+        # links between consecutive halo layers (_halo_xgat_backward_deferred_d): this layer's
+        # state for the layer above, whose backward starts this layer's exchanges early
+        if link_out is not None:
+            link_out["saved"] = ctx.saved
+        ctx.link_in, ctx.link_out = link_in, link_out
         ctx.hg, ctx.comm, ctx.stages = hg, comm, stages
         ctx.plans = [rows_in.plan(c) for c in ("u", "i") if c not in rows_in.local]
         ctx.att_shapes = (att_src.shape, att_dst.shape)
@@ -776,14 +782,18 @@ class _HaloLayerX(torch.autograd.Function):
         hg, comm, st, plans = ctx.hg, ctx.comm, ctx.stages, ctx.plans
         dev = g.device
         if source_homed_backward(hg):
+            pre = ctx.link_out.pop("pre", None) if ctx.link_out is not None else None
             dx, dW, datt_src, datt_dst, dbias = _halo_xgat_backward(ctx.saved, g, hg, comm, st,
-                                                                    ctx.needs_input_grad[5])
+                                                                    ctx.needs_input_grad[5], pre=pre,
+                                                                    link_in=ctx.link_in)
             ctx.saved = None
+            if ctx.link_out is not None:
+                ctx.link_out.clear()
             # every input gradient of an own row is complete here (its out-edges live on this
             # rank); the halo rows' -- incl. the first layer's locally computed halo items -- are
             # their owners' business
             return (dx, None, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                    None, None, None, None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None, None, None, None, None)
         pending = {}
 
         def a2a_back(dx_halo):
@@ -816,7 +826,7 @@ class _HaloLayerX(torch.autograd.Function):
             st.return_add(dx_own, ret, plan.ret_ptr, plan.ret_pos)
         d_items = dx[hg.n_own + hg.n_halo_u:] if ctx.local_items else None
         return (dx_own, d_items, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def source_homed_backward(hg: "HaloGraph") -> bool:
@@ -827,7 +837,7 @@ def source_homed_backward(hg: "HaloGraph") -> bool:
 
 
 def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Comm", stages,
-                        want_bias_grad: bool):
+                        want_bias_grad: bool, pre=None, link_in: Optional[dict] = None):
     """Backward of the multi-head halo layer with every edge processed at its SOURCE's owner.
 
     The forward ran each edge at its destination's owner (the aggregation needs a destination's
@@ -863,10 +873,10 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
     n0, R, sv = hg.n_own, hg.R, hg.src_views
     E = sv.n_edges
     g = g.contiguous()
+    if os.environ.get("PPGAT_XGAT_GATHER") != "g":
+        return _halo_xgat_backward_deferred_d(saved, g, hg, comm, stages, want_bias_grad, pre, link_in)
     gtab = HaloRows(hg, comm, stages, C, g)
     gtab.x[:n0].copy_(g)
-    if os.environ.get("PPGAT_XGAT_GATHER") != "g":
-        return _halo_xgat_backward_deferred_d(saved, g, hg, comm, stages, want_bias_grad, gtab)
     for cls in ("u", "i"):
         gtab.start(cls, g)
     # 1. destination state of the own rows
@@ -948,13 +958,45 @@ def _partials_home(hg: "HaloGraph", comm: "Comm", stages, part: torch.Tensor) ->
     return own
 
 
+def _bwd_tables(saved: dict, hg: "HaloGraph", comm: "Comm", stages, g_width: int, dev):
+    """The backward's row tables of one multi-head halo layer: g [R, C] (own rows to be filled)
+    and the softmax state nstate {s_dst, m, inv_l, .} [R, 4H] (own rows filled here)."""
+    lib = _lib.load()
+    s_dst, m, inv_l = saved["s_dst"], saved["m"], saved["inv_l"]
+    H = saved["meta"][0]
+    n0 = hg.n_own
+    nst = torch.empty(max(n0, 1), 4 * H, dtype=torch.float32, device=dev)
+    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H, nst.data_ptr(),
+                                     _lib.stream_handle(dev)), "xgat_nstate")
+    nst = nst[:n0]
+    ntab = HaloRows(hg, comm, stages, 4 * H, nst)
+    ntab.x[:n0].copy_(nst)
+    gtab = HaloRows(hg, comm, stages, g_width, nst)
+    return gtab, ntab, nst
+
+
+def _bwd_start(hg: "HaloGraph", gtab: "HaloRows", ntab: "HaloRows", nst, g):
+    """Both tables of the smaller halo class first (the same order on every rank: it is decided
+    from the global segment sizes), so the phase that reads it starts while the other class is
+    still on the wire."""
+    for cls in _small_class_first(hg):
+        ntab.start(cls, nst)
+        gtab.start(cls, g)
+
+
 def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm", stages, want_bias_grad: bool,
-                                   gtab: "HaloRows"):
+                                   pre=None, link_in: Optional[dict] = None):
     """_halo_xgat_backward with D deferred (the single-GPU default): no gt GEMM
     and no prologue.  nstate {s_dst, m, inv_l, .} of the own rows goes out with g at once; the
     edge pass writes dalpha and beta dalpha per edge; D_i = sum_j beta dalpha is summed per table
     row, the halo rows' partials go home and the completed D of the own rows back out (H floats
-    per row each way); then the dz pass, ds_dst (partials home again) and the own rows' GEMMs."""
+    per row each way); then the dz pass, ds_dst (partials home again) and the own rows' GEMMs.
+
+    ``pre``: the tables with their exchanges already started by the layer above (its backward
+    wrote this layer's g into the table and started it before its own weight-gradient GEMMs);
+    ``link_in``: the link to the layer below -- when it is a halo layer too, this layer's input
+    gradient is written straight into the layer below's g table and its exchanges start before
+    this layer's weight gradients, so they run beside them."""
     from . import hip_ops as O
     lib = _lib.load()
     x, W, A = saved["x"], saved["W"], saved["A"]
@@ -965,19 +1007,17 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     n0, R, sv = hg.n_own, hg.R, hg.src_views
     E = sv.n_edges
     seed_buf = saved["seed_buf"]
-    nst = torch.empty(max(n0, 1), 4 * H, dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H, nst.data_ptr(),
-                                     st), "xgat_nstate")
-    nst = nst[:n0]
-    ntab = HaloRows(hg, comm, stages, 4 * H, nst)
-    ntab.x[:n0].copy_(nst)
-    # both tables of the smaller halo class first (the same order on every rank: it is decided
-    # from the global segment sizes), so the phase that reads it starts while the other class
-    # is still on the wire
     order = _small_class_first(hg)
-    for cls in order:
-        ntab.start(cls, nst)
-        gtab.start(cls, g)
+    if pre is not None:
+        # started by the layer above from its dx -- which is g: HaloPyGGAT links a layer only to
+        # the one consumer of its output (every rank takes this branch alike: the collectives match)
+        gtab, ntab, nst = pre
+        if gtab.x.data_ptr() != g.data_ptr():
+            gtab.x[:n0].copy_(g)
+    else:
+        gtab, ntab, nst = _bwd_tables(saved, hg, comm, stages, C, dev)
+        gtab.x[:n0].copy_(g)
+        _bwd_start(hg, gtab, ntab, nst, g)
     hs = O.gemm_nn(x[:n0], W, 1, H * C, alpha=1.0 / H)
     acc = torch.empty(max(n0, 1), H * C, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
@@ -1033,11 +1073,22 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     S = S[:n0]
     S[:, H:].copy_(_partials_home(hg, comm, stages, dsd))
     del dsd
-    dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
-        torch.zeros(0, K, dtype=torch.float32, device=dev)
+    # the weight-gradient bound's all_reduce now, before any exchange of the layer below is
+    # started on the communication stream: no two collectives of one communicator in flight on
+    # two streams (the comm stream's start waits for this stream's work so far)
+    xbits = _source_colmax_bits(x[:n0], hg, comm)
+    below = link_in.get("saved") if link_in is not None else None
+    if below is not None and n0:
+        # the layer below's g = this dx: straight into its table, its exchanges started now
+        gtab1, ntab1, nst1 = _bwd_tables(below, hg, comm, stages, K, dev)
+        dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K)), out=gtab1.x[:n0])
+        _bwd_start(hg, gtab1, ntab1, nst1, dx)
+        link_in["pre"] = (gtab1, ntab1, nst1)
+    else:
+        dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
+            torch.zeros(0, K, dtype=torch.float32, device=dev)
     del acc
-    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0],
-                                xbits=_source_colmax_bits(x[:n0], hg, comm))
+    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0], xbits=xbits)
 
 
 class _ShardedBase(torch.nn.Module):
@@ -1131,7 +1182,7 @@ class HaloPyGGAT(_ShardedBase):
     def forward(self, item_feats):
         from .hip_ops import xgat_att_proj
         hg = self.dg
-        rows = None
+        rows = link_in = None
         if self._x_path(0):
             # the first layer's halo user rows are parameters: their exchange starts before
             # the item projections (the own and the halo items' rows) are computed
@@ -1152,16 +1203,17 @@ class HaloPyGGAT(_ShardedBase):
                     # aggregate-then-transform on the local rows: no halo projection; the next
                     # layer's halo rows start moving as this layer's phases finish, and the
                     # return of the halo gradients overlaps the own rows' backward
-                    nxt = None
+                    nxt = link_out = None
                     if li + 1 < len(self.convs) and self._x_path(li + 1):
                         nxt = HaloRows(hg, self.comm, self.stages, conv.out_channels, x)
                         cn = self.convs[li + 1]
                         nxt.enable_scores(xgat_att_proj(cn.lin.weight, cn.att_src, cn.att_dst, cn.heads,
                                                         cn.out_channels))
+                        link_out = {}
                     x = _HaloLayerX.apply(x, xh, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg,
                                           self.comm, self.stages, conv.heads, conv.out_channels,
-                                          float(conv.negative_slope), p, seed, rows, nxt)
-                    rows = nxt
+                                          float(conv.negative_slope), p, seed, rows, nxt, link_in, link_out)
+                    rows, link_in = nxt, link_out
                     continue
                 h = self.stages.linear(halo_exchange(x, hg, self.comm, self.stages, xh), conv.lin.weight, None)
             else:
