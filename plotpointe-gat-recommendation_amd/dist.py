@@ -1018,13 +1018,19 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
         gtab, ntab, nst = _bwd_tables(saved, hg, comm, stages, C, dev)
         gtab.x[:n0].copy_(g)
         _bwd_start(hg, gtab, ntab, nst, g)
-    hs = O.gemm_nn(x[:n0], W, 1, H * C, alpha=1.0 / H)
+    hs = torch.empty(max(n0, 1), H * C, dtype=torch.float32, device=dev)
     acc = torch.empty(max(n0, 1), H * C, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
     pdal = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
-    by_need = {"i": (hg.src_sched_u, 0, "i"), "u": (hg.src_sched_i, hg.n_own_u, "u")}  # user sources read items
+    nu = hg.n_own_u
+    by_need = {"i": (hg.src_sched_u, 0, "i"), "u": (hg.src_sched_i, nu, "u")}  # user sources read items
     phases = [by_need[c] for c in order] if hg.bipartite else [(sv.bwd_sched, 0, None)]
     for sched, base, need in phases:  # dalpha (into dz) and beta dalpha per edge, acc per own source
+        # hs = x W^T / H of this phase's sources, while its class of halo rows is on the wire
+        # (per row the GEMM gives the same bits whatever the row range)
+        r0, r1 = ((0, nu) if base == 0 else (nu, n0)) if need is not None else (0, n0)
+        if r1 > r0:
+            O.gemm_nn(x[r0:r1], W, 1, H * C, alpha=1.0 / H, out=hs[r0:r1])
         for tab in (gtab, ntab):
             tab.wait_all() if need is None else tab.wait(need)
         nbytes = ctypes.c_size_t(0)
