@@ -999,8 +999,7 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     this layer's weight gradients, so they run beside them."""
     from . import hip_ops as O
     lib = _lib.load()
-    x, W, A = saved["x"], saved["W"], saved["A"]
-    s_src, s_dst, m, inv_l = saved["s_src"], saved["s_dst"], saved["m"], saved["inv_l"]
+    x, W, A, s_src = saved["x"], saved["W"], saved["A"], saved["s_src"]
     H, C, K, slope, p, seed, has_bias = saved["meta"]
     dev = x.device
     st = _lib.stream_handle(dev)
@@ -1027,7 +1026,7 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     phases = [by_need[c] for c in order] if hg.bipartite else [(sv.bwd_sched, 0, None)]
     for sched, base, need in phases:  # dalpha (into dz) and beta dalpha per edge, acc per own source
         # hs = x W^T / H of this phase's sources, while its class of halo rows is on the wire
-        # (per row the GEMM gives the same bits whatever the row range)
+        # (on the large-M fp16 kernel each row's result depends on that row alone)
         r0, r1 = ((0, nu) if base == 0 else (nu, n0)) if need is not None else (0, n0)
         if r1 > r0:
             O.gemm_nn(x[r0:r1], W, 1, H * C, alpha=1.0 / H, out=hs[r0:r1])
