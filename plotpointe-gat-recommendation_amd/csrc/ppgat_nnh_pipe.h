@@ -57,7 +57,11 @@ __device__ __forceinline__ void wait_vm() {
 // BD: B fragments read BD MFMA steps ahead (1: the step before, as k_gemm_nnh2; 2: two steps,
 // eight more VGPRs, for LDS latency under eight waves of reads).  PRIO: waves 4-7 (the second-
 // dispatched half, the issue-arbitration loser) at s_setprio 1 for the whole loop.
-template <int NT, int BD = 1, bool PRIO = false, class LoadX>
+// LAB (diagnostics only, PPGAT_NNH2_LAB with PPGAT_NNH2=3; results wrong), bits: 1 = no X loads
+// after the first two chunks, 2 = no B DMA after the first two chunks, 16 = no B fragment reads
+// inside a chunk's MFMA steps (the first BD per chunk only), 32 = no preparation of the next
+// chunk (its fragments reused)
+template <int NT, int BD = 1, bool PRIO = false, int LAB = 0, class LoadX>
 __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int chunks, const LoadX& loadx,
                                           split::f32x16 (&acc)[NT], int& erow, float* sFw, int wv, int lane) {
   static_assert(BD == 1 || BD == 2, "B read depth");
@@ -137,8 +141,8 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
                   split::u32x4 (&fxn)[2][2], auto has_next) {
     constexpr bool NEXT = decltype(has_next)::value;
     const bool ahead = c + 2 < chunks;
-    if (ahead) issue(c + 2);
-    loadx(ahead ? c + 2 : chunks - 1, xl);  // the last two chunks re-read chunk chunks - 1 (same waits)
+    if (ahead && !(LAB & 2)) issue(c + 2);
+    if (!(LAB & 1)) loadx(ahead ? c + 2 : chunks - 1, xl);  // the last two chunks re-read chunk chunks - 1
     const uint16_t* sb = sB + (c % 3) * I::ELEMS;
     auto read_b = [&](int i, split::u32x4 (&f)[2]) {
       const int off = (32 * (i % NT) + r) * LDK + 16 * (i / NT) + 8 * hf;
@@ -151,9 +155,9 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
 #pragma unroll
     for (int i = 0; i < STEPS; ++i) {
       const int u = i / NT, t = i % NT;
-      if (i + BD < STEPS) read_b(i + BD, fb[(i + BD) % (BD + 1)]);
-      acc[t] = split::mfma32_h3(fxc[u], fb[i % (BD + 1)], acc[t]);
-      if constexpr (NEXT) {
+      if (!(LAB & 16) && i + BD < STEPS) read_b(i + BD, fb[(i + BD) % (BD + 1)]);
+      acc[t] = split::mfma32_h3(fxc[u], fb[(LAB & 16) ? 0 : i % (BD + 1)], acc[t]);
+      if constexpr (NEXT && !(LAB & 32)) {
         if (i >= STEPS / 2) {
 #pragma unroll
           for (int k = 0; k < PPS; ++k) prep((i - STEPS / 2) * PPS + k, xn, fxn);
@@ -167,10 +171,12 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
       __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (NEXT) commit();
+    if constexpr (NEXT && !(LAB & 32)) commit();
     // DMA(c + 1) has landed (issued after it: X(c + 1), DMA(c + 2) if any, X(c + 2)) and every
     // wave is done with buffer c % 3 before DMA(c + 3) (issued in chunk c + 1) overwrites it
-    if (ahead) {
+    if (LAB) {
+      wait_vm<0>();
+    } else if (ahead) {
       if (full) wait_vm<4 + ND + 4>(); else wait_vm<4 + ND - 1 + 4>();
     } else {
       wait_vm<4 + 4>();

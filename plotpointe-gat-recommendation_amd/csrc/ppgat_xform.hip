@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
 // k_gemm_nnh3: k_gemm_nnh2's pipeline with the next chunk prepared inside the current chunk's
 // MFMA sequence (ppgat_nnh_pipe.h: nnh3_loop), same products in the same order as k_gemm_nnh.
 // ---------------------------------------------------------------------------
-template <int NT, bool RK, int BD = 1, bool PRIO = false>
+template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
@@ -911,7 +911,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* _
   };
   f32x16 acc[NT];
   int erow = 0;
-  nnh3_loop<NT, BD, PRIO>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv, lane);
+  nnh3_loop<NT, BD, PRIO, LAB>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv,
+                               lane);
   float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
   split::row_unscale(erow, sF[wv], r, hf, fr);
   const int64_t row0 = rb * kPBM + wv * 32;
@@ -952,7 +953,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* _
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int64_t row = row0 + (q & 3) + 8 * (q >> 2) + 4 * hf;
-        if (row < M) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
+        if (row < M && (!(LAB & 4) || acc[0][q] != acc[0][q])) a.Y[row * a.ldy + col] = fmaf(acc[t][q] * fr[q], ic, bv);
       }
     }
   }
@@ -2315,6 +2316,13 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       if (e != hipSuccess) return e;
       if (nnh_pipeline_variant() >= 3 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh3 runs chunk pairs
         const int v = nnh_pipeline_variant();
+        if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {  // diagnostics (results wrong)
+#define PPGAT_LAB3(L) \
+  if (lab == L) hipLaunchKernelGGL((k_gemm_nnh3<8, false, 1, false, L>), dim3(grid), dim3(512), 0, st, a, img, ecol)
+          PPGAT_LAB3(1); PPGAT_LAB3(3); PPGAT_LAB3(7); PPGAT_LAB3(23); PPGAT_LAB3(39); PPGAT_LAB3(55);
+#undef PPGAT_LAB3
+          return hipGetLastError();
+        }
 #define PPGAT_NNH3(BD, PR)                                                                              \
   do {                                                                                                  \
     if (nv > 0) {                                                                                       \
