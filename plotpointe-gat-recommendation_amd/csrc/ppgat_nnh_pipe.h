@@ -61,9 +61,16 @@ __device__ __forceinline__ void wait_vm() {
 // after the first two chunks, 2 = no B DMA after the first two chunks, 16 = no B fragment reads
 // inside a chunk's MFMA steps (the first BD per chunk only), 32 = no preparation of the next
 // chunk (its fragments reused)
-template <int NT, int BD = 1, bool PRIO = false, int LAB = 0, class LoadX>
+// XT: loadx(c, x) delivers the chunk COALESCED -- lane l holds floats [4 (l & 7), +4) of rows
+// (l >> 3) + 8 j, j = 0..3 (each load instruction reads 8 whole 128-B row segments, not 32-B
+// pieces of 32 rows) -- and the preparation turns it into the fragment layout through this
+// wave's LDS scratch sXw [32 rows][36 floats] (4 ds_write_b128 + 4 ds_read_b128 per chunk,
+// conflict-free with the 36-float row stride).  The same values in the same fragment slots: the
+// products are bitwise those of the direct layout.
+template <int NT, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false, class LoadX>
 __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int chunks, const LoadX& loadx,
-                                          split::f32x16 (&acc)[NT], int& erow, float* sFw, int wv, int lane) {
+                                          split::f32x16 (&acc)[NT], int& erow, float* sFw, int wv, int lane,
+                                          float* sXw = nullptr) {
   static_assert(BD == 1 || BD == 2, "B read depth");
   using I = NnhImg<NT>;
   constexpr int LDK = I::LDK, PART = I::PART, NI = I::BYTES / 1024;
@@ -96,10 +103,32 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
   // sink the split past the MFMAs to its use in the next chunk)
   auto pin = [](split::u32x4 (&f)[2]) { asm volatile("" : "+v"(f[0]), "+v"(f[1])); };
   // phase ph of preparing the chunk in xn into fragments fxn (phases 0..7; 7 is empty)
-  auto prep = [&](int ph, const float4 (&xn)[4], split::u32x4 (&fxn)[2][2]) {
+  auto prep = [&](int ph, float4 (&xn)[4], split::u32x4 (&fxn)[2][2]) {
     switch (ph) {
-      case 0: pmx = fmaxf(fmaxf(0.f, split::absmax4(xn[0])), split::absmax4(xn[1])); break;
-      case 1: pmx = fmaxf(fmaxf(pmx, split::absmax4(xn[2])), split::absmax4(xn[3])); break;
+      case 0:
+        if constexpr (XT) {  // coalesced rows -> fragment layout, in place
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            *reinterpret_cast<float4*>(sXw + ((lane >> 3) + 8 * j) * 36 + 4 * (lane & 7)) = xn[j];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int g = 0; g < 4; ++g) xn[g] = *reinterpret_cast<const float4*>(sXw + r * 36 + 8 * g + 4 * hf);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+          pmx = fmaxf(fmaxf(0.f, split::absmax4(xn[0])), split::absmax4(xn[1]));
+        }
+        break;
+      case 1:
+        if constexpr (XT)
+          pmx = fmaxf(fmaxf(fmaxf(fmaxf(0.f, split::absmax4(xn[0])), split::absmax4(xn[1])), split::absmax4(xn[2])),
+                      split::absmax4(xn[3]));
+        else
+          pmx = fmaxf(fmaxf(pmx, split::absmax4(xn[2])), split::absmax4(xn[3]));
+        break;
       case 2:
         pneed = split::row_scale_plan(pmx, erow, set, pen);
         ps = __builtin_ldexpf(1.f, pen);
@@ -137,7 +166,7 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
   __builtin_amdgcn_s_barrier();
 
   // chunk c from fxc; X(c + 2) -> xl (the set chunk c came from); chunk c + 1 prepared from xn
-  auto body = [&](const int c, float4 (&xl)[4], const float4 (&xn)[4], const split::u32x4 (&fxc)[2][2],
+  auto body = [&](const int c, float4 (&xl)[4], float4 (&xn)[4], const split::u32x4 (&fxc)[2][2],
                   split::u32x4 (&fxn)[2][2], auto has_next) {
     constexpr bool NEXT = decltype(has_next)::value;
     const bool ahead = c + 2 < chunks;

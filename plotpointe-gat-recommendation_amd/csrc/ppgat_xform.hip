@@ -886,13 +886,14 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
 // k_gemm_nnh3: k_gemm_nnh2's pipeline with the next chunk prepared inside the current chunk's
 // MFMA sequence (ppgat_nnh_pipe.h: nnh3_loop), same products in the same order as k_gemm_nnh.
 // ---------------------------------------------------------------------------
-template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0>
+template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
   constexpr int KC = I::KC;
   __shared__ __attribute__((aligned(16))) uint16_t sB[3 * I::ELEMS];
   __shared__ __attribute__((aligned(16))) float sF[8][32];  // per wave: a factor per row (rescale, epilogue)
+  __shared__ __attribute__((aligned(16))) float sX[XT ? 8 : 1][XT ? 32 * 36 : 4];  // per wave: X transpose (XT)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -905,14 +906,30 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* _
   const int chunks = a.K / KC;
   const int64_t m = rb * kPBM + wv * 32 + r;
   const float* xrow = a.X + (m < M ? m : M - 1) * a.ldx + 4 * hf;  // rows past M re-read row M-1 (never stored)
-  auto loadx = [&](int c, float4 (&x)[4]) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) x[g] = ld4(xrow + c * KC + 8 * g);
-  };
   f32x16 acc[NT];
   int erow = 0;
-  nnh3_loop<NT, BD, PRIO, LAB>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv,
-                               lane);
+  if constexpr (XT) {
+    // coalesced: lane l reads floats [4 (l & 7), +4) of rows (l >> 3) + 8 j of the wave's 32
+    const float* xr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t row = rb * kPBM + wv * 32 + (lane >> 3) + 8 * j;
+      xr[j] = a.X + (row < M ? row : M - 1) * a.ldx + 4 * (lane & 7);
+    }
+    auto loadx = [&](int c, float4 (&x)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = ld4(xr[j] + c * KC);
+    };
+    nnh3_loop<NT, BD, PRIO, LAB, true>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv],
+                                       wv, lane, sX[wv]);
+  } else {
+    auto loadx = [&](int c, float4 (&x)[4]) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) x[g] = ld4(xrow + c * KC + 8 * g);
+    };
+    nnh3_loop<NT, BD, PRIO, LAB>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv,
+                                 lane);
+  }
   float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
   split::row_unscale(erow, sF[wv], r, hf, fr);
   const int64_t row0 = rb * kPBM + wv * 32;
@@ -2264,7 +2281,8 @@ int nnh_pipeline_variant() {
   static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
     if (e && strcmp(e, "0") == 0) return 1;
-    if (e && (strcmp(e, "2") == 0 || strcmp(e, "4") == 0 || strcmp(e, "5") == 0)) return e[0] - '0';
+    if (e && (strcmp(e, "2") == 0 || strcmp(e, "4") == 0 || strcmp(e, "5") == 0 || strcmp(e, "6") == 0))
+      return e[0] - '0';
     return 3;
   }();
   return v;
@@ -2323,20 +2341,21 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
 #undef PPGAT_LAB3
           return hipGetLastError();
         }
-#define PPGAT_NNH3(BD, PR)                                                                              \
-  do {                                                                                                  \
-    if (nv > 0) {                                                                                       \
-      if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, true, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol); \
-      else hipLaunchKernelGGL((k_gemm_nnh3<4, true, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol);    \
-    } else if (w8) {                                                                                    \
-      hipLaunchKernelGGL((k_gemm_nnh3<8, false, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
-    } else {                                                                                            \
-      hipLaunchKernelGGL((k_gemm_nnh3<4, false, BD, PR>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
-    }                                                                                                   \
+#define PPGAT_NNH3(BD, PR, XT)                                                                                   \
+  do {                                                                                                           \
+    if (nv > 0) {                                                                                                \
+      if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, true, BD, PR, 0, XT>), dim3(grid), dim3(512), 0, st, a, img, ecol); \
+      else hipLaunchKernelGGL((k_gemm_nnh3<4, true, BD, PR, 0, XT>), dim3(grid), dim3(512), 0, st, a, img, ecol);    \
+    } else if (w8) {                                                                                             \
+      hipLaunchKernelGGL((k_gemm_nnh3<8, false, BD, PR, 0, XT>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
+    } else {                                                                                                     \
+      hipLaunchKernelGGL((k_gemm_nnh3<4, false, BD, PR, 0, XT>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
+    }                                                                                                            \
   } while (0)
-        if (v == 3) PPGAT_NNH3(1, false);
-        else if (v == 4) PPGAT_NNH3(2, false);
-        else PPGAT_NNH3(2, true);
+        if (v == 3) PPGAT_NNH3(1, false, false);
+        else if (v == 4) PPGAT_NNH3(2, false, false);
+        else if (v == 5) PPGAT_NNH3(2, true, false);
+        else PPGAT_NNH3(1, false, true);
 #undef PPGAT_NNH3
         return hipGetLastError();
       }
