@@ -2275,8 +2275,9 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
 // the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2, =3 k_gemm_nnh3 (and
 // k_fusion_fwdh3; the default: 2-3 % faster than k_gemm_nnh2 at config-5 shapes, bitwise equal,
 // profiles/r04/v8_gemm5_nnh*.log), =4 k_gemm_nnh3 with B read two steps ahead, =5 that with the
-// second half of the waves at s_setprio 1 (both within 1 % of 3: kept as measured negatives;
-// the fusion kernel runs its variant-3 loop for 3..5).  Read once per process.
+// second half of the waves at s_setprio 1, =6 X loaded as whole row segments and transposed
+// through LDS (all within 1-2 % of 3: kept as measured negatives, v8/v22_gemm5_nnh*.log; the
+// fusion kernel runs its variant-3 loop for 3..6).  Read once per process.
 int nnh_pipeline_variant() {
   static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
