@@ -686,6 +686,25 @@ class HaloRows:
             self.wait(cls)
 
 
+class _CatInto(torch.autograd.Function):
+    """torch.cat([a, b]) written into ``dest`` (a preallocated [len(a) + len(b), C] buffer: the own
+    rows of a halo layer's input table) and returned as that buffer, so the layer finds its own
+    rows in place (one copy of them, not two)."""
+
+    @staticmethod
+    def forward(ctx, dest, a, b):
+        na = a.size(0)
+        dest[:na].copy_(a)
+        dest[na:].copy_(b)
+        ctx.na = na
+        ctx.mark_dirty(dest)
+        return dest
+
+    @staticmethod
+    def backward(ctx, g):
+        return None, g[:ctx.na], g[ctx.na:]
+
+
 def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows]):
     """The phases of a halo layer's forward (hip_ops.XPhase).  On a bipartite graph the user
     destinations read item sources only and the item destinations user sources only, so each
@@ -1162,9 +1181,13 @@ class HaloPyGGAT(_ShardedBase):
     """PyGGAT with row-sharded users and items and halo all_to_all exchange (module doc).
     ``forward`` returns the own rows [n_own, C]: own users, then own items."""
 
-    def node_features(self, item_feats):
+    def node_features(self, item_feats, into: Optional[torch.Tensor] = None):
+        """[own users | own items] input rows; ``into``: write them there (the first halo layer's
+        table) instead of a new tensor."""
         f = self.stages.gather_rows(item_feats, self.dg.own_items)
         x_items = self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
+        if into is not None:
+            return _CatInto.apply(into, self.user_emb_local, x_items)
         return torch.cat([self.user_emb_local, x_items], 0)
 
     @staticmethod
@@ -1196,7 +1219,8 @@ class HaloPyGGAT(_ShardedBase):
             rows.enable_scores(xgat_att_proj(c0.lin.weight, c0.att_src, c0.att_dst, c0.heads, c0.out_channels))
             rows.score_rows(self.user_emb_local.detach(), 0, hg.n_own_u)  # sent beside the user rows
             rows.start("u", self.user_emb_local.detach())
-        x = self.node_features(item_feats)
+        # the own rows go straight into the first layer's table when it has one
+        x = self.node_features(item_feats, into=rows.x[:hg.n_own] if rows is not None else None)
         for li, conv in enumerate(self.convs):
             p = float(conv.dropout) if self.training else 0.0
             seed = self.layer_seed(conv)
