@@ -51,8 +51,6 @@ hipError_t launch_bwd_epi(const int32_t* rowptr, int64_t n, int heads, int C, co
                           int64_t blocks, hipStream_t st);
 hipError_t launch_col_reduce(const float* partial, int64_t rows, int cols, int split, float* out_a, float* out_b,
                              hipStream_t st);
-hipError_t launch_fwd_merge(int C, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, int heads,
-                            const float* partial, float eps, float* m, float* invl, float* agg, hipStream_t st);
 
 // graph preprocessing (ppgat_graph.hip)
 size_t csr_workspace_bytes(int64_t n_nodes, int64_t n_edges);

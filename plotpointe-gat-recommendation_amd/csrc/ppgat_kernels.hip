@@ -1115,16 +1115,6 @@ hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid
   return hipGetLastError();
 }
 
-// hub merge of per-head aggregates only (aggregate-then-transform forward, ppgat_xform.hip)
-hipError_t launch_fwd_merge(int C, const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, int heads,
-                            const float* partial, float eps, float* m, float* invl, float* agg, hipStream_t st) {
-  if (n_hubs <= 0) return hipSuccess;
-  PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st, hub_row,
-                                         hub_ptr, n_hubs, heads, partial, nullptr, kModePyg, eps, nullptr, m, invl,
-                                         agg));
-  return hipGetLastError();
-}
-
 hipError_t launch_bwd_pro(const float* go, const float* out, const float* agg, const float* bias, const float* sd,
                           const float* m, const float* invl, int64_t n, int heads, int C, float gscale,
                           float* nstate, float* bias_part, int64_t blocks, hipStream_t st) {

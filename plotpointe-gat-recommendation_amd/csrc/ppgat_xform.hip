@@ -1432,7 +1432,7 @@ struct XItems {
 // forward edge pass: one wave per destination item (CSR), the neighbour row x_j (K floats)
 // gathered ONCE per edge for all H heads: ax^h += p^h x_j with the online softmax per head.
 // K = 256: one float4 per lane, one edge at a time across the wave, 8 rows in flight.
-// Hub pieces leave [ax^h (K) | m | l | - -] per (item, head) for k_fwd_merge.
+// Hub pieces leave [ax^h (K) | m | l | - -] per (item, head) for k_fwd_merge_wg.
 // ---------------------------------------------------------------------------
 template <int K, int H>
 __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restrict__ col,
