@@ -224,3 +224,30 @@ def test_edges_symmetric_and_source_homed_views():
         assert np.array_equal(allids, np.arange(ei.size(1)))
         seen.append(len(allids))
     assert seen[0] == seen[1]
+
+
+def test_cat_into_keeps_the_table_off_the_graph():
+    """dist._CatInto writes [a | b] into a preallocated table slice and returns it: the result
+    aliases the table, the gradients split back to a and b, and the table itself does not join
+    the autograd graph (an in-place write to a tensor input would hang it there via CopySlices)."""
+    import importlib
+    D = importlib.import_module("plotpointe-gat-recommendation_amd.dist")
+    table = torch.zeros(9, 4, dtype=torch.float64)
+    a = torch.randn(3, 4, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(2, 4, dtype=torch.float64, requires_grad=True)
+    y = D._CatInto.apply([table[:5]], a, b * 1.0)
+    assert y.data_ptr() == table.data_ptr() and torch.equal(table[:5], torch.cat([a, b]).detach())
+    assert not table.requires_grad and table.grad_fn is None
+    w = torch.arange(20, dtype=torch.float64).view(5, 4)
+    (y * w).sum().backward()
+    assert torch.equal(a.grad, w[:3]) and torch.equal(b.grad, w[3:])
+
+
+def test_small_class_first_is_global():
+    """The backward's exchange order comes from the global segment sizes only (every rank must
+    issue its all_to_alls in the same order)."""
+    import importlib
+    from types import SimpleNamespace
+    D = importlib.import_module("plotpointe-gat-recommendation_amd.dist")
+    assert D._small_class_first(SimpleNamespace(n_nodes=15, n_users=10)) == ("i", "u")
+    assert D._small_class_first(SimpleNamespace(n_nodes=15, n_users=5)) == ("u", "i")
