@@ -138,6 +138,18 @@ def build_model(cfg: Config, n_users: int, n_items: int, feat_dim: int):
     return m
 
 
+def epoch_step(model, opt, item_feats, edge_index, n_users: int, u, i, j, loss: str = "bpr"):
+    """One epoch's optimisation step on one GPU (train_gat_custom.py:349-362, identical
+    train_gat_pyg.py:307-323): the training forward over the whole graph, the BPR/BCE loss of
+    the epoch's sampled triples, zero_grad, backward, ``opt.step()``.  Returns the loss."""
+    Z = model(item_feats, edge_index)
+    lo = model_mod.bpr_loss(Z, n_users, u, i, j, loss)
+    opt.zero_grad()
+    lo.backward()
+    opt.step()
+    return lo
+
+
 class _GlobalRows(torch.nn.Module):
     """A row-sharded model seen as the single-GPU one by eval_sampled / export: forward returns
     every node's rows on every rank (an all_gather; evaluation only, not the training path)."""
@@ -280,12 +292,7 @@ def main(argv=None):
             i = torch.from_numpy(i_arr).long().to(device)
             j = torch.from_numpy(j_arr).long().to(device)
         if sharded is None:
-            Z = model(item_feats, edge_index)
-            loss = model_mod.bpr_loss(Z, n_users, u, i, j, cfg.loss)
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-            loss_val = float(loss.item())
+            loss_val = float(epoch_step(model, opt, item_feats, edge_index, n_users, u, i, j, cfg.loss).item())
         else:
             # each rank: its own users' triples (the sum over ranks is the reference's mean),
             # dense gradients all-reduced, user rows updated by their owner

@@ -24,11 +24,17 @@ reference's outputs), written as .npz / .json next to this script:
                      export forward, per-epoch loss / val metrics, test metrics; run with
                      the default torch thread count and 1, 2, 4 threads to record the
                      reference's own run-to-run envelope (per-epoch drift, top-20 agreement).
+  onestep_cfg1.*     the same main() run's full state (params, Adam moments, both RNG
+                     streams) after 0, 1, 2, 5, 8, 12, 16, 19 steps, each replayed one epoch
+                     by the reference at threads 8/1/2/4 and in float64: the chaos-free
+                     one-step spread the GPU test holds our epoch to.
 
     python tests/golden/make_golden.py trajectory    # only the trajectory fixture
+    python tests/golden/make_golden.py onestep       # only the one-step fixture
 """
 from __future__ import annotations
 
+import copy
 import importlib.util
 import json
 import random
@@ -303,7 +309,7 @@ def knn_case():
     print(f"knn: {m.nnz} edges over {n} items")
 
 
-def trajectory_case(ref, epochs: int = 20):
+def trajectory_case(ref, epochs: int = 20, capture=None):
     """The reference trainer's own ``main()`` (train_gat_custom.py:227-400) end to end on the
     config-1 synthetic inputs: ``epochs`` epochs of one 200k-triple BPR batch + Adam, eval each
     epoch (``--eval-neg-k 100``), best-val checkpoint, reload, test eval, metrics JSON.  GCS is
@@ -353,14 +359,21 @@ def trajectory_case(ref, epochs: int = 20):
         def bucket(self, name):
             return _Bucket()
 
-    rec = {"val": [], "loss": [], "triples": None, "items": []}
+    rec = {"val": [], "loss": [], "triples": None, "items": [], "model": None, "opt": None, "n_sample": 0}
     base_gat, base_eval, base_sample = ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch
+    base_adam = torch.optim.Adam
+
+    class _RecAdam(base_adam):  # main()'s optimizer, recorded so its state can be captured
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            rec["opt"] = self
 
     class _NoDropGAT(base_gat):
         def __init__(self, *a, **k):
             super().__init__(*a, **k)
             for layer in self.layers:
                 layer.drop.p = 0.0
+            rec["model"] = self
 
         def forward(self, item_feats, edge_index):
             Z = super().forward(item_feats, edge_index)
@@ -380,12 +393,21 @@ def trajectory_case(ref, epochs: int = 20):
         return m
 
     def _sample(*a, **k):
+        # called at the top of epoch n_sample + 1, i.e. after n_sample optimizer steps: the
+        # state a one-step replay starts from (params, Adam moments, both RNG streams)
+        if capture is not None and rec["n_sample"] in capture["after_steps"]:
+            capture["states"][rec["n_sample"]] = {
+                "params": {kk: v.detach().clone() for kk, v in rec["model"].state_dict().items()},
+                "opt": copy.deepcopy(rec["opt"].state_dict()),
+                "py_random": random.getstate(), "np_random": np.random.get_state()}
+        rec["n_sample"] += 1
         rec["triples"] = base_sample(*a, **k)
         return rec["triples"]
 
     old_storage = ref.storage
     ref.storage = types.SimpleNamespace(Client=_Client)
     ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch = _NoDropGAT, _eval, _sample
+    torch.optim.Adam = _RecAdam
     argv, cwd = sys.argv, os.getcwd()
     try:
         os.chdir(work)
@@ -402,7 +424,7 @@ def trajectory_case(ref, epochs: int = 20):
                          layers=ckpt["config"].get("layers", 2))
         model.load_state_dict(ckpt["state_dict"])
         model.eval()
-        train_raw, _, _ = ref.build_splits(pd_read(work / "tmp" / "interactions.parquet"))
+        train_raw, val_raw, _ = ref.build_splits(pd_read(work / "tmp" / "interactions.parquet"))
         u2i = {k: int(v) for k, v in maps["user_to_idx"].items()}
         i2i = {k: int(v) for k, v in maps["item_to_idx"].items()}
         tr = {}
@@ -410,16 +432,20 @@ def trajectory_case(ref, epochs: int = 20):
             ii = [i2i[str(t)] for t in items if str(t) in i2i]
             if str(u_raw) in u2i and ii:
                 tr[u2i[str(u_raw)]] = np.array(ii, dtype=np.int64)
+        va = {u2i[str(u_raw)]: i2i[str(it)] for u_raw, it in val_raw.items() if str(u_raw) in u2i and str(it) in i2i}
         ei = ref.build_edge_index(n_users, n_items, tr)
         with torch.no_grad():
             Z = model(torch.from_numpy(feats), ei)
             I = Z[n_users:].detach().cpu().numpy().astype(np.float32)
             U = Z[:n_users].detach().cpu().numpy().astype(np.float32)
+        if capture is not None:
+            capture["inputs"] = dict(tr=tr, va=va, ei=ei, feats=feats, n_users=n_users, n_items=n_items)
     finally:
         sys.argv = argv
         os.chdir(cwd)
         ref.storage = old_storage
         ref.CustomGAT, ref.eval_sampled, ref.sample_bpr_epoch = base_gat, base_eval, base_sample
+        torch.optim.Adam = base_adam
         shutil.rmtree(work, ignore_errors=True)
     best_epoch = 1 + int(np.argmax([v["ndcg@20"] for v in rec["val"][:epochs]]))
     metrics["config"] = {k: v for k, v in metrics["config"].items() if not k.endswith("_prefix")}
@@ -525,6 +551,145 @@ def trajectory_fixture(ref, epochs: int = 20):
           f"pairs {pair}; top-20 {top}")
 
 
+ONESTEP_AFTER = (0, 1, 2, 5, 8, 12, 16, 19)  # saved states: after this many optimizer steps
+ONESTEP_THREADS = (8, 1, 2, 4)             # the reference's one-step replays per saved state
+ADAM_LR, ADAM_WD = 1e-3, 1e-4              # train_gat_custom.py Config.lr / l2 (:53-54)
+
+
+def _replay_step(ref, st, inp, threads, dtype):
+    """One training epoch of train_gat_custom.py main() (:341-377) from a captured state:
+    sample_bpr_epoch from the saved ``random`` state, the training forward, the BPR loss,
+    zero_grad / backward / Adam.step, then the eval forward and eval_sampled from the saved
+    ``np.random`` state.  The reference's own classes; ``dtype`` float64 gives the rounding-
+    free step (gradients, loss) the fp32 runs are measured against."""
+    torch.set_num_threads(threads)
+    n_users, n_items = inp["n_users"], inp["n_items"]
+    model = ref.CustomGAT(n_users, n_items, item_feat_dim=inp["feats"].shape[1], hidden=128, layers=2)
+    for layer in model.layers:
+        layer.drop.p = 0.0
+    model.load_state_dict(st["params"])
+    model = model.to(dtype)
+    opt = torch.optim.Adam(model.parameters(), lr=ADAM_LR, weight_decay=ADAM_WD)
+    opt.load_state_dict(copy.deepcopy(st["opt"]))
+    random.setstate(st["py_random"])
+    u_arr, i_arr, j_arr = ref.sample_bpr_epoch(inp["tr"], n_items, 200_000)
+    u, i, j = (torch.from_numpy(a).long() for a in (u_arr, i_arr, j_arr))
+    feats = torch.from_numpy(inp["feats"]).to(dtype)
+    model.train()
+    Z = model(feats, inp["ei"])
+    U, I = Z[:n_users], Z[n_users:]
+    pos = (U[u] * I[i]).sum(dim=-1)
+    neg = (U[u] * I[j]).sum(dim=-1)
+    loss = -torch.log(torch.sigmoid(pos - neg) + 1e-8).mean()
+    opt.zero_grad()
+    loss.backward()
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    opt.step()
+    model.eval()
+    np.random.set_state(st["np_random"])
+    val = ref.eval_sampled(model, types.SimpleNamespace(eval_neg_k=100), feats, inp["ei"], inp["tr"], inp["va"])
+    with torch.no_grad():
+        Zn = model(feats, inp["ei"])
+    return dict(loss=float(loss.item()), grads=grads, items=Zn[n_users:].numpy(), users=Zn[:n_users].numpy(),
+                params={k: v.detach().clone() for k, v in model.state_dict().items()}, val=val,
+                triples_head=[int(u_arr[0]), int(i_arr[0]), int(j_arr[0])])
+
+
+def grad_stats(g, g64):
+    """A gradient against the float64 one of the same state: max |g - g64| / max |g64| per
+    tensor, and the count of entries whose sign differs from g64's (g64 != 0) -- an early Adam
+    step is ~lr * sign(g), so these are the entries that become lr-sized parameter differences."""
+    out = {}
+    for k, ref64 in g64.items():
+        a = np.asarray(g[k], np.float64)
+        b = np.asarray(ref64, np.float64)
+        out[k] = {"maxabs_rel": float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)),
+                  "sign_flips": int(((np.sign(a) != np.sign(b)) & (b != 0)).sum())}
+    return out
+
+
+def onestep_fixture(ref, epochs: int = 20):
+    """Chaos-free training-step parity: the reference trainer's own
+    ``main()`` run (default thread count) captures its full state -- state_dict, Adam
+    ``exp_avg`` / ``exp_avg_sq`` / ``step``, ``random`` and ``np.random`` states -- at the top of
+    the epoch following ``ONESTEP_AFTER`` optimizer steps; every saved state is then replayed
+    one epoch by the reference's classes at each of ``ONESTEP_THREADS`` torch thread counts
+    (fp32) and once in float64.  The GPU test starts OUR epoch from the same state and holds its
+    gradients, next item rows and val metrics to the reference's one-step spread.
+
+    Written: ``onestep_cfg1.npz`` (per state ``s<k>__``: params, Adam moments, step count and
+    the two RNG states -- the exact state, nothing derived) and ``onestep_cfg1.json`` (per
+    state: losses, the gradient statistics of each fp32 replay against float64, the pairwise
+    next-item-row spread of the fp32 replays, each fp32 replay's distance to the float64 one,
+    lr-sized parameter differences, val metrics, and checksums of the float64 replay -- its
+    gradient norms and next item rows -- which pin the test's own float64 restatement of the
+    step, ``oracle.custom_gat_model`` + Adam in float64, to the reference's)."""
+    cap = {"after_steps": set(ONESTEP_AFTER), "states": {}}
+    trajectory_case(ref, epochs, capture=cap)
+    inp = cap["inputs"]
+    arrays, meta = {}, {"after_steps": list(ONESTEP_AFTER), "threads": list(ONESTEP_THREADS),
+                        "adam": {"lr": ADAM_LR, "weight_decay": ADAM_WD}, "states": {}}
+    threads0 = torch.get_num_threads()
+    try:
+        for s in ONESTEP_AFTER:
+            st = cap["states"][s]
+            r64 = _replay_step(ref, st, inp, threads0, torch.float64)
+            reps = {t: _replay_step(ref, st, inp, t, torch.float32) for t in ONESTEP_THREADS}
+            g64 = {k: v.numpy() for k, v in r64["grads"].items()}
+            names = [f"t{t}" for t in ONESTEP_THREADS]
+            pair = {}
+            for x in range(len(names)):
+                for y in range(x + 1, len(names)):
+                    a, b = reps[ONESTEP_THREADS[x]]["items"], reps[ONESTEP_THREADS[y]]["items"]
+                    pair[f"{names[x]}~{names[y]}"] = max(row_rel_np(a, b), row_rel_np(b, a))
+            # Adam steps in units of lr that differ from the float64 replay's by more than lr/2
+            # (a sign flip of a near-zero gradient entry moves its parameter by ~2 lr)
+            lr_flips = {f"t{t}": int(sum(int((np.abs(reps[t]["params"][k].double().numpy()
+                                                     - r64["params"][k].numpy()) > 0.5 * ADAM_LR).sum())
+                                         for k in g64)) for t in ONESTEP_THREADS}
+            meta["states"][str(s)] = {
+                "step_count": float(st["opt"]["state"][0]["step"]) if st["opt"]["state"] else 0.0,
+                "loss": {"f64": r64["loss"], **{f"t{t}": reps[t]["loss"] for t in ONESTEP_THREADS}},
+                "triples_head": r64["triples_head"],
+                "grad_vs_f64": {f"t{t}": grad_stats({k: v.numpy() for k, v in reps[t]["grads"].items()}, g64)
+                                for t in ONESTEP_THREADS},
+                "next_items_pairwise_row_rel": pair,
+                "next_items_spread": max(pair.values()),
+                "next_items_vs_f64_row_rel": {f"t{t}": row_rel_np(reps[t]["items"], r64["items"])
+                                              for t in ONESTEP_THREADS},
+                "next_params_lr_flips_vs_f64": lr_flips,
+                "val": {"f64": r64["val"], **{f"t{t}": reps[t]["val"] for t in ONESTEP_THREADS}},
+            }
+            meta["states"][str(s)]["f64_checksums"] = {
+                "grad_l2": {k: float(np.linalg.norm(v)) for k, v in g64.items()},
+                "grad_maxabs": {k: float(np.abs(v).max()) for k, v in g64.items()},
+                "next_items_l2": float(np.linalg.norm(r64["items"])),
+                "next_items_sum": float(r64["items"].sum())}
+            p = f"s{s}__"
+            params = st["params"]
+            ost = st["opt"]["state"]
+            arrays[p + "step"] = np.float64(ost[0]["step"] if ost else 0.0)
+            for n, k in enumerate(params):   # Adam's state_dict indexes parameters in named order
+                arrays[p + "param__" + k] = params[k].numpy()
+                if ost:
+                    arrays[p + "exp_avg__" + k] = ost[n]["exp_avg"].numpy()
+                    arrays[p + "exp_avg_sq__" + k] = ost[n]["exp_avg_sq"].numpy()
+            ver, mt, gauss = st["py_random"]
+            arrays[p + "py_random"] = np.array(mt, dtype=np.int64)
+            meta["states"][str(s)]["py_random_version_gauss"] = [ver, gauss]
+            kind, key, pos, has_g, cg = st["np_random"]
+            arrays[p + "np_random_key"] = np.asarray(key, np.uint32)
+            meta["states"][str(s)]["np_random"] = [kind, int(pos), int(has_g), float(cg)]
+            print(f"onestep s={s}: loss64 {r64['loss']:.8f}, spread {max(pair.values()):.3e}, "
+                  f"vs f64 {meta['states'][str(s)]['next_items_vs_f64_row_rel']}, lr flips {lr_flips}")
+    finally:
+        torch.set_num_threads(threads0)
+    assert [n for n, _ in ref.CustomGAT(2, 2, 4, 128, 2).named_parameters()] == list(cap["states"][1]["params"])
+    np.savez_compressed(HERE / "onestep_cfg1.npz", **arrays)
+    with open(HERE / "onestep_cfg1.json", "w") as f:
+        json.dump(meta, f, indent=2)
+
+
 def pd_read(path):
     import pandas as pd
     return pd.read_parquet(path)
@@ -535,6 +700,9 @@ def main():
     ref = load_reference_custom()
     if only == ["trajectory"]:
         trajectory_fixture(ref)
+        return
+    if only == ["onestep"]:
+        onestep_fixture(ref)
         return
     knn_case()
     fusion_case()

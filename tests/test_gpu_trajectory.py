@@ -24,7 +24,8 @@ reference runs (torch threads 8, 1, 2, 4): the largest pairwise final item-row s
 envelope our run is held to (no multiplier), and every user whose top-20 differs must differ
 by less than that envelope in score.  The count of users whose top-20 differ beyond SURVEY.md
 8(d)'s 1e-6 near-tie rule is reported next to the same count between reference runs (up to 1
-of 1,500 there; it is not asserted: it follows the chaotic final drift).  Per-epoch drift (ours and each reference run against the primary run) and
+of 1,500 there) and asserted with a slack of 2 users, a tripwire only: it follows the chaotic
+final drift; tests/test_gpu_onestep.py is the chaos-free check.  Per-epoch drift (ours and each reference run against the primary run) and
 both top-20 rules go to ``gpurun_out/parity/trajectory_cfg1<tag>.json`` (committed under
 profiles/); ``PPGAT_REPORT_TAG`` names a variant run (e.g. ``PPGAT_GEMM=fp32``).
 """
@@ -187,6 +188,12 @@ def test_reference_trajectory_cfg1(pkg, oracle, cuda, tmp_path, capsys, monkeypa
     assert z_items == 0.0
     assert r_items <= envelope, (r_items, envelope)
     # every user whose top-20 differs does so by less than the reference's own run-to-run
-    # spread; the 1e-6 rule (reported above, next to the reference pairs' counts) is not
-    # asserted: after 20 chaotic Adam epochs the reference runs themselves differ beyond it
+    # spread
     assert mism_env == 0, rep["top20"]
+    # SURVEY 8(d)'s 1e-6 rule: after 20 chaotic Adam epochs the reference runs themselves
+    # differ beyond it (up to ref_beyond users between two of them), so our run -- one more
+    # draw -- is held to that count plus a stated slack of 2 users (measured: 2 against the
+    # primary run on the default path, 0 with PPGAT_FUSED_DXW=0, profiles/r04/parity).  This
+    # is a regression tripwire; the precise training-step check is test_gpu_onestep.py, which
+    # starts from the reference's own saved states and has no chaotic amplification.
+    assert beyond <= ref_beyond + 2, rep["top20"]["rule_1e-6"]
