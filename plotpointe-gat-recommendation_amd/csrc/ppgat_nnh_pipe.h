@@ -57,7 +57,8 @@ __device__ __forceinline__ void wait_vm() {
 // BD: B fragments read BD MFMA steps ahead (1: the step before, as k_gemm_nnh2; 2: two steps,
 // eight more VGPRs, for LDS latency under eight waves of reads).  PRIO: waves 4-7 (the second-
 // dispatched half, the issue-arbitration loser) at s_setprio 1 for the whole loop.
-// LAB (diagnostics only, PPGAT_NNH2_LAB with PPGAT_NNH2=3; results wrong), bits: 1 = no X loads
+// LAB (diagnostics only, instantiated in lab builds -DPPGAT_LAB_BUILD=1, never in libppgat.so;
+// PPGAT_NNH2_LAB with PPGAT_NNH2=3; results wrong), bits: 1 = no X loads
 // after the first two chunks, 2 = no B DMA after the first two chunks, 16 = no B fragment reads
 // inside a chunk's MFMA steps (the first BD per chunk only), 32 = no preparation of the next
 // chunk (its fragments reused)

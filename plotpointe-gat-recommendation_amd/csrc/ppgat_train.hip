@@ -818,6 +818,7 @@ static hipError_t skinny_product(const float* A, int64_t lda, const float* B, in
 
 hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
                    float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st) {
+  if (M <= 0 || K <= 0) return hipSuccess;  // nothing to write (the ABI refuses these sizes; internal callers too)
   if (skinny_ok(M, K, (V && nv > 0) ? nv : 0) && N > 0) {
     // workspace: [split partials | ones float4 | colsum staging M x 4] (skinny_ws)
     char* p = static_cast<char*>(ws);

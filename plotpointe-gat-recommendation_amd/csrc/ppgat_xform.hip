@@ -739,7 +739,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __
 // Global issue order per wave: DMA(0) X(0) DMA(1) X(1) | chunk c: DMA(c+2) X(c+2) ...
 // ---------------------------------------------------------------------------
 
-// LAB (diagnostics only, PPGAT_NNH2_LAB; results wrong), bits: 1 = no X loads after the first
+// LAB (diagnostics only, lab builds -DPPGAT_LAB_BUILD=1, never in libppgat.so; PPGAT_NNH2_LAB;
+// results wrong), bits: 1 = no X loads after the first
 // two chunks (registers reused), 2 = no B DMA after the first two chunks (LDS reused), 4 = no
 // epilogue stores (a row is stored only if its first accumulator is NaN), 8 = no chunk barrier
 template <int NT, bool RK, int LAB = 0>
@@ -2272,23 +2273,28 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
   return hipGetLastError();
 }
 
-// the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2, =3 k_gemm_nnh3 (and
-// k_fusion_fwdh3; the default: 2-3 % faster than k_gemm_nnh2 at config-5 shapes, bitwise equal,
-// profiles/r04/v8_gemm5_nnh*.log), =4 k_gemm_nnh3 with B read two steps ahead, =5 that with the
-// second half of the waves at s_setprio 1, =6 X loaded as whole row segments and transposed
-// through LDS (all within 1-2 % of 3: kept as measured negatives, v8/v22_gemm5_nnh*.log; the
-// fusion kernel runs its variant-3 loop for 3..6).  Read once per process.
+// the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2, otherwise k_gemm_nnh3
+// (and k_fusion_fwdh3; the default: 2-3 % faster than k_gemm_nnh2 at config-5 shapes, profiles/
+// r04/v8_gemm5_nnh*.log).  All three compute the same products in the same order (bitwise equal,
+// tests/test_gpu_gemm_f16.py::test_nnh2_bitwise_equals_nnh).  Read once per process.
+// The measured-negative nnh3 variants (4: B read two steps ahead, 5: + s_setprio, 6: X through
+// LDS; all within 1-2 % of 3, v8/v22_gemm5_nnh*.log) and the diagnostic lab kernels
+// (PPGAT_NNH2_LAB: parts of the loop removed, results WRONG) exist only in a lab build:
+// tools/build_variants.sh ppgat_xform.hip lab:"-DPPGAT_LAB_BUILD=1" -- never in libppgat.so.
 int nnh_pipeline_variant() {
   static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
     if (e && strcmp(e, "0") == 0) return 1;
-    if (e && (strcmp(e, "2") == 0 || strcmp(e, "4") == 0 || strcmp(e, "5") == 0 || strcmp(e, "6") == 0))
-      return e[0] - '0';
+    if (e && strcmp(e, "2") == 0) return 2;
+#ifdef PPGAT_LAB_BUILD
+    if (e && (strcmp(e, "4") == 0 || strcmp(e, "5") == 0 || strcmp(e, "6") == 0)) return e[0] - '0';
+#endif
     return 3;
   }();
   return v;
 }
 
+#ifdef PPGAT_LAB_BUILD
 static int nnh2_lab() {
   static const int lab = [] {
     const char* e = getenv("PPGAT_NNH2_LAB");
@@ -2296,6 +2302,7 @@ static int nnh2_lab() {
   }();
   return lab;
 }
+#endif
 
 static size_t nnq_bytes(int K, int N) {  // image + column exponents, either family
   const int nt = N % 256 == 0 ? 8 : 4;
@@ -2335,6 +2342,7 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       if (e != hipSuccess) return e;
       if (nnh_pipeline_variant() >= 3 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh3 runs chunk pairs
         const int v = nnh_pipeline_variant();
+#ifdef PPGAT_LAB_BUILD
         if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {  // diagnostics (results wrong)
 #define PPGAT_LAB3(L) \
   if (lab == L) hipLaunchKernelGGL((k_gemm_nnh3<8, false, 1, false, L>), dim3(grid), dim3(512), 0, st, a, img, ecol)
@@ -2342,6 +2350,7 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
 #undef PPGAT_LAB3
           return hipGetLastError();
         }
+#endif
 #define PPGAT_NNH3(BD, PR, XT)                                                                                   \
   do {                                                                                                           \
     if (nv > 0) {                                                                                                \
@@ -2353,14 +2362,19 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
       hipLaunchKernelGGL((k_gemm_nnh3<4, false, BD, PR, 0, XT>), dim3(grid), dim3(512), 0, st, a, img, ecol);        \
     }                                                                                                            \
   } while (0)
-        if (v == 3) PPGAT_NNH3(1, false, false);
-        else if (v == 4) PPGAT_NNH3(2, false, false);
+#ifdef PPGAT_LAB_BUILD
+        if (v == 4) PPGAT_NNH3(2, false, false);
         else if (v == 5) PPGAT_NNH3(2, true, false);
-        else PPGAT_NNH3(1, false, true);
+        else if (v == 6) PPGAT_NNH3(1, false, true);
+        else
+#endif
+        PPGAT_NNH3(1, false, false);
+        (void)v;
 #undef PPGAT_NNH3
         return hipGetLastError();
       }
       if (nnh_pipeline_variant() == 2 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
+#ifdef PPGAT_LAB_BUILD
         if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {
 #define PPGAT_LAB(L) \
   if (lab == L) hipLaunchKernelGGL((k_gemm_nnh2<8, false, L>), dim3(grid), dim3(512), 0, st, a, img, ecol)
@@ -2368,6 +2382,7 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
 #undef PPGAT_LAB
           return hipGetLastError();
         }
+#endif
         if (nv > 0) {
           if (w8) hipLaunchKernelGGL((k_gemm_nnh2<8, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
           else hipLaunchKernelGGL((k_gemm_nnh2<4, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);

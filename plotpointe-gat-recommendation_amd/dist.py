@@ -1029,11 +1029,17 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     seed_buf = saved["seed_buf"]
     order = _small_class_first(hg)
     if pre is not None:
-        # started by the layer above from its dx -- which is g: HaloPyGGAT links a layer only to
-        # the one consumer of its output (every rank takes this branch alike: the collectives match)
+        # started by the layer above from its dx, which is g when nothing sits between the two
+        # layers (HaloPyGGAT links a layer only to the one consumer of its output).  If autograd
+        # hands over another tensor (a hook, a residual, an activation in between), the halo rows
+        # already sent carry the old values: wait for those exchanges and redo them from the real
+        # g.  The branch is structural, so every rank takes it alike and the collectives match.
         gtab, ntab, nst = pre
         if gtab.x.data_ptr() != g.data_ptr():
+            gtab.wait_all()
             gtab.x[:n0].copy_(g)
+            for cls in order:
+                gtab.start(cls, g)
     else:
         gtab, ntab, nst = _bwd_tables(saved, hg, comm, stages, C, dev)
         gtab.x[:n0].copy_(g)

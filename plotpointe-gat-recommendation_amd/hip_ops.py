@@ -771,6 +771,10 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     split = B.size(0)
     nb = split + (B_items.size(0) if B_items is not None else 0)
     _require(A.size(0) == nb, "gemm_tn: A [N,M], B [N,K]")
+    if A.size(1) == 0 or B.size(1) == 0 or nb == 0:  # empty product or empty reduction: zeros
+        M0, K0, nv0 = A.size(1), B.size(1), (0 if V is None else V.size(1))
+        z = A.new_zeros
+        return z(M0, K0), (z(M0) if want_colsum else None), (z(nv0, K0) if nv0 else None)
     if not all(_aligned_rows(t) for t in (A, B) + ((B_items,) if B_items is not None else ())):
         # the kernels read 16-byte row segments: zero-pad the columns of any operand whose rows
         # are not 16-byte aligned (e.g. the [B, B] logit gradient of a ragged InfoNCE batch);

@@ -67,8 +67,11 @@ def _setup(dev, heads=1, size="toy"):
     return pkg, g, ei, feats, full, [torch.from_numpy(a).to(dev) for a in (u, i, j)]
 
 
-def _run(rank, world, out_dir, heads, part, size="toy"):
-    dev = torch.device("cuda", 0)
+def _run(rank, world, out_dir, heads, part, size="toy", dev_index=0):
+    dev = torch.device("cuda", dev_index)
+    torch.cuda.set_device(dev)
+    if part.endswith("fsplit"):  # the forward split by destination class (read at first use)
+        os.environ["PPGAT_FWD_SPLIT"] = "1"
     if part == "halo-dstbwd":  # the round-3 multi-head halo backward (edges at the destination's owner)
         os.environ["PPGAT_HALO_BWD"] = "dst"
         part = "halo"
@@ -77,6 +80,16 @@ def _run(rank, world, out_dir, heads, part, size="toy"):
         part = "halo"
     pkg, g, ei, feats, full, (u, i, j) = _setup(dev, heads, size)
     D = pkg.dist
+    if part == "halo-g2":
+        # the gradient reaching the lower layer is a NEW tensor (2 g, as if a hook sat between the
+        # layers) while the layer above has already started that layer's halo exchange from its
+        # own dx: the backward must redo the exchange from the real g (dist.py)
+        orig = D._halo_xgat_backward_deferred_d
+
+        def _two_g(saved, g_, hg, comm_, stages, want_bias_grad, pre=None, link_in=None):
+            return orig(saved, g_ * 2 if pre is not None else g_, hg, comm_, stages, want_bias_grad, pre, link_in)
+        D._halo_xgat_backward_deferred_d = _two_g
+        part = "halo"
     comm = D.Comm()
     if part == "halo":
         dg = D.build_halo_graph(ei, g.n_nodes, g.n_users, world, rank)
@@ -110,12 +123,16 @@ def _run(rank, world, out_dir, heads, part, size="toy"):
                    os.path.join(out_dir, f"sharded_{world}.pt"))
 
 
-def _worker(rank, world, port, out_dir, heads, part, size="toy"):
+def _worker(rank, world, port, out_dir, heads, part, size="toy", backend="gloo"):
     sys.path.insert(0, str(ROOT))
     store = dist.TCPStore("127.0.0.1", port, None, is_master=False)  # the parent holds the server
-    dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
+    if backend == "nccl":  # one GPU per rank (RCCL): the comm-stream overlap paths run for real
+        dev = torch.device("cuda", rank)
+        dist.init_process_group("nccl", store=store, rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
     try:
-        _run(rank, world, out_dir, heads, part, size)
+        _run(rank, world, out_dir, heads, part, size, dev_index=rank if backend == "nccl" else 0)
     finally:
         dist.destroy_process_group()
 
@@ -179,14 +196,37 @@ def test_sharded_world1_rccl(cuda, tmp_path, monkeypatch, heads, part):
 
 
 @pytest.mark.parametrize("heads,part", [(1, "halo"), (2, "halo"), (4, "halo"), (4, "halo-dstbwd"), (4, "halo-srcg"),
-                                        (1, "replicated"),
+                                        (4, "halo-g2"), (1, "replicated"),
                                         (2, "replicated"), (1, "replicated-staged")])
 def test_sharded_world2_shared_gpu(cuda, tmp_path, heads, part):
     store = _master_store()
     mp.start_processes(_worker, args=(2, store.port, str(tmp_path), heads, part), nprocs=2, join=True,
                        start_method="spawn")
     del store
-    _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), _oracle(heads))
+    Z, loss, grads = _oracle(heads)
+    if part == "halo-g2":  # the lower layer saw 2 g: its parameters' and its inputs' gradients double
+        grads = {k: v * 2 if k.startswith(("convs.0.", "item_proj.", "user_emb.")) else v for k, v in grads.items()}
+    _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), (Z, loss, grads))
+
+
+@pytest.mark.parametrize("heads,part", [(4, "halo"), (4, "halo-g2"), (1, "halo"), (1, "replicated"),
+                                        (2, "replicated-fsplit")])
+def test_sharded_world2_rccl(cuda, tmp_path, heads, part):
+    """World 2 over RCCL, one process per GPU: the communication-stream paths (HaloRows.start's
+    overlapped all_to_alls, the backward's early start of the layer below, the Dtab exchange
+    beside the main-stream partial exchanges and the column-bound all_reduce; the replicated
+    partition's item-row merges on the comm stream) with real cross-rank ordering -- gloo takes
+    the synchronous branch.  Needs two visible GPUs: skipped on a one-GPU box."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs (one process per GPU over RCCL)")
+    store = _master_store()
+    mp.start_processes(_worker, args=(2, store.port, str(tmp_path), heads, part, "toy", "nccl"), nprocs=2,
+                       join=True, start_method="spawn")
+    del store
+    Z, loss, grads = _oracle(heads)
+    if part == "halo-g2":
+        grads = {k: v * 2 if k.startswith(("convs.0.", "item_proj.", "user_emb.")) else v for k, v in grads.items()}
+    _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), (Z, loss, grads))
 
 
 @pytest.mark.timeout(600)

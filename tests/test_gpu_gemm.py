@@ -138,6 +138,18 @@ def test_gemm_tn_segments(pkg, cuda):
     assert torch.equal(out, out1) and torch.equal(vo, vo1)
 
 
+def test_gemm_tn_empty_operands(pkg, cuda):
+    """Zero-width operands (an empty product) and zero rows (an empty reduction) give zeros of
+    the right shape -- no recursion through the unaligned-row padding."""
+    ops = _ops()
+    A = torch.randn(1000, 8, device=cuda)
+    for a, b, shape in ((A[:, :0], A, (0, 8)), (A, A[:, :0], (8, 0)), (A[:0], A[:0], (8, 8))):
+        out, cs, vo = ops.gemm_tn(a, b, want_colsum=True, V=A[: a.size(0), :2])
+        assert out.shape == shape and not out.any()
+        assert cs.shape == (shape[0],) and not cs.any()
+        assert vo.shape == (2, shape[1]) and not vo.any()
+
+
 @pytest.mark.parametrize("heads,C,K", [(1, 128, 128), (2, 64, 96), (4, 32, 128)])
 def test_weight_grads_vs_fp64(pkg, cuda, heads, C, K):
     ops = _ops()

@@ -245,9 +245,10 @@ print(json.dumps(out))
 
 
 def test_nnh2_bitwise_equals_nnh(cuda):
-    """The pipelined NN kernels (k_gemm_nnh3, the default; k_gemm_nnh2 and the nnh3 variants:
-    PPGAT_NNH2=2 / 4 / 5; the FusionMLP's k_fusion_fwdh3 beside k_fusion_fwdh) and k_gemm_nnh
-    (PPGAT_NNH2=0) compute the same products in the same order: bitwise equal outputs, with and
+    """The pipelined NN kernels (k_gemm_nnh3, the default; k_gemm_nnh2: PPGAT_NNH2=2; the
+    FusionMLP's k_fusion_fwdh3 beside k_fusion_fwdh) and k_gemm_nnh (PPGAT_NNH2=0) -- every NN
+    fp16 kernel libppgat.so can select -- compute the same products in the same order: bitwise
+    equal outputs, with and
     without the fused rank epilogue, on both B layouts, a ragged row count, the shortest
     pipelined K (two chunks), an odd chunk count (K = 864: k_gemm_nnh runs it for every variant),
     rows that take the rescale path (in the second chunk, mid-way) and a row whose scale is set
@@ -259,7 +260,7 @@ def test_nnh2_bitwise_equals_nnh(cuda):
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
     res = []
-    for v in ("3", "0", "2", "4", "5", "6"):
+    for v in ("3", "0", "2", "6"):  # "6": a lab-build-only value selects the default in libppgat.so
         r = subprocess.run([sys.executable, "-c", _NNH2_CHECK, str(root)], env=dict(os.environ, PPGAT_NNH2=v),
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]

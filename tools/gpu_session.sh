@@ -44,7 +44,7 @@ for s in $STEPS; do
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
             python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
     nnhpmc) run "nnhpmc${NNHV:-3}" 500 env GEMM_ARGS=--cfg5 GEMM_TAG="_nnh${NNHV:-3}" PPGAT_NNH2="${NNHV:-3}" bash tools/gemm_pmc.sh ;;
-    nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
+    nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_LIB=build_variants/lab/libppgat.so PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
     profprobe) (cd /tmp && run rocprof_probe5 900 rocprofv3 --kernel-trace --stats -d "$OUT/profprobe" -o run --output-format csv -- python "$R/tools/scale_probe.py" --config 5 --world 8 --rank ${PROBE_RANK:-7} --streams --steps 3 --warmup 1) ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
