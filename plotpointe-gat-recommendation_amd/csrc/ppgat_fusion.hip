@@ -748,9 +748,31 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh(const float* __restrict_
 // k_fusion_fwdh with GEMM1 on the pipelined loop of k_gemm_nnh3 (ppgat_nnh_pipe.h: W1 chunks by
 // LDS-DMA into three buffers two chunks ahead, x two chunks ahead, the next chunk's row scale
 // and fp16 split inside the current chunk's MFMA sequence, one bare barrier per chunk) -- the
-// same products in the same order (bitwise equal outputs); GEMM2 and the epilogue unchanged.
-// Even chunk counts (the reference's 384 + 512 = 28 chunks); LDS 3 x 40,960 B.
+// same products in the same order (bitwise equal outputs).  Even chunk counts (the reference's
+// 384 + 512 = 28 chunks); LDS 3 x 40,960 B.
+// GEMM2 (round 5): k_fusion_fwdh waited for every 20-KB W2 slice at a __syncthreads (vmcnt(0))
+// right after issuing it, eight exposed L2 round trips per workgroup.  Here the four first slices
+// go out by LDS-DMA the moment GEMM1's loop has released its buffers, into four buffers beside the
+// wave patches, and slice c + 4 follows as soon as every wave is done with slice c; each slice
+// waits only for its own DMA (exact per-wave vmcnt counts); b1 / e1 / b2 / e2 are staged in LDS
+// by LDS-DMA ahead of GEMM1, so the h epilogue issues no global load behind the W2 DMAs.
 // ---------------------------------------------------------------------------
+constexpr int kH2Bytes = kH2Img * 2;           // one 32-deep W2 slice image
+constexpr int kH2Pieces = kH2Bytes / 1024;     // 1-KB wave copies per slice (20)
+
+template <int K>
+__device__ __forceinline__ void wait_w2(bool full) {  // this wave's DMA of K later slices may stay in flight
+  constexpr int F = (kH2Pieces + 7) / 8, P = kH2Pieces / 8;
+  if (full) wait_vm<K * F>();
+  else wait_vm<K * P>();
+}
+
+__device__ __forceinline__ i32x4 raw_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t base = reinterpret_cast<uint64_t>(p);
+  return {__builtin_amdgcn_readfirstlane((int)(uint32_t)base), __builtin_amdgcn_readfirstlane((int)((base >> 32) & 0xffff)),
+          __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+
 __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict__ txt, const float* __restrict__ img,
                                                         const int32_t* __restrict__ img_index,
                                                         const float* __restrict__ img_fallback, int64_t B, int Dt,
@@ -759,11 +781,13 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
                                                         const uint16_t* __restrict__ w2i_g, const int* __restrict__ e2,
                                                         const float* __restrict__ b2, int normalize,
                                                         float* __restrict__ out, float* __restrict__ z1_out) {
-  static_assert(kH1Img * 2 % 1024 == 0 && kH2Img * 2 % 1024 == 0, "1-KB wave copies");
-  static_assert(kPatchB + 2 * kH2Img * 2 <= 3 * kH1Img * 2, "GEMM2 fits GEMM1's LDS");
+  static_assert(kH1Img * 2 % 1024 == 0 && kH2Bytes % 1024 == 0, "1-KB wave copies");
+  static_assert(kPatchB % 1024 == 0 && kPatchB + 4 * kH2Bytes <= 3 * kH1Img * 2, "GEMM2 fits GEMM1's LDS");
   static_assert(kH1Img == NnhImg<8>::ELEMS, "W1 chunks are k_gemm_nnh's 256-column images");
+  static_assert(H1 == 256 && DO == 128 && H1 / BK == 8, "staged parameter rows: 1 KB (H1) / 512 B (DO)");
   __shared__ __attribute__((aligned(16))) uint16_t lds[3 * kH1Img];
   __shared__ __attribute__((aligned(16))) float sF[8][32];  // per wave: a factor per row
+  __shared__ __attribute__((aligned(16))) float sPar[4][256];  // b1 | e1 (int bits) | b2 | e2 (int bits)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -784,11 +808,30 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
 #pragma unroll
     for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
   };
+  const uint32_t voff = (uint32_t)lane * 16u;
+  // b1, e1, b2, e2 -> sPar by LDS-DMA (one wave each; older than GEMM1's first DMA, so the loop's
+  // first wait covers them, and its barriers publish them; lanes past a 512-B row read zeros)
+  if (w < 4) {
+    const void* src = w == 0 ? (const void*)b1 : w == 1 ? (const void*)e1 : w == 2 ? (const void*)b2 : (const void*)e2;
+    dma_lds16(raw_rsrc(src, w < 2 ? 4 * H1 : 4 * DO), (uint32_t)reinterpret_cast<uintptr_t>(&sPar[w][0]), voff, 0);
+  }
 
   // ---- GEMM1: the pipelined fp16 two-term loop (ppgat_nnh_pipe.h), rows scaled online ----
   f32x16 acc[8];
   int erow = 0;
   nnh3_loop<8>(w1i, lds, chunks, load_x_chunk, acc, erow, sF[w], w, lane);
+
+  // ---- W2 slices 0..3 -> buffers 0..3 beside the patches (the loop ended on a barrier after
+  // every wave's last reads of its buffers) ----
+  const uint32_t w2l = (uint32_t)reinterpret_cast<uintptr_t>(lds) + (uint32_t)kPatchB;
+  const i32x4 rs2 = raw_rsrc(w2i_g, (uint32_t)(H1 / BK) * kH2Bytes);
+  const bool full2 = (kH2Pieces % 8 == 0) || w < kH2Pieces % 8;
+  auto issue2 = [&](int c) {
+    const uint32_t dst = w2l + (uint32_t)((c & 3) * kH2Bytes);
+    for (int i = w; i < kH2Pieces; i += 8) dma_lds16(rs2, dst + i * 1024, voff, (uint32_t)(c * kH2Bytes + i * 1024));
+  };
+#pragma unroll
+  for (int c = 0; c < 4; ++c) issue2(c);
 
   // ---- h = relu(z), z = acc / (s_row s_col) + b1 (exact unscale); h's row maxima ----
   float fr[16];
@@ -799,7 +842,7 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int col = BK * t + r;
-    const float fc = ldexpf(1.f, -e1[col]), bias = b1[col];
+    const float fc = ldexpf(1.f, -__float_as_int(sPar[1][col])), bias = sPar[0][col];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float z = fmaf(acc[t][q] * fr[q], fc, bias);
@@ -810,6 +853,7 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
       hm[q] = fmaxf(hm[q], h);
     }
   }
+  if (z1_out != nullptr) wait_vm<0>();  // training forward: stores share the counter; keep the slice counts exact
   float fr2[16];  // 1 / s_h of this lane's accumulator rows (GEMM2 epilogue)
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -825,18 +869,21 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
 
   // ---- GEMM2 over eight 32-column slices of h ----
   float* hp = reinterpret_cast<float*>(lds) + w * 32 * XLH;   // this wave's patch [32][XLH]
-  uint16_t* w2s = lds + kPatchB / 2;                           // [2][kH2Img]
+  const uint16_t* w2s = lds + kPatchB / 2;                     // [4][kH2Img]
   f32x16 acc2[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc2[u] = f32x16{};
-  glds_copy(w2i_g, w2s, kH2Img * 2, w, lane);
 #pragma unroll
   for (int c = 0; c < H1 / BK; ++c) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) hp[row_of(q, hf) * XLH + r] = acc[c][q];
-    __syncthreads();  // vmcnt(0): slice c landed; the patch is written
-    if (c + 1 < H1 / BK) glds_copy(w2i_g + (int64_t)(c + 1) * kH2Img, w2s + ((c + 1) & 1) * kH2Img, kH2Img * 2, w, lane);
-    const uint16_t* ws2 = w2s + (c & 1) * kH2Img;
+    for (int q = 0; q < 16; ++q) hp[row_of(q, hf) * XLH + r] = acc[c][q];  // own patch: in-order LDS
+    // slice c has landed: this wave's DMAs of up to three later slices may still be in flight
+    if (c <= 4) wait_w2<3>(full2);
+    else if (c == 5) wait_w2<2>(full2);
+    else if (c == 6) wait_w2<1>(full2);
+    else wait_w2<0>(full2);
+    __builtin_amdgcn_s_barrier();  // every wave's part of slice c
+    const uint16_t* ws2 = w2s + (c & 3) * kH2Img;
     auto read_w2 = [&](int i, split::u32x4 (&f)[2]) {
       const int off = (32 * (i & 3) + r) * HLDK + 16 * (i >> 2) + 8 * hf;
 #pragma unroll
@@ -852,7 +899,10 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
       acc2[uu] = split::mfma32_h3(fh, fb2[i & 1], acc2[uu]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // the patch and this slice's buffer are free again
+    if (c + 4 < H1 / BK) {
+      __builtin_amdgcn_s_barrier();  // every wave is done with buffer c & 3
+      issue2(c + 4);
+    }
   }
 
   // ---- unscale, bias, row L2 norm (inside the wave), store ----
@@ -862,7 +912,7 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int col = 32 * u + r;
-    const float fc = ldexpf(1.f, -e2[col]), bias2 = b2[col];
+    const float fc = ldexpf(1.f, -__float_as_int(sPar[3][col])), bias2 = sPar[2][col];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       acc2[u][q] = fmaf(acc2[u][q] * fr2[q], fc, bias2);

@@ -53,6 +53,45 @@ def row_rel(a, b):
     return float(r[k]), int(np.flatnonzero(nz)[k]), zmax
 
 
+def dx_rows(dx, dx_r, dxm_r, att_scale, ei=None, top: int = 5):
+    """Per-row dx errors against the fp64 oracle, judged on the scale of the terms each row sums
+    before they cancel.  dx_j = message term (oracle.pyg_gat_conv_chunked dx_message: ``dxm_r``)
+    + attention term, and the attention term is a sum of softmax-backward pieces
+    alpha e'(z) (dalpha - D) whose exact value can vanish (a destination with one in-edge:
+    alpha = 1, D = dalpha) while an fp32 implementation keeps ~u (|dalpha| + |D|) of them;
+    ``att_scale`` (oracle.pyg_dx_attention_scale) is the sum of those pieces' magnitudes.  So
+    s_j = |dxm_j| + att_scale_j bounds what row j sums, and every fp32 implementation's error on
+    it is a few u s_j.  Returns (max_j |dx_j - dx_r_j| / s_j, report dict): the plain per-row
+    max beside it and the worst plain rows with their norms, s_j / |dx_r_j| and degrees."""
+    import torch
+    dev = dx_r.device
+    d = dx.to(dev).double()
+    err = (d - dx_r).norm(dim=1)
+    nr = dx_r.norm(dim=1)
+    nm = dxm_r.norm(dim=1)
+    na = (dx_r - dxm_r).norm(dim=1)
+    U = att_scale.to(dev).double()
+    s = nm + U
+    cond = torch.where(s > 0, err / s.clamp_min(1e-300), err)   # a row with no terms must come out zero
+    plain = torch.where(nr > 0, err / nr.clamp_min(1e-300), err)
+    worst = torch.topk(plain, min(top, plain.numel())).indices
+    out_deg = in_deg = None
+    if ei is not None:
+        out_deg = torch.bincount(ei[0].to(dev), minlength=dx_r.size(0))
+        in_deg = torch.bincount(ei[1].to(dev), minlength=dx_r.size(0))
+    rows = []
+    for i in worst.tolist():
+        rows.append({"row": i, "plain_rel": float(plain[i]), "cond_rel": float(cond[i]), "dx_norm": float(nr[i]),
+                     "message_norm": float(nm[i]), "attention_norm": float(na[i]), "attention_scale": float(U[i]),
+                     "scale_over_dx": float(s[i] / nr[i]) if float(nr[i]) > 0 else float("inf"),
+                     "out_degree": int(out_deg[i]) if out_deg is not None else None,
+                     "in_degree": int(in_deg[i]) if in_deg is not None else None})
+    rep = {"plain_row_rel_max": float(plain.max()), "cond_row_rel_max": float(cond.max()),
+           "rows_plain_over_1e-5": int((plain > 1e-5).sum()), "dx_norm_median": float(nr.median()),
+           "attention_term_within_scale": bool((na <= U * (1 + 1e-9) + 1e-300).all()), "worst_rows": rows}
+    return float(cond.max()), rep
+
+
 def kink_sides(entries, n_edges: int, heads: int, n_layers: int):
     """Per layer, the LeakyReLU side [E, heads] bool the HIP kernels took (hip_ops.KINK_TAP
     entries of one forward, in layer order; ``entries`` may concatenate several ranks' lists,

@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import assert_kink_ties, check_att_dst, kink_report, kink_sides, row_rel, write_report
+from conftest import assert_kink_ties, check_att_dst, dx_rows, kink_report, kink_sides, row_rel, write_report
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
@@ -357,9 +357,12 @@ def test_cfg5_share_halo_world2(cuda, tmp_path):
     P = {k: v.detach().to(cuda) for k, v in conv.named_parameters()}
     kst = []
     ei = torch.from_numpy(ei_np).to(cuda)
-    out_r, dx_r, gr = O.pyg_gat_conv_chunked(P, x.to(cuda), ei, G.to(cuda), H, float(conv.dropout), CFG5_SEED,
-                                             kink_pos=sides[0].to(cuda), kink_stats=kst)
-    del ei
+    out_r, dx_r, gr, dxm_r = O.pyg_gat_conv_chunked(P, x.to(cuda), ei, G.to(cuda), H, float(conv.dropout), CFG5_SEED,
+                                                    kink_pos=sides[0].to(cuda), kink_stats=kst, dx_message=True)
+    U = O.pyg_dx_attention_scale(P, x.to(cuda), ei, G.to(cuda), H, float(conv.dropout), CFG5_SEED)
+    cond_dx, dx_rep = dx_rows(dx, dx_r, dxm_r, U, ei)
+    del U
+    del ei, dxm_r
     names = ("lin.weight", "att_src", "att_dst", "bias")
     err = {"out": _rel(out, out_r.cpu()), "dx": _rel(dx, dx_r.cpu())}
     err.update({k: _rel(grads[k], gr[k].cpu()) for k in names})
@@ -367,7 +370,8 @@ def test_cfg5_share_halo_world2(cuda, tmp_path):
     rb = plans[0]["row_bytes"]
     write_report("cfg5_share_halo_world2", {
         "edges": E, "nodes": N, "heads": H, "world": 2, "rel": err,
-        "row_rel_max": {"out": row_rel(out, out_r.cpu())[0], "dx": row_rel(dx, dx_r.cpu())[0]},
+        "row_rel_max": {"out": row_rel(out, out_r.cpu())[0], "dx": row_rel(dx, dx_r.cpu())[0], "dx_cond": cond_dx},
+        "dx_rows": dx_rep,
         "kink_ties": kink_report(kst), "plans": plans,
         "exchange_bytes_per_direction": [
             {"recv": (p_["n_halo_users"] + p_["n_halo_items"]) * rb, "send": (p_["send_users"] + p_["send_items"]) * rb}
@@ -378,6 +382,8 @@ def test_cfg5_share_halo_world2(cuda, tmp_path):
     assert err["out"] <= 1e-5 and err["dx"] <= 1e-5 and err["lin.weight"] <= 1e-5 and err["bias"] <= 1e-5, err
     assert err["att_src"] <= 1e-4, err
     check_att_dst(err["att_dst"] * float(gr["att_dst"].abs().max()), gr["att_dst"].cpu(), gr["att_src"].cpu(), 1e-4)
+    # every row of dx within 1e-5 of the scale of its terms (conftest.dx_rows), as single-GPU
+    assert cond_dx <= 1e-5, dx_rep
 
 
 class _StubComm:

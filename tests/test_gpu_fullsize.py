@@ -29,7 +29,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_kink_ties, check_att_dst, kink_report, kink_sides, row_rel, write_report
+from conftest import assert_kink_ties, check_att_dst, dx_rows, kink_report, kink_sides, row_rel, write_report
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(170)]
 
@@ -172,6 +172,9 @@ def test_cfg3_full_train_step(pkg, oracle, cuda, cfg2):
     _train_step_check(pkg, oracle, cuda, g, ei3, feats_np, triples, "cfg3_train_step")
 
 
+DX_ROW_TOL = 1e-5  # per row, relative to |message term| + |attention term| (conftest.dx_rows)
+
+
 # ---------------------------------------------------------------------------
 # config 5: one GPU's share, d=256, heads=4, the whole layer against a chunked fp64 oracle
 # ---------------------------------------------------------------------------
@@ -226,16 +229,20 @@ def test_cfg5_share_layer_full_gradients(pkg, oracle, cuda):
     torch.cuda.empty_cache()
     P = {k: v.detach() for k, v in conv.named_parameters()}
     kst = []
-    out_r, dx_r, grads = oracle.pyg_gat_conv_chunked(P, x.to(cuda), ei, Gd, H, 0.1, 424242, kink_pos=sides[0].to(cuda),
-                                                     kink_stats=kst)
+    out_r, dx_r, grads, dxm_r = oracle.pyg_gat_conv_chunked(P, x.to(cuda), ei, Gd, H, 0.1, 424242,
+                                                            kink_pos=sides[0].to(cuda), kink_stats=kst, dx_message=True)
     refs = (out_r, dx_r, grads["lin.weight"], grads["att_src"], grads["att_dst"], grads["bias"])
     errs = {n: rel(a, b) for n, a, b in zip(names, res1, refs)}
-    rows = {"out": row_rel(res1[0], refs[0])[0]}
+    U = oracle.pyg_dx_attention_scale(P, x.to(cuda), ei, Gd, H, 0.1, 424242)
+    cond_dx, dx_rep = dx_rows(res1[1], dx_r, dxm_r, U, ei)
+    del U
+    rows = {"out": row_rel(res1[0], refs[0])[0], "dx": dx_rep["plain_row_rel_max"], "dx_cond": cond_dx}
     ties = sum(n for n, _, _ in kst)
     worst_tie = max((r for _, r, _ in kst), default=0.0)
     worst_bound = max((rb for _, _, rb in kst), default=0.0)
     write_report("cfg5_share_layer", {"edges": E, "nodes": N, "heads": H, "channels": C, "rel": errs,
-                                      "row_rel_max": rows, "kink_ties": ties, "kink_tie_max_abs_z_rel": worst_tie,
+                                      "row_rel_max": rows, "dx_rows": dx_rep, "kink_ties": ties,
+                                      "kink_tie_max_abs_z_rel": worst_tie,
                                       "kink_tie_max_abs_z_over_fp32_bound": worst_bound,
                                       "oracle": "chunked fp64 pyg_gat_conv on the device, LeakyReLU sides as the "
                                                 "kernels took them"})
@@ -243,3 +250,6 @@ def test_cfg5_share_layer_full_gradients(pkg, oracle, cuda):
     tol = {"out": 1e-5, "dx": 1e-5, "lin.weight": 1e-5, "att_src": 1e-4, "att_dst": 1e-4, "bias": 1e-5}
     for n in names:
         assert errs[n] <= tol[n], (n, errs[n])
+    # every row of dx within 1e-5 of the scale of its terms (conftest.dx_rows: a row whose
+    # message and attention terms cancel is judged on the terms, not on their small sum)
+    assert rows["out"] <= 1e-5 and cond_dx <= DX_ROW_TOL, dx_rep

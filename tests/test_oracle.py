@@ -144,6 +144,27 @@ def test_chunked_oracle_equals_whole_graph(oracle):
     assert _rel(dx_c, xw.grad) <= 1e-12
     for k in P:
         assert _rel(gr_c[k], Q[k].grad) <= 1e-11, k
+    # the gradient-path split behind the config-5 per-row dx bound: the message path (attention
+    # weights detached) and the attention path (h detached in the message) add up to dx
+    _, dx_c2, _, dxm_c = oracle.pyg_gat_conv_chunked(P, x, ei, G, H, 0.1, 77, max_edges=700, dx_message=True)
+    assert torch.equal(dx_c2, dx_c)
+    parts = []
+    for det in ("alpha", "msg_h"):
+        xp = x.clone().requires_grad_(True)
+        o = oracle.pyg_gat_conv(xp, ei, P["lin.weight"], P["att_src"], P["att_dst"], P["bias"], H, dropout_p=0.1,
+                                seed=77, detach=det)
+        assert torch.equal(o, out.detach())                 # the same forward value
+        parts.append(torch.autograd.grad((o * G).sum(), xp)[0])
+    assert _rel(dxm_c, parts[0]) <= 1e-12
+    assert _rel(parts[0] + parts[1], xw.grad) <= 1e-12
+    assert float((parts[1]).abs().max()) > 1e-3 * float(parts[0].abs().max())  # both paths carry weight
+    # the attention path's pre-cancellation scale bounds its value on every row, and stays
+    # nonzero on a destination with a single in-edge whose own softmax piece cancels exactly
+    U = oracle.pyg_dx_attention_scale(P, x, ei, G, H, 0.1, 77, max_edges=1000)
+    assert U.shape == (n,) and bool((parts[1].norm(dim=1) <= U * (1 + 1e-9) + 1e-300).all())
+    indeg = torch.bincount(ei[1], minlength=n)
+    one = int(torch.nonzero(indeg == 1)[0])
+    assert float(U[one]) > 0
 
 
 def test_kink_sides_option(oracle):
