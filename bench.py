@@ -449,6 +449,7 @@ def main():
                                    if part == "replicated" else
                                    f"row-sharded x{world}, RCCL all_to_all halo + grad all_reduce")},
         "hip_graph": graph is not None,
+        "device_mem_peak_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
         "formulation": ("aggregate-then-transform (x_j gathered once per edge for all heads)" if xform_k else
                         "transform-then-aggregate (h_j gathered per edge)"),
         "gemm": ("fp32 MFMA, exact fp32 FMA chains (PPGAT_GEMM=fp32)" if os.environ.get("PPGAT_GEMM") == "fp32" else

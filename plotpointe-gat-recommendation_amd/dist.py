@@ -784,7 +784,8 @@ class _HaloLayerX(torch.autograd.Function):
         dest = rows_out.x[:hg.n_own] if rows_out is not None and rows_out.x.size(1) == C else None
         scores = (rows_in.s, rows_in.s_dst) if rows_in.s is not None else None
         out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed,
-                                      phases=_halo_phases(hg, rows_in, rows_out), out=dest, scores=scores)
+                                      phases=_halo_phases(hg, rows_in, rows_out), out=dest, scores=scores,
+                                      keep_agg=True)  # the halo backward's weight gradient reads agg
         rows_in.wait_all()
         # links between consecutive halo layers (_halo_xgat_backward_deferred_d): this layer's
         # state for the layer above, whose backward starts this layer's exchanges early

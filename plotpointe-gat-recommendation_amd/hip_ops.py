@@ -1157,7 +1157,8 @@ def xgat_scores_rows(x_rows, A, s_src, s_dst=None):
 
 
 def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: int, slope: float, p: float,
-                 seed: int, phases: Optional[list] = None, out: Optional[torch.Tensor] = None, scores=None):
+                 seed: int, phases: Optional[list] = None, out: Optional[torch.Tensor] = None, scores=None,
+                 keep_agg: Optional[bool] = None):
     """Forward of the aggregate-then-transform layer; returns (out [n_dst, C], saved state).
 
     ``phases`` (a list of XPhase partitioning [0, n_dst) in order): the node scores of the
@@ -1167,7 +1168,8 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     contiguous [n_dst, C] destination (the next halo layer's own rows: no copy there).
     ``scores`` = (s_src [n_src, H], s_dst [>= n_dst, H]): the node scores, already computed
     (the halo partition: the owners computed them with the rows and sent them along, ready by
-    each phase's ``before``) -- no score pass here."""
+    each phase's ``before``) -- no score pass here.  ``keep_agg``: keep the aggregates for the
+    backward (None: _xgat_keep_agg decides; the halo partition's backward needs them)."""
     lib = _lib.load()
     x = x.contiguous()
     dev = x.device
@@ -1226,9 +1228,32 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
         if ph.after is not None:
             ph.after(out)
     _tap_kinks(v.rowptr, v.col, v.csr_eid, s_src, s_dst, H)
+    if not (keep_agg if keep_agg is not None else _xgat_keep_agg(v.n_dst, v.n_src, H, K, C, dev)):
+        agg = None  # the backward's weight gradient comes from acc^T x (_xgat_weight_grads)
     saved = dict(x=x, W=W, a_s=a_s, a_d=a_d, A=A, s_src=s_src, s_dst=s_dst, agg=agg, m=m, inv_l=inv_l,
                  seed_buf=seed_buf, v=v, meta=(H, C, K, slope, p, seed, bias is not None))
     return out, saved
+
+
+def _xgat_keep_agg(n_dst: int, n_src: int, H: int, K: int, C: int, dev) -> bool:
+    """Whether the forward's aggregates agg [n_dst, H, C_in] stay alive for the backward's weight
+    gradient G = g^T agg.  The same G is acc^T x (permuted): G[c, (h, k)] = sum_i g_i[c] agg^h_i[k]
+    = sum_i sum_j beta^h_ij g_i[c] x_j[k] = sum_j acc^h_j[c] x_j[k], and the default backward
+    builds acc [n_src, H, C] anyway -- so agg is only worth keeping while memory is not short: the
+    acc^T x form costs an exact column-max pass over acc (4 H C bytes per source) instead of one
+    over g (4 C per destination).  PPGAT_XGAT_AGG=keep / free forces a form; by default agg is
+    dropped when four tensors of its size -- two layers' agg, the backward's hs and acc -- would
+    take more than half of the device's memory: the whole 200M-edge graph on one GPU (61 GB each;
+    tools/mem_probe.py: the agg-free step's peak is 239 GB there), not its 1/8 share (7.7 GB)."""
+    mode = os.environ.get("PPGAT_XGAT_AGG", "auto")
+    if mode == "keep":
+        return True
+    if _xgat_gather_mode(C, H, n_src, n_dst) != "gd":
+        return True  # the gt / g passes read agg in their prologue
+    if mode == "free":
+        return False
+    total = torch.cuda.get_device_properties(dev).total_memory
+    return 4 * (4.0 * H * max(K, C) * max(n_dst, n_src)) <= 0.5 * total
 
 
 def xgat_backward(saved: dict, g: torch.Tensor, want_bias_grad: bool, halo_hook=None):
@@ -1397,8 +1422,10 @@ def _xgat_backward_deferred_d(lib, saved: dict, g, S, dz, nstate, want_bias_grad
         gemm_nn(acc, W, 0, K, alpha=1.0 / H, out=dx, rank=(S, A2))
         if halo_hook is not None:
             halo_hook(dx[n0:])
-    del acc
-    return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
+    if saved["agg"] is not None:
+        del acc
+        return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
+    return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, acc=acc)
 
 
 def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[int] = None, ld: Optional[int] = None):
@@ -1418,14 +1445,23 @@ def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[in
                                          dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
-def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None, xbits=None):
+def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None, xbits=None, acc=None):
     """dW, datt, dbias from G = g^T agg and GV = S^T x (``x_rows``: the rows of x that S covers,
     default all of the layer's source rows; ``xbits``: a precomputed column bound of the source
-    rows of x, colmax_abs bits, e.g. the maximum over the ranks of their own rows')."""
+    rows of x, colmax_abs bits, e.g. the maximum over the ranks of their own rows).  Without a
+    saved agg (_xgat_keep_agg): G from ``acc`` [n_src, H * C] as (acc^T x) permuted."""
     x, W, a_s, a_d, agg, v = saved["x"], saved["W"], saved["a_s"], saved["a_d"], saved["agg"], saved["v"]
     H, C, K, slope, p, seed, has_bias = saved["meta"]
     dev = x.device
     GV = gemm_tn(S, x if x_rows is None else x_rows)[0]
+    if agg is None:
+        _require(acc is not None and x_rows is None, "xgat weight gradients: no agg saved and no acc given")
+        # G'[(h, c), k] = sum_j acc^h_j[c] x_j[k]; B = x with its exact column maxima over ALL rows
+        # (a row without out-edges has acc_j = 0 but its x_j still meets the fp16 split)
+        Gp = gemm_tn_big(acc, x, b_bound=(colmax_abs(x), K, 1.0))
+        G = Gp.view(H, C, K).permute(1, 0, 2).reshape(C, H * K).contiguous()
+        del Gp
+        return (dx,) + _xgat_weight_grads_from_G(lib, saved, G, GV, g, want_bias_grad, st)
     # |agg^h_i[k]| = |sum_j beta_ij x_j[k]| <= max_j |x_j[k]| / (1 - p) over i's sources j (the
     # attention weights sum to 1, the kept ones scaled by 1 / (1 - p)): a column bound of agg from
     # the column maxima of the SOURCE rows of x (1 KB per row; a row with no out-edge -- however
@@ -1434,6 +1470,14 @@ def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_r
     xbound = (colmax_abs(x, v.colptr) if xbits is None else xbits, K,
               (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
     G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound)
+    dW, datt_src, datt_dst, dbias = _xgat_weight_grads_from_G(lib, saved, G, GV, g, want_bias_grad, st)
+    return dx, dW, datt_src, datt_dst, dbias
+
+
+def _xgat_weight_grads_from_G(lib, saved: dict, G, GV, g, want_bias_grad: bool, st):
+    W, a_s, a_d = saved["W"], saved["a_s"], saved["a_d"]
+    H, C, K, slope, p, seed, has_bias = saved["meta"]
+    dev = W.device
     dW = torch.empty_like(W)
     datt_src = torch.empty(H, C, dtype=torch.float32, device=dev)
     datt_dst = torch.empty(H, C, dtype=torch.float32, device=dev)
@@ -1441,7 +1485,7 @@ def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_r
                                            H, C, K, dW.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(), st),
                "xgat_weight_grads")
     dbias = colsum(g) if (has_bias and want_bias_grad) else None
-    return dx, dW, datt_src, datt_dst, dbias
+    return dW, datt_src, datt_dst, dbias
 
 
 class GATLayerX(torch.autograd.Function):

@@ -97,13 +97,16 @@ def _graph(rng, n, e, hub_rows=0):
     return np.stack([src, dst]).astype(np.int64)
 
 
-@pytest.mark.parametrize("gather", ["gd", "g", "gt"])
+@pytest.mark.parametrize("gather", ["gd", "gd-free", "g", "gt"])
 @pytest.mark.parametrize("n,e,C,heads,p,hubs", [(2000, 20_000, 256, 4, 0.0, 0), (1500, 30_000, 256, 4, 0.2, 3),
                                                 (1200, 12_000, 128, 2, 0.1, 0), (900, 25_000, 256, 2, 0.0, 2)])
 def test_gatconv_aggregate_then_transform_vs_oracle(pkg, oracle, cuda, monkeypatch, n, e, C, heads, p, hubs, gather):
     """Both backward edge passes: gathering g_i (hs = x W^T / H per source, acc, dx = acc W / H;
-    ppgat_xgat_bwd_edges_g, C == 256) and gathering gt_i (ppgat_xgat_bwd_edges)."""
-    monkeypatch.setenv("PPGAT_XGAT_GATHER", gather)
+    ppgat_xgat_bwd_edges_g, C == 256) and gathering gt_i (ppgat_xgat_bwd_edges).  "gd-free": the
+    default pass without the forward's aggregates kept -- the weight gradient as acc^T x
+    (hip_ops._xgat_keep_agg, the whole 200M-edge graph on one GPU)."""
+    monkeypatch.setenv("PPGAT_XGAT_GATHER", gather.split("-")[0])
+    monkeypatch.setenv("PPGAT_XGAT_AGG", "free" if gather.endswith("free") else "keep")
     ops = _ops()
     assert ops.xgat_supported(256, heads, C)
     rng = np.random.default_rng(n + heads)
@@ -187,3 +190,46 @@ def test_weight_grad_bound_ignores_rows_without_out_edges(pkg, oracle, cuda):
     assert rel(out, ref) <= 1e-5
     assert rel(conv.lin.weight.grad, P["lin.weight"].grad) <= 1e-5, rel(conv.lin.weight.grad, P["lin.weight"].grad)
     assert rel(x.grad, xr.grad) <= 1e-5
+
+
+def test_agg_free_weight_grad_fp16_path(pkg, oracle, cuda, monkeypatch):
+    """The weight gradient without the forward's aggregates (PPGAT_XGAT_AGG=free, the form the
+    whole 200M-edge graph takes on one GPU): G = (acc^T x) permuted on the fp16 TN kernel (>= 64k
+    rows), acc's column maxima exact, x's over every row.  dW, dx, datt within the usual bounds
+    of the fp64 oracle, and dW within 1e-5 of the default (agg kept) form."""
+    rng = np.random.default_rng(12)
+    n, e, heads, C = 70_000, 600_000, 4, 256
+    ei = np.stack([rng.integers(0, n, e), rng.integers(0, n, e)]).astype(np.int64)
+    torch.manual_seed(6)
+    conv = pkg.GATConv(256, C, heads=heads, dropout=0.1, add_self_loops=False, concat=False)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.1, 0.1)
+    conv = conv.to(cuda).train()
+    x64 = torch.from_numpy(rng.standard_normal((n, 256)))
+    G64 = torch.from_numpy(rng.standard_normal((n, C)))
+    cm = importlib.import_module("plotpointe-gat-recommendation_amd.conv")
+    orig = cm._dropout_seed
+    cm._dropout_seed = lambda: 777
+    grads = {}
+    try:
+        for mode in ("keep", "free"):
+            monkeypatch.setenv("PPGAT_XGAT_AGG", mode)
+            conv.zero_grad(set_to_none=True)
+            x = x64.float().to(cuda).requires_grad_(True)
+            out = conv(x, torch.from_numpy(ei).to(cuda))
+            (out * G64.float().to(cuda)).sum().backward()
+            grads[mode] = {"dx": x.grad.clone(), **{k: v.grad.clone() for k, v in conv.named_parameters()}}
+    finally:
+        cm._dropout_seed = orig
+    P = {k: v.detach().double().requires_grad_(True) for k, v in conv.named_parameters()}
+    xr = x64.to(cuda).requires_grad_(True)
+    ref = oracle.pyg_gat_conv(xr, torch.from_numpy(ei).to(cuda), P["lin.weight"], P["att_src"], P["att_dst"],
+                              P["bias"], heads, dropout_p=0.1, seed=777)
+    (ref * G64.to(cuda)).sum().backward()
+    f = grads["free"]
+    assert rel(f["lin.weight"], P["lin.weight"].grad) <= 1e-5
+    assert rel(f["lin.weight"], grads["keep"]["lin.weight"].double()) <= 1e-5
+    assert rel(f["dx"], xr.grad) <= 1e-5
+    assert torch.equal(f["dx"], grads["keep"]["dx"])          # dx does not involve the weight-gradient form
+    assert rel(f["att_src"], P["att_src"].grad) <= 1e-4 and rel(f["att_dst"], P["att_dst"].grad) <= 1e-4
+    assert rel(f["bias"], P["bias"].grad) <= 1e-4
