@@ -1433,6 +1433,11 @@ __device__ __forceinline__ uint2 ld_tr16(const unsigned char* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// PPGAT_DXW_LAB (lab builds only, results WRONG): 1 = no MFMA work (compute skipped), 2 = no
+// global loads after the first step (registers reused), 4 = no staging after the first step
+#ifndef PPGAT_DXW_LAB
+#define PPGAT_DXW_LAB 0
+#endif
 __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dxw_lds[];
   float* const sS = reinterpret_cast<float*>(dxw_lds + 2 * kDxwBuf);  // [2][32][2]
@@ -1640,14 +1645,14 @@ __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
 
   // one register stage, the loop unrolled by two so each half's LDS buffer is a constant
   for (int st = 0; st < steps; st += 2) {
-    load(rbeg + (int64_t)(st + 1) * kDxwRows, R0);
-    compute(0, rbeg + (int64_t)st * kDxwRows);
-    if (st + 1 < steps) put(1, rbeg + (int64_t)(st + 1) * kDxwRows, R0);
+    if (!(PPGAT_DXW_LAB & 2)) load(rbeg + (int64_t)(st + 1) * kDxwRows, R0);
+    if (!(PPGAT_DXW_LAB & 1)) compute(0, rbeg + (int64_t)st * kDxwRows);
+    if (st + 1 < steps && !(PPGAT_DXW_LAB & 4)) put(1, rbeg + (int64_t)(st + 1) * kDxwRows, R0);
     __syncthreads();
     if (st + 1 >= steps) break;
-    load(rbeg + (int64_t)(st + 2) * kDxwRows, R0);
-    compute(1, rbeg + (int64_t)(st + 1) * kDxwRows);
-    if (st + 2 < steps) put(0, rbeg + (int64_t)(st + 2) * kDxwRows, R0);
+    if (!(PPGAT_DXW_LAB & 2)) load(rbeg + (int64_t)(st + 2) * kDxwRows, R0);
+    if (!(PPGAT_DXW_LAB & 1)) compute(1, rbeg + (int64_t)(st + 1) * kDxwRows);
+    if (st + 2 < steps && !(PPGAT_DXW_LAB & 4)) put(0, rbeg + (int64_t)(st + 2) * kDxwRows, R0);
     __syncthreads();
   }
 

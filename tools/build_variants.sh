@@ -1,8 +1,9 @@
 #!/bin/bash
 # Build experiment variants of libppgat.so that differ in one translation unit:
 #   tools/build_variants.sh SRC NAME:"-DFLAG=1 ..." [NAME2:"..."] ...
-# Each variant: build_variants/NAME/libppgat.so (the other objects from csrc/build).
-# Use with PPGAT_LIB=build_variants/NAME/libppgat.so python tools/bench_gemm.py
+# Each variant: $OUTDIR/NAME/libppgat.so (OUTDIR default build_variants; the other objects from
+# csrc/build).  build_variants/ stays here (.gpurunignore); OUTDIR=lab_build travels to the box.
+# Use with PPGAT_LIB=$OUTDIR/NAME/libppgat.so python tools/bench_gemm.py
 set -e
 cd "$(dirname "$0")/.."
 C=plotpointe-gat-recommendation_amd/csrc
@@ -12,13 +13,14 @@ base=$(basename "$SRC" .hip)
 others=$(ls $C/build/*.o | grep -v "/$base.o")
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  mkdir -p build_variants/$name
+  mkdir -p ${OUTDIR:-build_variants}/$name
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $flags -I$C \
-    -c "$SRC" -o build_variants/$name/$base.o &
+    -c "$SRC" -o ${OUTDIR:-build_variants}/$name/$base.o &
 done
 wait
 for spec in "$@"; do
   name=${spec%%:*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/$name/libppgat.so build_variants/$name/$base.o $others
-  echo "built build_variants/$name/libppgat.so"
+  O=${OUTDIR:-build_variants}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/$name/libppgat.so $O/$name/$base.o $others
+  echo "built $O/$name/libppgat.so"
 done
