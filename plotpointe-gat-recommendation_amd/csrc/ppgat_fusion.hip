@@ -757,10 +757,6 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh(const float* __restrict_
 // waits only for its own DMA (exact per-wave vmcnt counts); b1 / e1 / b2 / e2 are staged in LDS
 // by LDS-DMA ahead of GEMM1, so the h epilogue issues no global load behind the W2 DMAs.
 // ---------------------------------------------------------------------------
-#ifndef PPGAT_XASM
-#define PPGAT_XASM 0
-#endif
-constexpr bool kFusionXasm = PPGAT_XASM != 0;  // GEMM1's x loads untracked (ppgat_nnh_pipe.h gload16)
 constexpr int kH2Bytes = kH2Img * 2;           // one 32-deep W2 slice image
 constexpr int kH2Pieces = kH2Bytes / 1024;     // 1-KB wave copies per slice (20)
 
@@ -810,10 +806,7 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
     const int k0 = c * BK;
     const float* src = k0 < Dt ? trow + k0 : irow + (k0 - Dt);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if constexpr (kFusionXasm) gload16(xv[g], src + 8 * g);
-      else xv[g] = ld4(src + 8 * g);
-    }
+    for (int g = 0; g < 4; ++g) xv[g] = ld4(src + 8 * g);
   };
   const uint32_t voff = (uint32_t)lane * 16u;
   // b1, e1, b2, e2 -> sPar by LDS-DMA (one wave each; older than GEMM1's first DMA, so the loop's
@@ -826,7 +819,7 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh3(const float* __restrict
   // ---- GEMM1: the pipelined fp16 two-term loop (ppgat_nnh_pipe.h), rows scaled online ----
   f32x16 acc[8];
   int erow = 0;
-  nnh3_loop<8, 1, false, 0, false, kFusionXasm>(w1i, lds, chunks, load_x_chunk, acc, erow, sF[w], w, lane);
+  nnh3_loop<8>(w1i, lds, chunks, load_x_chunk, acc, erow, sF[w], w, lane);
 
   // ---- W2 slices 0..3 -> buffers 0..3 beside the patches (the loop ended on a barrier after
   // every wave's last reads of its buffers) ----

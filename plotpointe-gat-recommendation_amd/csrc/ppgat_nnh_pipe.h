@@ -49,23 +49,6 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// 16 B from global memory into v, issued in inline asm: the compiler does not count it, so its
-// own vmcnt waits (before the X registers' first use) cannot also demand the LDS-DMA issued after
-// this load -- with compiler-visible X loads the wait before chunk c + 1's preparation (in chunk
-// c's MFMA sequence) also drained chunk c + 2's DMA, issued at the top of chunk c.  The caller
-// waits explicitly (wait_x) before reading v.
-__device__ __forceinline__ void gload16(float4& v, const float* p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(get_native_vector(v)) : "v"(p));
-}
-
-// s_waitcnt vmcnt(N) that also "rewrites" the four X registers, so no read of them is
-// scheduled before it (XASM loads)
-template <int N>
-__device__ __forceinline__ void wait_x(float4 (&x)[4]) {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(get_native_vector(x[0])), "+v"(get_native_vector(x[1])), "+v"(get_native_vector(x[2])), "+v"(get_native_vector(x[3])) : "n"(N));
-}
-
 // acc (NT 32x32 tiles of this wave's 32 rows) = sum over chunks of X chunk x B chunk, scaled:
 // acc = (X s_row) (B s_col) with erow the row's final exponent (s_row = 2^erow).  img: this
 // column block's chunk images (chunks x NnhImg<NT>::ELEMS); sB: LDS, 3 x ELEMS; sFw: this wave's
@@ -85,9 +68,7 @@ __device__ __forceinline__ void wait_x(float4 (&x)[4]) {
 // wave's LDS scratch sXw [32 rows][36 floats] (4 ds_write_b128 + 4 ds_read_b128 per chunk,
 // conflict-free with the 36-float row stride).  The same values in the same fragment slots: the
 // products are bitwise those of the direct layout.
-// XASM: loadx issues its four loads with gload16 (untracked); the loop waits for X(c + 1) by
-// exact count before its preparation: issued after it are only DMA(c + 2) (if any) and X(c + 2).
-template <int NT, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false, bool XASM = false, class LoadX>
+template <int NT, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false, class LoadX>
 __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int chunks, const LoadX& loadx,
                                           split::f32x16 (&acc)[NT], int& erow, float* sFw, int wv, int lane,
                                           float* sXw = nullptr) {
@@ -175,20 +156,10 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
   if (PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
   float4 xA[4], xB[4];
   split::u32x4 fxA[2][2], fxB[2][2];
-  // X(c + 1) has landed: issued after it, DMA(c + 2) when ahead (ND or ND - 1 instructions of
-  // this wave) and the four loads of X(c + 2)
-  auto xwait = [&](float4 (&x)[4], bool ahead) {
-    if constexpr (XASM) {
-      if (!ahead) wait_x<4>(x);
-      else if (full) wait_x<ND + 4>(x);
-      else wait_x<ND - 1 + 4>(x);
-    }
-  };
   issue(0);
   loadx(0, xA);
   issue(1);
   loadx(1, xB);
-  xwait(xA, true);  // X(0): DMA(1) and X(1) issued after it
 #pragma unroll
   for (int ph = 0; ph < PH; ++ph) prep(ph, xA, fxA);
   commit();
@@ -217,7 +188,6 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
       if (!(LAB & 16) && i + BD < STEPS) read_b(i + BD, fb[(i + BD) % (BD + 1)]);
       acc[t] = split::mfma32_h3(fxc[u], fb[(LAB & 16) ? 0 : i % (BD + 1)], acc[t]);
       if constexpr (NEXT && !(LAB & 32)) {
-        if (i == STEPS / 2) xwait(xn, ahead);
         if (i >= STEPS / 2) {
 #pragma unroll
           for (int k = 0; k < PPS; ++k) prep((i - STEPS / 2) * PPS + k, xn, fxn);
@@ -251,10 +221,6 @@ __device__ __forceinline__ void nnh3_loop(const uint16_t* img, uint16_t* sB, int
   }
   body(chunks - 2, xA, xB, fxA, fxB, yes{});
   body(chunks - 1, xB, xA, fxB, fxA, no{});
-  if constexpr (XASM) {  // the last two bodies' (unused) X re-reads land before any register reuse
-    wait_x<0>(xA);
-    wait_x<0>(xB);
-  }
   if (PRIO && wv >= 4) __builtin_amdgcn_s_setprio(0);
 }
 

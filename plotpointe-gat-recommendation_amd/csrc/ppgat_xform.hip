@@ -599,10 +599,6 @@ __global__ void __launch_bounds__(256) k_nnh_presplit(const float* __restrict__ 
 }
 
 constexpr int kNnhRank = 8;  // rank terms the fused epilogue keeps in registers
-#ifndef PPGAT_XASM
-#define PPGAT_XASM 0
-#endif
-constexpr bool kNnhXasm = PPGAT_XASM != 0;  // X loads untracked by the compiler (ppgat_nnh_pipe.h gload16)
 
 template <int NT, bool RK>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh(NnArg a, const uint16_t* __restrict__ img,
@@ -930,13 +926,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* _
   } else {
     auto loadx = [&](int c, float4 (&x)[4]) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if constexpr (kNnhXasm) gload16(x[g], xrow + c * KC + 8 * g);
-        else x[g] = ld4(xrow + c * KC + 8 * g);
-      }
+      for (int g = 0; g < 4; ++g) x[g] = ld4(xrow + c * KC + 8 * g);
     };
-    nnh3_loop<NT, BD, PRIO, LAB, false, kNnhXasm>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow,
-                                                  sF[wv], wv, lane);
+    nnh3_loop<NT, BD, PRIO, LAB>(img + (int64_t)nb * chunks * I::ELEMS, sB, chunks, loadx, acc, erow, sF[wv], wv,
+                                 lane);
   }
   float fr[16];  // unscale: 1 / (s_row s_col), both exact powers of two
   split::row_unscale(erow, sF[wv], r, hf, fr);
