@@ -262,6 +262,9 @@ def main():
     # gloo rehearsal whose collectives run on the host
     use_graph = args.graph == "on" or (args.graph == "auto" and not (dist_path and args.dist_backend == "gloo"))
     opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=use_graph)
+    # the loss backward's sort on a side stream beside the forward: off by default, measured no
+    # faster inside the captured step (1.890 vs 1.881 ms, profiles/r05/w1_bench.log)
+    bpr_overlap = os.environ.get("PPGAT_BPR_OVERLAP", "0") == "1"
 
     def step():
         model.train()
@@ -275,8 +278,9 @@ def main():
             loss.backward()
             model.allreduce_grads()
         else:
+            prep =pkg.hip_ops.bpr_prepare(N, g.n_users, g.n_items, args.hidden, tu, ti, tj) if bpr_overlap else None
             Z = model(feats, ei)
-            loss = pkg.bpr_loss(Z, g.n_users, tu, ti, tj)
+            loss = pkg.bpr_loss(Z, g.n_users, tu, ti, tj, prepared=prep)
             opt.zero_grad(set_to_none=True)
             loss.backward()
         opt.step()

@@ -229,6 +229,18 @@ int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
                   int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
                   const float* coef, const float* grad_loss, float* grad_Z,
                   void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_bpr_bwd in two calls: the part that depends on the triples only (their destination
+ * rows, sorted; the touched-row marks) and the rest.  The first may run on another stream while
+ * the model computes Z (train_gat_pyg.py:313-322 samples the triples before the forward); the
+ * second must be stream-ordered after it and after ppgat_bpr_fwd, on the same workspace, with
+ * the same sizes, row_map and u, i, j.  Same result as ppgat_bpr_bwd, bit for bit. */
+int ppgat_bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int channels,
+                          const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+                          void* workspace, size_t workspace_bytes, void* stream);
+int ppgat_bpr_bwd_prepared(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                           int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+                           const float* coef, const float* grad_loss, float* grad_Z,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- projection weight gradient ----------------------------------------------
  * Replaces: the weight (and bias) gradient of torch.nn.Linear in GATConv.lin /

@@ -498,6 +498,37 @@ int ppgat_bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
   return PPGAT_OK;
 }
 
+int ppgat_bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int channels,
+                          const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  const float dummy = 0.f;  // check_bpr wants a Z; the prepare never reads one
+  if (int rc = check_bpr(n_users, n_items, channels, n_samples, &dummy, u, i, j, "bpr_bwd_prepare")) return rc;
+  if (row_map == nullptr ? n_rows != n_users + n_items : n_rows < 1)
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd_prepare: n_rows must be n_users + n_items without a row_map");
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_rows, n_samples, channels))
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd_prepare: workspace too small");
+  hipError_t e = ppgat::bpr_bwd_prepare(n_rows, n_users, n_items, row_map, channels, u, i, j, n_samples, workspace,
+                                        workspace_bytes, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "bpr_bwd_prepare");
+  return PPGAT_OK;
+}
+
+int ppgat_bpr_bwd_prepared(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                           int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
+                           const float* coef, const float* grad_loss, float* grad_Z, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_bwd_prepared")) return rc;
+  if (row_map == nullptr ? n_rows != n_users + n_items : n_rows < 1)
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd_prepared: n_rows must be n_users + n_items without a row_map");
+  if (!grad_Z || !grad_loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_bwd_prepared: null pointer");
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_rows, n_samples, channels))
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd_prepared: workspace too small");
+  hipError_t e = ppgat::bpr_bwd_finish(Z, n_rows, n_users, n_items, row_map, channels, u, i, j, n_samples, coef,
+                                       grad_loss, grad_Z, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "bpr_bwd_prepared");
+  return PPGAT_OK;
+}
+
 // workspace covers both GEMM variants (the choice also depends on V's alignment)
 static size_t tn_ws(int64_t n, int m, int k, int nv) {
   const size_t a = ppgat::tn128_workspace_bytes(n), b = ppgat::gemm_tn_workspace_bytes(n, m, k, nv);

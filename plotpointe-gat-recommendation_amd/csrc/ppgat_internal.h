@@ -72,6 +72,12 @@ hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32
 hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
                    const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st);
+hipError_t bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                           const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, void* ws,
+                           size_t ws_bytes, hipStream_t st);
+hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                          int C, const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
+                          const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st);
 size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv);
 hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
                    float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st);

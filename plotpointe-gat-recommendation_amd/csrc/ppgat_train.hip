@@ -675,49 +675,89 @@ hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32
   return hipGetLastError();
 }
 
-hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
-                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
-                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
-  const int64_t N = n_rows;
-  if (S == 0) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_zero_untouched
-  hipError_t err = hipSuccess;
+// the backward's part of the workspace (after the forward's block partials)
+struct BprWs {
+  int32_t *keys, *vals, *skeys, *scid;  // (skeys, scid): where the sorted pairs end up
+  float* slots;
+  void* tmp;
+  uint8_t* touched;
+};
+
+static BprWs bpr_ws(void* ws, int64_t N, int64_t S, int C) {
   const int64_t total = 4 * S;
   const int64_t chunks = (total + kChunk - 1) / kChunk;
   char* p = static_cast<char*>(ws) + align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4);
   const size_t e4 = align_up((size_t)total * 4);
-  int32_t* keys = reinterpret_cast<int32_t*>(p);
-  int32_t* vals = reinterpret_cast<int32_t*>(p + e4);
-  int32_t* skeys = reinterpret_cast<int32_t*>(p + 2 * e4);
-  int32_t* scid = reinterpret_cast<int32_t*>(p + 3 * e4);
-  float* slots = reinterpret_cast<float*>(p + 4 * e4);
-  void* tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
-  uint8_t* touched = static_cast<uint8_t*>(tmp) + rs_workspace_bytes(total, key_bits(N + 1));
+  BprWs w;
+  w.keys = reinterpret_cast<int32_t*>(p);
+  w.vals = reinterpret_cast<int32_t*>(p + e4);
+  const bool in1 = (rs_plan(total, key_bits(N + 1)).passes & 1) != 0;  // odd pass count: in the second pair
+  w.skeys = in1 ? reinterpret_cast<int32_t*>(p + 2 * e4) : w.keys;
+  w.scid = in1 ? reinterpret_cast<int32_t*>(p + 3 * e4) : w.vals;
+  w.slots = reinterpret_cast<float*>(p + 4 * e4);
+  w.tmp = p + 4 * e4 + align_up((size_t)chunks * 2 * C * 4);
+  w.touched = static_cast<uint8_t*>(w.tmp) + rs_workspace_bytes(total, key_bits(N + 1));
+  return w;
+}
+
+// The part of the backward that depends on the triples only (not on Z or the loss): the
+// contributions' destination rows, sorted, and the touched-row bytes.  Launched on its own
+// stream it runs beside the model's forward (bench.py / train.epoch_step).
+hipError_t bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                           const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, void* ws,
+                           size_t ws_bytes, hipStream_t st) {
+  const int64_t N = n_rows;
+  if (S == 0) return hipSuccess;
   if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
-  err = hipMemsetAsync(touched, 0, (size_t)N, st);
+  const int64_t total = 4 * S;
+  const BprWs w = bpr_ws(ws, N, S, C);
+  hipError_t err = hipMemsetAsync(w.touched, 0, (size_t)N, st);
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
-                     n_items, row_map, N, keys, vals);
+                     n_items, row_map, N, w.keys, w.vals);
+  int32_t* k1 = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(w.keys) + 2 * align_up((size_t)total * 4));
+  int32_t* v1 = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(w.keys) + 3 * align_up((size_t)total * 4));
   bool in1 = false;
-  err = rs_sort(keys, vals, skeys, scid, total, key_bits(N + 1), tmp, &in1, st);
+  err = rs_sort(w.keys, w.vals, k1, v1, total, key_bits(N + 1), w.tmp, &in1, st);
   if (err != hipSuccess) return err;
-  if (!in1) {  // even pass count: the result is back in (keys, vals)
-    skeys = keys;
-    scid = vals;
-  }
+  if ((in1 ? k1 : w.keys) != w.skeys) return hipErrorUnknown;  // bpr_ws's parity rule disagrees with rs_sort
+  if (N > 0)
+    hipLaunchKernelGGL(k_bpr_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w.skeys, total, N,
+                       w.touched);
+  return hipGetLastError();
+}
+
+// The rest, after bpr_bwd_prepare on the same workspace (stream-ordered after it).
+hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
+                          int C, const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
+                          const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t N = n_rows;
+  if (S == 0) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_zero_untouched
+  if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
+  const int64_t total = 4 * S;
+  const int64_t chunks = (total + kChunk - 1) / kChunk;
+  const BprWs w = bpr_ws(ws, N, S, C);
   PPGAT_DISPATCH_LOSS_C(C, {
     constexpr int SPB = 256 / (CC / 4);
     const unsigned g = (unsigned)((chunks + SPB - 1) / SPB);
-    hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, skeys, scid, total, u, i, j, n_users, n_items,
-                       row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, slots);
-    hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, skeys, total, slots, N, dZ);
+    hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, w.skeys, w.scid, total, u, i, j, n_users,
+                       n_items, row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, w.slots);
+    hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, w.skeys, total, w.slots, N, dZ);
     if (N > 0) {
-      hipLaunchKernelGGL(k_bpr_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, skeys, total, N, touched);
       int64_t gz = (N + SPB - 1) / SPB;
       if (gz > 4096) gz = 4096;
-      hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, touched, N, dZ);
+      hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, w.touched, N, dZ);
     }
   });
   return hipGetLastError();
+}
+
+hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+                   const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
+                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
+  hipError_t err = bpr_bwd_prepare(n_rows, n_users, n_items, row_map, C, u, i, j, S, ws, ws_bytes, st);
+  if (err != hipSuccess) return err;
+  return bpr_bwd_finish(Z, n_rows, n_users, n_items, row_map, C, u, i, j, S, coef, grad_loss, dZ, ws, ws_bytes, st);
 }
 
 // ---- skinny A^T B (M <= 16): the multi-head layer's GV = S^T x (S = [ds_src | ds_dst], 2H

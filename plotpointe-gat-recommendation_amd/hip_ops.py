@@ -1557,33 +1557,100 @@ def check_bpr_indices():
     _BadIndex.raise_pending(wait=True)
 
 
+_side_streams = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    if dev.index not in _side_streams:
+        _side_streams[dev.index] = torch.cuda.Stream(device=dev)
+    return _side_streams[dev.index]
+
+
+class BprPrepared:
+    """The triple-only half of the loss backward (ppgat_bpr_bwd_prepare), launched on a side
+    stream: made before the model's forward it runs beside it.  Hand it to ``bpr_loss(...,
+    prepared=)`` with the same triples and Z shape; the loss joins the side stream back into
+    the current one after its own forward kernels, so nothing after the loss can see a
+    half-built workspace and the workspace is not freed under the side stream."""
+
+    def __init__(self, n_rows: int, n_users: int, n_items: int, C: int, u, i, j, row_map=None):
+        lib = _lib.load()
+        dev = u.device
+        _require(u.is_cuda, "bpr_prepare: ppgat runs on ROCm devices only; there is no CPU path")
+        if C not in (32, 64, 128, 256):
+            raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
+        self.given = tuple(t.data_ptr() for t in (u, i, j))
+        self.u, self.i, self.j = (t.contiguous().to(torch.int64) for t in (u, i, j))
+        for name, t in (("u", self.u), ("i", self.i), ("j", self.j)):
+            _check_dev(name, t, torch.int64, dev)
+        if row_map is not None:
+            _check_dev("row_map", row_map, torch.int32, dev)
+        self.row_map = row_map
+        self.meta = (int(n_rows), int(n_users), int(n_items), int(C), self.u.numel())
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(lib.ppgat_bpr_workspace_bytes(int(n_rows), self.u.numel(), int(C), ctypes.byref(nbytes)),
+                   "bpr_workspace_bytes")
+        self.ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
+        main = torch.cuda.current_stream(dev)
+        self.side = _side_stream(dev)
+        self.side.wait_stream(main)  # the triples and the workspace come from the current stream
+        _lib.check(lib.ppgat_bpr_bwd_prepare(int(n_rows), int(n_users), int(n_items), _lib.ptr(row_map), int(C),
+                                             self.u.data_ptr(), self.i.data_ptr(), self.j.data_ptr(), self.u.numel(),
+                                             self.ws.data_ptr(), self.ws.numel(), self.side.cuda_stream),
+                   "bpr_bwd_prepare")
+        self.used = False
+
+    def take(self, n_rows, n_users, n_items, C, u, i, j, row_map):
+        """(u, i, j, workspace) of this handle, after checking it was made for exactly this
+        call (the same triple tensors, sizes and row map), once."""
+        _require(not self.used, "bpr_loss: a prepared handle serves one loss call")
+        _require(self.meta == (n_rows, n_users, n_items, C, u.numel())
+                 and self.given == tuple(t.data_ptr() for t in (u, i, j))
+                 and _lib.ptr(row_map) == _lib.ptr(self.row_map),
+                 "bpr_loss: prepared for other triples / sizes")
+        self.used = True
+        return self.u, self.i, self.j, self.ws
+
+
+def bpr_prepare(n_rows: int, n_users: int, n_items: int, C: int, u, i, j, row_map=None) -> BprPrepared:
+    """Start the triple-only half of the loss backward on a side stream (see BprPrepared)."""
+    return BprPrepared(n_rows, n_users, n_items, C, u, i, j, row_map)
+
+
 class _BPRLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map):
+    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map, prep=None):
         lib = _lib.load()
         Z = Z.contiguous()
         _check_dev("Z", Z, torch.float32)
         n_rows, C = Z.shape
         S = u.numel()
+        if prep is not None:
+            u, i, j, ws = prep.take(n_rows, n_users, n_items, C, u, i, j, row_map)
         u, i, j = (t.contiguous().to(torch.int64) for t in (u, i, j))
         for name, t in (("u", u), ("i", i), ("j", j)):
             _check_dev(name, t, torch.int64, Z.device)
         if row_map is not None:
             _check_dev("row_map", row_map, torch.int32, Z.device)
         _BadIndex.raise_pending()
-        nbytes = ctypes.c_size_t(0)
-        _lib.check(lib.ppgat_bpr_workspace_bytes(n_rows, S, C, ctypes.byref(nbytes)), "bpr_workspace_bytes")
-        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=Z.device)
+        if prep is None:
+            nbytes = ctypes.c_size_t(0)
+            _lib.check(lib.ppgat_bpr_workspace_bytes(n_rows, S, C, ctypes.byref(nbytes)), "bpr_workspace_bytes")
+            ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=Z.device)
         loss = torch.empty(1, dtype=torch.float32, device=Z.device)
         coef = torch.empty(max(S, 1), 2, dtype=torch.float32, device=Z.device)
         bad = torch.empty(1, dtype=torch.int32, device=Z.device)
+        # the forward only touches the workspace's block partials, which the prepare leaves alone
         _lib.check(lib.ppgat_bpr_fwd(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(row_map), C, u.data_ptr(),
                                      i.data_ptr(), j.data_ptr(), S, kind, loss.data_ptr(), coef.data_ptr(),
-                                     bad.data_ptr(), ws.data_ptr(), nbytes.value, _lib.stream_handle(Z.device)),
+                                     bad.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(Z.device)),
                    "bpr_fwd")
+        if prep is not None:
+            torch.cuda.current_stream(Z.device).wait_stream(prep.side)
         _BadIndex.track(bad)
         ctx.save_for_backward(Z, u, i, j, coef)
         ctx.ws = ws
+        ctx.prepared = prep is not None
         ctx.row_map = row_map
         ctx.meta = (n_rows, n_users, n_items, C, S)
         return loss[0]
@@ -1596,27 +1663,29 @@ class _BPRLoss(torch.autograd.Function):
         gl = gl.reshape(1).to(torch.float32).contiguous()
         dZ = torch.empty_like(Z)
         ws = ctx.ws
-        _lib.check(lib.ppgat_bpr_bwd(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(ctx.row_map), C, u.data_ptr(),
-                                     i.data_ptr(), j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(),
-                                     ws.data_ptr(), ws.numel(), _lib.stream_handle(Z.device)), "bpr_bwd")
+        fn = lib.ppgat_bpr_bwd_prepared if ctx.prepared else lib.ppgat_bpr_bwd
+        _lib.check(fn(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(ctx.row_map), C, u.data_ptr(), i.data_ptr(),
+                      j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(), ws.numel(),
+                      _lib.stream_handle(Z.device)), "bpr_bwd")
         ctx.ws = None
-        return dZ, None, None, None, None, None, None, None
+        return dZ, None, None, None, None, None, None, None, None
 
 
-def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch.Tensor:
-    """Fused loss of train_gat_pyg.py:313-322 (``loss`` in {"bpr", "bce"})."""
+def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr", prepared: BprPrepared = None) -> torch.Tensor:
+    """Fused loss of train_gat_pyg.py:313-322 (``loss`` in {"bpr", "bce"}); ``prepared`` from
+    ``bpr_prepare`` (made before the forward) moves the backward's sort off the critical path."""
     _require(Z.is_cuda, "bpr_loss: ppgat runs on ROCm devices only; there is no CPU path")
     if Z.size(1) not in (32, 64, 128, 256):
         raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
-    return _BPRLoss.apply(Z, u, i, j, int(n_users), Z.size(0) - int(n_users), LOSS_KINDS[loss], None)
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), Z.size(0) - int(n_users), LOSS_KINDS[loss], None, prepared)
 
 
 def bpr_loss_mapped(Z: torch.Tensor, n_users: int, n_items: int, row_map: torch.Tensor, u, i, j,
-                    loss: str = "bpr") -> torch.Tensor:
+                    loss: str = "bpr", prepared: BprPrepared = None) -> torch.Tensor:
     """bpr_loss over a Z whose rows are laid out by row_map (node id -> row)."""
     if Z.size(1) not in (32, 64, 128, 256):
         raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
-    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map)
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map, prepared)
 
 
 # ---------------------------------------------------------------------------

@@ -67,7 +67,8 @@ class CustomGAT(torch.nn.Module):
         return _stack(self.user_emb.weight, self.item_proj, item_feats, self.layers, edge_index)
 
 
-def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr") -> torch.Tensor:
+def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr", prepared=None) -> torch.Tensor:
     """Loss of the train step, scripts/train_gat_pyg.py:313-322 (BPR or BCE), fused on the
-    device (ppgat_bpr_fwd / ppgat_bpr_bwd)."""
-    return hip_ops.bpr_loss(Z, n_users, u, i, j, loss)
+    device (ppgat_bpr_fwd / ppgat_bpr_bwd; with ``prepared`` from ``hip_ops.bpr_prepare`` the
+    backward's triple sort has already run beside the forward)."""
+    return hip_ops.bpr_loss(Z, n_users, u, i, j, loss, prepared=prepared)

@@ -141,9 +141,16 @@ def build_model(cfg: Config, n_users: int, n_items: int, feat_dim: int):
 def epoch_step(model, opt, item_feats, edge_index, n_users: int, u, i, j, loss: str = "bpr"):
     """One epoch's optimisation step on one GPU (train_gat_custom.py:349-362, identical
     train_gat_pyg.py:307-323): the training forward over the whole graph, the BPR/BCE loss of
-    the epoch's sampled triples, zero_grad, backward, ``opt.step()``.  Returns the loss."""
+    the epoch's sampled triples, zero_grad, backward, ``opt.step()``.  Returns the loss.
+    ``PPGAT_BPR_OVERLAP=1`` starts the loss backward's triple sort (it needs the triples only)
+    on a side stream before the forward (hip_ops.bpr_prepare; measured no faster at config 2,
+    DESIGN.md section 4)."""
+    prep = None
+    if os.environ.get("PPGAT_BPR_OVERLAP", "0") == "1":
+        C = model.user_emb.weight.size(1)
+        prep = model_mod.hip_ops.bpr_prepare(n_users + model.n_items, n_users, model.n_items, C, u, i, j)
     Z = model(item_feats, edge_index)
-    lo = model_mod.bpr_loss(Z, n_users, u, i, j, loss)
+    lo = model_mod.bpr_loss(Z, n_users, u, i, j, loss, prepared=prep)
     opt.zero_grad()
     lo.backward()
     opt.step()

@@ -170,6 +170,47 @@ def test_bpr_sparse_keys_zero_untouched_rows(pkg, oracle, cuda):
     assert int((Zd.grad != 0).any(1).sum()) <= 3 * S
 
 
+@pytest.mark.parametrize("n_users,n_items,S,C,mapped", [(3000, 500, 20_000, 128, False), (1_100_000, 2_000, 30_000, 32,
+                                                                                        False),
+                                                         (3000, 500, 20_000, 256, True), (50, 40, 0, 64, False),
+                                                         (7, 5, 1, 32, True)])
+def test_bpr_prepared_bitwise(pkg, cuda, n_users, n_items, S, C, mapped):
+    """ppgat_bpr_bwd_prepare on a side stream (started before Z exists) + ppgat_bpr_bwd_prepared
+    == the one-call ppgat_bpr_bwd, bit for bit: 2- and 3-pass sorts (odd/even pass parity of the
+    sorted pairs' home), a row map with unheld users (-1), no triples at all."""
+    from importlib import import_module
+    ops = import_module("plotpointe-gat-recommendation_amd.hip_ops")
+    rng = np.random.default_rng(S + C)
+    u, i, j = (torch.from_numpy(rng.integers(0, n, S)).to(cuda) for n in (n_users, n_items, n_items))
+    N = n_users + n_items
+    row_map = None
+    if mapped:
+        perm = rng.permutation(N + 3)[:N].astype(np.int32)
+        perm[rng.random(N) < 0.2] = -1                     # users not held here
+        perm[n_users:] = np.abs(perm[n_users:])          # items always held
+        row_map = torch.from_numpy(perm).to(cuda)
+        n_rows = N + 3
+    else:
+        n_rows = N
+    Z0 = torch.from_numpy(rng.standard_normal((n_rows, C)).astype(np.float32) * 0.3).to(cuda)
+    grads, losses = [], []
+    for use_prep in (False, True):
+        Z = Z0.clone()
+        prep = ops.bpr_prepare(n_rows, n_users, n_items, C, u, i, j, row_map) if use_prep else None
+        torch.cuda._sleep(2_000_000) if use_prep else None   # the forward still running on the main stream
+        Z = (Z * 1.0).requires_grad_(True)
+        L = (ops.bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, prepared=prep) if mapped
+             else ops.bpr_loss(Z, n_users, u, i, j, prepared=prep))
+        (L * 2.0).backward()
+        grads.append(Z.grad.clone())
+        losses.append(L.detach().clone())
+    assert torch.equal(grads[0], grads[1]) and torch.equal(losses[0], losses[1])
+    prep = ops.bpr_prepare(n_rows, n_users, n_items, C, u, i, j, row_map)
+    with pytest.raises(RuntimeError):                      # other triples / sizes than prepared
+        ops.bpr_loss_mapped(Z0, n_users, n_items + 1 if S == 0 else n_items, row_map, u.clone(), i, j, prepared=prep)
+    torch.cuda.synchronize()
+
+
 def _two_layer_grads(pkg, cuda, steps=1, zero=True):
     g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
     ei = torch.from_numpy(g.edge_index_numpy()).to(cuda)
