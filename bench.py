@@ -278,7 +278,7 @@ def main():
             loss.backward()
             model.allreduce_grads()
         else:
-            prep =pkg.hip_ops.bpr_prepare(N, g.n_users, g.n_items, args.hidden, tu, ti, tj) if bpr_overlap else None
+            prep = pkg.hip_ops.bpr_prepare(N, g.n_users, g.n_items, args.hidden, tu, ti, tj) if bpr_overlap else None
             Z = model(feats, ei)
             loss = pkg.bpr_loss(Z, g.n_users, tu, ti, tj, prepared=prep)
             opt.zero_grad(set_to_none=True)

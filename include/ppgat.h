@@ -296,6 +296,20 @@ int ppgat_project_bwd_fused(const float* D, int64_t ldd, const float* S, int64_t
                             const float* x1, int64_t ldx1, int64_t split, int64_t n, int k, const float* w,
                             int64_t ldw, const float* att_src, const float* att_dst, float* dx, int64_t lddx,
                             float* G, float* GV, void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_project_bwd_fused (dx required) that also does the backward prologue of the layer that
+ * produced x, when x IS that layer's output (heads = 1, no op in between: the stacked convs of
+ * train_gat_pyg.py:86-87) and dx is its whole grad_out -- ppgat_bwd_prologue's outputs for that
+ * layer, from dx while it is still on chip instead of a second pass over dx and x:
+ *   prev_nstate[r] = {prev_s_dst[r], prev_m[r], prev_inv_l[r], prev_gscale <dx_r, x_r - prev_bias>}
+ *   prev_grad_bias = sum_r dx_r                       (prev_bias / prev_grad_bias nullable)
+ * Same dx, G, GV as ppgat_project_bwd_fused, bit for bit; deterministic. */
+int ppgat_project_bwd_fused_producer(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0,
+                                     int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int k,
+                                     const float* w, int64_t ldw, const float* att_src, const float* att_dst,
+                                     float* dx, int64_t lddx, float* G, float* GV, const float* prev_bias,
+                                     const float* prev_s_dst, const float* prev_m, const float* prev_inv_l,
+                                     float prev_gscale, float* prev_nstate, float* prev_grad_bias, void* workspace,
+                                     size_t workspace_bytes, void* stream);
 /* Weight and attention-vector gradients from G = dh_msg^T x [H*C, K] and
  * GV = [ds_src^T x ; ds_dst^T x] [2H, K] (ppgat_gemm_tn with V):
  *   dW = G + att_src (x) GV[:H] + att_dst (x) GV[H:],  datt_src[h] = W_h GV[h],  datt_dst[h] = W_h GV[H + h]. */

@@ -79,6 +79,9 @@ SIGNATURES = {
     "ppgat_project_bwd_fused_workspace_bytes": (c_int, [c_i64, ctypes.POINTER(c_sz)]),
     "ppgat_project_bwd_fused": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_vp,
                                         c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_project_bwd_fused_producer": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64,
+                                                 c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                                 c_vp, c_vp, c_f, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "ppgat_adam_max_tensors": (c_int, []),
     "ppgat_adam_step": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double,

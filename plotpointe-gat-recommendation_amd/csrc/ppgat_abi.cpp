@@ -625,10 +625,11 @@ int ppgat_project_bwd_fused_workspace_bytes(int64_t n, size_t* bytes) {
   return PPGAT_OK;
 }
 
-int ppgat_project_bwd_fused(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0,
-                            const float* x1, int64_t ldx1, int64_t split, int64_t n, int k, const float* w,
-                            int64_t ldw, const float* att_src, const float* att_dst, float* dx, int64_t lddx,
-                            float* G, float* GV, void* workspace, size_t workspace_bytes, void* stream) {
+static int project_bwd_fused_impl(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0,
+                                  int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int k,
+                                  const float* w, int64_t ldw, const float* att_src, const float* att_dst, float* dx,
+                                  int64_t lddx, float* G, float* GV, const ppgat::DxwProducer* prod, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
   if (!ppgat::dxw_ok(k, k)) return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_fused: needs k == 128 and the split GEMMs");
   if (n < 0 || split < 0 || split > n) return fail(PPGAT_ERR_INVALID, "project_bwd_fused: bad sizes");
   if (ldd < k || (ldd % 4) || ldx0 < k || (ldx0 % 4) || (x1 && (ldx1 < k || (ldx1 % 4))) || ldw < k ||
@@ -643,9 +644,33 @@ int ppgat_project_bwd_fused(const float* D, int64_t ldd, const float* S, int64_t
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_PROJ_BWD, st);
   hipError_t e = ppgat::dxw(D, ldd, S, lds, x0, ldx0, x1, ldx1, x1 ? split : n, n, w, ldw, att_src, att_dst, dx, lddx,
-                            G, GV, workspace, st);
+                            G, GV, workspace, st, prod);
   if (e != hipSuccess) return hip_fail(e, "project_bwd_fused");
   return PPGAT_OK;
+}
+
+int ppgat_project_bwd_fused(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0,
+                            const float* x1, int64_t ldx1, int64_t split, int64_t n, int k, const float* w,
+                            int64_t ldw, const float* att_src, const float* att_dst, float* dx, int64_t lddx,
+                            float* G, float* GV, void* workspace, size_t workspace_bytes, void* stream) {
+  return project_bwd_fused_impl(D, ldd, S, lds, x0, ldx0, x1, ldx1, split, n, k, w, ldw, att_src, att_dst, dx, lddx, G,
+                                GV, nullptr, workspace, workspace_bytes, stream);
+}
+
+int ppgat_project_bwd_fused_producer(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0,
+                                     int64_t ldx0, const float* x1, int64_t ldx1, int64_t split, int64_t n, int k,
+                                     const float* w, int64_t ldw, const float* att_src, const float* att_dst,
+                                     float* dx, int64_t lddx, float* G, float* GV, const float* prev_bias,
+                                     const float* prev_s_dst, const float* prev_m, const float* prev_inv_l,
+                                     float prev_gscale, float* prev_nstate, float* prev_grad_bias, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (n > 0 && (!dx || !prev_s_dst || !prev_m || !prev_inv_l || !prev_nstate))
+    return fail(PPGAT_ERR_INVALID, "project_bwd_fused_producer: dx and the producer's state are required");
+  if ((prev_nstate && !al16(prev_nstate)) || (prev_bias && !al16(prev_bias)) || (prev_grad_bias && !al16(prev_grad_bias)))
+    return fail(PPGAT_ERR_UNSUPPORTED, "project_bwd_fused_producer: nstate / bias 16-byte aligned");
+  const ppgat::DxwProducer prod{prev_bias, prev_s_dst, prev_m, prev_inv_l, prev_gscale, prev_nstate, prev_grad_bias};
+  return project_bwd_fused_impl(D, ldd, S, lds, x0, ldx0, x1, ldx1, split, n, k, w, ldw, att_src, att_dst, dx, lddx, G,
+                                GV, &prod, workspace, workspace_bytes, stream);
 }
 
 int ppgat_weight_grads(const float* G, const float* GV, const float* w, const float* att_src, const float* att_dst,

@@ -1378,7 +1378,7 @@ constexpr int kDxwWaves = 8;
 constexpr int kDxwRows = 32;                        // rows per step
 constexpr int kDxwImg = kDxwRows * kPT * 2;         // bytes per bf16 term image (8 KB)
 constexpr int kDxwBuf = 6 * kDxwImg;                // D and x, three terms each (48 KB)
-constexpr size_t kDxwLds = 2 * kDxwBuf + (2 * kDxwRows * 2 + 2 * kPT) * sizeof(float);
+constexpr size_t kDxwLds = 2 * kDxwBuf + (2 * kDxwRows * 2 + 2 * kPT + 2 * kDxwWaves * kDxwRows) * sizeof(float);
 
 struct DxwArg {
   const float* D;   // [n, 128] at ldd
@@ -1400,6 +1400,16 @@ struct DxwArg {
   int64_t rows_per_wg;
   float* part;      // [gridDim.x][128][128]
   float* vpart;     // [gridDim.x][2][128]
+  // the producer layer's backward prologue (x = its output, heads = 1), from dx = its grad_out:
+  // pnstate[r] = {p_sdst, p_m, p_invl, pgscale <dx_r, x_r - p_bias>}; pbpart = block partial
+  // column sums of dx (its dbias).  pnstate NULL: off.
+  const float* p_bias;  // nullable
+  const float* p_sdst;
+  const float* p_m;
+  const float* p_invl;
+  float pgscale;
+  float4* pnstate;
+  float* pbpart;        // nullable: [gridDim.x][128]
 };
 
 struct DxwRegs {
@@ -1442,6 +1452,7 @@ __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dxw_lds[];
   float* const sS = reinterpret_cast<float*>(dxw_lds + 2 * kDxwBuf);  // [2][32][2]
   float* const sA = sS + 2 * kDxwRows * 2;                            // [2][128]: A_src, A_dst
+  float* const sDp = sA + 2 * kPT;  // [2][waves][32]: per-wave partial <dx_r, x_r - p_bias> (producer prologue)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int jl = lane & 15, kq = lane >> 4;  // dx lane roles
@@ -1567,6 +1578,12 @@ __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
     }
   }
 
+  // producer prologue (a.pnstate): this lane's 4 dx columns of p_bias, and its column sums of dx
+  const bool pro = want_dx && a.pnstate != nullptr;
+  const float4 pbias = (pro && a.p_bias) ? *reinterpret_cast<const float4*>(a.p_bias + 16 * w + 4 * kq)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 pbsum = make_float4(0.f, 0.f, 0.f, 0.f);
+
   // One step's 12 MFMA groups in a fixed order -- dx (rb, s) for 8 groups, then G (ks, i) --
   // each group's LDS reads issued one group ahead, during the previous group's MFMAs.
   auto compute = [&](const int b, int64_t row0) {
@@ -1619,6 +1636,26 @@ __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
           const float4 o = make_float4(fmaf(dv.y, vb.x, fmaf(dv.x, va.x, acc[0])), fmaf(dv.y, vb.y, fmaf(dv.x, va.y, acc[1])),
                                        fmaf(dv.y, vb.z, fmaf(dv.x, va.z, acc[2])), fmaf(dv.y, vb.w, fmaf(dv.x, va.w, acc[3])));
           if (row < rend) st4(a.dx + row * a.lddx + c0, o);
+          if (pro) {
+            // x[row][c0 .. +3] = hi + mid + lo of its bf16 images (the three-term split is exact);
+            // rows past rend were staged as zeros, so o = 0 there and they add nothing
+            const unsigned char* xi = img + 3 * kDxwImg + dxw_off(lr, c0 >> 3) + 8 * ((c0 >> 2) & 1);
+            const uint2 th = *reinterpret_cast<const uint2*>(xi);
+            const uint2 tm = *reinterpret_cast<const uint2*>(xi + kDxwImg);
+            const uint2 tl = *reinterpret_cast<const uint2*>(xi + 2 * kDxwImg);
+            const float x0v = (split::bf_lo(th.x) + split::bf_lo(tm.x)) + split::bf_lo(tl.x);
+            const float x1v = (split::bf_hi(th.x) + split::bf_hi(tm.x)) + split::bf_hi(tl.x);
+            const float x2v = (split::bf_lo(th.y) + split::bf_lo(tm.y)) + split::bf_lo(tl.y);
+            const float x3v = (split::bf_hi(th.y) + split::bf_hi(tm.y)) + split::bf_hi(tl.y);
+            float d = o.x * (x0v - pbias.x);
+            d = fmaf(o.y, x1v - pbias.y, d);
+            d = fmaf(o.z, x2v - pbias.z, d);
+            d = fmaf(o.w, x3v - pbias.w, d);
+            d += __shfl_xor(d, 16);  // (kq 0 + 1) and (2 + 3), then their sum: the same bits in every lane
+            d += __shfl_xor(d, 32);
+            if (kq == 0) sDp[(b * kDxwWaves + w) * kDxwRows + lr] = d;
+            pbsum = make_float4(pbsum.x + o.x, pbsum.y + o.y, pbsum.z + o.z, pbsum.w + o.w);
+          }
           acc = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -1643,17 +1680,53 @@ __global__ void __launch_bounds__(64 * kDxwWaves, 1) k_dxw(DxwArg a) {
     accg[1] = mfma32_x6(fa[1], fb[1], accg[1]);
   };
 
+  // producer prologue of a finished step (after its barrier): the 8 wave partials of each row
+  // in wave order, packed with the producer's forward state (buffer b is next written two
+  // barriers later)
+  // (the producer's forward state of a step's rows is loaded one step ahead, so the wave that
+  // packs it never waits on HBM in front of the next barrier)
+  float pf_s = 0.f, pf_m = 0.f, pf_l = 0.f;
+  auto pro_pref = [&](int64_t row0) {
+    const int64_t row = min(row0 + tid, rend - 1);
+    pf_s = a.p_sdst[row];
+    pf_m = a.p_m[row];
+    pf_l = a.p_invl[row];
+  };
+  if (pro && tid < kDxwRows) pro_pref(rbeg);
+  auto pro_fin = [&](const int b, int64_t row0) {
+    if (!pro || tid >= kDxwRows) return;
+    const int64_t row = row0 + tid;
+    if (row < rend) {
+      const float* s = sDp + b * kDxwWaves * kDxwRows + tid;
+      float d = s[0];
+#pragma unroll
+      for (int q = 1; q < kDxwWaves; ++q) d += s[q * kDxwRows];
+      a.pnstate[row] = make_float4(pf_s, pf_m, pf_l, d * a.pgscale);
+    }
+    pro_pref(row0 + kDxwRows);
+  };
+
   // one register stage, the loop unrolled by two so each half's LDS buffer is a constant
   for (int st = 0; st < steps; st += 2) {
     if (!(PPGAT_DXW_LAB & 2)) load(rbeg + (int64_t)(st + 1) * kDxwRows, R0);
     if (!(PPGAT_DXW_LAB & 1)) compute(0, rbeg + (int64_t)st * kDxwRows);
     if (st + 1 < steps && !(PPGAT_DXW_LAB & 4)) put(1, rbeg + (int64_t)(st + 1) * kDxwRows, R0);
     __syncthreads();
+    pro_fin(0, rbeg + (int64_t)st * kDxwRows);
     if (st + 1 >= steps) break;
     if (!(PPGAT_DXW_LAB & 2)) load(rbeg + (int64_t)(st + 2) * kDxwRows, R0);
     if (!(PPGAT_DXW_LAB & 1)) compute(1, rbeg + (int64_t)(st + 1) * kDxwRows);
     if (st + 2 < steps && !(PPGAT_DXW_LAB & 4)) put(0, rbeg + (int64_t)(st + 2) * kDxwRows, R0);
     __syncthreads();
+    pro_fin(1, rbeg + (int64_t)(st + 1) * kDxwRows);
+  }
+  if (pro && a.pbpart != nullptr) {  // column sums of dx over this workgroup's rows: the 16 row lanes, fixed tree
+    float t[4] = {pbsum.x, pbsum.y, pbsum.z, pbsum.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int sh = 1; sh < 16; sh <<= 1) t[e] += __shfl_xor(t[e], sh);
+    if (jl == 0) st4(a.pbpart + (int64_t)blockIdx.x * kPT + 16 * w + 4 * kq, make_float4(t[0], t[1], t[2], t[3]));
   }
 
   // ---- partials: G straight from the accumulators, GV through LDS in row-lane order ----
@@ -1862,15 +1935,17 @@ bool dxw_ok(int hc, int k) { return gemm_split_enabled() && hc == kPT && k == kP
 
 size_t dxw_workspace_bytes(int64_t n) {
   const int64_t nb = dxw_blocks(n);
-  return align_up((size_t)nb * kPT * kPT * 4) + align_up((size_t)nb * 2 * kPT * 4);
+  return align_up((size_t)nb * kPT * kPT * 4) + align_up((size_t)nb * 2 * kPT * 4) + align_up((size_t)nb * kPT * 4);
 }
 
 hipError_t dxw(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0, const float* x1,
                int64_t ldx1, int64_t split, int64_t n, const float* W, int64_t ldw, const float* att_src,
-               const float* att_dst, float* dx, int64_t lddx, float* G, float* GV, void* ws, hipStream_t st) {
+               const float* att_dst, float* dx, int64_t lddx, float* G, float* GV, void* ws, hipStream_t st,
+               const DxwProducer* prod) {
   if (n <= 0) {
     hipError_t e = hipMemsetAsync(G, 0, (size_t)kPT * kPT * 4, st);
     if (e == hipSuccess) e = hipMemsetAsync(GV, 0, (size_t)2 * kPT * 4, st);
+    if (e == hipSuccess && prod && prod->grad_bias) e = hipMemsetAsync(prod->grad_bias, 0, (size_t)kPT * 4, st);
     return e;
   }
   static const bool attr = [] {
@@ -1888,12 +1963,21 @@ hipError_t dxw(const float* D, int64_t ldd, const float* S, int64_t lds, const f
   a.rows_per_wg = rpw;
   a.part = reinterpret_cast<float*>(p);
   a.vpart = reinterpret_cast<float*>(p + align_up((size_t)dxw_blocks(n) * kPT * kPT * 4));
+  if (prod != nullptr && dx != nullptr) {
+    a.p_bias = prod->bias; a.p_sdst = prod->s_dst; a.p_m = prod->m; a.p_invl = prod->inv_l;
+    a.pgscale = prod->gscale;
+    a.pnstate = reinterpret_cast<float4*>(prod->nstate);
+    a.pbpart = prod->grad_bias ? reinterpret_cast<float*>(p + align_up((size_t)dxw_blocks(n) * kPT * kPT * 4) +
+                                                          align_up((size_t)dxw_blocks(n) * 2 * kPT * 4))
+                               : nullptr;
+  }
   hipLaunchKernelGGL(k_dxw, dim3((unsigned)nb), dim3(64 * kDxwWaves), kDxwLds, st, a);
   TnReduceArg ra{};
   ra.part = a.part; ra.vpart = a.vpart; ra.cpart = nullptr; ra.splits = nb; ra.M = kPT; ra.K = kPT; ra.nv = 2;
   ra.out = G; ra.vout = GV; ra.colsum = nullptr;
   const int64_t elems = kPT * kPT + 2 * kPT;
   hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((elems + 63) / 64)), dim3(1024), 0, st, ra);
+  if (a.pbpart != nullptr) return launch_col_reduce(a.pbpart, nb, kPT, kPT, prod->grad_bias, nullptr, st);
   return hipGetLastError();
 }
 

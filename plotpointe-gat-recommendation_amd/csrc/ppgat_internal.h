@@ -98,9 +98,20 @@ hipError_t wgrad_assemble(const float* G, const float* GV, const float* W, const
                           int heads, int C, int K, float* dW, float* datt_src, float* datt_dst, hipStream_t st);
 bool dxw_ok(int hc, int k);
 size_t dxw_workspace_bytes(int64_t n);
+// the backward prologue of the layer that produced x (heads = 1), fused into k_dxw's epilogue
+struct DxwProducer {
+  const float* bias;  // nullable
+  const float* s_dst;
+  const float* m;
+  const float* inv_l;
+  float gscale;
+  float* nstate;      // [n, 4]
+  float* grad_bias;   // nullable: [128]
+};
 hipError_t dxw(const float* D, int64_t ldd, const float* S, int64_t lds, const float* x0, int64_t ldx0, const float* x1,
                int64_t ldx1, int64_t split, int64_t n, const float* W, int64_t ldw, const float* att_src,
-               const float* att_dst, float* dx, int64_t lddx, float* G, float* GV, void* ws, hipStream_t st);
+               const float* att_dst, float* dx, int64_t lddx, float* G, float* GV, void* ws, hipStream_t st,
+               const DxwProducer* prod = nullptr);
 int adam_max_tensors();
 hipError_t dropout_epoch(int set, uint64_t value, hipStream_t st);
 // replicated-item merge (ppgat_dist.hip): phase 0 max, 1 pack, 2 finish

@@ -924,8 +924,9 @@ __global__ void __launch_bounds__(256) k_bwd_epi(const int32_t* __restrict__ row
 }
 
 // Ordered column reduction of block partials [rows, cols] -> out_a[0:split], out_b[0:cols-split].
-// One 1024-thread block per 64 columns: wave w sums rows w, w+16, ... (4 loads in flight);
-// then the 16 wave sums are added in wave order.
+// One 1024-thread block per 64 columns: wave w sums rows w, w+16, ... in that order (16 loads
+// in flight: the few hundred partial rows of a launch are one or two HBM round trips, not a
+// chain of them); then the 16 wave sums are added in wave order.
 __global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ partial, int64_t rows, int cols,
                                                      int split, float* __restrict__ out_a,
                                                      float* __restrict__ out_b) {
@@ -935,10 +936,12 @@ __global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ p
   float s = 0.f;
   if (c < cols) {
     int64_t r = wv;
-    for (; r + 48 < rows; r += 64) {
-      const float a = partial[r * cols + c], b = partial[(r + 16) * cols + c];
-      const float d = partial[(r + 32) * cols + c], e = partial[(r + 48) * cols + c];
-      s += a; s += b; s += d; s += e;
+    for (; r + 15 * 16 < rows; r += 16 * 16) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = partial[(r + 16 * k) * cols + c];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += v[k];
     }
     for (; r < rows; r += 16) s += partial[r * cols + c];
   }

@@ -555,6 +555,26 @@ def _run_on_side(dev, inputs, fn):
     return outs
 
 
+def _producer_fusion_enabled() -> bool:
+    """The producer layer's backward prologue inside this layer's dx kernel
+    (ppgat_project_bwd_fused_producer); PPGAT_PRODUCER_PROLOGUE=0 runs it separately."""
+    return _fused_dxw_enabled() and os.environ.get("PPGAT_PRODUCER_PROLOGUE", "1") != "0"
+
+
+def _producer_of(x: torch.Tensor, N: int):
+    """The backward node of the GATLayer whose output x is -- nothing in between, x unmodified
+    since -- when that layer (heads = 1, no replicated rows) can hand its backward prologue to
+    the consumer's dx kernel; else None."""
+    node = x.grad_fn
+    if node is None or not isinstance(node, GATLayer._backward_cls):
+        return None
+    if getattr(node, "pro_state", None) is None or x.size(0) != N or x.size(1) != 128:
+        return None
+    if getattr(node, "out_version", None) != x._version:
+        return None
+    return node
+
+
 class GATLayer(torch.autograd.Function):
     """One whole GAT layer x -> out with the projection inside:
     forward  h = x W^T with the node scores fused (ppgat_project; BLAS + ppgat_node_scores
@@ -570,6 +590,7 @@ class GATLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, heads: int, channels: int, mode: int,
                 slope: float, dropout_p: float, seed: int, x_items=None, rep=None):
+        x_arg = x
         x = x.contiguous()
         x_items = x_items.contiguous() if x_items is not None else None
         W = weight.detach().contiguous()
@@ -620,6 +641,13 @@ class GATLayer(torch.autograd.Function):
         ctx.meta = (heads, channels, mode, slope, dropout_p, seed, bias is not None, agg is not None, fused,
                     x_items is not None, had_items, split)
         ctx.att_shapes = (att_src.shape, att_dst.shape)
+        # x straight from another heads = 1 layer (the stacked convs, train_gat_pyg.py:86-87): this
+        # layer's dx kernel also does that layer's backward prologue (_producer_of)
+        ctx.producer = _producer_of(x_arg, N=h.size(0)) if (need and fused and rep is None and x_items is None
+                                                            and _producer_fusion_enabled()) else None
+        ctx.pro_state = (b, s_dst, m, inv_l) if (need and heads == 1 and rep is None and agg is None) else None
+        ctx.pro_result = None
+        ctx.out_version = out._version
         return out
 
     @staticmethod
@@ -661,7 +689,14 @@ class GATLayer(torch.autograd.Function):
 
         D = torch.empty(N, HC, dtype=torch.float32, device=dev)
         S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
-        if rep is None:
+        pre, ctx.pro_result = ctx.pro_result, None
+        if (rep is None and pre is not None and pre[0] == g_out.data_ptr() and pre[1] == g_out._version
+                and (not want_db or pre[3] is not None)):
+            # the consumer layer's dx kernel already did this prologue (ppgat_project_bwd_fused_producer)
+            nstate = pre[2]
+            dbias = pre[3] if want_db else None
+            _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed, ctx.seed_buf)
+        elif rep is None:
             prologue(0, N, dbias)
             _bwd_edges_dst(g, h, s_src, nstate, g_out, D, S, heads, C, mode, slope, p, seed, ctx.seed_buf)
         else:  # the replicated item rows enter dbias on one rank only
@@ -697,11 +732,24 @@ class GATLayer(torch.autograd.Function):
             x0, x1, sp = (x, xi, split) if seg else (x, None, N)
             if seg and split == 0:  # no user rows: every row from the item segment
                 x0, x1, sp = xi, None, N
-            _lib.check(lib.ppgat_project_bwd_fused(D.data_ptr(), HC, S.data_ptr(), 2, x0.data_ptr(), K, _lib.ptr(x1),
-                                                   K, sp, N, K, W.data_ptr(), K, a_s.data_ptr(),
-                                                   a_d.data_ptr(), _lib.ptr(dx), K, G.data_ptr(), GV.data_ptr(),
-                                                   ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)),
-                       "project_bwd_fused")
+            prod = ctx.producer
+            if prod is not None and dx is not None and prod.pro_state is not None:
+                # also the producer layer's prologue: its nstate and dbias from dx (= its grad_out)
+                pb, ps_dst, pm, pinv_l = prod.pro_state
+                p_nstate = torch.empty(N, 1, 4, dtype=torch.float32, device=dev)
+                p_dbias = torch.empty(K, dtype=torch.float32, device=dev) if pb is not None else None
+                _lib.check(lib.ppgat_project_bwd_fused_producer(
+                    D.data_ptr(), HC, S.data_ptr(), 2, x0.data_ptr(), K, _lib.ptr(x1), K, sp, N, K, W.data_ptr(), K,
+                    a_s.data_ptr(), a_d.data_ptr(), dx.data_ptr(), K, G.data_ptr(), GV.data_ptr(), _lib.ptr(pb),
+                    ps_dst.data_ptr(), pm.data_ptr(), pinv_l.data_ptr(), 1.0, p_nstate.data_ptr(), _lib.ptr(p_dbias),
+                    ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "project_bwd_fused_producer")
+                prod.pro_result = (dx.data_ptr(), dx._version, p_nstate, p_dbias)
+            else:
+                _lib.check(lib.ppgat_project_bwd_fused(D.data_ptr(), HC, S.data_ptr(), 2, x0.data_ptr(), K,
+                                                       _lib.ptr(x1), K, sp, N, K, W.data_ptr(), K, a_s.data_ptr(),
+                                                       a_d.data_ptr(), _lib.ptr(dx), K, G.data_ptr(), GV.data_ptr(),
+                                                       ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)),
+                           "project_bwd_fused")
             dW, datt_src, datt_dst = weight_grads(G, GV, W, a_s, a_d, heads, C)
             dx_u = dx[:split] if (dx is not None and had_items) else dx
             dx_i = dx[split:] if (dx is not None and had_items) else None
@@ -1555,15 +1603,6 @@ class _BadIndex:
 def check_bpr_indices():
     """Raise IndexError if any earlier bpr_loss call saw out-of-range indices (syncs)."""
     _BadIndex.raise_pending(wait=True)
-
-
-_side_streams = {}
-
-
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    if dev.index not in _side_streams:
-        _side_streams[dev.index] = torch.cuda.Stream(device=dev)
-    return _side_streams[dev.index]
 
 
 class BprPrepared:

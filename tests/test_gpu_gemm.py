@@ -123,6 +123,99 @@ def test_project_bwd_fused_vs_fp64(pkg, cuda, N, split, with_dx):
     assert torch.equal(G, G2) and torch.equal(GV, GV2) and (dx is None or torch.equal(dx, dx2))
 
 
+@pytest.mark.parametrize("N,with_bias", [(1, True), (33, True), (8193, False), (255_404, True)])
+def test_project_bwd_fused_producer(pkg, cuda, N, with_bias):
+    """ppgat_project_bwd_fused_producer: dx, G, GV bit for bit those of ppgat_project_bwd_fused,
+    plus the producer layer's prologue from dx -- nstate = {s_dst, m, inv_l, <dx, x - b>} and
+    dbias = sum_r dx_r -- against fp64 (and the fp32 ppgat_bwd_prologue within 1e-5)."""
+    lib = pkg._lib.load()
+    if not lib.ppgat_project_bwd_fused_supported(128):
+        pytest.skip("fused dx/dW needs the split GEMM family")
+    g = torch.Generator().manual_seed(N + 3)
+    HC = K = 128
+    D = torch.randn(N, HC, generator=g, dtype=torch.float64)
+    S = torch.randn(N, 2, generator=g, dtype=torch.float64)
+    x = torch.randn(N, K, generator=g, dtype=torch.float64)
+    W = torch.randn(HC, K, generator=g, dtype=torch.float64) / 11
+    a_s, a_d, b = (torch.randn(HC, generator=g, dtype=torch.float64) for _ in range(3))
+    sd, m, il = (torch.randn(N, generator=g, dtype=torch.float64) for _ in range(3))
+    Dd, Sd, xd, Wd, asd, add, bd, sdd, md, ild = (t.float().to(cuda).contiguous()
+                                                  for t in (D, S, x, W, a_s, a_d, b, sd, m, il))
+    nbytes = ctypes.c_size_t(0)
+    pkg._lib.check(lib.ppgat_project_bwd_fused_workspace_bytes(N, ctypes.byref(nbytes)), "ws")
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=cuda)
+    st = pkg._lib.stream_handle(cuda)
+    outs = []
+    for producer in (False, True):
+        dx = torch.full((N, K), float("nan"), device=cuda)
+        G, GV = torch.empty(HC, K, device=cuda), torch.empty(2, K, device=cuda)
+        ns = torch.full((N, 4), float("nan"), device=cuda)
+        db = torch.full((K,), float("nan"), device=cuda)
+        common = (Dd.data_ptr(), HC, Sd.data_ptr(), 2, xd.data_ptr(), K, None, K, N, N, K, Wd.data_ptr(), K,
+                  asd.data_ptr(), add.data_ptr(), dx.data_ptr(), K, G.data_ptr(), GV.data_ptr())
+        if producer:
+            pkg._lib.check(lib.ppgat_project_bwd_fused_producer(
+                *common, bd.data_ptr() if with_bias else None, sdd.data_ptr(), md.data_ptr(), ild.data_ptr(), 1.0,
+                ns.data_ptr(), db.data_ptr() if with_bias else None, ws.data_ptr(), nbytes.value, st), "producer")
+        else:
+            pkg._lib.check(lib.ppgat_project_bwd_fused(*common, ws.data_ptr(), nbytes.value, st), "fused")
+        outs.append((dx, G, GV, ns, db))
+    (dx0, G0, GV0, _, _), (dx1, G1, GV1, ns, db) = outs
+    assert torch.equal(dx0, dx1) and torch.equal(G0, G1) and torch.equal(GV0, GV1)
+    dx64 = dx1.double().cpu()
+    xb = x - (b if with_bias else 0.0)
+    Dref = (dx64 * xb).sum(1)
+    scale = (dx64.abs() * xb.abs()).sum(1).clamp_min(1e-30)   # pre-cancellation size of each row's dot
+    assert float(((ns[:, 3].double().cpu() - Dref).abs() / scale).max()) <= 1e-6
+    assert torch.equal(ns[:, :3].cpu(), torch.stack([sdd, md, ild], 1).cpu())
+    if with_bias:
+        assert rel(db, dx64.sum(0)) <= 1e-5
+    # the separate prologue on the same dx (ppgat_bwd_prologue) agrees to fp32 rounding
+    ns2 = torch.empty(N, 4, device=cuda)
+    db2 = torch.empty(K, device=cuda)
+    part = torch.empty(max(int(lib.ppgat_bwd_partial_rows(N)), 1) * K, device=cuda)
+    out = xd  # x IS the producer's output (bias included)
+    pkg._lib.check(lib.ppgat_bwd_prologue(dx1.data_ptr(), out.data_ptr(), None, bd.data_ptr() if with_bias else None,
+                                          sdd.data_ptr(), md.data_ptr(), ild.data_ptr(), N, 1, K, 0, ns2.data_ptr(),
+                                          db2.data_ptr() if with_bias else None, part.data_ptr() if with_bias else None,
+                                          st), "bwd_prologue")
+    assert float(((ns2[:, 3].double().cpu() - ns[:, 3].double().cpu()).abs() / scale).max()) <= 1e-5
+    if with_bias:
+        assert rel(db, db2.double()) <= 1e-5
+
+
+def test_producer_prologue_in_the_model(pkg, cuda, monkeypatch):
+    """Two stacked heads = 1 layers: layer 1's backward prologue runs inside layer 2's dx kernel
+    (once per backward), and every gradient matches the unfused path within 1e-5."""
+    from importlib import import_module
+    ops = import_module("plotpointe-gat-recommendation_amd.hip_ops")
+    gr = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
+    ei = torch.from_numpy(gr.edge_index_numpy()).to(cuda)
+    feats = torch.from_numpy(pkg.data.synthetic_item_features(gr.n_items, 64, seed=5)).to(cuda)
+    u, i, j = (torch.from_numpy(a).to(cuda) for a in pkg.data.sample_bpr_numpy(gr.user_ptr, gr.user_items,
+                                                                                 gr.n_items, 20_000, seed=1))
+    calls = {"n": 0}
+    real = ops._producer_of
+
+    def counting(x, N):
+        r = real(x, N)
+        calls["n"] += r is not None
+        return r
+    monkeypatch.setattr(ops, "_producer_of", counting)
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PPGAT_PRODUCER_PROLOGUE", flag)
+        torch.manual_seed(0)
+        model = pkg.PyGGAT(gr.n_users, gr.n_items, item_feat_dim=64, hidden=128, layers=2, heads=1,
+                           attn_dropout=0.1).to(cuda).train()
+        torch.manual_seed(100)
+        pkg.bpr_loss(model(feats, ei), gr.n_users, u, i, j).backward()
+        grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters()})
+    assert calls["n"] == 1
+    for n in grads[0]:
+        assert rel(grads[0][n], grads[1][n].double()) <= 1e-5, n
+
+
 def test_gemm_tn_segments(pkg, cuda):
     ops = _ops()
     g = torch.Generator().manual_seed(11)
