@@ -241,6 +241,19 @@ int ppgat_bpr_bwd_prepared(const float* Z, int64_t n_rows, int64_t n_users, int6
                            int channels, const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples,
                            const float* coef, const float* grad_loss, float* grad_Z,
                            void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_bpr_bwd (row_map NULL, after ppgat_bpr_fwd on the same workspace) that also does the
+ * backward prologue of the GAT layer whose output Z is (heads = 1; the last conv of
+ * train_gat_pyg.py:86-87 feeding the loss of :313-322) -- ppgat_bwd_prologue's outputs for that
+ * layer from grad_Z while its rows are on chip, instead of a second pass over grad_Z and Z:
+ *   prev_nstate[r] = {prev_s_dst[r], prev_m[r], prev_inv_l[r], prev_gscale <dZ_r, Z_r - prev_bias>}
+ *   prev_grad_bias = sum_r dZ_r                    (prev_bias / prev_grad_bias nullable)
+ * Z_r is loaded with the row's last contributions, so the dot adds no round trip.  grad_Z bit
+ * for bit that of ppgat_bpr_bwd; deterministic. */
+int ppgat_bpr_bwd_producer(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, int channels,
+                           const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, const float* coef,
+                           const float* grad_loss, float* grad_Z, const float* prev_bias, const float* prev_s_dst,
+                           const float* prev_m, const float* prev_inv_l, float prev_gscale, float* prev_nstate,
+                           float* prev_grad_bias, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- projection weight gradient ----------------------------------------------
  * Replaces: the weight (and bias) gradient of torch.nn.Linear in GATConv.lin /

@@ -65,6 +65,8 @@ SIGNATURES = {
     "ppgat_bpr_bwd_prepare": (c_int, [c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_sz, c_vp]),
     "ppgat_bpr_bwd_prepared": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                        c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_bpr_bwd_producer": (c_int, [c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp, c_f, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_gemm_tn_workspace_bytes": (c_int, [c_i64, c_int, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_gemm_tn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp,
                               c_vp, c_sz, c_vp]),

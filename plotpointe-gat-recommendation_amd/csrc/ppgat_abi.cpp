@@ -476,7 +476,7 @@ int ppgat_bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_ite
   if (!loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_fwd: null output");
   if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_rows, n_samples, channels))
     return fail(PPGAT_ERR_INVALID, "bpr_fwd: workspace too small");
-  hipError_t e = ppgat::bpr_fwd(Z, n_users, n_items, row_map, channels, u, i, j, n_samples, loss_kind, loss, coef,
+  hipError_t e = ppgat::bpr_fwd(Z, n_rows, n_users, n_items, row_map, channels, u, i, j, n_samples, loss_kind, loss, coef,
                                 bad_count, workspace, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "bpr_fwd");
   return PPGAT_OK;
@@ -526,6 +526,27 @@ int ppgat_bpr_bwd_prepared(const float* Z, int64_t n_rows, int64_t n_users, int6
   hipError_t e = ppgat::bpr_bwd_finish(Z, n_rows, n_users, n_items, row_map, channels, u, i, j, n_samples, coef,
                                        grad_loss, grad_Z, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "bpr_bwd_prepared");
+  return PPGAT_OK;
+}
+
+int ppgat_bpr_bwd_producer(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, int channels,
+                           const int64_t* u, const int64_t* i, const int64_t* j, int64_t n_samples, const float* coef,
+                           const float* grad_loss, float* grad_Z, const float* prev_bias, const float* prev_s_dst,
+                           const float* prev_m, const float* prev_inv_l, float prev_gscale, float* prev_nstate,
+                           float* prev_grad_bias, void* workspace, size_t workspace_bytes, void* stream) {
+  if (int rc = check_bpr(n_users, n_items, channels, n_samples, Z, u, i, j, "bpr_bwd_producer")) return rc;
+  if (n_rows != n_users + n_items) return fail(PPGAT_ERR_INVALID, "bpr_bwd_producer: n_rows must be n_users + n_items");
+  if (!grad_Z || !grad_loss || (n_samples > 0 && !coef)) return fail(PPGAT_ERR_INVALID, "bpr_bwd_producer: null pointer");
+  if (!prev_s_dst || !prev_m || !prev_inv_l || !prev_nstate)
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd_producer: the producer's state is required");
+  if ((reinterpret_cast<uintptr_t>(prev_nstate) | reinterpret_cast<uintptr_t>(prev_bias)) % 16)
+    return fail(PPGAT_ERR_UNSUPPORTED, "bpr_bwd_producer: nstate / bias 16-byte aligned");
+  if (!workspace || workspace_bytes < ppgat::bpr_workspace_bytes(n_rows, n_samples, channels))
+    return fail(PPGAT_ERR_INVALID, "bpr_bwd_producer: workspace too small");
+  const ppgat::BprProducer prod{prev_bias, prev_s_dst, prev_m, prev_inv_l, prev_gscale, prev_nstate, prev_grad_bias};
+  hipError_t e = ppgat::bpr_bwd(Z, n_rows, n_users, n_items, nullptr, channels, u, i, j, n_samples, coef, grad_loss,
+                                grad_Z, workspace, workspace_bytes, static_cast<hipStream_t>(stream), &prod);
+  if (e != hipSuccess) return hip_fail(e, "bpr_bwd_producer");
   return PPGAT_OK;
 }
 

@@ -65,19 +65,31 @@ hipError_t schedule_build(const int32_t* ptr, int64_t N, int32_t T, int32_t* ite
 
 // training-step kernels (ppgat_train.hip)
 bool bpr_channels_ok(int C);
+// the backward prologue of the layer that produced Z (heads = 1), fused into the loss backward
+struct BprProducer {
+  const float* bias;  // nullable
+  const float* s_dst;
+  const float* m;
+  const float* inv_l;
+  float gscale;
+  float* nstate;      // [n_rows, 4]
+  float* grad_bias;   // nullable: [C]
+};
 size_t bpr_workspace_bytes(int64_t N, int64_t S, int C);
-hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+hipError_t bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, int kind, float* loss,
                    float* coef, int32_t* bad, void* ws, hipStream_t st);
 hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
-                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st);
+                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st,
+                   const BprProducer* prod = nullptr);
 hipError_t bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                            const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, void* ws,
                            size_t ws_bytes, hipStream_t st);
 hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
                           int C, const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
-                          const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st);
+                          const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st,
+                          const BprProducer* prod = nullptr);
 size_t gemm_tn_workspace_bytes(int64_t N, int M, int K, int nv);
 hipError_t gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t N, int M, int K, float* out,
                    float* colsum, const float* V, int64_t ldv, int nv, float* vout, void* ws, hipStream_t st);

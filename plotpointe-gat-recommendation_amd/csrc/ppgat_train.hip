@@ -301,6 +301,34 @@ __global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restr
 // ---------------------------------------------------------------------------
 constexpr int kChunk = 32;
 
+// The backward prologue of the GAT layer that produced Z (heads = 1; the layer's own
+// ppgat_bwd_prologue, done here while the finished dZ row is in registers): for every row r
+//   nstate[r] = {s_dst[r], m[r], inv_l[r], gscale <dZ_r, Z_r - bias>}
+// (Z_r loaded with the segment's contributions, so the dot costs no extra round trip), and
+// grad_bias = sum_r dZ_r = the sum of every contribution (block partials bpart, reduced in block
+// order).  nstate == NULL: off.
+struct BprPro {
+  const float* bias;   // nullable
+  const float* sdst;
+  const float* m;
+  const float* invl;
+  float gscale;
+  float4* nstate;
+  float* bpart;        // nullable: [gridDim.x][C]
+};
+
+// <a, z> over the LPR lanes of a subgroup (4 columns per lane), accumulated in fp64 over a fixed
+// tree: the prologue's D feeds the logit gradients alpha (d - D), whose destination sums
+// cancel -- D is rounded once, from the fp32 dZ and Z values, not at every partial sum
+template <int LPR>
+__device__ __forceinline__ float subgroup_dot(float4 a, float4 z) {
+  double v = fma((double)a.w, (double)z.w, fma((double)a.z, (double)z.z, fma((double)a.y, (double)z.y,
+                                                                              (double)a.x * (double)z.x)));
+#pragma unroll
+  for (int sh = 1; sh < LPR; sh <<= 1) v += __shfl_xor(v, sh);
+  return (float)v;
+}
+
 template <int C>
 __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ skey, const int32_t* __restrict__ scid,
                                                     int64_t total, const int64_t* __restrict__ u,
@@ -309,17 +337,20 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
                                                     const int32_t* __restrict__ row_map,
                                                     const float2* __restrict__ coef,
                                                     const float* __restrict__ grad_loss, const float* __restrict__ Z,
-                                                    int64_t n_rows, float* __restrict__ dZ, float* __restrict__ slots) {
+                                                    int64_t n_rows, float* __restrict__ dZ, float* __restrict__ slots,
+                                                    BprPro pro) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   __shared__ int32_t s_src[SPB][kChunk];
   __shared__ int32_t s_dst[SPB][kChunk];
   __shared__ float s_cf[SPB][kChunk];
+  __shared__ float4 s_bp[SPB][LPR];
   const int tid = threadIdx.x;
   const int sg = tid / LPR, sl = tid % LPR;
   const int64_t ch = (int64_t)blockIdx.x * SPB + sg;
   const int64_t b0 = ch * kChunk;
   const float g = grad_loss[0];
+  const bool pon = pro.nstate != nullptr;
   if (b0 < total) {
     for (int q = sl; q < kChunk; q += LPR) {
       const int64_t p = b0 + q;
@@ -343,36 +374,59 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
     }
   }
   __syncthreads();
-  if (b0 >= total) return;
-  const int len = (int)min((int64_t)kChunk, total - b0);
-  const bool starts_before = b0 > 0 && skey[b0 - 1] == s_dst[sg][0];
-  const bool ends_after = b0 + len < total && skey[b0 + len] == s_dst[sg][len - 1];
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  int seg_start = 0;
-  constexpr int U = 4;
-  for (int q0 = 0; q0 < len; q0 += U) {
-    float4 v[U];
+  float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);  // producer dbias: every contribution of this subgroup
+  const float4 bb = (pon && pro.bias) ? ld4(pro.bias + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (b0 < total) {
+    const int len = (int)min((int64_t)kChunk, total - b0);
+    const bool starts_before = b0 > 0 && skey[b0 - 1] == s_dst[sg][0];
+    const bool ends_after = b0 + len < total && skey[b0 + len] == s_dst[sg][len - 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int seg_start = 0;
+    constexpr int U = 4;
+    for (int q0 = 0; q0 < len; q0 += U) {
+      float4 v[U], zd[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int q = q0 + k;
-      v[k] = q < len ? ld4(Z + (int64_t)s_src[sg][q] * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+      for (int k = 0; k < U; ++k) {
+        const int q = q0 + k;
+        v[k] = q < len ? ld4(Z + (int64_t)s_src[sg][q] * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        // the destination row itself where a segment finishing in this chunk ends (prologue)
+        const bool fin = pon && q < len && (q == len - 1 ? !ends_after : s_dst[sg][q + 1] != s_dst[sg][q]) &&
+                         s_dst[sg][q] < n_rows;
+        zd[k] = fin ? ld4(Z + (int64_t)s_dst[sg][q] * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int q = q0 + k;
-      if (q >= len) break;
-      acc = fma4(s_cf[sg][q], v[k], acc);
-      const bool last_of_seg = q == len - 1 || s_dst[sg][q + 1] != s_dst[sg][q];
-      if (last_of_seg) {
-        const int32_t r = s_dst[sg][q];
-        const bool first = seg_start == 0, last = q == len - 1;
-        if (first && starts_before) st4(slots + (ch * 2 + 0) * C + sl * 4, acc);
-        else if (last && ends_after) st4(slots + (ch * 2 + 1) * C + sl * 4, acc);
-        else if (r < n_rows) st4(dZ + (int64_t)r * C + sl * 4, acc);
-        acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        seg_start = q + 1;
+      for (int k = 0; k < U; ++k) {
+        const int q = q0 + k;
+        if (q >= len) break;
+        acc = fma4(s_cf[sg][q], v[k], acc);
+        const bool last_of_seg = q == len - 1 || s_dst[sg][q + 1] != s_dst[sg][q];
+        if (last_of_seg) {
+          const int32_t r = s_dst[sg][q];
+          const bool first = seg_start == 0, last = q == len - 1;
+          if (first && starts_before) st4(slots + (ch * 2 + 0) * C + sl * 4, acc);
+          else if (last && ends_after) st4(slots + (ch * 2 + 1) * C + sl * 4, acc);
+          else if (r < n_rows) {
+            st4(dZ + (int64_t)r * C + sl * 4, acc);
+            if (pon) {  // (uniform over the subgroup: its lanes share the segment)
+              const float4 zr = make_float4(zd[k].x - bb.x, zd[k].y - bb.y, zd[k].z - bb.z, zd[k].w - bb.w);
+              const float d = subgroup_dot<LPR>(acc, zr);
+              if (sl == 0) pro.nstate[r] = make_float4(pro.sdst[r], pro.m[r], pro.invl[r], d * pro.gscale);
+            }
+          }
+          if (pon) bsum = add4(bsum, acc);
+          acc = make_float4(0.f, 0.f, 0.f, 0.f);
+          seg_start = q + 1;
+        }
       }
     }
+  }
+  if (!pon || pro.bpart == nullptr) return;
+  s_bp[sg][sl] = bsum;
+  __syncthreads();
+  if (tid < LPR) {  // the block's subgroups in order
+    float4 s = s_bp[0][tid];
+    for (int q = 1; q < SPB; ++q) s = add4(s, s_bp[q][tid]);
+    st4(pro.bpart + (int64_t)blockIdx.x * C + tid * 4, s);
   }
 }
 
@@ -389,20 +443,23 @@ __global__ void __launch_bounds__(256) k_bpr_mark(const int32_t* __restrict__ sk
 
 template <int C>
 __global__ void __launch_bounds__(256) k_bpr_zero_untouched(const uint8_t* __restrict__ touched, int64_t n_rows,
-                                                            float* __restrict__ dZ) {
+                                                            float* __restrict__ dZ, BprPro pro) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
   for (int64_t r = (int64_t)blockIdx.x * SPB + sg; r < n_rows; r += (int64_t)gridDim.x * SPB)
-    if (!touched[r]) st4(dZ + r * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (!touched[r]) {
+      st4(dZ + r * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+      if (pro.nstate != nullptr && sl == 0) pro.nstate[r] = make_float4(pro.sdst[r], pro.m[r], pro.invl[r], 0.f);
+    }
 }
 
 // Fix-up: the chunk in which a chunk-spanning segment starts sums its tail slot and the
 // head slots of the following chunks, in chunk order, and writes the row.
 template <int C>
 __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ skey, int64_t total,
-                                                   const float* __restrict__ slots, int64_t n_rows,
-                                                   float* __restrict__ dZ) {
+                                                   const float* __restrict__ slots, const float* __restrict__ Z,
+                                                   int64_t n_rows, float* __restrict__ dZ, BprPro pro) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
@@ -414,6 +471,8 @@ __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ s
   const int32_t r = skey[b1 - 1];
   if (skey[b1] != r || r >= n_rows) return;            // last segment does not continue / sentinel
   if (skey[b0] == r && b0 > 0 && skey[b0 - 1] == r) return;  // segment started in an earlier chunk
+  const bool pon = pro.nstate != nullptr;
+  const float4 zd = pon ? ld4(Z + (int64_t)r * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc = ld4(slots + (ch * 2 + 1) * C + sl * 4);
   for (int64_t c2 = ch + 1;; ++c2) {
     const int64_t e0 = c2 * kChunk;
@@ -422,6 +481,38 @@ __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ s
     if (!(skey[e1 - 1] == r && e1 < total && skey[e1] == r)) break;
   }
   st4(dZ + (int64_t)r * C + sl * 4, acc);
+  if (pon) {
+    const float4 bb = pro.bias ? ld4(pro.bias + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 zr = make_float4(zd.x - bb.x, zd.y - bb.y, zd.z - bb.z, zd.w - bb.w);
+    const float d = subgroup_dot<LPR>(acc, zr);
+    if (sl == 0) pro.nstate[r] = make_float4(pro.sdst[r], pro.m[r], pro.invl[r], d * pro.gscale);
+  }
+}
+
+// Ordered column sums of block partials in two stages: block (column slab, row group) sums its
+// <= 256 rows (wave w: rows w, w + 16, ... in order, 16 loads in flight; waves in order) into
+// out[group]; a second launch over the groups gives the total.
+__global__ void __launch_bounds__(1024) k_col_sum_groups(const float* __restrict__ part, int64_t rows, int cols,
+                                                         float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * 256, r1 = min(rows, r0 + 256);
+  float s = 0.f;
+  if (c < cols) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = r0 + wv + 16 * k < r1 ? part[(r0 + wv + 16 * k) * cols + c] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += v[k];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && c < cols) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    out[(int64_t)blockIdx.y * cols + c] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -647,18 +738,53 @@ static int64_t bpr_fwd_blocks(int64_t S, int C) {
   return b < 16384 ? b : 16384;
 }
 
-// workspace: block_loss | keys | vals | skeys | scid | slots | radix sort
-size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
+// workspace: block_loss | keys | vals | skeys | scid | slots | radix sort | touched | producer
+// prologue (block partials [chunk blocks][C] | their group sums [groups][C])
+static int64_t bpr_chunk_blocks(int64_t S, int C) {
+  const int64_t chunks = (4 * S + kChunk - 1) / kChunk;
+  const int64_t spb = 256 / (C / 4);
+  return (chunks + spb - 1) / spb;
+}
+
+static size_t bpr_base_bytes(int64_t N, int64_t S, int C) {
   const int64_t c4 = 4 * S > 0 ? 4 * S : 1;
   const int64_t chunks = (c4 + kChunk - 1) / kChunk;
   return align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4) + 4 * align_up((size_t)c4 * 4) +
          align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N + 1)) + align_up((size_t)N + 1);
 }
 
-hipError_t bpr_fwd(const float* Z, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
+struct BprExtra {
+  float* bpart;
+  float* groups;
+};
+
+// byte offsets of the producer-prologue region: bpart, groups, end
+static void bpr_extra_offsets(int64_t N, int64_t S, int C, size_t off[3]) {
+  const int64_t blocks = bpr_chunk_blocks(S, C);
+  const int64_t groups = (blocks + 255) / 256;
+  off[0] = bpr_base_bytes(N, S, C);
+  off[1] = off[0] + align_up((size_t)(blocks > 0 ? blocks : 1) * C * 4);
+  off[2] = off[1] + align_up((size_t)(groups > 0 ? groups : 1) * C * 4);
+}
+
+static BprExtra bpr_extra(void* ws, int64_t N, int64_t S, int C) {
+  size_t off[3];
+  bpr_extra_offsets(N, S, C, off);
+  char* p = static_cast<char*>(ws);
+  return BprExtra{reinterpret_cast<float*>(p + off[0]), reinterpret_cast<float*>(p + off[1])};
+}
+
+size_t bpr_workspace_bytes(int64_t N, int64_t S, int C) {
+  size_t off[3];
+  bpr_extra_offsets(N, S, C, off);
+  return off[2];
+}
+
+hipError_t bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, int kind, float* loss,
                    float* coef, int32_t* bad, void* ws, hipStream_t st) {
   float* block_loss = static_cast<float*>(ws);
+  (void)n_rows;
   const int64_t nb = bpr_fwd_blocks(S, C);
   if (bad != nullptr) {
     hipError_t e = hipMemsetAsync(bad, 0, sizeof(int32_t), st);
@@ -727,26 +853,51 @@ hipError_t bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, con
   return hipGetLastError();
 }
 
-// The rest, after bpr_bwd_prepare on the same workspace (stream-ordered after it).
+// The rest, after bpr_bwd_prepare on the same workspace (stream-ordered after it).  prod !=
+// NULL: also the producer layer's backward prologue (BprPro, row_map must be NULL).
 hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map,
                           int C, const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
-                          const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
+                          const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st,
+                          const BprProducer* prod) {
   const int64_t N = n_rows;
-  if (S == 0) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_zero_untouched
   if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
+  BprPro pk{};
+  if (prod != nullptr) {
+    const BprExtra x = bpr_extra(ws, N, S, C);
+    pk.bias = prod->bias; pk.sdst = prod->s_dst; pk.m = prod->m; pk.invl = prod->inv_l;
+    pk.gscale = prod->gscale; pk.nstate = reinterpret_cast<float4*>(prod->nstate);
+    pk.bpart = prod->grad_bias ? x.bpart : nullptr;
+  }
+  const BprWs w = bpr_ws(ws, N, S, C);
+  if (S == 0) {
+    if (prod == nullptr) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_zero_untouched
+    hipError_t e = hipMemsetAsync(w.touched, 0, (size_t)N, st);
+    if (e == hipSuccess && prod->grad_bias) e = hipMemsetAsync(prod->grad_bias, 0, (size_t)C * 4, st);
+    if (e != hipSuccess) return e;
+  }
   const int64_t total = 4 * S;
   const int64_t chunks = (total + kChunk - 1) / kChunk;
-  const BprWs w = bpr_ws(ws, N, S, C);
   PPGAT_DISPATCH_LOSS_C(C, {
     constexpr int SPB = 256 / (CC / 4);
     const unsigned g = (unsigned)((chunks + SPB - 1) / SPB);
-    hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, w.skeys, w.scid, total, u, i, j, n_users,
-                       n_items, row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, w.slots);
-    hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, w.skeys, total, w.slots, N, dZ);
+    if (S > 0) {
+      hipLaunchKernelGGL(k_bpr_chunks<CC>, dim3(g), dim3(256), 0, st, w.skeys, w.scid, total, u, i, j, n_users,
+                         n_items, row_map, reinterpret_cast<const float2*>(coef), grad_loss, Z, N, dZ, w.slots, pk);
+      hipLaunchKernelGGL(k_bpr_fixup<CC>, dim3(g), dim3(256), 0, st, w.skeys, total, w.slots, Z, N, dZ, pk);
+    }
     if (N > 0) {
       int64_t gz = (N + SPB - 1) / SPB;
       if (gz > 4096) gz = 4096;
-      hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, w.touched, N, dZ);
+      hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, w.touched, N, dZ, pk);
+    }
+    if (pk.bpart != nullptr && S > 0) {  // grad_bias: the chunk blocks' partials in two ordered stages
+      const int64_t groups = ((int64_t)g + 255) / 256;
+      const unsigned cs = (unsigned)((CC + 63) / 64);
+      float* out1 = groups > 1 ? bpr_extra(ws, N, S, C).groups : prod->grad_bias;
+      hipLaunchKernelGGL(k_col_sum_groups, dim3(cs, (unsigned)groups), dim3(1024), 0, st, pk.bpart, (int64_t)g, CC,
+                         out1);
+      if (groups > 1)
+        hipLaunchKernelGGL(k_col_sum_groups, dim3(cs, 1), dim3(1024), 0, st, out1, groups, CC, prod->grad_bias);
     }
   });
   return hipGetLastError();
@@ -754,10 +905,12 @@ hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64
 
 hipError_t bpr_bwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_items, const int32_t* row_map, int C,
                    const int64_t* u, const int64_t* i, const int64_t* j, int64_t S, const float* coef,
-                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st) {
+                   const float* grad_loss, float* dZ, void* ws, size_t ws_bytes, hipStream_t st,
+                   const BprProducer* prod) {
   hipError_t err = bpr_bwd_prepare(n_rows, n_users, n_items, row_map, C, u, i, j, S, ws, ws_bytes, st);
   if (err != hipSuccess) return err;
-  return bpr_bwd_finish(Z, n_rows, n_users, n_items, row_map, C, u, i, j, S, coef, grad_loss, dZ, ws, ws_bytes, st);
+  return bpr_bwd_finish(Z, n_rows, n_users, n_items, row_map, C, u, i, j, S, coef, grad_loss, dZ, ws, ws_bytes, st,
+                        prod);
 }
 
 // ---- skinny A^T B (M <= 16): the multi-head layer's GV = S^T x (S = [ds_src | ds_dst], 2H

@@ -561,14 +561,14 @@ def _producer_fusion_enabled() -> bool:
     return _fused_dxw_enabled() and os.environ.get("PPGAT_PRODUCER_PROLOGUE", "1") != "0"
 
 
-def _producer_of(x: torch.Tensor, N: int):
+def _producer_of(x: torch.Tensor, N: int, C: int = 128):
     """The backward node of the GATLayer whose output x is -- nothing in between, x unmodified
     since -- when that layer (heads = 1, no replicated rows) can hand its backward prologue to
-    the consumer's dx kernel; else None."""
+    the consumer's backward (its dx kernel, or the loss backward); else None."""
     node = x.grad_fn
     if node is None or not isinstance(node, GATLayer._backward_cls):
         return None
-    if getattr(node, "pro_state", None) is None or x.size(0) != N or x.size(1) != 128:
+    if getattr(node, "pro_state", None) is None or x.dim() != 2 or x.size(0) != N or x.size(1) != C:
         return None
     if getattr(node, "out_version", None) != x._version:
         return None
@@ -1660,6 +1660,9 @@ class _BPRLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map, prep=None):
         lib = _lib.load()
+        # Z straight from a heads = 1 GATLayer: the loss backward also does that layer's prologue
+        ctx.producer = (_producer_of(Z, N=Z.size(0), C=Z.size(1))
+                        if (row_map is None and prep is None and _producer_fusion_enabled()) else None)
         Z = Z.contiguous()
         _check_dev("Z", Z, torch.float32)
         n_rows, C = Z.shape
@@ -1702,10 +1705,23 @@ class _BPRLoss(torch.autograd.Function):
         gl = gl.reshape(1).to(torch.float32).contiguous()
         dZ = torch.empty_like(Z)
         ws = ctx.ws
-        fn = lib.ppgat_bpr_bwd_prepared if ctx.prepared else lib.ppgat_bpr_bwd
-        _lib.check(fn(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(ctx.row_map), C, u.data_ptr(), i.data_ptr(),
-                      j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(), ws.numel(),
-                      _lib.stream_handle(Z.device)), "bpr_bwd")
+        prod, ctx.producer = ctx.producer, None
+        if prod is not None and prod.pro_state is not None:
+            # also the producing layer's backward prologue (its nstate and dbias) from dZ
+            pb, ps_dst, pm, pinv_l = prod.pro_state
+            p_nstate = torch.empty(n_rows, 1, 4, dtype=torch.float32, device=Z.device)
+            p_dbias = torch.empty(C, dtype=torch.float32, device=Z.device) if pb is not None else None
+            _lib.check(lib.ppgat_bpr_bwd_producer(
+                Z.data_ptr(), n_rows, n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S,
+                coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), _lib.ptr(pb), ps_dst.data_ptr(), pm.data_ptr(),
+                pinv_l.data_ptr(), 1.0, p_nstate.data_ptr(), _lib.ptr(p_dbias), ws.data_ptr(), ws.numel(),
+                _lib.stream_handle(Z.device)), "bpr_bwd_producer")
+            prod.pro_result = (dZ.data_ptr(), dZ._version, p_nstate, p_dbias)
+        else:
+            fn = lib.ppgat_bpr_bwd_prepared if ctx.prepared else lib.ppgat_bpr_bwd
+            _lib.check(fn(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(ctx.row_map), C, u.data_ptr(),
+                          i.data_ptr(), j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(),
+                          ws.numel(), _lib.stream_handle(Z.device)), "bpr_bwd")
         ctx.ws = None
         return dZ, None, None, None, None, None, None, None, None
 

@@ -186,7 +186,8 @@ def test_project_bwd_fused_producer(pkg, cuda, N, with_bias):
 
 def test_producer_prologue_in_the_model(pkg, cuda, monkeypatch):
     """Two stacked heads = 1 layers: layer 1's backward prologue runs inside layer 2's dx kernel
-    (once per backward), and every gradient matches the unfused path within 1e-5."""
+    and layer 2's inside the loss backward (two hand-offs per backward, no ppgat_bwd_prologue
+    call), and every gradient matches the unfused path within 1e-5."""
     from importlib import import_module
     ops = import_module("plotpointe-gat-recommendation_amd.hip_ops")
     gr = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
@@ -197,13 +198,22 @@ def test_producer_prologue_in_the_model(pkg, cuda, monkeypatch):
     calls = {"n": 0}
     real = ops._producer_of
 
-    def counting(x, N):
-        r = real(x, N)
+    def counting(x, N, C=128):
+        r = real(x, N, C)
         calls["n"] += r is not None
         return r
     monkeypatch.setattr(ops, "_producer_of", counting)
-    grads = []
+    lib = pkg._lib.load()
+    real_pro = lib.ppgat_bwd_prologue
+    pro_calls = {"n": 0}
+
+    def counting_pro(*a):
+        pro_calls["n"] += 1
+        return real_pro(*a)
+    monkeypatch.setattr(lib, "ppgat_bwd_prologue", counting_pro)
+    grads, pros = [], []
     for flag in ("1", "0"):
+        pro_calls["n"] = 0
         monkeypatch.setenv("PPGAT_PRODUCER_PROLOGUE", flag)
         torch.manual_seed(0)
         model = pkg.PyGGAT(gr.n_users, gr.n_items, item_feat_dim=64, hidden=128, layers=2, heads=1,
@@ -211,7 +221,8 @@ def test_producer_prologue_in_the_model(pkg, cuda, monkeypatch):
         torch.manual_seed(100)
         pkg.bpr_loss(model(feats, ei), gr.n_users, u, i, j).backward()
         grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters()})
-    assert calls["n"] == 1
+        pros.append(pro_calls["n"])
+    assert calls["n"] == 2 and pros == [0, 2]
     for n in grads[0]:
         assert rel(grads[0][n], grads[1][n].double()) <= 1e-5, n
 

@@ -211,6 +211,63 @@ def test_bpr_prepared_bitwise(pkg, cuda, n_users, n_items, S, C, mapped):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("n_users,n_items,S,C,with_bias", [(3000, 500, 20_000, 128, True), (2000, 300, 5000, 256, True),
+                                                           (400, 100, 3000, 32, False), (50, 40, 0, 128, True),
+                                                           (4, 3, 5000, 64, True)])
+def test_bpr_bwd_producer(pkg, cuda, n_users, n_items, S, C, with_bias):
+    """ppgat_bpr_bwd_producer: grad_Z bit for bit that of ppgat_bpr_bwd, plus the producing
+    layer's prologue -- nstate = {s_dst, m, inv_l, <dZ_r, Z_r - b>} from the forward's dot
+    products and dbias = sum_r dZ_r -- against fp64 of the same dZ (per-row bound relative to
+    the pre-cancellation size sum |dZ| |Z - b|); rows spanning many chunks (one user, one item
+    pair); no triples at all."""
+    import ctypes
+    lib = pkg._lib.load()
+    rng = np.random.default_rng(S + C)
+    u, i, j = (torch.from_numpy(rng.integers(0, n, S)).to(cuda) for n in (n_users, n_items, n_items))
+    N = n_users + n_items
+    Z = torch.from_numpy(rng.standard_normal((N, C)).astype(np.float32) * 0.3).to(cuda)
+    b = torch.from_numpy(rng.standard_normal(C).astype(np.float32) * 0.1).to(cuda)
+    sd, m, il = (torch.from_numpy(rng.standard_normal(N).astype(np.float32)).to(cuda) for _ in range(3))
+    nbytes = ctypes.c_size_t(0)
+    pkg._lib.check(lib.ppgat_bpr_workspace_bytes(N, S, C, ctypes.byref(nbytes)), "ws")
+    st = pkg._lib.stream_handle(cuda)
+    gl = torch.tensor([1.7], device=cuda)
+    res = []
+    for producer in (False, True):
+        ws = torch.full((int(nbytes.value),), 255, dtype=torch.uint8, device=cuda)
+        loss = torch.empty(1, device=cuda)
+        coef = torch.empty(max(S, 1), 2, device=cuda)
+        pkg._lib.check(lib.ppgat_bpr_fwd(Z.data_ptr(), N, n_users, n_items, None, C, u.data_ptr(), i.data_ptr(),
+                                         j.data_ptr(), S, 0, loss.data_ptr(), coef.data_ptr(), None, ws.data_ptr(),
+                                         nbytes.value, st), "fwd")
+        dZ = torch.full((N, C), float("nan"), device=cuda)
+        ns = torch.full((N, 4), float("nan"), device=cuda)
+        db = torch.full((C,), float("nan"), device=cuda)
+        if producer:
+            pkg._lib.check(lib.ppgat_bpr_bwd_producer(
+                Z.data_ptr(), N, n_users, n_items, C, u.data_ptr(), i.data_ptr(), j.data_ptr(), S, coef.data_ptr(),
+                gl.data_ptr(), dZ.data_ptr(), b.data_ptr() if with_bias else None, sd.data_ptr(), m.data_ptr(),
+                il.data_ptr(), 1.0, ns.data_ptr(), db.data_ptr() if with_bias else None, ws.data_ptr(), nbytes.value,
+                st), "bwd_producer")
+        else:
+            pkg._lib.check(lib.ppgat_bpr_bwd(Z.data_ptr(), N, n_users, n_items, None, C, u.data_ptr(), i.data_ptr(),
+                                             j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(),
+                                             ws.data_ptr(), nbytes.value, st), "bwd")
+        res.append((dZ, ns, db))
+    (dZ0, _, _), (dZ1, ns, db) = res
+    assert torch.equal(dZ0, dZ1)
+    dz64, z64 = dZ1.double().cpu(), Z.double().cpu()
+    zb = z64 - (b.double().cpu() if with_bias else 0.0)
+    Dref = (dz64 * zb).sum(1)
+    scale = (dz64.abs() * zb.abs()).sum(1)
+    err = (ns[:, 3].double().cpu() - Dref).abs()
+    assert bool((err <= 1e-5 * scale + 1e-30).all()), float((err / scale.clamp_min(1e-30)).max())
+    assert torch.equal(ns[:, :3].cpu(), torch.stack([sd, m, il], 1).cpu())
+    if with_bias:
+        ref = dz64.sum(0)
+        assert float((db.double().cpu() - ref).abs().max()) <= 1e-5 * max(float(dz64.abs().sum(0).max()), 1e-30)
+
+
 def _two_layer_grads(pkg, cuda, steps=1, zero=True):
     g = pkg.data.synthetic_ui_graph(n_users=3000, n_items=800, n_interactions=40_000, seed=5)
     ei = torch.from_numpy(g.edge_index_numpy()).to(cuda)
