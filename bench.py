@@ -265,6 +265,7 @@ def main():
     # the loss backward's sort on a side stream beside the forward: off by default, measured no
     # faster inside the captured step (1.890 vs 1.881 ms, profiles/r05/w1_bench.log)
     bpr_overlap = os.environ.get("PPGAT_BPR_OVERLAP", "0") == "1"
+    one = torch.ones((), dtype=torch.float32, device=dev)  # loss.backward()'s seed, made once (no fill per step)
 
     def step():
         model.train()
@@ -275,14 +276,14 @@ def main():
             loss_fn = pkg.dist.replicated_bpr_loss if part == "replicated" else pkg.dist.halo_bpr_loss
             loss = loss_fn(Z, dg, comm, tu, ti, tj, g.n_users, g.n_items, plan_key="bench")  # fixed triples
             opt.zero_grad(set_to_none=True)
-            loss.backward()
+            loss.backward(one)
             model.allreduce_grads()
         else:
             prep = pkg.hip_ops.bpr_prepare(N, g.n_users, g.n_items, args.hidden, tu, ti, tj) if bpr_overlap else None
             Z = model(feats, ei)
             loss = pkg.bpr_loss(Z, g.n_users, tu, ti, tj, prepared=prep)
             opt.zero_grad(set_to_none=True)
-            loss.backward()
+            loss.backward(one)
         opt.step()
         return loss
 

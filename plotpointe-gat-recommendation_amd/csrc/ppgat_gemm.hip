@@ -1973,11 +1973,11 @@ hipError_t dxw(const float* D, int64_t ldd, const float* S, int64_t lds, const f
   }
   hipLaunchKernelGGL(k_dxw, dim3((unsigned)nb), dim3(64 * kDxwWaves), kDxwLds, st, a);
   TnReduceArg ra{};
-  ra.part = a.part; ra.vpart = a.vpart; ra.cpart = nullptr; ra.splits = nb; ra.M = kPT; ra.K = kPT; ra.nv = 2;
-  ra.out = G; ra.vout = GV; ra.colsum = nullptr;
-  const int64_t elems = kPT * kPT + 2 * kPT;
+  // (the producer's dbias partials ride along as the reduction's column-sum rows)
+  ra.part = a.part; ra.vpart = a.vpart; ra.cpart = a.pbpart; ra.splits = nb; ra.M = kPT; ra.K = kPT; ra.nv = 2;
+  ra.out = G; ra.vout = GV; ra.colsum = a.pbpart ? prod->grad_bias : nullptr;
+  const int64_t elems = kPT * kPT + 2 * kPT + (a.pbpart ? kPT : 0);
   hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((elems + 63) / 64)), dim3(1024), 0, st, ra);
-  if (a.pbpart != nullptr) return launch_col_reduce(a.pbpart, nb, kPT, kPT, prod->grad_bias, nullptr, st);
   return hipGetLastError();
 }
 

@@ -59,10 +59,12 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
                                                  const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
                                                  const int64_t* __restrict__ jj, int64_t S, int kind,
                                                  float2* __restrict__ coef, float* __restrict__ block_loss,
-                                                 int32_t* __restrict__ bad, const int32_t* __restrict__ row_map) {
+                                                 int32_t* __restrict__ block_bad, const int32_t* __restrict__ row_map) {
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;  // subgroups (triples in flight) per block
   __shared__ float sl_loss[SPB];
+  __shared__ int sl_bad[SPB];
+  int nbad = 0;  // out-of-range triples of this subgroup (counted per block: no zeroed counter needed)
   const int tid = threadIdx.x;
   const int sg = tid / LPR, sl = tid % LPR;
   float lsum = 0.f;  // this subgroup's triples, in order (fixed grid => fixed partition)
@@ -82,7 +84,7 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
         pos = dot4(a, ld4(Z + ir * C + sl * 4));
         neg = dot4(a, ld4(Z + jr * C + sl * 4));
       }
-      if (bad != nullptr && sl == 0 && oob) atomicAdd(bad, 1);  // indices were clamped; the caller raises
+      nbad += oob ? 1 : 0;  // indices were clamped; the caller raises
     }
     pos = group_reduce<Op::Sum, 1, LPR / 2>(pos);  // DPP / permlane steps, no LDS round trips
     neg = group_reduce<Op::Sum, 1, LPR / 2>(neg);
@@ -105,28 +107,50 @@ __global__ void __launch_bounds__(256) k_bpr_fwd(const float* __restrict__ Z, in
       lsum += l;
     }
   }
-  if (sl == 0) sl_loss[sg] = lsum;
+  if (sl == 0) {
+    sl_loss[sg] = lsum;
+    sl_bad[sg] = nbad;
+  }
   __syncthreads();
   if (tid == 0) {
     float s = 0.f;
-    for (int k = 0; k < SPB; ++k) s += sl_loss[k];
+    int b = 0;
+    for (int k = 0; k < SPB; ++k) {
+      s += sl_loss[k];
+      b += sl_bad[k];
+    }
     block_loss[blockIdx.x] = s;
+    block_bad[blockIdx.x] = b;
   }
 }
 
 // ordered sum of the block losses -> loss (mean)
-__global__ void __launch_bounds__(1024) k_bpr_loss(const float* __restrict__ block_loss, int64_t nb, float denom,
-                                                   float* __restrict__ loss) {
+// (and the total of the blocks' out-of-range counts -> *bad, when asked)
+__global__ void __launch_bounds__(1024) k_bpr_loss(const float* __restrict__ block_loss,
+                                                   const int32_t* __restrict__ block_bad, int64_t nb, float denom,
+                                                   float* __restrict__ loss, int32_t* __restrict__ bad) {
   __shared__ float red[1024];
+  __shared__ int redb[1024];
   float s = 0.f;
-  for (int64_t b = threadIdx.x; b < nb; b += 1024) s += block_loss[b];
+  int c = 0;
+  for (int64_t b = threadIdx.x; b < nb; b += 1024) {
+    s += block_loss[b];
+    c += block_bad[b];
+  }
   red[threadIdx.x] = s;
+  redb[threadIdx.x] = c;
   __syncthreads();
   for (int w = 512; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    if ((int)threadIdx.x < w) {
+      red[threadIdx.x] += red[threadIdx.x + w];
+      redb[threadIdx.x] += redb[threadIdx.x + w];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) loss[0] = red[0] / denom;
+  if (threadIdx.x == 0) {
+    loss[0] = red[0] / denom;
+    if (bad != nullptr) bad[0] = redb[0];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -314,12 +338,17 @@ struct BprPro {
   const float* invl;
   float gscale;
   float4* nstate;
-  float* bpart;        // nullable: [gridDim.x][C]
+  float* bpart;        // nullable: [chunk blocks][C]
+  int64_t nbpart;      // chunk blocks
+  float* groups;       // [ceil(nbpart / kBpGroup)][C]: stage 1 of the ordered dbias sum (k_bpr_fixup)
+  float* grad_bias;    // stage 2 (k_bpr_zero_untouched)
 };
 
 // <a, z> over the LPR lanes of a subgroup (4 columns per lane), accumulated in fp64 over a fixed
 // tree: the prologue's D feeds the logit gradients alpha (d - D), whose destination sums
 // cancel -- D is rounded once, from the fp32 dZ and Z values, not at every partial sum
+constexpr int kBpGroup = 32;  // chunk-block partials per stage-1 group of the producer's dbias
+
 template <int LPR>
 __device__ __forceinline__ float subgroup_dot(float4 a, float4 z) {
   double v = fma((double)a.w, (double)z.w, fma((double)a.z, (double)z.z, fma((double)a.y, (double)z.y,
@@ -385,14 +414,20 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
     constexpr int U = 4;
     for (int q0 = 0; q0 < len; q0 += U) {
       float4 v[U], zd[U];
+      float ps[U], pm[U], pl[U];
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const int q = q0 + k;
         v[k] = q < len ? ld4(Z + (int64_t)s_src[sg][q] * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        // the destination row itself where a segment finishing in this chunk ends (prologue)
-        const bool fin = pon && q < len && (q == len - 1 ? !ends_after : s_dst[sg][q + 1] != s_dst[sg][q]) &&
-                         s_dst[sg][q] < n_rows;
-        zd[k] = fin ? ld4(Z + (int64_t)s_dst[sg][q] * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        // where a segment finishing in this chunk ends: the destination row itself and its
+        // forward state (prologue), loaded with the contributions -- no round trip at the end
+        const int32_t rq = s_dst[sg][q < len ? q : 0];
+        const bool fin = pon && q < len && (q == len - 1 ? !ends_after : s_dst[sg][q + 1] != rq) && rq < n_rows;
+        zd[k] = fin ? ld4(Z + (int64_t)rq * C + sl * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool fin0 = fin && sl == 0;
+        ps[k] = fin0 ? pro.sdst[rq] : 0.f;
+        pm[k] = fin0 ? pro.m[rq] : 0.f;
+        pl[k] = fin0 ? pro.invl[rq] : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
@@ -410,7 +445,7 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
             if (pon) {  // (uniform over the subgroup: its lanes share the segment)
               const float4 zr = make_float4(zd[k].x - bb.x, zd[k].y - bb.y, zd[k].z - bb.z, zd[k].w - bb.w);
               const float d = subgroup_dot<LPR>(acc, zr);
-              if (sl == 0) pro.nstate[r] = make_float4(pro.sdst[r], pro.m[r], pro.invl[r], d * pro.gscale);
+              if (sl == 0) pro.nstate[r] = make_float4(ps[k], pm[k], pl[k], d * pro.gscale);
             }
           }
           if (pon) bsum = add4(bsum, acc);
@@ -447,6 +482,18 @@ __global__ void __launch_bounds__(256) k_bpr_zero_untouched(const uint8_t* __res
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
+  if (pro.bpart != nullptr && blockIdx.x == 0 && (int)threadIdx.x < C) {  // the producer's dbias, stage 2
+    const int64_t ng = (pro.nbpart + kBpGroup - 1) / kBpGroup;
+    float t = 0.f;
+    for (int64_t q0 = 0; q0 < ng; q0 += 16) {  // 16 loads in flight, summed in order
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = q0 + k < ng ? pro.groups[(q0 + k) * C + threadIdx.x] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) t += v[k];
+    }
+    pro.grad_bias[threadIdx.x] = t;
+  }
   for (int64_t r = (int64_t)blockIdx.x * SPB + sg; r < n_rows; r += (int64_t)gridDim.x * SPB)
     if (!touched[r]) {
       st4(dZ + r * C + sl * 4, make_float4(0.f, 0.f, 0.f, 0.f));
@@ -463,6 +510,18 @@ __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ s
   constexpr int LPR = C / 4;
   constexpr int SPB = 256 / LPR;
   const int sg = threadIdx.x / LPR, sl = threadIdx.x % LPR;
+  if (pro.bpart != nullptr && (int64_t)blockIdx.x * kBpGroup < pro.nbpart && (int)threadIdx.x < C) {
+    // the producer's dbias, stage 1: column c of chunk-block partials [32 b, 32 b + 32), every
+    // load in flight at once, summed in order
+    const int64_t q0 = (int64_t)blockIdx.x * kBpGroup;
+    float v[kBpGroup];
+#pragma unroll
+    for (int k = 0; k < kBpGroup; ++k) v[k] = q0 + k < pro.nbpart ? pro.bpart[(q0 + k) * C + threadIdx.x] : 0.f;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kBpGroup; ++k) t += v[k];
+    pro.groups[(int64_t)blockIdx.x * C + threadIdx.x] = t;
+  }
   const int64_t ch = (int64_t)blockIdx.x * SPB + sg;
   const int64_t b0 = ch * kChunk;
   if (b0 >= total) return;
@@ -486,32 +545,6 @@ __global__ void __launch_bounds__(256) k_bpr_fixup(const int32_t* __restrict__ s
     const float4 zr = make_float4(zd.x - bb.x, zd.y - bb.y, zd.z - bb.z, zd.w - bb.w);
     const float d = subgroup_dot<LPR>(acc, zr);
     if (sl == 0) pro.nstate[r] = make_float4(pro.sdst[r], pro.m[r], pro.invl[r], d * pro.gscale);
-  }
-}
-
-// Ordered column sums of block partials in two stages: block (column slab, row group) sums its
-// <= 256 rows (wave w: rows w, w + 16, ... in order, 16 loads in flight; waves in order) into
-// out[group]; a second launch over the groups gives the total.
-__global__ void __launch_bounds__(1024) k_col_sum_groups(const float* __restrict__ part, int64_t rows, int cols,
-                                                         float* __restrict__ out) {
-  __shared__ float red[16][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  const int64_t r0 = (int64_t)blockIdx.y * 256, r1 = min(rows, r0 + 256);
-  float s = 0.f;
-  if (c < cols) {
-    float v[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = r0 + wv + 16 * k < r1 ? part[(r0 + wv + 16 * k) * cols + c] : 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s += v[k];
-  }
-  red[wv][lane] = s;
-  __syncthreads();
-  if (wv == 0 && c < cols) {
-    float t = 0.f;
-    for (int k = 0; k < 16; ++k) t += red[k][lane];
-    out[(int64_t)blockIdx.y * cols + c] = t;
   }
 }
 
@@ -746,10 +779,13 @@ static int64_t bpr_chunk_blocks(int64_t S, int C) {
   return (chunks + spb - 1) / spb;
 }
 
+// the forward's block partials: loss [nb] floats | out-of-range counts [nb] int32
+static size_t bpr_fwd_region(int64_t S, int C) { return align_up((size_t)bpr_fwd_blocks(S, C) * 8 + 4); }
+
 static size_t bpr_base_bytes(int64_t N, int64_t S, int C) {
   const int64_t c4 = 4 * S > 0 ? 4 * S : 1;
   const int64_t chunks = (c4 + kChunk - 1) / kChunk;
-  return align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4) + 4 * align_up((size_t)c4 * 4) +
+  return bpr_fwd_region(S, C) + 4 * align_up((size_t)c4 * 4) +
          align_up((size_t)chunks * 2 * C * 4) + rs_workspace_bytes(c4, key_bits(N + 1)) + align_up((size_t)N + 1);
 }
 
@@ -761,7 +797,7 @@ struct BprExtra {
 // byte offsets of the producer-prologue region: bpart, groups, end
 static void bpr_extra_offsets(int64_t N, int64_t S, int C, size_t off[3]) {
   const int64_t blocks = bpr_chunk_blocks(S, C);
-  const int64_t groups = (blocks + 255) / 256;
+  const int64_t groups = (blocks + kBpGroup - 1) / kBpGroup;
   off[0] = bpr_base_bytes(N, S, C);
   off[1] = off[0] + align_up((size_t)(blocks > 0 ? blocks : 1) * C * 4);
   off[2] = off[1] + align_up((size_t)(groups > 0 ? groups : 1) * C * 4);
@@ -786,18 +822,15 @@ hipError_t bpr_fwd(const float* Z, int64_t n_rows, int64_t n_users, int64_t n_it
   float* block_loss = static_cast<float*>(ws);
   (void)n_rows;
   const int64_t nb = bpr_fwd_blocks(S, C);
-  if (bad != nullptr) {
-    hipError_t e = hipMemsetAsync(bad, 0, sizeof(int32_t), st);
-    if (e != hipSuccess) return e;
-  }
+  int32_t* block_bad = reinterpret_cast<int32_t*>(block_loss + nb);
   if (S > 0) {
     PPGAT_DISPATCH_LOSS_C(C, hipLaunchKernelGGL(k_bpr_fwd<CC>, dim3((unsigned)nb), dim3(256), 0, st, Z, n_users,
                                                 n_items, u, i, j, S, kind, reinterpret_cast<float2*>(coef),
-                                                block_loss, bad, row_map));
+                                                block_loss, block_bad, row_map));
   }
   const float denom = kind == 0 ? (float)S : 2.f * (float)S;
-  hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(1024), 0, st, block_loss, S > 0 ? nb : 0, denom > 0 ? denom : 1.f,
-                     loss);
+  hipLaunchKernelGGL(k_bpr_loss, dim3(1), dim3(1024), 0, st, block_loss, block_bad, S > 0 ? nb : 0,
+                     denom > 0 ? denom : 1.f, loss, bad);
   return hipGetLastError();
 }
 
@@ -812,7 +845,7 @@ struct BprWs {
 static BprWs bpr_ws(void* ws, int64_t N, int64_t S, int C) {
   const int64_t total = 4 * S;
   const int64_t chunks = (total + kChunk - 1) / kChunk;
-  char* p = static_cast<char*>(ws) + align_up((size_t)bpr_fwd_blocks(S, C) * 4 + 4);
+  char* p = static_cast<char*>(ws) + bpr_fwd_region(S, C);
   const size_t e4 = align_up((size_t)total * 4);
   BprWs w;
   w.keys = reinterpret_cast<int32_t*>(p);
@@ -837,7 +870,7 @@ hipError_t bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, con
   if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
   const int64_t total = 4 * S;
   const BprWs w = bpr_ws(ws, N, S, C);
-  hipError_t err = hipMemsetAsync(w.touched, 0, (size_t)N, st);
+  hipError_t err = hipMemsetAsync(w.touched, 0, ((size_t)N + 15) & ~(size_t)15, st);  // (one fill kernel, no tail)
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
                      n_items, row_map, N, w.keys, w.vals);
@@ -866,12 +899,15 @@ hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64
     const BprExtra x = bpr_extra(ws, N, S, C);
     pk.bias = prod->bias; pk.sdst = prod->s_dst; pk.m = prod->m; pk.invl = prod->inv_l;
     pk.gscale = prod->gscale; pk.nstate = reinterpret_cast<float4*>(prod->nstate);
-    pk.bpart = prod->grad_bias ? x.bpart : nullptr;
+    pk.bpart = (prod->grad_bias && S > 0) ? x.bpart : nullptr;
+    pk.nbpart = bpr_chunk_blocks(S, C);
+    pk.groups = x.groups;
+    pk.grad_bias = prod->grad_bias;
   }
   const BprWs w = bpr_ws(ws, N, S, C);
   if (S == 0) {
     if (prod == nullptr) return hipMemsetAsync(dZ, 0, (size_t)N * C * 4, st);  // otherwise k_bpr_zero_untouched
-    hipError_t e = hipMemsetAsync(w.touched, 0, (size_t)N, st);
+    hipError_t e = hipMemsetAsync(w.touched, 0, ((size_t)N + 15) & ~(size_t)15, st);
     if (e == hipSuccess && prod->grad_bias) e = hipMemsetAsync(prod->grad_bias, 0, (size_t)C * 4, st);
     if (e != hipSuccess) return e;
   }
@@ -889,15 +925,6 @@ hipError_t bpr_bwd_finish(const float* Z, int64_t n_rows, int64_t n_users, int64
       int64_t gz = (N + SPB - 1) / SPB;
       if (gz > 4096) gz = 4096;
       hipLaunchKernelGGL(k_bpr_zero_untouched<CC>, dim3((unsigned)gz), dim3(256), 0, st, w.touched, N, dZ, pk);
-    }
-    if (pk.bpart != nullptr && S > 0) {  // grad_bias: the chunk blocks' partials in two ordered stages
-      const int64_t groups = ((int64_t)g + 255) / 256;
-      const unsigned cs = (unsigned)((CC + 63) / 64);
-      float* out1 = groups > 1 ? bpr_extra(ws, N, S, C).groups : prod->grad_bias;
-      hipLaunchKernelGGL(k_col_sum_groups, dim3(cs, (unsigned)groups), dim3(1024), 0, st, pk.bpart, (int64_t)g, CC,
-                         out1);
-      if (groups > 1)
-        hipLaunchKernelGGL(k_col_sum_groups, dim3(cs, 1), dim3(1024), 0, st, out1, groups, CC, prod->grad_bias);
     }
   });
   return hipGetLastError();

@@ -1695,7 +1695,7 @@ class _BPRLoss(torch.autograd.Function):
         ctx.prepared = prep is not None
         ctx.row_map = row_map
         ctx.meta = (n_rows, n_users, n_items, C, S)
-        return loss[0]
+        return loss.view(())  # (a view: its backward is a reshape, where loss[0]'s is a zero fill + copy)
 
     @staticmethod
     def backward(ctx, gl):
