@@ -548,6 +548,14 @@ int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, 
 int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
                               const unsigned* b_bound_bits, int bound_period, float bound_scale, float* out,
                               void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_gemm_tn_big_bounds: both bounds the caller's (either nullable: that operand's column-max
+ *   pass instead).  a_bound_bits[i] bounds |a[r, i]| over the rows r whose b row is NOT all zero
+ *   (e.g. g over the destinations that have an in-edge, from ppgat_xgat_bwd_edges_gd_colmax, for
+ *   G = g^T agg: agg_r = 0 without in-edges); the other rows' a values are clamped to the fp16
+ *   range in the split, so they add 0 as they must.  b_bound_bits as in _bounded. */
+int ppgat_gemm_tn_big_bounds(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                             const unsigned* a_bound_bits, const unsigned* b_bound_bits, int bound_period,
+                             float bound_scale, float* out, void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream);
 int ppgat_colmax_abs_sources(const float* x, int64_t ldx, int64_t n, int c, const int32_t* src_ptr,
                              unsigned* out_bits, void* stream);
@@ -586,6 +594,15 @@ int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const in
                    int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
                    const float* s_dst, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
                    float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_xgat_fwd that also merges into x_colmax_bits[k] (caller-initialised, e.g. zeros; 16-byte
+ * aligned) the IEEE bits of max |x_j[k]| over the rows it gathers -- every source of an edge,
+ * the rows ppgat_colmax_abs_sources covers -- by atomic max (order-free: deterministic).  The
+ * bound of |agg| the weight gradient's fp16 split needs, without a pass over x. */
+int ppgat_xgat_fwd_colmax(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
+                          int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
+                          const float* s_dst, float negative_slope, float dropout_p, uint64_t seed,
+                          uint64_t* seed_used, float* agg, float* m, float* inv_l, unsigned* x_colmax_bits,
+                          void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_xgat_bwd_prologue(const float* gt, const float* agg, const float* s_dst, const float* m, const float* inv_l,
                             int64_t n_dst, int in_channels, int heads, float* nstate, void* stream);
 int ppgat_xgat_bwd_workspace_bytes(int64_t n_hub_items, int in_channels, size_t* bytes);
@@ -621,6 +638,15 @@ int ppgat_xgat_bwd_edges_gd(const ppgat_schedule* src_sched, const int32_t* row,
                             float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
                             float* acc, float* dalpha, float* pdalpha, void* workspace, size_t workspace_bytes,
                             void* stream);
+/* ppgat_xgat_bwd_edges_gd that also merges into g_colmax_bits[c] the bits of max |g_i[c]| over the
+ * rows it gathers (every destination of an edge), as ppgat_xgat_fwd_colmax: the A bound of
+ * ppgat_gemm_tn_big_bounds for G = g^T agg. */
+int ppgat_xgat_bwd_edges_gd_colmax(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                                   const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                                   const float* s_src, const float* nstate, const float* g, int64_t ldg,
+                                   float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
+                                   float* acc, float* dalpha, float* pdalpha, unsigned* g_colmax_bits,
+                                   void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_xgat_nstate(const float* s_dst, const float* m, const float* inv_l, const float* D, int64_t n_dst, int heads,
                       float* nstate, void* stream);
 int ppgat_xgat_bwd_dz_workspace_bytes(int64_t n_hub_items, int heads, size_t* bytes);

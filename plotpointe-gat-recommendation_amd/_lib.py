@@ -123,6 +123,8 @@ SIGNATURES = {
     "ppgat_gemm_tn_big": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_gemm_tn_big_bounded": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_int, c_f, c_vp, c_vp,
                                           c_sz, c_vp]),
+    "ppgat_gemm_tn_big_bounds": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_f, c_vp,
+                                         c_vp, c_sz, c_vp]),
     "ppgat_colmax_abs": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "ppgat_colmax_abs_sources": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp]),
     "ppgat_colsum_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
@@ -133,6 +135,8 @@ SIGNATURES = {
     "ppgat_xgat_fwd_workspace_bytes": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_xgat_fwd": (c_int, [SP, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_f, c_f, c_u64,
                                c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_fwd_colmax": (c_int, [SP, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_f, c_f,
+                                      c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_xgat_bwd_prologue": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp]),
     "ppgat_xgat_bwd_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_xgat_bwd_edges": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
@@ -142,6 +146,8 @@ SIGNATURES = {
                                        c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_xgat_bwd_edges_gd": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64,
                                         c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ppgat_xgat_bwd_edges_gd_colmax": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                                               c_i64, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_xgat_nstate": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
     "ppgat_xgat_bwd_dz_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_xgat_bwd_dz": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_u64, c_vp, c_vp, c_vp,

@@ -1103,15 +1103,16 @@ int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, 
   return PPGAT_OK;
 }
 
-int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
-                              const unsigned* b_bound_bits, int bound_period, float bound_scale, float* out,
-                              void* workspace, size_t workspace_bytes, void* stream) {
+static int gemm_tn_big_bounds_impl(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma,
+                                   int nb, const unsigned* a_bound_bits, const unsigned* b_bound_bits,
+                                   int bound_period, float bound_scale, float* out, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
   if (m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
     return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big_bounded: needs ma, nb multiples of 128");
   if (lda < ma || ldb < nb || (lda % 4) || (ldb % 4))
     return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: bad leading dimension");
-  if (!out || !b_bound_bits || (m > 0 && (!a || !b))) return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: null pointer");
-  if (bound_period < 1 || nb % bound_period || !(bound_scale >= 1.f) || !(bound_scale < 3.4e38f))
+  if (!out || (m > 0 && (!a || !b))) return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: null pointer");
+  if (b_bound_bits && (bound_period < 1 || nb % bound_period || !(bound_scale >= 1.f) || !(bound_scale < 3.4e38f)))
     return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: period must divide nb, scale >= 1 and finite");
   if (!al16(a) || !al16(b)) return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big_bounded: 16-byte aligned rows");
   if (!workspace || workspace_bytes < ppgat::gemm_tn_big_workspace_bytes(m, ma, nb))
@@ -1119,9 +1120,24 @@ int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_GEMM_TN, st);
   hipError_t e = ppgat::gemm_tn_big(a, lda, b, ldb, m, ma, nb, out, workspace, st, b_bound_bits, bound_period,
-                                    bound_scale);
+                                    bound_scale, a_bound_bits);
   if (e != hipSuccess) return hip_fail(e, "gemm_tn_big_bounded");
   return PPGAT_OK;
+}
+
+int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                              const unsigned* b_bound_bits, int bound_period, float bound_scale, float* out,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (!b_bound_bits) return fail(PPGAT_ERR_INVALID, "gemm_tn_big_bounded: null pointer");
+  return gemm_tn_big_bounds_impl(a, lda, b, ldb, m, ma, nb, nullptr, b_bound_bits, bound_period, bound_scale, out,
+                                 workspace, workspace_bytes, stream);
+}
+
+int ppgat_gemm_tn_big_bounds(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                             const unsigned* a_bound_bits, const unsigned* b_bound_bits, int bound_period,
+                             float bound_scale, float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_tn_big_bounds_impl(a, lda, b, ldb, m, ma, nb, a_bound_bits, b_bound_bits, bound_period, bound_scale, out,
+                                 workspace, workspace_bytes, stream);
 }
 
 int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream) {
@@ -1198,10 +1214,11 @@ int ppgat_xgat_fwd_workspace_bytes(int64_t n_hub_items, int heads, int in_channe
   return PPGAT_OK;
 }
 
-int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
+static int xgat_fwd_impl(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
                    int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
                    const float* s_dst, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
-                   float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream) {
+                   float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream,
+                   unsigned* x_colmax_bits) {
   if (in_channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_fwd: shape");
   if (n_dst < 0 || n_edges < 0 || ldx < in_channels || (ldx % 4)) return fail(PPGAT_ERR_INVALID, "xgat_fwd: bad sizes");
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
@@ -1222,9 +1239,30 @@ int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const in
   if (e == hipSuccess)
     e = ppgat::xgat_fwd(it, col, csr_eid, x, ldx, in_channels, heads, s_src, s_dst, negative_slope, dropout_p, seed,
                         seed_used, agg, m, inv_l, static_cast<float*>(workspace), dst_sched->hub_row,
-                        dst_sched->hub_ptr, dst_sched->n_hubs, st);
+                        dst_sched->hub_ptr, dst_sched->n_hubs, st, x_colmax_bits);
   if (e != hipSuccess) return hip_fail(e, "xgat_fwd");
   return PPGAT_OK;
+}
+
+int ppgat_xgat_fwd(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
+                   int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
+                   const float* s_dst, float negative_slope, float dropout_p, uint64_t seed, uint64_t* seed_used,
+                   float* agg, float* m, float* inv_l, void* workspace, size_t workspace_bytes, void* stream) {
+  return xgat_fwd_impl(dst_sched, col, csr_eid, n_dst, n_edges, in_channels, heads, x, ldx, s_src, s_dst,
+                       negative_slope, dropout_p, seed, seed_used, agg, m, inv_l, workspace, workspace_bytes, stream,
+                       nullptr);
+}
+
+int ppgat_xgat_fwd_colmax(const ppgat_schedule* dst_sched, const int32_t* col, const int32_t* csr_eid, int64_t n_dst,
+                          int64_t n_edges, int in_channels, int heads, const float* x, int64_t ldx, const float* s_src,
+                          const float* s_dst, float negative_slope, float dropout_p, uint64_t seed,
+                          uint64_t* seed_used, float* agg, float* m, float* inv_l, unsigned* x_colmax_bits,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (!x_colmax_bits || (reinterpret_cast<uintptr_t>(x_colmax_bits) % 16))
+    return fail(PPGAT_ERR_INVALID, "xgat_fwd_colmax: x_colmax_bits [in_channels], 16-byte aligned");
+  return xgat_fwd_impl(dst_sched, col, csr_eid, n_dst, n_edges, in_channels, heads, x, ldx, s_src, s_dst,
+                       negative_slope, dropout_p, seed, seed_used, agg, m, inv_l, workspace, workspace_bytes, stream,
+                       x_colmax_bits);
 }
 
 int ppgat_xgat_bwd_prologue(const float* gt, const float* agg, const float* s_dst, const float* m, const float* inv_l,
@@ -1314,12 +1352,12 @@ int ppgat_xgat_bwd_edges_g(const ppgat_schedule* src_sched, const int32_t* row, 
   return PPGAT_OK;
 }
 
-int ppgat_xgat_bwd_edges_gd(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+static int xgat_bwd_edges_gd_impl(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
                             const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
                             const float* s_src, const float* nstate, const float* g, int64_t ldg,
                             float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
                             float* acc, float* dalpha, float* pdalpha, void* workspace, size_t workspace_bytes,
-                            void* stream) {
+                            void* stream, unsigned* g_colmax_bits) {
   if (channels != 256 || (heads != 2 && heads != 4)) return fail(PPGAT_ERR_UNSUPPORTED, "xgat_bwd_edges_gd: shape");
   if (n_edges < 0 || ldg < channels || (ldg % 4)) return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd: bad sizes");
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return fail(PPGAT_ERR_INVALID, "dropout p must be in [0, 1)");
@@ -1339,9 +1377,33 @@ int ppgat_xgat_bwd_edges_gd(const ppgat_schedule* src_sched, const int32_t* row,
   hipError_t e = ppgat::xgat_bwd_edges_g(it, row, csc_eid, dz_slot, hs, channels, heads, s_src, nstate, g, ldg,
                                          negative_slope, dropout_p, seed, seed_used, acc, nullptr, 0, dalpha,
                                          static_cast<float*>(workspace), src_sched->hub_row, src_sched->hub_ptr,
-                                         src_sched->n_hubs, st, pdalpha);
+                                         src_sched->n_hubs, st, pdalpha, g_colmax_bits);
   if (e != hipSuccess) return hip_fail(e, "xgat_bwd_edges_gd");
   return PPGAT_OK;
+}
+
+int ppgat_xgat_bwd_edges_gd(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                            const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                            const float* s_src, const float* nstate, const float* g, int64_t ldg,
+                            float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
+                            float* acc, float* dalpha, float* pdalpha, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  return xgat_bwd_edges_gd_impl(src_sched, row, csc_eid, dz_slot, n_edges, channels, heads, hs, s_src, nstate, g, ldg,
+                                negative_slope, dropout_p, seed, seed_used, acc, dalpha, pdalpha, workspace,
+                                workspace_bytes, stream, nullptr);
+}
+
+int ppgat_xgat_bwd_edges_gd_colmax(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
+                                   const int32_t* dz_slot, int64_t n_edges, int channels, int heads, const float* hs,
+                                   const float* s_src, const float* nstate, const float* g, int64_t ldg,
+                                   float negative_slope, float dropout_p, uint64_t seed, const uint64_t* seed_used,
+                                   float* acc, float* dalpha, float* pdalpha, unsigned* g_colmax_bits,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  if (!g_colmax_bits || (reinterpret_cast<uintptr_t>(g_colmax_bits) % 16))
+    return fail(PPGAT_ERR_INVALID, "xgat_bwd_edges_gd_colmax: g_colmax_bits [channels], 16-byte aligned");
+  return xgat_bwd_edges_gd_impl(src_sched, row, csc_eid, dz_slot, n_edges, channels, heads, hs, s_src, nstate, g, ldg,
+                                negative_slope, dropout_p, seed, seed_used, acc, dalpha, pdalpha, workspace,
+                                workspace_bytes, stream, g_colmax_bits);
 }
 
 int ppgat_xgat_nstate(const float* s_dst, const float* m, const float* inv_l, const float* D, int64_t n_dst, int heads,

@@ -211,7 +211,7 @@ bool gemm_tn_big_shape_ok(int Ma, int Nb);
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
                        void* ws, hipStream_t st, const unsigned* b_bound = nullptr, int b_period = 0,
-                       float b_scale = 1.f);
+                       float b_scale = 1.f, const unsigned* a_bound = nullptr);
 hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st,
                       const int32_t* src_ptr = nullptr);
 bool xgat_shape_ok(int K, int H, int C);
@@ -222,7 +222,8 @@ hipError_t xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_ds
 hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, const float* x, int64_t ldx, int K,
                     int H, const float* s_src, const float* s_dst, float slope, float p, uint64_t seed,
                     const uint64_t* seed_in, float* agg, float* m, float* invl, float* partial,
-                    const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st);
+                    const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st,
+                    unsigned* xmax = nullptr);
 hipError_t xgat_bwd_pro(const float* gt, const float* agg, const float* s_dst, const float* m, const float* invl,
                         int64_t n, int K, int H, float* nstate, hipStream_t st);
 hipError_t xgat_bwd_edges(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr,
@@ -235,7 +236,8 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                             const float* hs, int C, int H, const float* s_src, const float* nstate, const float* g,
                             int64_t ldg, float slope, float p, uint64_t seed, const uint64_t* seed_in, float* acc,
                             float* S, int64_t lds, float* dz, float* partial, const int32_t* hub_row,
-                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz = nullptr);
+                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz = nullptr,
+                            unsigned* gmax = nullptr);
 int nnh_pipeline_variant();  // the fp16 NN main loop: 1 k_gemm_nnh, 2 k_gemm_nnh2, 3 k_gemm_nnh3 (PPGAT_NNH2)
 hipError_t xgat_nstate(const float* s_dst, const float* m, const float* invl, const float* D, int64_t n, int H,
                        float* nstate, hipStream_t st);

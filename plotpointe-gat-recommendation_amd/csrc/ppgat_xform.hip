@@ -55,6 +55,19 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 __device__ __forceinline__ float4 mul4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
+__device__ __forceinline__ float4 absmax4(float4 m, float4 v) {
+  return make_float4(fmaxf(m.x, fabsf(v.x)), fmaxf(m.y, fabsf(v.y)), fmaxf(m.z, fabsf(v.z)), fmaxf(m.w, fabsf(v.w)));
+}
+// merge a lane's maxima of |v| for columns c0 .. c0 + 3 into bits (IEEE bits, ordered as unsigned
+// for v >= 0): read first, atomic only where larger -- after the first waves almost never.  A max
+// is order-free, so the result is deterministic.
+__device__ __forceinline__ void colmax_merge4(unsigned* bits, int c0, float4 m) {
+  const uint4 cur = *reinterpret_cast<const uint4*>(bits + c0);
+  if (__float_as_uint(m.x) > cur.x) atomicMax(bits + c0, __float_as_uint(m.x));
+  if (__float_as_uint(m.y) > cur.y) atomicMax(bits + c0 + 1, __float_as_uint(m.y));
+  if (__float_as_uint(m.z) > cur.z) atomicMax(bits + c0 + 2, __float_as_uint(m.z));
+  if (__float_as_uint(m.w) > cur.w) atomicMax(bits + c0 + 3, __float_as_uint(m.w));
+}
 __device__ __forceinline__ float dot4(float4 a, float4 b) {
   return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
 }
@@ -1179,6 +1192,7 @@ struct TnhArg {
   int tiles_a, tiles_b, splits;
   int64_t rows_per_split;
   const unsigned* amax;  // [Ma] column maxima (IEEE bits of |v|)
+  int aclamp;            // amax covers only the rows whose B row is nonzero: clamp A's scaled values
   const unsigned* bmax;  // B column n's bound: bmax[n % bperiod] * bscale
   int bperiod;
   float bscale;
@@ -1193,9 +1207,15 @@ __device__ __forceinline__ uint2 th_tr16(const unsigned char* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
-// 4 values times their column scales -> two fp16x4 terms (split2h's arithmetic)
-__device__ __forceinline__ void split2h_4(const float4& v, const float4& s, uint2& h, uint2& l) {
-  const float e[4] = {v.x * s.x, v.y * s.y, v.z * s.z, v.w * s.w};
+// 4 values times their column scales -> two fp16x4 terms (split2h's arithmetic); clamp: the
+// scaled values limited to the fp16 range first (rows a caller's bound does not cover, whose
+// product partners are zero: they add 0 instead of inf * 0)
+__device__ __forceinline__ void split2h_4(const float4& v, const float4& s, uint2& h, uint2& l, bool clamp = false) {
+  float e[4] = {v.x * s.x, v.y * s.y, v.z * s.z, v.w * s.w};
+  if (clamp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = fminf(fmaxf(e[i], -65504.f), 65504.f);
+  }
   uint32_t hh[2], ll[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1267,7 +1287,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
       const bool ok = row0 + lr < r1;
       const int off = th_off(lr, sc >> 3) + 8 * ((sc >> 2) & 1);
       uint2 h, l;
-      split2h_4(ok ? S.a[p] : f4(0.f), sa, h, l);
+      split2h_4(ok ? S.a[p] : f4(0.f), sa, h, l, a.aclamp != 0);
       *reinterpret_cast<uint2*>(img + off) = h;
       *reinterpret_cast<uint2*>(img + kThImg + off) = l;
       split2h_4(ok ? S.b0[p] : f4(0.f), sb0, h, l);
@@ -1442,7 +1462,10 @@ __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restr
                                                const float* __restrict__ s_dst, float slope, float p, float inv_keep,
                                                uint64_t seed, const uint64_t* __restrict__ seed_in,
                                                float* __restrict__ agg, float* __restrict__ m_out,
-                                               float* __restrict__ invl_out, float* __restrict__ partial) {
+                                               float* __restrict__ invl_out, float* __restrict__ partial,
+                                               unsigned* __restrict__ xmax) {
+  // xmax != NULL: the column maxima of |x_j| over the gathered rows (every source of an edge)
+  // merged into it -- the bound of |agg| the weight gradient's fp16 split needs, for free
   static_assert(K == 256, "k_fwd_x: K == 256 (one float4 per lane)");
   constexpr int U = 8;
   if (p > 0.f) seed = *seed_in;
@@ -1456,6 +1479,7 @@ __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restr
   const bool hub = w < it.n_hub_items;
   float sd[H], mh[H], lh[H];
   float4 acc[H];
+  float4 xm = f4(0.f);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     sd[h] = s_dst[i * H + h];
@@ -1496,10 +1520,12 @@ __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restr
         const int q = min(q0 + u, 63);
 #pragma unroll
         for (int h = 0; h < H; ++h) acc[h] = fma4(q0 + u < n ? recw[wv][h][q] : 0.f, v[u], acc[h]);
+        xm = absmax4(xm, v[u]);
       }
     }
     wave_sync();
   }
+  if (xmax != nullptr) colmax_merge4(xmax, lane * 4, xm);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     if (hub) {
@@ -1742,9 +1768,11 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
                                                float inv_keep, uint64_t seed, const uint64_t* __restrict__ seed_in,
                                                float* __restrict__ acc_out, float* __restrict__ S, int64_t lds,
                                                float* __restrict__ dz, float* __restrict__ partial,
-                                               float* __restrict__ pz) {
+                                               float* __restrict__ pz, unsigned* __restrict__ gmax) {
   // pz != NULL (deferred D): dz receives dalpha = g_i . hs_j and pz beta * dalpha per edge and
-  // head (D_i = sum_j beta dalpha by a destination sum, dz by k_xgat_dz); no ds_src here
+  // head (D_i = sum_j beta dalpha by a destination sum, dz by k_xgat_dz); no ds_src here.
+  // gmax != NULL: the column maxima of |g_i| over the gathered rows (every destination of an
+  // edge) merged into it
   static_assert(C == 256 && H <= 4, "k_bwd_g: C == 256, H <= 4");
   constexpr int U = 16 / H;  // edges per reduction group (16 partial dots per lane)
   if (p > 0.f) seed = *seed_in;
@@ -1757,6 +1785,7 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
   const int cs = it.beg[w], ce = it.end[w];
   const bool hub = w < it.n_hub_items;
   float4 hv[H], acc[H];
+  float4 gm = f4(0.f);
   float ss[H], dsa[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
@@ -1796,6 +1825,7 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
         const int q = q0 + u;
         const int64_t ii = recA[wv][min(q, 63)].x;
         gq[u] = q < n ? ld4(g + ii * ldg + lane * 4) : f4(0.f);
+        gm = absmax4(gm, gq[u]);
       }
       float part[16];
 #pragma unroll
@@ -1837,6 +1867,7 @@ __global__ void __launch_bounds__(256) k_bwd_g(XItems it, const int32_t* __restr
     }
     wave_sync();
   }
+  if (gmax != nullptr) colmax_merge4(gmax, lane * 4, gm);
   float ds[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) ds[h] = wave_sum(dsa[h]);
@@ -2517,7 +2548,8 @@ hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* o
 }
 
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
-                       void* ws, hipStream_t st, const unsigned* b_bound, int b_period, float b_scale) {
+                       void* ws, hipStream_t st, const unsigned* b_bound, int b_period, float b_scale,
+                       const unsigned* a_bound) {
   if (M <= 0) return hipMemsetAsync(out, 0, (size_t)Ma * Nb * 4, st);  // empty sum (no partials)
   if (tnh_ok(M, Ma, Nb)) {
     static const bool attr = [] {
@@ -2534,12 +2566,14 @@ hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb,
     a.rows_per_split = ((M + a.splits - 1) / a.splits + kTR - 1) / kTR * kTR;
     a.part = static_cast<float*>(ws);
     unsigned* mx = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + align_up((size_t)a.splits * Ma * Nb * 4));
-    a.amax = mx;
+    a.amax = a_bound ? a_bound : mx;       // a caller's bound of |A| (rows with nonzero B) skips A's pass
+    a.aclamp = a_bound ? 1 : 0;
     a.bmax = b_bound ? b_bound : mx + Ma;  // a caller's bound of |B| per column skips B's pass
     a.bperiod = b_bound ? b_period : Nb;
     a.bscale = b_bound ? b_scale : 1.f;
-    hipError_t e = hipMemsetAsync(mx, 0, (size_t)(b_bound ? Ma : Ma + Nb) * 4, st);
-    if (e == hipSuccess) e = colmax_bits(A, lda, M, Ma, mx, st);
+    hipError_t e = hipSuccess;
+    if (!a_bound || !b_bound) e = hipMemsetAsync(mx, 0, (size_t)(Ma + Nb) * 4, st);
+    if (e == hipSuccess && !a_bound) e = colmax_bits(A, lda, M, Ma, mx, st);
     if (e == hipSuccess && !b_bound) e = colmax_bits(B, ldb, M, Nb, mx + Ma, st);
     if (e != hipSuccess) return e;
     const unsigned grid = (unsigned)(8 * T * ((a.splits + 7) / 8));
@@ -2597,13 +2631,13 @@ hipError_t xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_ds
 hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, const float* x, int64_t ldx, int K,
                     int H, const float* s_src, const float* s_dst, float slope, float p, uint64_t seed,
                     const uint64_t* seed_in, float* agg, float* m, float* invl, float* partial,
-                    const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st) {
+                    const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, unsigned* xmax) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   if (it.n_items > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_fwd_x<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
                                    col, eid, x, ldx, s_src, s_dst, slope, p, inv_keep, seed, seed_in, agg, m, invl,
-                                   partial));
+                                   partial, xmax));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)K;
@@ -2647,13 +2681,13 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                             const float* hs, int C, int H, const float* s_src, const float* nstate, const float* g,
                             int64_t ldg, float slope, float p, uint64_t seed, const uint64_t* seed_in, float* acc,
                             float* S, int64_t lds, float* dz, float* partial, const int32_t* hub_row,
-                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz) {
+                            const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz, unsigned* gmax) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   if (it.n_items > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
                                    row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
-                                   slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz));
+                                   slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz, gmax));
   if (n_hubs > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs), dim3(64 * kMW), 0, st, hub_row,
                                    hub_ptr, partial, acc, S, lds));

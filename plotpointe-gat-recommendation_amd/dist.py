@@ -942,10 +942,10 @@ def _halo_xgat_backward(saved: dict, g: torch.Tensor, hg: "HaloGraph", comm: "Co
     del acc
     # 6. weight gradients (the sums over ranks: the dense all-reduce)
     return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0],
-                                xbits=_source_colmax_bits(x[:n0], hg, comm))
+                                xbits=_source_colmax_bits(x[:n0], hg, comm, saved))
 
 
-def _source_colmax_bits(x_own: torch.Tensor, hg: "HaloGraph", comm: "Comm") -> torch.Tensor:
+def _source_colmax_bits(x_own: torch.Tensor, hg: "HaloGraph", comm: "Comm", saved=None) -> torch.Tensor:
     """The column bound of the weight-gradient GEMM's aggregate operand (hip_ops._xgat_weight_grads):
     |agg_i[k]| <= max |x_j[k]| over i's sources j.  The exact set -- every table row with an edge
     into an own destination -- is 11M rows (11 GB) per rank at world 8 on config 5; instead each
@@ -953,9 +953,12 @@ def _source_colmax_bits(x_own: torch.Tensor, hg: "HaloGraph", comm: "Comm") -> t
     table rows' out-edges are their owners' own out-edges) and the ranks' maxima are combined by
     an all_reduce(MAX) of K int32 (IEEE bits of non-negative floats order as the floats): the
     maximum over every row with an out-edge anywhere, a superset of the sources, never a
-    row without one.  At world 1 it is the exact set."""
+    row without one.  At world 1 it is the exact set.  With the forward's own maxima (``saved``
+    xbits: gathered by its edge pass over this rank's destinations, halo sources included) the
+    all_reduce(MAX) of those is exactly the maximum over every source, and x is not read again."""
     from . import hip_ops as O
-    bits = O.colmax_abs(x_own, hg.src_views.colptr)
+    xb = saved.get("xbits") if saved is not None else None
+    bits = xb.clone() if xb is not None else O.colmax_abs(x_own, hg.src_views.colptr)
     return comm.all_reduce_(bits, op=dist.ReduceOp.MAX)
 
 
@@ -1049,6 +1052,7 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     acc = torch.empty(max(n0, 1), H * C, dtype=torch.float32, device=dev)
     dz = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
     pdal = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    gbits = torch.zeros(C, dtype=torch.int32, device=dev)  # |g| over the gathered table rows (A bound of G)
     nu = hg.n_own_u
     by_need = {"i": (hg.src_sched_u, 0, "i"), "u": (hg.src_sched_i, nu, "u")}  # user sources read items
     phases = [by_need[c] for c in order] if hg.bipartite else [(sv.bwd_sched, 0, None)]
@@ -1064,13 +1068,15 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
         _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
         ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
         cs = sched.cstruct()
-        _lib.check(lib.ppgat_xgat_bwd_edges_gd(ctypes.byref(cs), _lib.ptr(sv.row) if E else None,
-                                               _lib.ptr(sv.csc_eid) if E else None, None, E, C, H,
-                                               hs.data_ptr() + 4 * base * H * C, s_src.data_ptr() + 4 * base * H,
-                                               ntab.x.data_ptr(), gtab.x.data_ptr(), C, float(slope), float(p),
-                                               int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
-                                               acc.data_ptr() + 4 * base * H * C, dz.data_ptr(), pdal.data_ptr(),
-                                               ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_gd")
+        _lib.check(lib.ppgat_xgat_bwd_edges_gd_colmax(ctypes.byref(cs), _lib.ptr(sv.row) if E else None,
+                                                      _lib.ptr(sv.csc_eid) if E else None, None, E, C, H,
+                                                      hs.data_ptr() + 4 * base * H * C,
+                                                      s_src.data_ptr() + 4 * base * H, ntab.x.data_ptr(),
+                                                      gtab.x.data_ptr(), C, float(slope), float(p),
+                                                      int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                                      acc.data_ptr() + 4 * base * H * C, dz.data_ptr(),
+                                                      pdal.data_ptr(), gbits.data_ptr(), ws.data_ptr(), nbytes.value,
+                                                      st), "xgat_bwd_edges_gd_colmax")
     gtab.wait_all()
     ntab.wait_all()
     del hs
@@ -1109,7 +1115,16 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     # the weight-gradient bound's all_reduce now, before any exchange of the layer below is
     # started on the communication stream: no two collectives of one communicator in flight on
     # two streams (the comm stream's start waits for this stream's work so far)
-    xbits = _source_colmax_bits(x[:n0], hg, comm)
+    # (one all_reduce(MAX) for both bounds: the union over the ranks of the rows each edge pass
+    # gathered is every source / every destination with an edge -- a rank's own g rows may have
+    # their in-edges homed elsewhere, so its local g maxima alone would not cover them)
+    xb = saved.get("xbits")
+    if xb is not None:
+        both = comm.all_reduce_(torch.cat([xb, gbits]), op=dist.ReduceOp.MAX)
+        xbits, gbits = both[:K], both[K:]
+    else:
+        xbits = _source_colmax_bits(x[:n0], hg, comm, saved)
+        gbits = comm.all_reduce_(gbits, op=dist.ReduceOp.MAX)
     below = link_in.get("saved") if link_in is not None else None
     if below is not None and n0:
         # the layer below's g = this dx: straight into its table, its exchanges started now
@@ -1121,7 +1136,7 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
         dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \
             torch.zeros(0, K, dtype=torch.float32, device=dev)
     del acc
-    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0], xbits=xbits)
+    return O._xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, x_rows=x[:n0], xbits=xbits, gbits=gbits)
 
 
 class _ShardedBase(torch.nn.Module):

@@ -806,11 +806,30 @@ def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, s
 # ---------------------------------------------------------------------------
 # projection with the MFMA weight-gradient kernel, and the fused BPR/BCE loss
 # ---------------------------------------------------------------------------
+_CONST_BOUNDS = {}
+
+
+def _const_colmax(t: torch.Tensor) -> torch.Tensor:
+    """colmax_abs(t) for a tensor the step does not change (the item features of the config-5
+    projection's weight gradient): computed once per (tensor object, version), so the column-max
+    pass over it leaves the training step."""
+    import weakref
+    e = _CONST_BOUNDS.get(id(t))
+    if e is not None and e[0]() is t and e[1] == t._version:
+        return e[2]
+    bits = colmax_abs(t)
+    for k in [k for k, v in _CONST_BOUNDS.items() if v[0]() is None]:
+        del _CONST_BOUNDS[k]
+    _CONST_BOUNDS[id(t)] = (weakref.ref(t), t._version, bits)
+    return bits
+
+
 def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Optional[torch.Tensor] = None,
-            B_items: Optional[torch.Tensor] = None):
+            B_items: Optional[torch.Tensor] = None, b_const: bool = False):
     """A [N,M], B [N,K] (row strides may exceed the widths) -> (A^T B [M,K], colsum(A) [M]
     or None, V^T B [nv,K] or None), deterministic.  With ``B_items`` the B rows are
-    cat(B, B_items) (two row segments, not concatenated)."""
+    cat(B, B_items) (two row segments, not concatenated).  ``b_const``: B does not change between
+    calls (its column bound for the fp16 TN kernel is cached, _const_colmax)."""
     lib = _lib.load()
     for name, t in (("A", A), ("B", B)) + ((("B_items", B_items),) if B_items is not None else ()):
         _require(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32,
@@ -837,7 +856,7 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     if B_items is None and M * K > 128 * 128 and gemm_tn_big_supported(M, K):
         # beyond one 128 x 128 tile (config 5: 1024 x 256 over 1.9M rows): the matrix-core TN
         # kernel (ppgat_gemm_tn_big); column sums and V^T B through the small kernels
-        out = gemm_tn_big(A, B)
+        out = gemm_tn_big(A, B, b_bound=(_const_colmax(B), K, 1.0) if b_const else None)
         cs = colsum(A) if want_colsum else None
         vout = None
         if nv:  # V^T B by the small kernel, V padded to a multiple of 4 columns (16-byte rows)
@@ -878,8 +897,10 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias):
+        x_const = not x.requires_grad  # (an input the step does not differentiate: the item features)
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
+        ctx.x_keep = x if x_const else None  # the object itself: its cached column bound is found by identity
         ctx.has_bias = bias is not None
         W = weight.detach().contiguous()
         b = bias.detach().contiguous() if bias is not None else None
@@ -902,7 +923,8 @@ class _Linear(torch.autograd.Function):
                 dx = mm_nn(g, W, 0, W.size(1))
         dW = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dW, db, _ = gemm_tn(g, x, want_colsum=ctx.has_bias)
+            xk = ctx.x_keep
+            dW, db, _ = gemm_tn(g, xk if xk is not None else x, want_colsum=ctx.has_bias, b_const=xk is not None)
         return dx, dW, db if ctx.has_bias else None
 
 
@@ -1044,11 +1066,12 @@ def colmax_abs(X: torch.Tensor, src_ptr: Optional[torch.Tensor] = None) -> torch
     return out
 
 
-def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None) -> torch.Tensor:
+def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None, a_bits=None) -> torch.Tensor:
     """A [M, ma]^T B [M, nb] on the matrix cores (ppgat_gemm_tn_big), deterministic.  ``b_bound``
     = (bits [period] from colmax_abs, period, scale >= 1): an upper bound of |B| per column
     (column j: bits[j % period] * scale) that replaces the fp16 kernel's column-max pass over B
-    (ppgat_gemm_tn_big_bounded)."""
+    (ppgat_gemm_tn_big_bounded).  ``a_bits`` [ma]: a bound of |A| over the rows whose B row is not
+    zero (ppgat_gemm_tn_big_bounds: the other rows are clamped) in place of A's pass."""
     lib = _lib.load()
     _check_rows("A", A, torch.float32)
     _check_rows("B", B, torch.float32, A.device)
@@ -1059,6 +1082,14 @@ def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None) -> torch.Tensor:
     ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=A.device)
     out = torch.empty(ma, nb, dtype=torch.float32, device=A.device)
     lda, ldb, st = A.stride(0) if M > 1 else ma, B.stride(0) if M > 1 else nb, _lib.stream_handle(A.device)
+    if a_bits is not None:
+        _require(a_bits.dtype == torch.int32 and a_bits.numel() == ma and a_bits.device == A.device,
+                 "gemm_tn_big: a_bits must be int32 [ma] on A's device")
+        bits, period, scale = b_bound if b_bound is not None else (None, 1, 1.0)
+        _lib.check(lib.ppgat_gemm_tn_big_bounds(A.data_ptr(), lda, B.data_ptr(), ldb, M, ma, nb, a_bits.data_ptr(),
+                                                _lib.ptr(bits), int(period), float(scale), out.data_ptr(),
+                                                ws.data_ptr(), nbytes.value, st), "gemm_tn_big_bounds")
+        return out
     if b_bound is not None:
         bits, period, scale = b_bound
         _require(bits.dtype == torch.int32 and bits.numel() == period and bits.device == A.device,
@@ -1253,6 +1284,9 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     _require(out.shape == (v.n_dst, C) and out.is_contiguous(), "xgat_forward: out must be contiguous [n_dst, C]")
     seed_buf = seed_buffer(p, dev)
     E = v.n_edges
+    # column maxima of |x| over the rows the edge pass gathers (every source): the weight
+    # gradient's bound of |agg| (_xgat_weight_grads), with no pass of its own over x
+    xbits = torch.zeros(K, dtype=torch.int32, device=dev)
     for ph in phases:
         if ph.before is not None:
             ph.before()
@@ -1265,12 +1299,13 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
         _lib.check(lib.ppgat_xgat_fwd_workspace_bytes(ph.sched.n_hub_items, H, K, ctypes.byref(nbytes)), "xgat_ws")
         ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
         cs = ph.sched.cstruct()
-        _lib.check(lib.ppgat_xgat_fwd(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
-                                      _lib.ptr(v.csr_eid) if E else None, nd, E, K, H, x.data_ptr(), K,
-                                      s_src.data_ptr(), s_dst.data_ptr() + 4 * ph.d0 * H, float(slope), float(p),
-                                      int(seed) & (2**64 - 1), _lib.ptr(seed_buf), agg.data_ptr() + 4 * ph.d0 * H * K,
-                                      m.data_ptr() + 4 * ph.d0 * H, inv_l.data_ptr() + 4 * ph.d0 * H, ws.data_ptr(),
-                                      nbytes.value, st), "xgat_fwd")
+        _lib.check(lib.ppgat_xgat_fwd_colmax(ctypes.byref(cs), _lib.ptr(v.col) if E else None,
+                                             _lib.ptr(v.csr_eid) if E else None, nd, E, K, H, x.data_ptr(), K,
+                                             s_src.data_ptr(), s_dst.data_ptr() + 4 * ph.d0 * H, float(slope),
+                                             float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                             agg.data_ptr() + 4 * ph.d0 * H * K, m.data_ptr() + 4 * ph.d0 * H,
+                                             inv_l.data_ptr() + 4 * ph.d0 * H, xbits.data_ptr(), ws.data_ptr(),
+                                             nbytes.value, st), "xgat_fwd_colmax")
         if nd > 0:
             gemm_nn(agg[ph.d0:ph.d1].view(nd, H * K), Wt, 0, C, alpha=1.0 / H, bias=b, out=out[ph.d0:ph.d1])
         if ph.after is not None:
@@ -1279,7 +1314,7 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
     if not (keep_agg if keep_agg is not None else _xgat_keep_agg(v.n_dst, v.n_src, H, K, C, dev)):
         agg = None  # the backward's weight gradient comes from acc^T x (_xgat_weight_grads)
     saved = dict(x=x, W=W, a_s=a_s, a_d=a_d, A=A, s_src=s_src, s_dst=s_dst, agg=agg, m=m, inv_l=inv_l,
-                 seed_buf=seed_buf, v=v, meta=(H, C, K, slope, p, seed, bias is not None))
+                 seed_buf=seed_buf, v=v, xbits=xbits, meta=(H, C, K, slope, p, seed, bias is not None))
     return out, saved
 
 
@@ -1419,6 +1454,7 @@ def _xgat_backward_deferred_d(lib, saved: dict, g, S, dz, nstate, want_bias_grad
     hs = gemm_nn(x, W, 1, H * C, alpha=1.0 / H)
     acc = torch.empty(v.n_src, H * C, dtype=torch.float32, device=dev)
     pdal = torch.empty(max(E, 1) * H, dtype=torch.float32, device=dev)
+    gbits = torch.zeros(C, dtype=torch.int32, device=dev)  # |g| over the gathered rows: the G product's A bound
     split = halo_hook is not None and v.bwd_sched_halo is not None
     scheds = [(v.bwd_sched_halo, n0), (v.bwd_sched_own, 0)] if split else [(v.bwd_sched, 0)]
     for sched, base in scheds:  # dalpha (into dz) and beta dalpha per edge, acc per source
@@ -1426,13 +1462,15 @@ def _xgat_backward_deferred_d(lib, saved: dict, g, S, dz, nstate, want_bias_grad
         _lib.check(lib.ppgat_xgat_bwd_g_workspace_bytes(sched.n_hub_items, C, H, ctypes.byref(nbytes)), "xgat_g_ws")
         ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=dev)
         cs = sched.cstruct()
-        _lib.check(lib.ppgat_xgat_bwd_edges_gd(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
-                                               _lib.ptr(v.csc_eid) if E else None, _lib.ptr(v.dz_slot) if E else None,
-                                               E, C, H, hs.data_ptr() + 4 * base * H * C,
-                                               s_src.data_ptr() + 4 * base * H, nstate.data_ptr(), g.data_ptr(), C,
-                                               float(slope), float(p), int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
-                                               acc.data_ptr() + 4 * base * H * C, dz.data_ptr(), pdal.data_ptr(),
-                                               ws.data_ptr(), nbytes.value, st), "xgat_bwd_edges_gd")
+        _lib.check(lib.ppgat_xgat_bwd_edges_gd_colmax(ctypes.byref(cs), _lib.ptr(v.row) if E else None,
+                                                      _lib.ptr(v.csc_eid) if E else None,
+                                                      _lib.ptr(v.dz_slot) if E else None, E, C, H,
+                                                      hs.data_ptr() + 4 * base * H * C, s_src.data_ptr() + 4 * base * H,
+                                                      nstate.data_ptr(), g.data_ptr(), C, float(slope), float(p),
+                                                      int(seed) & (2**64 - 1), _lib.ptr(seed_buf),
+                                                      acc.data_ptr() + 4 * base * H * C, dz.data_ptr(),
+                                                      pdal.data_ptr(), gbits.data_ptr(), ws.data_ptr(), nbytes.value,
+                                                      st), "xgat_bwd_edges_gd_colmax")
     del hs
     D = torch.empty(max(n0, 1), H, dtype=torch.float32, device=dev)
     _xgat_dst_sum(lib, v, pdal, D, H, E, st, col0=0, ld=H)  # D_i = sum_j beta dalpha
@@ -1472,7 +1510,7 @@ def _xgat_backward_deferred_d(lib, saved: dict, g, S, dz, nstate, want_bias_grad
             halo_hook(dx[n0:])
     if saved["agg"] is not None:
         del acc
-        return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st)
+        return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, gbits=gbits)
     return _xgat_weight_grads(lib, saved, g, S, dx, want_bias_grad, st, acc=acc)
 
 
@@ -1493,10 +1531,12 @@ def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[in
                                          dws.data_ptr(), dws.numel() * 4, st), "bwd_dst_sum")
 
 
-def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None, xbits=None, acc=None):
+def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_rows=None, xbits=None, acc=None,
+                       gbits=None):
     """dW, datt, dbias from G = g^T agg and GV = S^T x (``x_rows``: the rows of x that S covers,
-    default all of the layer's source rows; ``xbits``: a precomputed column bound of the source
-    rows of x, colmax_abs bits, e.g. the maximum over the ranks of their own rows).  Without a
+    default all of the layer's source rows; ``xbits``: a column bound of the source rows of x,
+    colmax_abs bits -- default the forward's, gathered by its edge pass; ``gbits``: a column bound
+    of |g| over the destinations with an in-edge, from the backward's edge pass).  Without a
     saved agg (_xgat_keep_agg): G from ``acc`` [n_src, H * C] as (acc^T x) permuted."""
     x, W, a_s, a_d, agg, v = saved["x"], saved["W"], saved["a_s"], saved["a_d"], saved["agg"], saved["v"]
     H, C, K, slope, p, seed, has_bias = saved["meta"]
@@ -1515,9 +1555,12 @@ def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_r
     # the column maxima of the SOURCE rows of x (1 KB per row; a row with no out-edge -- however
     # large -- never enters an aggregate and must not loosen the bound: the fp16 split's error is
     # relative to it) instead of a pass over agg (4 KB per row); 2^-10 margin for fp32 rounding
+    if xbits is None:
+        xbits = saved.get("xbits")
     xbound = (colmax_abs(x, v.colptr) if xbits is None else xbits, K,
               (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
-    G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound)
+    # (rows of g without an in-edge are outside gbits; their agg rows are zero: clamped, they add 0)
+    G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound, a_bits=gbits)
     dW, datt_src, datt_dst, dbias = _xgat_weight_grads_from_G(lib, saved, G, GV, g, want_bias_grad, st)
     return dx, dW, datt_src, datt_dst, dbias
 

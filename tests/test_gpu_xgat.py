@@ -169,7 +169,10 @@ def test_weight_grad_bound_ignores_rows_without_out_edges(pkg, oracle, cuda):
     bound comes from the source rows only (ppgat_colmax_abs_sources), so dW stays within 1e-5 of
     the fp64 oracle.  (The rows are isolated -- no in-edges either: as destinations their 1e4
     larger attention terms would swamp the per-edge logits' fp32 resolution, an fp32 property
-    of any implementation.)  70,000 rows: the fp16 TN kernel's range (>= 64k rows)."""
+    of any implementation.)  70,000 rows: the fp16 TN kernel's range (>= 64k rows).  Both bounds
+    come from the edge passes (the rows they gather: every source / every destination with an
+    edge) and equal those sets' exact maxima; the isolated rows' g is 1e6 larger as well -- outside
+    the g bound, clamped in the split, adding the 0 their empty aggregates give."""
     rng = np.random.default_rng(11)
     n, e, heads, C = 70_000, 500_000, 4, 256
     out_rows = np.arange(n - 10, n)
@@ -179,9 +182,32 @@ def test_weight_grad_bound_ignores_rows_without_out_edges(pkg, oracle, cuda):
     x64 = torch.from_numpy(rng.standard_normal((n, 256)))
     x64[out_rows] *= 1e4
     G64 = torch.from_numpy(rng.standard_normal((n, C)))
+    G64[out_rows] *= 1e6  # their g rows too: no in-edge, so outside the gathered bound of g (clamped, adding 0)
     x = x64.float().to(cuda).requires_grad_(True)
-    out = conv(x, torch.from_numpy(ei).to(cuda))
-    (out * G64.float().to(cuda)).sum().backward()
+    ops = _ops()
+    seen = {}
+    real = ops._xgat_weight_grads
+
+    def spy(*a, **k):
+        seen.update(k)
+        seen["xbits"] = a[1].get("xbits")
+        return real(*a, **k)
+    import pytest as _pt
+    mp = _pt.MonkeyPatch()
+    mp.setattr(ops, "_xgat_weight_grads", spy)
+    try:
+        out = conv(x, torch.from_numpy(ei).to(cuda))
+        (out * G64.float().to(cuda)).sum().backward()
+    finally:
+        mp.undo()
+    # the bounds the weight gradient used came from the edge passes, and equal the exact sets' maxima
+    src_rows = np.unique(ei[0])
+    dst_rows = np.unique(ei[1])
+    xb = torch.from_numpy(np.abs(x64.float().numpy()[src_rows]).max(0)).view(torch.int32)
+    gb = torch.from_numpy(np.abs(G64.float().numpy()[dst_rows]).max(0)).view(torch.int32)
+    assert seen.get("gbits") is not None and torch.equal(seen["gbits"].cpu(), gb)
+    assert seen.get("xbits") is not None and torch.equal(seen["xbits"].cpu(), xb)
+    assert not torch.equal(ops.colmax_abs(x.detach()).cpu(), xb)  # (the isolated rows set the all-rows maxima)
     P = {k: v.detach().double().requires_grad_(True) for k, v in conv.named_parameters()}
     xr = x64.to(cuda).requires_grad_(True)
     ref = oracle.pyg_gat_conv(xr, torch.from_numpy(ei).to(cuda), P["lin.weight"], P["att_src"], P["att_dst"],
@@ -190,6 +216,32 @@ def test_weight_grad_bound_ignores_rows_without_out_edges(pkg, oracle, cuda):
     assert rel(out, ref) <= 1e-5
     assert rel(conv.lin.weight.grad, P["lin.weight"].grad) <= 1e-5, rel(conv.lin.weight.grad, P["lin.weight"].grad)
     assert rel(x.grad, xr.grad) <= 1e-5
+
+
+def test_linear_constant_input_bound_cached(pkg, cuda):
+    """item_proj's weight gradient on the fp16 TN kernel (>= 64k rows) with the item features as a
+    constant input: their column bound is computed once (hip_ops._const_colmax) and reused while
+    the tensor is unchanged; dW within 1e-5 of fp64 both times, recomputed after an in-place change."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(1)
+    n = 70_000
+    x = torch.randn(n, 256, generator=g, dtype=torch.float64)
+    W = torch.randn(256, 256, generator=g, dtype=torch.float64) * 0.05
+    b = torch.randn(256, generator=g, dtype=torch.float64)
+    G = torch.randn(n, 256, generator=g, dtype=torch.float64)
+    xd = x.float().to(cuda)                       # no grad: a constant input
+    ref = G.t() @ x
+    for it in range(3):
+        Wd = W.float().to(cuda).requires_grad_(True)
+        bd = b.float().to(cuda).requires_grad_(True)
+        (ops.linear(xd, Wd, bd) * G.float().to(cuda)).sum().backward()
+        assert rel(Wd.grad, ref) <= 1e-5
+        e = ops._CONST_BOUNDS.get(id(xd))
+        assert e is not None and e[0]() is xd and e[1] == xd._version
+        if it == 1:
+            xd.mul_(2.0)                          # a new version: the bound is recomputed
+            x = x * 2.0
+            ref = G.t() @ x
 
 
 def test_agg_free_weight_grad_fp16_path(pkg, oracle, cuda, monkeypatch):
