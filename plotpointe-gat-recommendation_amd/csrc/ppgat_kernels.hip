@@ -274,21 +274,47 @@ constexpr int kSU = PPGAT_SHORT_U;
 static_assert(kSU == 4 || kSU == 8 || kSU == 16, "short-item unroll");
 
 template <int C>
+__device__ __forceinline__ void fwd_merge_wave(int64_t hb, const int32_t* __restrict__ hub_row,
+                                               const int32_t* __restrict__ hub_ptr, int heads,
+                                               const float* __restrict__ partial, const float* __restrict__ bias,
+                                               int mode, float eps, float* __restrict__ out, float* __restrict__ m_out,
+                                               float* __restrict__ invl_out, float* __restrict__ agg_out);
+
+// hub merges riding at the head of a short-item launch (the hub pieces come from the long-item
+// kernel launched before it): blocks [0, mblocks) merge hubs 4 per block, one per wave
+struct HubMerge {
+  const int32_t* hub_row;
+  const int32_t* hub_ptr;
+  int64_t n_hubs;
+  int heads;
+  const float* partial;
+  int64_t mblocks;
+};
+
+template <int C>
 __global__ void __launch_bounds__(256) k_fwd_short(Items it, int64_t first, const int32_t* __restrict__ col,
                                                    const int32_t* __restrict__ eid, const float* __restrict__ h,
                                                    const float* __restrict__ s_src, const float* __restrict__ s_dst,
                                                    const float* __restrict__ bias, int mode, float slope, float eps,
                                                    float p, float inv_keep, uint64_t seed, float* __restrict__ out,
                                                    float* __restrict__ m_out, float* __restrict__ invl_out,
-                                                   float* __restrict__ agg_out, uint64_t* __restrict__ seed_out) {
+                                                   float* __restrict__ agg_out, uint64_t* __restrict__ seed_out,
+                                                   HubMerge mg) {
   if (p > 0.f) seed = epoch_seed(seed);
   if (seed_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) seed_out[0] = seed;  // the backward's mask seed
   constexpr int NV = C / 64;  // float4 columns per lane
   static_assert(NV >= 1, "k_fwd_short: C >= 64");
   __shared__ int2 rec[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if ((int64_t)blockIdx.x < mg.mblocks) {
+    const int64_t hb = (int64_t)blockIdx.x * 4 + wv;
+    if (hb < mg.n_hubs)
+      fwd_merge_wave<C>(hb, mg.hub_row, mg.hub_ptr, mg.heads, mg.partial, bias, mode, eps, out, m_out, invl_out,
+                        agg_out);
+    return;
+  }
   const int qr = lane >> 4, ql = lane & 15;
-  const int64_t item = first + ((int64_t)blockIdx.x * 4 + wv) * 4 + qr;
+  const int64_t item = first + (((int64_t)blockIdx.x - mg.mblocks) * 4 + wv) * 4 + qr;
   const bool live = item < it.n_items;
   const int64_t ic = live ? item : first;
   const int64_t i = it.row[ic];
@@ -349,18 +375,16 @@ __global__ void __launch_bounds__(256) k_fwd_short(Items it, int64_t first, cons
 // Merge the pieces of each hub row.  One wave per hub row: the piece maxima and
 // rescaled sums are lane-parallel (wave reductions), the C-wide partial rows are taken
 // by the subgroups in turn (piece q -> subgroup q mod EPW, two loads in flight each) and
-// combined across subgroups -- a fixed order, so the merge is deterministic.
+// combined across subgroups -- a fixed order, so the merge is deterministic.  One wave's
+// share, called by k_fwd_merge or by the merge blocks at the head of k_fwd_short.
 template <int C>
-__global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ hub_row,
-                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
-                                                   const float* __restrict__ partial,
-                                                   const float* __restrict__ bias, int mode, float eps,
-                                                   float* __restrict__ out, float* __restrict__ m_out,
-                                                   float* __restrict__ invl_out, float* __restrict__ agg_out) {
+__device__ __forceinline__ void fwd_merge_wave(int64_t hb, const int32_t* __restrict__ hub_row,
+                                               const int32_t* __restrict__ hub_ptr, int heads,
+                                               const float* __restrict__ partial, const float* __restrict__ bias,
+                                               int mode, float eps, float* __restrict__ out, float* __restrict__ m_out,
+                                               float* __restrict__ invl_out, float* __restrict__ agg_out) {
   using G = Geo<C>;
   const int lane = threadIdx.x & 63;
-  const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (hb >= n_hubs) return;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
   const int64_t i = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
@@ -409,6 +433,18 @@ __global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ h
   if (heads > 1) osum = mul4(osum, 1.f / (float)heads);
   if (bias != nullptr) osum = add4(osum, ld4(bias + sl * 4));
   if (sg == 0) st4s(out + i * C + sl * 4, osum);
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) k_fwd_merge(const int32_t* __restrict__ hub_row,
+                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
+                                                   const float* __restrict__ partial,
+                                                   const float* __restrict__ bias, int mode, float eps,
+                                                   float* __restrict__ out, float* __restrict__ m_out,
+                                                   float* __restrict__ invl_out, float* __restrict__ agg_out) {
+  const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;
+  fwd_merge_wave<C>(hb, hub_row, hub_ptr, heads, partial, bias, mode, eps, out, m_out, invl_out, agg_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -573,6 +609,12 @@ __global__ void __launch_bounds__(256) k_bwd_src(Items it, const int32_t* __rest
 // one per 16-lane row, as k_fwd_short.  Lane ql builds the record of edge rs + ql and, after
 // the 16-lane reduction of <g_i, h_j> for its edge, writes that edge's dz.
 template <int C>
+__device__ __forceinline__ void bwd_merge_wave(int64_t hb, const int32_t* __restrict__ hub_row,
+                                               const int32_t* __restrict__ hub_ptr, int heads,
+                                               const float* __restrict__ partial, float* __restrict__ dh,
+                                               int64_t ld_dh, float* __restrict__ ds_src, int64_t ld_ds);
+
+template <int C>
 __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, const int32_t* __restrict__ row,
                                                        const int32_t* __restrict__ csc_eid,
                                                        const int32_t* __restrict__ csc2csr,
@@ -583,14 +625,19 @@ __global__ void __launch_bounds__(256) k_bwd_src_short(Items it, int64_t first, 
     const uint64_t* __restrict__ seed_in,
                                                        float* __restrict__ dh, int64_t ld_dh,
                                                        float* __restrict__ ds_src, int64_t ld_ds,
-                                                       float* __restrict__ dz) {
+                                                       float* __restrict__ dz, HubMerge mg) {
   if (p > 0.f) seed = seed_in != nullptr ? *seed_in : epoch_seed(seed);
   constexpr int NV = C / 64;
   static_assert(NV >= 1, "k_bwd_src_short: C >= 64");
   __shared__ int2 rec[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if ((int64_t)blockIdx.x < mg.mblocks) {  // hub merges first (the long-item kernel ran before)
+    const int64_t hb = (int64_t)blockIdx.x * 4 + wv;
+    if (hb < mg.n_hubs) bwd_merge_wave<C>(hb, mg.hub_row, mg.hub_ptr, mg.heads, mg.partial, dh, ld_dh, ds_src, ld_ds);
+    return;
+  }
   const int qr = lane >> 4, ql = lane & 15;
-  const int64_t item = first + ((int64_t)blockIdx.x * 4 + wv) * 4 + qr;
+  const int64_t item = first + (((int64_t)blockIdx.x - mg.mblocks) * 4 + wv) * 4 + qr;
   const bool live = item < it.n_items;
   const int64_t ic = live ? item : first;
   const int64_t j = it.row[ic];
@@ -821,14 +868,12 @@ __global__ void __launch_bounds__(256) k_bwd_src_mh(Items it, const int32_t* __r
 }
 
 template <int C>
-__global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ hub_row,
-                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
-                                                   const float* __restrict__ partial, float* __restrict__ dh,
-                                                   int64_t ld_dh, float* __restrict__ ds_src, int64_t ld_ds) {
+__device__ __forceinline__ void bwd_merge_wave(int64_t hb, const int32_t* __restrict__ hub_row,
+                                               const int32_t* __restrict__ hub_ptr, int heads,
+                                               const float* __restrict__ partial, float* __restrict__ dh,
+                                               int64_t ld_dh, float* __restrict__ ds_src, int64_t ld_ds) {
   using G = Geo<C>;
   const int lane = threadIdx.x & 63;
-  const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (hb >= n_hubs) return;
   const int sg = lane / G::LPR, sl = lane % G::LPR;
   const int64_t j = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
@@ -847,6 +892,16 @@ __global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ h
     if (sg == 0) st4s(dh + j * ld_dh + hd * C + sl * 4, acc);
     if (lane == 0) ds_src[j * ld_ds + hd] = ds;
   }
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) k_bwd_merge(const int32_t* __restrict__ hub_row,
+                                                   const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
+                                                   const float* __restrict__ partial, float* __restrict__ dh,
+                                                   int64_t ld_dh, float* __restrict__ ds_src, int64_t ld_ds) {
+  const int64_t hb = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;
+  bwd_merge_wave<C>(hb, hub_row, hub_ptr, heads, partial, dh, ld_dh, ds_src, ld_ds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1103,14 +1158,17 @@ hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid
                                            eid, heads, h, ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m,
                                            invl, agg, partial, seed_out));
   }
-  if (n_long < it.n_items) {
+  // the hub merges ride at the head of the short-item launch when there is one (one launch fewer)
+  const bool fold = n_long < it.n_items;
+  if (fold) {
     const Items all{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-    const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16);  // 4 waves x 4 items per block
+    const HubMerge mg{hub_row, hub_ptr, n_hubs, heads, partial, n_hubs > 0 ? (n_hubs + 3) / 4 : 0};
+    const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16 + mg.mblocks);  // 4 waves x 4 items per block
     PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_fwd_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, col, eid, h,
                                              ss, sd, bias, mode, slope, eps, p, inv_keep, seed, out, m, invl, agg,
-                                             n_long > 0 ? nullptr : seed_out));
+                                             n_long > 0 ? nullptr : seed_out, mg));
   }
-  if (n_hubs > 0) {
+  if (n_hubs > 0 && !fold) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_fwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,
                                            hub_row, hub_ptr, n_hubs, heads, partial, bias, mode, eps, out, m, invl,
                                            agg));
@@ -1137,13 +1195,6 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int64_t n_long = short_begin(it, heads, C);
   const Items its{it.row, it.beg, it.end, n_long, it.n_hub_items};
-  if (n_long < it.n_items) {
-    const Items all{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
-    const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16);
-    PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_bwd_src_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, row,
-                                             csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go,
-                                             mode, slope, gscale, p, inv_keep, seed, seed_in, dh, ld_dh, ds_src, ld_ds, dz));
-  }
   if (n_long > 0) {
     const bool mh = heads > 1 && C >= 32 && (heads == 2 || heads == 4 || heads == 8);
     if (mh) {  // every head of an edge in one pass (one grad_out gather per edge)
@@ -1162,7 +1213,18 @@ hipError_t launch_bwd_src(const ItemsArg& it, const int32_t* row, const int32_t*
                                              inv_keep, seed, seed_in, dh, ld_dh, ds_src, ld_ds, dz, partial));
     }
   }
-  if (n_hubs > 0) {
+  // the short items after the long ones, with the hub merges at the head of that launch
+  const bool fold = n_long < it.n_items;
+  if (fold) {
+    const Items all{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+    const HubMerge mg{hub_row, hub_ptr, n_hubs, heads, partial, n_hubs > 0 ? (n_hubs + 3) / 4 : 0};
+    const unsigned g = (unsigned)((it.n_items - n_long + 15) / 16 + mg.mblocks);
+    PPGAT_DISPATCH_C64(C, hipLaunchKernelGGL(k_bwd_src_short<CC>, dim3(g), dim3(256), 0, st, all, n_long, row,
+                                             csc_eid, csc2csr, h, ss, reinterpret_cast<const float4*>(nstate), go,
+                                             mode, slope, gscale, p, inv_keep, seed, seed_in, dh, ld_dh, ds_src, ld_ds,
+                                             dz, mg));
+  }
+  if (n_hubs > 0 && !fold) {
     PPGAT_DISPATCH_C(C, hipLaunchKernelGGL(k_bwd_merge<CC>, dim3(blocks_for(n_hubs * 64)), dim3(256), 0, st,
                                            hub_row, hub_ptr, n_hubs, heads, partial, dh, ld_dh, ds_src, ld_ds));
   }
