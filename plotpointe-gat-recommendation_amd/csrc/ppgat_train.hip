@@ -194,7 +194,8 @@ __global__ void __launch_bounds__(kRsThreads) k_rs_hist(const int32_t* __restric
 __global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const int32_t* __restrict__ kin,
                                                            const int32_t* __restrict__ vin, int64_t n, int shift,
                                                            int db, const int32_t* __restrict__ goff, int64_t tiles,
-                                                           int32_t* __restrict__ kout, int32_t* __restrict__ vout) {
+                                                           int32_t* __restrict__ kout, int32_t* __restrict__ vout,
+                                                           uint8_t* __restrict__ mark, int64_t mark_n) {
   extern __shared__ int32_t sm[];
   const int nd = 1 << db;
   int32_t* wc = sm;                   // [kRsWaves][nd]
@@ -236,6 +237,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const int32_t* __rest
       const int64_t pos = wc[w * nd + d] + rank;
       kout[pos] = k;
       vout[pos] = v;
+      if (mark != nullptr && k < mark_n) mark[k] = 1;  // (last pass, when asked: the keys present)
     }
     __syncthreads();
   }
@@ -267,9 +269,10 @@ size_t rs_workspace_bytes(int64_t n, unsigned bits) {
   return 2 * align_up((size_t)pl.cells * 4) + align_up(pl.scan_bytes);
 }
 
-// sorts (k0, v0) using (k1, v1) as the ping-pong pair; *result_in_1 says where it ended
+// sorts (k0, v0) using (k1, v1) as the ping-pong pair; *result_in_1 says where it ended.
+// mark != NULL: the last pass also sets mark[k] = 1 for every key k < mark_n.
 hipError_t rs_sort(int32_t* k0, int32_t* v0, int32_t* k1, int32_t* v1, int64_t n, unsigned bits, void* ws,
-                   bool* result_in_1, hipStream_t st) {
+                   bool* result_in_1, hipStream_t st, uint8_t* mark = nullptr, int64_t mark_n = 0) {
   const RsPlan pl = rs_plan(n, bits);
   char* p = static_cast<char*>(ws);
   int32_t* ghist = reinterpret_cast<int32_t*>(p);
@@ -290,7 +293,7 @@ hipError_t rs_sort(int32_t* k0, int32_t* v0, int32_t* k1, int32_t* v1, int64_t n
                                            rocprim::plus<int32_t>(), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)pl.tiles), dim3(kRsThreads), (kRsWaves + 1) * nd * 4, st, ki, vi,
-                       n, shift, pl.db, goff, pl.tiles, ko, vo);
+                       n, shift, pl.db, goff, pl.tiles, ko, vo, ps + 1 == pl.passes ? mark : nullptr, mark_n);
     in1 = !in1;
   }
   *result_in_1 = in1;
@@ -303,8 +306,11 @@ hipError_t rs_sort(int32_t* k0, int32_t* v0, int32_t* k1, int32_t* v1, int64_t n
 __global__ void k_bpr_keys(const int64_t* __restrict__ u, const int64_t* __restrict__ ii,
                            const int64_t* __restrict__ jj, int64_t S, int64_t n_users, int64_t n_items,
                            const int32_t* __restrict__ row_map, int64_t n_rows, int32_t* __restrict__ key,
-                           int32_t* __restrict__ val) {
+                           int32_t* __restrict__ val, uint8_t* __restrict__ touched) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the touched-row map cleared here (16 B per thread; the region is a multiple of 16 B), set by
+  // the sort's last pass: no fill or mark launch of its own
+  if (c * 16 < n_rows) *reinterpret_cast<uint4*>(touched + c * 16) = make_uint4(0u, 0u, 0u, 0u);
   if (c >= 4 * S) return;
   const int64_t t = c >> 2;
   const int kd = (int)(c & 3);
@@ -465,17 +471,12 @@ __global__ void __launch_bounds__(256) k_bpr_chunks(const int32_t* __restrict__ 
   }
 }
 
-// Rows no contribution reaches are zeroed by two row-parallel passes over a byte map of the
-// rows (whatever the key distribution: a rank whose triples are all sentinels, few triples, a
-// huge Z): k_bpr_mark sets touched[key] for every sorted key (plain byte stores of one value,
-// no atomics needed), k_bpr_zero_untouched writes zero rows where the byte is clear.  Every
-// row of [0, n_rows) is still written exactly once (k_bpr_chunks / k_bpr_fixup, or here).
-__global__ void __launch_bounds__(256) k_bpr_mark(const int32_t* __restrict__ skey, int64_t total, int64_t n_rows,
-                                                  uint8_t* __restrict__ touched) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p < total && (int64_t)skey[p] < n_rows) touched[skey[p]] = 1;
-}
-
+// Rows no contribution reaches are zeroed by a row-parallel pass over a byte map of the rows
+// (whatever the key distribution: a rank whose triples are all sentinels, few triples, a huge
+// Z): k_bpr_keys clears the map, the sort's last scatter pass sets touched[key] for every key
+// (plain byte stores of one value, no atomics needed), k_bpr_zero_untouched writes zero rows
+// where the byte is clear.  Every row of [0, n_rows) is still written exactly once
+// (k_bpr_chunks / k_bpr_fixup, or here).
 template <int C>
 __global__ void __launch_bounds__(256) k_bpr_zero_untouched(const uint8_t* __restrict__ touched, int64_t n_rows,
                                                             float* __restrict__ dZ, BprPro pro) {
@@ -870,19 +871,16 @@ hipError_t bpr_bwd_prepare(int64_t n_rows, int64_t n_users, int64_t n_items, con
   if (ws_bytes < bpr_workspace_bytes(N, S, C)) return hipErrorInvalidValue;
   const int64_t total = 4 * S;
   const BprWs w = bpr_ws(ws, N, S, C);
-  hipError_t err = hipMemsetAsync(w.touched, 0, ((size_t)N + 15) & ~(size_t)15, st);  // (one fill kernel, no tail)
-  if (err != hipSuccess) return err;
-  hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
-                     n_items, row_map, N, w.keys, w.vals);
+  hipError_t err = hipSuccess;
+  const int64_t kthreads = total > (N + 15) / 16 ? total : (N + 15) / 16;  // (enough threads to clear the map)
+  hipLaunchKernelGGL(k_bpr_keys, dim3((unsigned)((kthreads + 255) / 256)), dim3(256), 0, st, u, i, j, S, n_users,
+                     n_items, row_map, N, w.keys, w.vals, w.touched);
   int32_t* k1 = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(w.keys) + 2 * align_up((size_t)total * 4));
   int32_t* v1 = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(w.keys) + 3 * align_up((size_t)total * 4));
   bool in1 = false;
-  err = rs_sort(w.keys, w.vals, k1, v1, total, key_bits(N + 1), w.tmp, &in1, st);
+  err = rs_sort(w.keys, w.vals, k1, v1, total, key_bits(N + 1), w.tmp, &in1, st, w.touched, N);
   if (err != hipSuccess) return err;
   if ((in1 ? k1 : w.keys) != w.skeys) return hipErrorUnknown;  // bpr_ws's parity rule disagrees with rs_sort
-  if (N > 0)
-    hipLaunchKernelGGL(k_bpr_mark, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w.skeys, total, N,
-                       w.touched);
   return hipGetLastError();
 }
 
