@@ -439,10 +439,10 @@ def project_supported(k: int, out_cols: int) -> bool:
 
 def project(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
             att_src: Optional[torch.Tensor] = None, att_dst: Optional[torch.Tensor] = None,
-            x_items: Optional[torch.Tensor] = None):
+            x_items: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
     """y = [x; x_items] W^T (+ bias) on the matrix cores (include/ppgat.h ppgat_project), with
     s_src = y.att_src and s_dst = y.att_dst fused when att_src is given (heads = 1).
-    Returns y, or (y, s_src, s_dst)."""
+    Returns y (``out`` if given: contiguous [rows, HC]), or (y, s_src, s_dst)."""
     lib = _lib.load()
     _check_dev("x", x, torch.float32)
     _check_dev("weight", weight, torch.float32, x.device)
@@ -454,7 +454,7 @@ def project(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] 
         _check_dev("x_items", x_items, torch.float32, x.device)
     K, HC = weight.size(1), weight.size(0)
     dev = x.device
-    y = torch.empty(n, HC, dtype=torch.float32, device=dev)
+    y = out if out is not None else torch.empty(n, HC, dtype=torch.float32, device=dev)
     s_src = s_dst = None
     if att_src is not None:
         s_src = torch.empty(n, dtype=torch.float32, device=dev)
@@ -796,7 +796,7 @@ def gat_layer(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, s
     if (mode == _lib.MODE_PYG and heads > 1 and heads * channels > x.size(1) and rep is None
             and xgat_supported(x.size(1), heads, channels)):
         # multi-head layers wider than their input: aggregate x, then transform (config 5)
-        xx = torch.cat([x, x_items], 0) if x_items is not None else x
+        xx = join_rows(x, x_items) if x_items is not None else x
         return gat_layer_x(xx, weight, att_src, att_dst, bias, XViews.of_graph(graph), heads, channels, slope,
                            dropout_p, seed)
     return GATLayer.apply(x, weight, att_src, att_dst, bias, graph, heads, channels, mode, slope, dropout_p, seed,
@@ -896,7 +896,7 @@ class _Linear(torch.autograd.Function):
     split over the chip).  No vendor BLAS on any shape."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, out_holder=None):
         x_const = not x.requires_grad  # (an input the step does not differentiate: the item features)
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
@@ -904,11 +904,14 @@ class _Linear(torch.autograd.Function):
         ctx.has_bias = bias is not None
         W = weight.detach().contiguous()
         b = bias.detach().contiguous() if bias is not None else None
+        out = out_holder[0] if out_holder is not None else None  # (in a list: a buffer, not an autograd input)
         if project_supported(x.size(1), weight.size(0)):
-            return project(x, W, b)
-        if gemm_nn_supported(x.size(0), x.size(1), weight.size(0), 1):
-            return gemm_nn(x, W, 1, weight.size(0), bias=b)
-        return mm_nn(x, W, 1, weight.size(0), bias=b)
+            return project(x, W, b, out=out)
+        elif gemm_nn_supported(x.size(0), x.size(1), weight.size(0), 1):
+            return gemm_nn(x, W, 1, weight.size(0), bias=b, out=out)
+        else:
+            y = mm_nn(x, W, 1, weight.size(0), bias=b)
+        return y if out is None else out.copy_(y)
 
     @staticmethod
     def backward(ctx, g):
@@ -925,14 +928,47 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             xk = ctx.x_keep
             dW, db, _ = gemm_tn(g, xk if xk is not None else x, want_colsum=ctx.has_bias, b_const=xk is not None)
-        return dx, dW, db if ctx.has_bias else None
+        return dx, dW, db if ctx.has_bias else None, None
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x W^T + b; with ``out`` (contiguous [rows, out_features]) written there and returned."""
     _require(x.is_cuda, "linear: ppgat runs on ROCm devices only; there is no CPU path")
     if x.dtype != torch.float32 or x.dim() != 2:
         raise NotImplementedError("ppgat linear: fp32 2-D input only")
-    return _Linear.apply(x, weight, bias)
+    if out is not None:
+        _require(out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()
+                 and out.shape == (x.size(0), weight.size(0)), "linear: out must be contiguous [rows, out_features]")
+    return _Linear.apply(x, weight, bias, [out] if out is not None else None)
+
+
+class _JoinRows(torch.autograd.Function):
+    """cat([a, b]) of two row blocks that already lie back to back in one storage: the joined
+    tensor is a new header on that storage (no copy); the gradient splits at the seam."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.n = a.size(0)
+        return a.new_empty(0).set_(a.untyped_storage(), a.storage_offset(), (a.size(0) + b.size(0), a.size(1)),
+                                   (a.size(1), 1))
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:ctx.n], g[ctx.n:]
+
+
+def rows_adjacent(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """b's rows start where a's end, in one storage, both contiguous with the same width."""
+    return (a.dim() == 2 and b.dim() == 2 and a.size(1) == b.size(1) and a.dtype == b.dtype and a.device == b.device
+            and a.is_contiguous() and b.is_contiguous()
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.storage_offset() == a.storage_offset() + a.numel())
+
+
+def join_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """torch.cat([a, b], 0), without the copy when the blocks are adjacent (model.node_table)."""
+    return _JoinRows.apply(a, b) if rows_adjacent(a, b) else torch.cat([a, b], 0)
 
 
 # ---------------------------------------------------------------------------
