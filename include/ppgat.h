@@ -556,6 +556,15 @@ int ppgat_gemm_tn_big_bounded(const float* a, int64_t lda, const float* b, int64
 int ppgat_gemm_tn_big_bounds(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
                              const unsigned* a_bound_bits, const unsigned* b_bound_bits, int bound_period,
                              float bound_scale, float* out, void* workspace, size_t workspace_bytes, void* stream);
+/* ppgat_gemm_tn_big_colsum: ppgat_gemm_tn_big_bounds (either bound nullable) that also writes
+ *   colsum_out[i] = sum_r a[r, i] (the bias gradient beside a weight gradient: Linear.bias,
+ *   GATConv.bias) -- on the fp16 TN kernel from the rows its staging threads already hold (no
+ *   second pass over a), in a fixed order: deterministic.  Replaces the reference's separate
+ *   autograd sum for the bias (torch.nn.Linear / PyG GATConv bias, train_gat_pyg.py:75-77). */
+int ppgat_gemm_tn_big_colsum(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                             const unsigned* a_bound_bits, const unsigned* b_bound_bits, int bound_period,
+                             float bound_scale, float* out, float* colsum_out, void* workspace,
+                             size_t workspace_bytes, void* stream);
 int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream);
 int ppgat_colmax_abs_sources(const float* x, int64_t ldx, int64_t n, int c, const int32_t* src_ptr,
                              unsigned* out_bits, void* stream);

@@ -125,6 +125,8 @@ SIGNATURES = {
                                           c_sz, c_vp]),
     "ppgat_gemm_tn_big_bounds": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_f, c_vp,
                                          c_vp, c_sz, c_vp]),
+    "ppgat_gemm_tn_big_colsum": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_f, c_vp,
+                                         c_vp, c_vp, c_sz, c_vp]),
     "ppgat_colmax_abs": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "ppgat_colmax_abs_sources": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp]),
     "ppgat_colsum_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),

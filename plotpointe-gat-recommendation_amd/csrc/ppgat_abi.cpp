@@ -1106,7 +1106,7 @@ int ppgat_gemm_tn_big(const float* a, int64_t lda, const float* b, int64_t ldb, 
 static int gemm_tn_big_bounds_impl(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma,
                                    int nb, const unsigned* a_bound_bits, const unsigned* b_bound_bits,
                                    int bound_period, float bound_scale, float* out, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
+                                   size_t workspace_bytes, void* stream, float* colsum_out = nullptr) {
   if (m < 0 || !ppgat::gemm_tn_big_shape_ok(ma, nb))
     return fail(PPGAT_ERR_UNSUPPORTED, "gemm_tn_big_bounded: needs ma, nb multiples of 128");
   if (lda < ma || ldb < nb || (lda % 4) || (ldb % 4))
@@ -1120,7 +1120,7 @@ static int gemm_tn_big_bounds_impl(const float* a, int64_t lda, const float* b, 
   hipStream_t st = static_cast<hipStream_t>(stream);
   Timed t(PPGAT_K_GEMM_TN, st);
   hipError_t e = ppgat::gemm_tn_big(a, lda, b, ldb, m, ma, nb, out, workspace, st, b_bound_bits, bound_period,
-                                    bound_scale, a_bound_bits);
+                                    bound_scale, a_bound_bits, colsum_out);
   if (e != hipSuccess) return hip_fail(e, "gemm_tn_big_bounded");
   return PPGAT_OK;
 }
@@ -1138,6 +1138,15 @@ int ppgat_gemm_tn_big_bounds(const float* a, int64_t lda, const float* b, int64_
                              float bound_scale, float* out, void* workspace, size_t workspace_bytes, void* stream) {
   return gemm_tn_big_bounds_impl(a, lda, b, ldb, m, ma, nb, a_bound_bits, b_bound_bits, bound_period, bound_scale, out,
                                  workspace, workspace_bytes, stream);
+}
+
+int ppgat_gemm_tn_big_colsum(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t m, int ma, int nb,
+                             const unsigned* a_bound_bits, const unsigned* b_bound_bits, int bound_period,
+                             float bound_scale, float* out, float* colsum_out, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  if (!colsum_out) return fail(PPGAT_ERR_INVALID, "gemm_tn_big_colsum: null pointer");
+  return gemm_tn_big_bounds_impl(a, lda, b, ldb, m, ma, nb, a_bound_bits, b_bound_bits, bound_period, bound_scale, out,
+                                 workspace, workspace_bytes, stream, colsum_out);
 }
 
 int ppgat_colmax_abs(const float* x, int64_t ldx, int64_t n, int c, unsigned* out_bits, void* stream) {

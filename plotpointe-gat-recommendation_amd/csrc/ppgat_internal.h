@@ -211,7 +211,7 @@ bool gemm_tn_big_shape_ok(int Ma, int Nb);
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb);
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
                        void* ws, hipStream_t st, const unsigned* b_bound = nullptr, int b_period = 0,
-                       float b_scale = 1.f, const unsigned* a_bound = nullptr);
+                       float b_scale = 1.f, const unsigned* a_bound = nullptr, float* colsum_out = nullptr);
 hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st,
                       const int32_t* src_ptr = nullptr);
 bool xgat_shape_ok(int K, int H, int C);

@@ -1150,7 +1150,7 @@ __global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ par
 // k_dxw).  The tiles of one row split run on one XCD, so the rows leave HBM once.
 constexpr int kThImg = kTR * 128 * 2;       // bytes per fp16 image [32][128]
 constexpr int kThBuf = 6 * kThImg;          // A hi/lo, B half 0 hi/lo, B half 1 hi/lo (48 KB)
-constexpr size_t kThLds = 2 * kThBuf + (2 * 128 + 2 * 256) * sizeof(float);
+constexpr size_t kThLds = 2 * kThBuf + (2 * 128 + 2 * 256 + 16 * 128) * sizeof(float);  // + sC (colsum)
 
 // column maxima of |X| over rows [r0, r1) of a row block, merged into out[] as IEEE bits;
 // with rp (CSC pointers [M + 1]) only over the rows that are the source of an edge
@@ -1197,6 +1197,7 @@ struct TnhArg {
   int bperiod;
   float bscale;
   float* part;           // [splits, Ma, Nb]
+  float* cpart;          // nullable: [splits, Ma] column sums of A (the workgroups of B tile 0)
 };
 
 __device__ __forceinline__ int th_off(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
@@ -1279,6 +1280,12 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
       S.b1[p] = ld4(Bb + row * a.ldb + 128);
     }
   };
+  // column sums of A over this split's rows (cpart; the B tile 0 workgroups of each A tile): the
+  // staging thread's 4 columns over its rows in chunk order, the raw values (before any clamp),
+  // kept in its own LDS slot sC[slr][sc .. +3] (no registers held across the loop)
+  const bool csum = a.cpart != nullptr && tb == 0;
+  float4* const sCs = reinterpret_cast<float4*>(sFb + 2 * 256) + slr * 32 + (sc >> 2);  // sC: [16][128]
+  if (csum) *sCs = f4(0.f);
   auto put = [&](int buf, int64_t row0, const Stage& S) {
     unsigned char* img = th_lds + buf * kThBuf;
 #pragma unroll
@@ -1286,6 +1293,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
       const int lr = slr + 16 * p;
       const bool ok = row0 + lr < r1;
       const int off = th_off(lr, sc >> 3) + 8 * ((sc >> 2) & 1);
+      if (csum && ok) {
+        const float4 c = *sCs;
+        *sCs = make_float4(c.x + S.a[p].x, c.y + S.a[p].y, c.z + S.a[p].z, c.w + S.a[p].w);
+      }
       uint2 h, l;
       split2h_4(ok ? S.a[p] : f4(0.f), sa, h, l, a.aclamp != 0);
       *reinterpret_cast<uint2*>(img + off) = h;
@@ -1378,6 +1389,16 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
     for (int q = 0; q < 16; ++q) {
       const int ml = 32 * wa + (q & 3) + 8 * (q >> 2) + 4 * hf;
       P[(size_t)(ta * 128 + ml) * a.Nb + col] = acc[t][q] * sFa[128 + ml] * fb;
+    }
+  }
+  if (csum) {  // (workgroup-uniform) the 16 row threads of each column in row-thread order
+    const float* sC = sFb + 2 * 256;
+    __syncthreads();
+    if (tid < 128) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += sC[q * 128 + tid];
+      a.cpart[(size_t)split * a.Ma + ta * 128 + tid] = s;
     }
   }
 }
@@ -2517,13 +2538,15 @@ static int tnh_splits(int64_t M, int T) {  // one workgroup per CU: splits * til
   return s;
 }
 
+// (+ the column sums' partials: [splits, Ma] on the fp16 path, the colsum kernel's otherwise)
 size_t gemm_tn_big_workspace_bytes(int64_t M, int Ma, int Nb) {
   if (tnh_ok(M, Ma, Nb)) {
     const int T = (Ma / 128) * (Nb / 256);
-    return align_up((size_t)tnh_splits(M, T) * Ma * Nb * 4) + align_up((size_t)(Ma + Nb) * 4);
+    const int s = tnh_splits(M, T);
+    return align_up((size_t)s * Ma * Nb * 4) + align_up((size_t)(Ma + Nb) * 4) + align_up((size_t)s * Ma * 4);
   }
   const int T = (Ma / kTA) * (Nb / (Nb % 256 == 0 ? 256 : 128));
-  return align_up((size_t)tn_splits(M, T) * Ma * Nb * 4);
+  return align_up((size_t)tn_splits(M, T) * Ma * Nb * 4) + align_up((size_t)colsum_blocks(M) * 256 * 4);
 }
 
 static hipError_t colmax_bits(const float* X, int64_t ldx, int64_t M, int C, unsigned* out, hipStream_t st,
@@ -2549,8 +2572,12 @@ hipError_t colmax_abs(const float* X, int64_t ldx, int64_t M, int C, unsigned* o
 
 hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int Ma, int Nb, float* out,
                        void* ws, hipStream_t st, const unsigned* b_bound, int b_period, float b_scale,
-                       const unsigned* a_bound) {
-  if (M <= 0) return hipMemsetAsync(out, 0, (size_t)Ma * Nb * 4, st);  // empty sum (no partials)
+                       const unsigned* a_bound, float* colsum_out) {
+  if (M <= 0) {  // empty sums (no partials)
+    hipError_t e = hipMemsetAsync(out, 0, (size_t)Ma * Nb * 4, st);
+    if (e == hipSuccess && colsum_out) e = hipMemsetAsync(colsum_out, 0, (size_t)Ma * 4, st);
+    return e;
+  }
   if (tnh_ok(M, Ma, Nb)) {
     static const bool attr = [] {
       return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tnh), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2571,6 +2598,8 @@ hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb,
     a.bmax = b_bound ? b_bound : mx + Ma;  // a caller's bound of |B| per column skips B's pass
     a.bperiod = b_bound ? b_period : Nb;
     a.bscale = b_bound ? b_scale : 1.f;
+    a.cpart = colsum_out ? reinterpret_cast<float*>(reinterpret_cast<char*>(mx) + align_up((size_t)(Ma + Nb) * 4))
+                         : nullptr;
     hipError_t e = hipSuccess;
     if (!a_bound || !b_bound) e = hipMemsetAsync(mx, 0, (size_t)(Ma + Nb) * 4, st);
     if (e == hipSuccess && !a_bound) e = colmax_bits(A, lda, M, Ma, mx, st);
@@ -2580,6 +2609,9 @@ hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb,
     hipLaunchKernelGGL(k_gemm_tnh, dim3(grid), dim3(512), kThLds, st, a);
     const int64_t n4 = (int64_t)Ma * Nb / 4;
     hipLaunchKernelGGL(k_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, n4, a.splits, out);
+    if (colsum_out)
+      hipLaunchKernelGGL(k_split_sum, dim3((unsigned)((Ma / 4 + 255) / 256)), dim3(256), 0, st, a.cpart,
+                         (int64_t)Ma / 4, a.splits, colsum_out);
     return hipGetLastError();
   }
   const bool wide = Nb % 256 == 0;
@@ -2596,6 +2628,13 @@ hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb,
   else hipLaunchKernelGGL((k_gemm_tn<128>), dim3(grid), dim3(256), 0, st, a);
   const int64_t n4 = (int64_t)Ma * Nb / 4;
   hipLaunchKernelGGL(k_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, n4, a.splits, out);
+  if (colsum_out) {  // the colsum kernel over 256- (or 128-) column slabs of A
+    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)a.splits * Ma * Nb * 4));
+    for (int c0 = 0; c0 < Ma; c0 += 256) {
+      const hipError_t e = colsum(A + c0, lda, M, Ma - c0 >= 256 ? 256 : 128, colsum_out + c0, part, st);
+      if (e != hipSuccess) return e;
+    }
+  }
   return hipGetLastError();
 }
 

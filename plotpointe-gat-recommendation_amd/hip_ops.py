@@ -856,8 +856,11 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, want_colsum: bool = False, V: Opti
     if B_items is None and M * K > 128 * 128 and gemm_tn_big_supported(M, K):
         # beyond one 128 x 128 tile (config 5: 1024 x 256 over 1.9M rows): the matrix-core TN
         # kernel (ppgat_gemm_tn_big); column sums and V^T B through the small kernels
-        out = gemm_tn_big(A, B, b_bound=(_const_colmax(B), K, 1.0) if b_const else None)
-        cs = colsum(A) if want_colsum else None
+        bb = (_const_colmax(B), K, 1.0) if b_const else None
+        if want_colsum:  # colsum(A) from the same pass over A
+            out, cs = gemm_tn_big(A, B, b_bound=bb, want_colsum=True)
+        else:
+            out, cs = gemm_tn_big(A, B, b_bound=bb), None
         vout = None
         if nv:  # V^T B by the small kernel, V padded to a multiple of 4 columns (16-byte rows)
             Vp = torch.zeros(N, (nv + 3) // 4 * 4, dtype=torch.float32, device=A.device)
@@ -1102,12 +1105,14 @@ def colmax_abs(X: torch.Tensor, src_ptr: Optional[torch.Tensor] = None) -> torch
     return out
 
 
-def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None, a_bits=None) -> torch.Tensor:
+def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None, a_bits=None, want_colsum: bool = False):
     """A [M, ma]^T B [M, nb] on the matrix cores (ppgat_gemm_tn_big), deterministic.  ``b_bound``
     = (bits [period] from colmax_abs, period, scale >= 1): an upper bound of |B| per column
     (column j: bits[j % period] * scale) that replaces the fp16 kernel's column-max pass over B
     (ppgat_gemm_tn_big_bounded).  ``a_bits`` [ma]: a bound of |A| over the rows whose B row is not
-    zero (ppgat_gemm_tn_big_bounds: the other rows are clamped) in place of A's pass."""
+    zero (ppgat_gemm_tn_big_bounds: the other rows are clamped) in place of A's pass.
+    ``want_colsum``: returns (out, colsum(A)), the column sums from the same pass over A
+    (ppgat_gemm_tn_big_colsum)."""
     lib = _lib.load()
     _check_rows("A", A, torch.float32)
     _check_rows("B", B, torch.float32, A.device)
@@ -1118,6 +1123,19 @@ def gemm_tn_big(A: torch.Tensor, B: torch.Tensor, b_bound=None, a_bits=None) -> 
     ws = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=A.device)
     out = torch.empty(ma, nb, dtype=torch.float32, device=A.device)
     lda, ldb, st = A.stride(0) if M > 1 else ma, B.stride(0) if M > 1 else nb, _lib.stream_handle(A.device)
+    if want_colsum:
+        if a_bits is not None:
+            _require(a_bits.dtype == torch.int32 and a_bits.numel() == ma and a_bits.device == A.device,
+                     "gemm_tn_big: a_bits must be int32 [ma] on A's device")
+        bits, period, scale = b_bound if b_bound is not None else (None, 1, 1.0)
+        if bits is not None:
+            _require(bits.dtype == torch.int32 and bits.numel() == period and bits.device == A.device,
+                     "gemm_tn_big: b_bound bits must be int32 [period] on A's device")
+        cs = torch.empty(ma, dtype=torch.float32, device=A.device)
+        _lib.check(lib.ppgat_gemm_tn_big_colsum(A.data_ptr(), lda, B.data_ptr(), ldb, M, ma, nb, _lib.ptr(a_bits),
+                                                _lib.ptr(bits), int(period), float(scale), out.data_ptr(),
+                                                cs.data_ptr(), ws.data_ptr(), nbytes.value, st), "gemm_tn_big_colsum")
+        return out, cs
     if a_bits is not None:
         _require(a_bits.dtype == torch.int32 and a_bits.numel() == ma and a_bits.device == A.device,
                  "gemm_tn_big: a_bits must be int32 [ma] on A's device")
@@ -1596,12 +1614,15 @@ def _xgat_weight_grads(lib, saved: dict, g, S, dx, want_bias_grad: bool, st, x_r
     xbound = (colmax_abs(x, v.colptr) if xbits is None else xbits, K,
               (1.0 / (1.0 - p) if p > 0 else 1.0) * (1.0 + 2.0 ** -10))
     # (rows of g without an in-edge are outside gbits; their agg rows are zero: clamped, they add 0)
-    G = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound, a_bits=gbits)
-    dW, datt_src, datt_dst, dbias = _xgat_weight_grads_from_G(lib, saved, G, GV, g, want_bias_grad, st)
+    if saved["meta"][6] and want_bias_grad:  # dbias = colsum(g) from the same pass over g
+        G, gsum = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound, a_bits=gbits, want_colsum=True)
+    else:
+        G, gsum = gemm_tn_big(g, agg.view(v.n_dst, H * K), b_bound=xbound, a_bits=gbits), None
+    dW, datt_src, datt_dst, dbias = _xgat_weight_grads_from_G(lib, saved, G, GV, g, want_bias_grad, st, gsum)
     return dx, dW, datt_src, datt_dst, dbias
 
 
-def _xgat_weight_grads_from_G(lib, saved: dict, G, GV, g, want_bias_grad: bool, st):
+def _xgat_weight_grads_from_G(lib, saved: dict, G, GV, g, want_bias_grad: bool, st, gsum=None):
     W, a_s, a_d = saved["W"], saved["a_s"], saved["a_d"]
     H, C, K, slope, p, seed, has_bias = saved["meta"]
     dev = W.device
@@ -1611,7 +1632,7 @@ def _xgat_weight_grads_from_G(lib, saved: dict, G, GV, g, want_bias_grad: bool, 
     _lib.check(lib.ppgat_xgat_weight_grads(G.data_ptr(), GV.data_ptr(), W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(),
                                            H, C, K, dW.data_ptr(), datt_src.data_ptr(), datt_dst.data_ptr(), st),
                "xgat_weight_grads")
-    dbias = colsum(g) if (has_bias and want_bias_grad) else None
+    dbias = (gsum if gsum is not None else colsum(g)) if (has_bias and want_bias_grad) else None
     return dW, datt_src, datt_dst, dbias
 
 

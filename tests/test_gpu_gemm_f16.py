@@ -128,6 +128,28 @@ def test_tnh_random_vs_fp64(pkg, cuda, M, Ma, Nb):
     assert torch.equal(G, G2)
 
 
+@pytest.mark.parametrize("M,Ma,Nb", [(200_000, 256, 1024), (70_001, 128, 256), (33_333, 384, 256), (1, 128, 256)])
+def test_tn_big_colsum(pkg, cuda, M, Ma, Nb):
+    """ppgat_gemm_tn_big_colsum: the same A^T B bit for bit as the plain call, plus colsum(A) --
+    from the fp16 TN kernel's own staging of A (M >= 65536) or the colsum kernel (shorter
+    reductions), within 1e-6 of fp64, bitwise repeatable; with A's and B's bounds given too."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + Ma + 1)
+    A = torch.randn(M, Ma, generator=g, dtype=torch.float64) + 0.5
+    B = torch.randn(M, Nb, generator=g, dtype=torch.float64)
+    Ad, Bd = A.float().to(cuda), B.float().to(cuda)
+    G0 = ops.gemm_tn_big(Ad, Bd)
+    G, cs = ops.gemm_tn_big(Ad, Bd, want_colsum=True)
+    assert torch.equal(G, G0)
+    ref = A.sum(0)
+    assert float((cs.double().cpu() - ref).abs().max() / A.abs().sum(0).max()) <= 1e-6
+    G2, cs2 = ops.gemm_tn_big(Ad, Bd, want_colsum=True)
+    assert torch.equal(G2, G) and torch.equal(cs2, cs)
+    ab, bb = ops.colmax_abs(Ad), ops.colmax_abs(Bd)
+    G3, cs3 = ops.gemm_tn_big(Ad, Bd, b_bound=(bb, Nb, 1.0), a_bits=ab, want_colsum=True)
+    assert torch.equal(G3, ops.gemm_tn_big(Ad, Bd, b_bound=(bb, Nb, 1.0), a_bits=ab)) and torch.equal(cs3, cs)
+
+
 def test_tnh_dynamic_range_columns(pkg, cuda):
     """Columns of A and B spanning 30 decades, zero columns, a column whose max sits in its last
     row, and rows far below their column's max: every element within 4e-6 of (|A|^T |B|)."""
