@@ -1088,17 +1088,23 @@ __global__ void __launch_bounds__(256) k_dst_sum_vh(Items it, const float* __res
   }
 }
 
+// One wave per hub: lane l sums pieces l, l + 64, ... (piece order), per head, then the 64
+// lanes in a fixed butterfly -- deterministic.  (One thread per (hub, head) walking every piece
+// in turn took 134 us per call at the config-5 share, whose top item is 490 pieces.)
 __global__ void __launch_bounds__(256) k_dst_merge(const int32_t* __restrict__ hub_row,
                                                    const int32_t* __restrict__ hub_ptr, int64_t n_hubs, int heads,
                                                    const float* __restrict__ partial, float* __restrict__ ds_dst,
                                                    int64_t ld) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_hubs * heads) return;
-  const int64_t hb = t / heads;
-  const int hd = (int)(t % heads);
-  float x = 0.f;
-  for (int q = hub_ptr[hb]; q < hub_ptr[hb + 1]; ++q) x += partial[(int64_t)q * heads + hd];
-  ds_dst[(int64_t)hub_row[hb] * ld + hd] = x;
+  const int lane = threadIdx.x & 63;
+  const int64_t hb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hb >= n_hubs) return;  // (wave-uniform)
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  for (int hd = 0; hd < heads; ++hd) {
+    float x = 0.f;
+    for (int q = p0 + lane; q < p1; q += 64) x += partial[(int64_t)q * heads + hd];
+    x = group_reduce<Op::Sum, 1, 32>(x);
+    if (lane == 0) ds_dst[(int64_t)hub_row[hb] * ld + hd] = x;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1269,7 +1275,7 @@ hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const 
     hipLaunchKernelGGL(k_dst_sum<false>, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, csr2csc,
                        ds_dst, ld, partial);
   if (n_hubs > 0)
-    hipLaunchKernelGGL(k_dst_merge, dim3(blocks_for(n_hubs * heads)), dim3(256), 0, st, hub_row, hub_ptr, n_hubs,
+    hipLaunchKernelGGL(k_dst_merge, dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st, hub_row, hub_ptr, n_hubs,
                        heads, partial, ds_dst, ld);
   return hipGetLastError();
 }

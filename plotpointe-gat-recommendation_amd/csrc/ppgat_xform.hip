@@ -1433,30 +1433,39 @@ __global__ void __launch_bounds__(256) k_wperm(const float* __restrict__ W, int 
 }
 
 // s_src[n][h] = x_n . A_src[h] (n < n_rows), s_dst[n][h] = x_n . A_dst[h] (n < n_dst).
-// LPR = K/4 lanes per row, 64/LPR rows per wave, grid-stride.
+// K = 256: a row is one float4 per lane; a wave takes 4 rows per iteration (their loads in
+// flight together), and each row's 2H lane partials are summed by one transposing butterfly
+// (lanes 64 / 2H * v .. hold score v): 2H - 1 exchanges + a short reduction instead of 2H
+// full-wave reductions.  (One row at a time with 2H six-step reductions ran at 3.0 TB/s.)
 template <int K, int H>
 __global__ void __launch_bounds__(256) k_xscores(const float* __restrict__ x, int64_t ldx, int64_t n_rows,
                                                  int64_t n_dst, const float* __restrict__ A, float* __restrict__ s_src,
                                                  float* __restrict__ s_dst) {
-  constexpr int LPR = K / 4, RPW = 64 / LPR, V = 2 * H;
+  static_assert(K == 256 && (H == 2 || H == 4), "k_xscores: K = 256, H in {2, 4}");
+  constexpr int V = 2 * H, R = 4, LV = 64 / V;
   const int lane = threadIdx.x & 63;
-  const int sl = lane % LPR, sr = lane / LPR;
   float4 av[V];
 #pragma unroll
-  for (int v = 0; v < V; ++v) av[v] = ld4(A + v * K + sl * 4);
+  for (int v = 0; v < V; ++v) av[v] = ld4(A + v * K + lane * 4);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW; base < n_rows; base += nw * RPW) {
-    const int64_t n = base + sr;
-    const float4 xv = ld4(x + (n < n_rows ? n : n_rows - 1) * ldx + sl * 4);
-    float res[V];
+  const int vi = lane / LV;  // the score this lane ends with
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * R; base < n_rows; base += nw * R) {
+    float4 xv[R];
 #pragma unroll
-    for (int v = 0; v < V; ++v) res[v] = group_reduce<Op::Sum, 1, LPR / 2>(dot4(xv, av[v]));
-    if (n < n_rows && sl == 0) {
+    for (int r = 0; r < R; ++r) {
+      const int64_t n = base + r;
+      xv[r] = ld4(x + (n < n_rows ? n : n_rows - 1) * ldx + lane * 4);
+    }
 #pragma unroll
-      for (int h = 0; h < H; ++h) s_src[n * H + h] = res[h];
-      if (n < n_dst) {
+    for (int r = 0; r < R; ++r) {
+      float pv[V];
 #pragma unroll
-        for (int h = 0; h < H; ++h) s_dst[n * H + h] = res[H + h];
+      for (int v = 0; v < V; ++v) pv[v] = dot4(xv[r], av[v]);
+      const float sum = transpose_reduce<64, V>(pv, lane);
+      const int64_t n = base + r;
+      if (n < n_rows && lane % LV == 0) {
+        if (vi < H) s_src[n * H + vi] = sum;
+        else if (n < n_dst) s_dst[n * H + vi - H] = sum;
       }
     }
   }
@@ -2659,7 +2668,7 @@ hipError_t xgat_weights(const float* W, const float* att_src, const float* att_d
 hipError_t xgat_scores(const float* x, int64_t ldx, int64_t n_rows, int64_t n_dst, int K, int H, const float* A,
                        float* s_src, float* s_dst, hipStream_t st) {
   if (n_rows <= 0) return hipSuccess;
-  int64_t blocks = (n_rows + 3) / 4;  // one row per wave (K = 256), grid-stride
+  int64_t blocks = (n_rows + 15) / 16;  // four rows per wave and iteration (K = 256), grid-stride
   if (blocks > 4096) blocks = 4096;
   PPGAT_XH(H, hipLaunchKernelGGL((k_xscores<256, HH>), dim3((unsigned)blocks), dim3(256), 0, st, x, ldx, n_rows, n_dst,
                                  A, s_src, s_dst));
