@@ -1129,7 +1129,8 @@ __global__ void __launch_bounds__(256) k_split_sum(const float* __restrict__ par
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= n4) return;
   float4 s = ld4(part + e * 4);
-  for (int k = 1; k < splits; ++k) s = add4(s, ld4(part + ((size_t)k * n4 + e) * 4));
+#pragma unroll 8
+  for (int k = 1; k < splits; ++k) s = add4(s, ld4(part + ((size_t)k * n4 + e) * 4));  // (loads in flight, adds in order)
   st4(out + e * 4, s);
 }
 
@@ -1407,17 +1408,32 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
 // aggregate-then-transform layer pieces
 // ===========================================================================
 // A[v][h][k] = sum_c att_v[h][c] W[h C + c][k]  (v = 0: src, 1: dst) -> [2, H, K]
+// (16 outputs per block, the c sum split over 16 threads in fixed 16-wide chunks and combined in
+// chunk order: 128 blocks instead of eight, each with 256-long serial chains, which left the
+// kernel at 98 us)
 __global__ void __launch_bounds__(256) k_att_proj(const float* __restrict__ W, const float* __restrict__ att_src,
                                                   const float* __restrict__ att_dst, int H, int C, int K,
                                                   float* __restrict__ A) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)2 * H * K) return;
-  const int v = (int)(t / ((int64_t)H * K));
-  const int h = (int)((t / K) % H), k = (int)(t % K);
-  const float* att = (v == 0 ? att_src : att_dst) + h * C;
+  __shared__ float red[16][16];
+  const int kl = threadIdx.x & 15, cq = threadIdx.x >> 4;
+  const int64_t t = (int64_t)blockIdx.x * 16 + kl;
+  const bool live = t < (int64_t)2 * H * K;
   float s = 0.f;
-  for (int c = 0; c < C; ++c) s = fmaf(att[c], W[(int64_t)(h * C + c) * K + k], s);
-  A[t] = s;
+  if (live) {
+    const int v = (int)(t / ((int64_t)H * K));
+    const int h = (int)((t / K) % H), k = (int)(t % K);
+    const float* att = (v == 0 ? att_src : att_dst) + h * C;
+    const int cw = (C + 15) / 16, c0 = cq * cw, c1 = min(C, c0 + cw);
+    for (int c = c0; c < c1; ++c) s = fmaf(att[c], W[(int64_t)(h * C + c) * K + k], s);
+  }
+  red[cq][kl] = s;
+  __syncthreads();
+  if (cq == 0 && live) {
+    float a = red[0][kl];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) a += red[q][kl];
+    A[t] = a;
+  }
 }
 
 // Wt[h K + k][c] = W[h C + c][k]  (the transform, [H K, C]) and Wg[c][h K + k] = W[h C + c][k] / H
@@ -2658,7 +2674,7 @@ bool xgat_shape_ok(int K, int H, int C) { return K == 256 && (H == 2 || H == 4) 
 hipError_t xgat_weights(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
                         float* Wt, float* Wg, hipStream_t st) {
   const int64_t na = (int64_t)2 * H * K;
-  if (A) hipLaunchKernelGGL(k_att_proj, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, st, W, att_src, att_dst, H, C,
+  if (A) hipLaunchKernelGGL(k_att_proj, dim3((unsigned)((na + 15) / 16)), dim3(256), 0, st, W, att_src, att_dst, H, C,
                             K, A);
   const int64_t nw = (int64_t)H * C * K;
   if (Wt || Wg) hipLaunchKernelGGL(k_wperm, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, W, H, C, K, Wt, Wg);
@@ -2789,7 +2805,7 @@ hipError_t xgat_bwd_epi(const float* S, int64_t lds, const float* A_dst, int64_t
 hipError_t att_proj(const float* W, const float* att_src, const float* att_dst, int H, int C, int K, float* A,
                     hipStream_t st) {
   const int64_t na = (int64_t)2 * H * K;
-  if (na > 0) hipLaunchKernelGGL(k_att_proj, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, st, W, att_src, att_dst,
+  if (na > 0) hipLaunchKernelGGL(k_att_proj, dim3((unsigned)((na + 15) / 16)), dim3(256), 0, st, W, att_src, att_dst,
                                  H, C, K, A);
   return hipGetLastError();
 }
