@@ -2035,7 +2035,8 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t 
 // 1M edges = 3,900 pieces of 256 edges, on the rank that owns it -- merging for 4 ms per call,
 // 10 ms per step of that rank (profiles/r04/v16_probe5_r0_kernel_stats.csv).
 // ---------------------------------------------------------------------------
-constexpr int kMW = 8;  // waves per hub
+constexpr int kMW = 8;    // waves per hub (forward and dz merges; 16 measured slower for the forward: 133 vs 94 us)
+constexpr int kMWb = 16;  // waves per hub in the backward merge (8: 89 us per call at the config-5 share; 16: 75)
 
 // aggregate-then-transform forward: agg[i,h] = sum_q e^(m_q - M) ax_q / sum_q e^(m_q - M) l_q
 __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __restrict__ hub_row,
@@ -2098,13 +2099,13 @@ __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __rest
 
 // hub sources of k_bwd_g: the pieces' [acc^h (C) x H | ds] summed, waves in order
 template <int C, int H>
-__global__ void __launch_bounds__(64 * kMW) k_bwd_g_merge_wg(const int32_t* __restrict__ hub_row,
+__global__ void __launch_bounds__(64 * kMWb) k_bwd_g_merge_wg(const int32_t* __restrict__ hub_row,
                                                              const int32_t* __restrict__ hub_ptr,
                                                              const float* __restrict__ partial,
                                                              float* __restrict__ acc_out, float* __restrict__ S,
                                                              int64_t lds) {
   static_assert(C == 256, "one float4 per lane");
-  __shared__ float4 red[kMW][H + 1][64];
+  __shared__ float4 red[kMWb][H + 1][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t hb = blockIdx.x;
   const int64_t j = hub_row[hb];
@@ -2114,9 +2115,27 @@ __global__ void __launch_bounds__(64 * kMW) k_bwd_g_merge_wg(const int32_t* __re
   for (int h = 0; h < H; ++h) a[h] = b[h] = f4(0.f);
   float4 da = f4(0.f), db = f4(0.f);
   int q = p0 + w;
-  for (; q + kMW < p1; q += 2 * kMW) {
+  // four pieces' loads in flight per wave (pieces q, q + kMWb into a, the other two into b)
+  for (; q + 3 * kMWb < p1; q += 4 * kMWb) {
+    float4 v[4][H], d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* su = partial + (int64_t)(q + u * kMWb) * (H * C + 4);
+#pragma unroll
+      for (int h = 0; h < H; ++h) v[u][h] = ld4(su + h * C + lane * 4);
+      d[u] = ld4(su + H * C);
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      a[h] = add4(add4(a[h], v[0][h]), v[1][h]);
+      b[h] = add4(add4(b[h], v[2][h]), v[3][h]);
+    }
+    da = add4(add4(da, d[0]), d[1]);
+    db = add4(add4(db, d[2]), d[3]);
+  }
+  for (; q + kMWb < p1; q += 2 * kMWb) {
     const float* s0 = partial + (int64_t)q * (H * C + 4);
-    const float* s1 = partial + (int64_t)(q + kMW) * (H * C + 4);
+    const float* s1 = partial + (int64_t)(q + kMWb) * (H * C + 4);
     float4 v0[H], v1[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
@@ -2146,7 +2165,7 @@ __global__ void __launch_bounds__(64 * kMW) k_bwd_g_merge_wg(const int32_t* __re
 #pragma unroll
   for (int h = 0; h <= H; ++h) {
     float4 acc = red[0][h][lane];
-    for (int k = 1; k < kMW; ++k) acc = add4(acc, red[k][h][lane]);
+    for (int k = 1; k < kMWb; ++k) acc = add4(acc, red[k][h][lane]);
     if (h < H) {
       st4(acc_out + (j * H + h) * C + lane * 4, acc);
     } else if (S != nullptr && lane < H) {
@@ -2753,7 +2772,7 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                                    row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
                                    slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz, gmax));
   if (n_hubs > 0)
-    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs), dim3(64 * kMW), 0, st, hub_row,
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs), dim3(64 * kMWb), 0, st, hub_row,
                                    hub_ptr, partial, acc, S, lds));
   (void)C;
   return hipGetLastError();
