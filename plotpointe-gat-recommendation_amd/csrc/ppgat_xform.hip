@@ -2052,7 +2052,8 @@ __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __rest
   const int64_t i = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
   auto slot = [&](int q, int hd) { return partial + ((int64_t)q * heads + hd) * (C + 4); };
-  for (int hd = 0; hd < heads; ++hd) {
+  {
+    const int hd = blockIdx.y;  // one workgroup per (hub, head): 3,740 hubs x 4 heads at the config-5 share
     float M = -INFINITY;
     for (int q = p0 + tid; q < p1; q += 64 * kMW) M = fmaxf(M, slot(q, hd)[C]);
     M = wave_max(M);
@@ -2093,11 +2094,11 @@ __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __rest
         invl_out[i * heads + hd] = invl;
       }
     }
-    __syncthreads();  // sr / red are the next head's
   }
 }
 
-// hub sources of k_bwd_g: the pieces' [acc^h (C) x H | ds] summed, waves in order
+// hub sources of k_bwd_g: the pieces' [acc^h (C) x H | ds] summed, waves in order; one workgroup
+// per (hub, component): blockIdx.y = h < H sums head h's row, blockIdx.y = H the ds quad
 template <int C, int H>
 __global__ void __launch_bounds__(64 * kMWb) k_bwd_g_merge_wg(const int32_t* __restrict__ hub_row,
                                                              const int32_t* __restrict__ hub_ptr,
@@ -2105,73 +2106,41 @@ __global__ void __launch_bounds__(64 * kMWb) k_bwd_g_merge_wg(const int32_t* __r
                                                              float* __restrict__ acc_out, float* __restrict__ S,
                                                              int64_t lds) {
   static_assert(C == 256, "one float4 per lane");
-  __shared__ float4 red[kMWb][H + 1][64];
+  __shared__ float4 red[kMWb][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t hb = blockIdx.x;
+  const int h = blockIdx.y;
+  if (h == H && S == nullptr) return;
   const int64_t j = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
-  float4 a[H], b[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) a[h] = b[h] = f4(0.f);
-  float4 da = f4(0.f), db = f4(0.f);
+  const int off = h < H ? h * C + lane * 4 : H * C;
+  float4 a = f4(0.f), b = f4(0.f);
   int q = p0 + w;
   // four pieces' loads in flight per wave (pieces q, q + kMWb into a, the other two into b)
   for (; q + 3 * kMWb < p1; q += 4 * kMWb) {
-    float4 v[4][H], d[4];
+    float4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float* su = partial + (int64_t)(q + u * kMWb) * (H * C + 4);
-#pragma unroll
-      for (int h = 0; h < H; ++h) v[u][h] = ld4(su + h * C + lane * 4);
-      d[u] = ld4(su + H * C);
-    }
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      a[h] = add4(add4(a[h], v[0][h]), v[1][h]);
-      b[h] = add4(add4(b[h], v[2][h]), v[3][h]);
-    }
-    da = add4(add4(da, d[0]), d[1]);
-    db = add4(add4(db, d[2]), d[3]);
+    for (int u = 0; u < 4; ++u) v[u] = ld4(partial + (int64_t)(q + u * kMWb) * (H * C + 4) + off);
+    a = add4(add4(a, v[0]), v[1]);
+    b = add4(add4(b, v[2]), v[3]);
   }
   for (; q + kMWb < p1; q += 2 * kMWb) {
-    const float* s0 = partial + (int64_t)q * (H * C + 4);
-    const float* s1 = partial + (int64_t)(q + kMWb) * (H * C + 4);
-    float4 v0[H], v1[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      v0[h] = ld4(s0 + h * C + lane * 4);
-      v1[h] = ld4(s1 + h * C + lane * 4);
-    }
-    const float4 d0 = ld4(s0 + H * C), d1 = ld4(s1 + H * C);
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      a[h] = add4(a[h], v0[h]);
-      b[h] = add4(b[h], v1[h]);
-    }
-    da = add4(da, d0);
-    db = add4(db, d1);
+    const float4 v0 = ld4(partial + (int64_t)q * (H * C + 4) + off);
+    const float4 v1 = ld4(partial + (int64_t)(q + kMWb) * (H * C + 4) + off);
+    a = add4(a, v0);
+    b = add4(b, v1);
   }
-  if (q < p1) {
-    const float* s0 = partial + (int64_t)q * (H * C + 4);
-#pragma unroll
-    for (int h = 0; h < H; ++h) a[h] = add4(a[h], ld4(s0 + h * C + lane * 4));
-    da = add4(da, ld4(s0 + H * C));
-  }
-#pragma unroll
-  for (int h = 0; h < H; ++h) red[w][h][lane] = add4(a[h], b[h]);
-  red[w][H][lane] = add4(da, db);
+  if (q < p1) a = add4(a, ld4(partial + (int64_t)q * (H * C + 4) + off));
+  red[w][lane] = add4(a, b);
   __syncthreads();
   if (w != 0) return;
-#pragma unroll
-  for (int h = 0; h <= H; ++h) {
-    float4 acc = red[0][h][lane];
-    for (int k = 1; k < kMWb; ++k) acc = add4(acc, red[k][h][lane]);
-    if (h < H) {
-      st4(acc_out + (j * H + h) * C + lane * 4, acc);
-    } else if (S != nullptr && lane < H) {
-      const float ds[4] = {acc.x, acc.y, acc.z, acc.w};
-      S[j * lds + lane] = ds[lane];
-    }
+  float4 acc = red[0][lane];
+  for (int k = 1; k < kMWb; ++k) acc = add4(acc, red[k][lane]);
+  if (h < H) {
+    st4(acc_out + (j * H + h) * C + lane * 4, acc);
+  } else if (lane < H) {
+    const float ds[4] = {acc.x, acc.y, acc.z, acc.w};
+    S[j * lds + lane] = ds[lane];
   }
 }
 
@@ -2725,7 +2694,7 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
   if (e != hipSuccess) return e;
   (void)K;
   if (n_hubs > 0)
-    hipLaunchKernelGGL(k_fwd_merge_wg, dim3((unsigned)n_hubs), dim3(64 * kMW), 0, st, hub_row, hub_ptr, H, partial,
+    hipLaunchKernelGGL(k_fwd_merge_wg, dim3((unsigned)n_hubs, (unsigned)H), dim3(64 * kMW), 0, st, hub_row, hub_ptr, H, partial,
                        1e-16f, m, invl, agg);
   return hipGetLastError();
 }
@@ -2772,7 +2741,7 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                                    row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
                                    slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz, gmax));
   if (n_hubs > 0)
-    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs), dim3(64 * kMWb), 0, st, hub_row,
+    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs, HH + 1), dim3(64 * kMWb), 0, st, hub_row,
                                    hub_ptr, partial, acc, S, lds));
   (void)C;
   return hipGetLastError();
