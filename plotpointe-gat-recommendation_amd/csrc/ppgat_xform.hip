@@ -2037,6 +2037,54 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t 
 // ---------------------------------------------------------------------------
 constexpr int kMW = 8;    // waves per hub (forward and dz merges; 16 measured slower for the forward: 133 vs 94 us)
 constexpr int kMWb = 16;  // waves per hub in the backward merge (8: 89 us per call at the config-5 share; 16: 75)
+// Hubs of at most kSmallP pieces (most of them: config 5's share has 3,740 hubs, few above a
+// dozen pieces) are merged by one wave per (hub, head) instead -- a workgroup of 8-16 waves on
+// a 3-piece hub leaves most of its waves idle through three barriers.  The workgroup kernels
+// skip those hubs.
+constexpr int kSmallP = 16;
+
+// one wave per (hub, head) for the small hubs: lanes hold the pieces' m and l, then the rows
+// in piece order, four loads in flight
+__global__ void __launch_bounds__(256) k_fwd_merge_small(const int32_t* __restrict__ hub_row,
+                                                         const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
+                                                         int heads, const float* __restrict__ partial, float eps,
+                                                         float* __restrict__ m_out, float* __restrict__ invl_out,
+                                                         float* __restrict__ agg_out) {
+  constexpr int C = 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= n_hubs * heads) return;
+  const int64_t hb = u / heads;
+  const int hd = (int)(u - hb * heads);
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  if (p1 - p0 > kSmallP) return;
+  const int64_t i = hub_row[hb];
+  auto slot = [&](int q) { return partial + ((int64_t)q * heads + hd) * (C + 4); };
+  float mq = -INFINITY, lq = 0.f;
+  if (p0 + lane < p1) {
+    mq = slot(p0 + lane)[C];
+    lq = slot(p0 + lane)[C + 1];
+  }
+  const float M = wave_max(mq);
+  const float l = wave_sum(p0 + lane < p1 ? lq * expf(mq - M) : 0.f);
+  float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
+  int q = p0;
+  for (; q + 3 < p1; q += 4) {
+    const float4 v0 = ld4(slot(q) + lane * 4), v1 = ld4(slot(q + 1) + lane * 4), v2 = ld4(slot(q + 2) + lane * 4),
+                 v3 = ld4(slot(q + 3) + lane * 4);
+    a0 = fma4(expf(__shfl(mq, q - p0) - M), v0, a0);
+    a1 = fma4(expf(__shfl(mq, q + 1 - p0) - M), v1, a1);
+    a2 = fma4(expf(__shfl(mq, q + 2 - p0) - M), v2, a2);
+    a3 = fma4(expf(__shfl(mq, q + 3 - p0) - M), v3, a3);
+  }
+  for (; q < p1; ++q) a0 = fma4(expf(__shfl(mq, q - p0) - M), ld4(slot(q) + lane * 4), a0);
+  const float invl = 1.f / (l + eps);
+  st4(agg_out + (i * heads + hd) * C + lane * 4, mul4(add4(add4(a0, a1), add4(a2, a3)), invl));
+  if (lane == 0) {
+    m_out[i * heads + hd] = M;
+    invl_out[i * heads + hd] = invl;
+  }
+}
 
 // aggregate-then-transform forward: agg[i,h] = sum_q e^(m_q - M) ax_q / sum_q e^(m_q - M) l_q
 __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __restrict__ hub_row,
@@ -2051,6 +2099,7 @@ __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __rest
   const int64_t hb = blockIdx.x;
   const int64_t i = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  if (p1 - p0 <= kSmallP) return;  // k_fwd_merge_small's
   auto slot = [&](int q, int hd) { return partial + ((int64_t)q * heads + hd) * (C + 4); };
   {
     const int hd = blockIdx.y;  // one workgroup per (hub, head): 3,740 hubs x 4 heads at the config-5 share
@@ -2111,8 +2160,9 @@ __global__ void __launch_bounds__(64 * kMWb) k_bwd_g_merge_wg(const int32_t* __r
   const int64_t hb = blockIdx.x;
   const int h = blockIdx.y;
   if (h == H && S == nullptr) return;
-  const int64_t j = hub_row[hb];
   const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  if (p1 - p0 <= kSmallP) return;  // k_bwd_g_merge_small's
+  const int64_t j = hub_row[hb];
   const int off = h < H ? h * C + lane * 4 : H * C;
   float4 a = f4(0.f), b = f4(0.f);
   int q = p0 + w;
@@ -2136,6 +2186,44 @@ __global__ void __launch_bounds__(64 * kMWb) k_bwd_g_merge_wg(const int32_t* __r
   if (w != 0) return;
   float4 acc = red[0][lane];
   for (int k = 1; k < kMWb; ++k) acc = add4(acc, red[k][lane]);
+  if (h < H) {
+    st4(acc_out + (j * H + h) * C + lane * 4, acc);
+  } else if (lane < H) {
+    const float ds[4] = {acc.x, acc.y, acc.z, acc.w};
+    S[j * lds + lane] = ds[lane];
+  }
+}
+
+// one wave per (hub, component) for the small hubs: the pieces in order, four loads in flight
+template <int C, int H>
+__global__ void __launch_bounds__(256) k_bwd_g_merge_small(const int32_t* __restrict__ hub_row,
+                                                           const int32_t* __restrict__ hub_ptr, int64_t n_hubs,
+                                                           const float* __restrict__ partial,
+                                                           float* __restrict__ acc_out, float* __restrict__ S,
+                                                           int64_t lds) {
+  static_assert(C == 256, "one float4 per lane");
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= n_hubs * (H + 1)) return;
+  const int64_t hb = u / (H + 1);
+  const int h = (int)(u - hb * (H + 1));
+  if (h == H && S == nullptr) return;
+  const int p0 = hub_ptr[hb], p1 = hub_ptr[hb + 1];
+  if (p1 - p0 > kSmallP) return;
+  const int64_t j = hub_row[hb];
+  const int off = h < H ? h * C + lane * 4 : H * C;
+  float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
+  int q = p0;
+  for (; q + 3 < p1; q += 4) {
+    const float* s = partial + (int64_t)q * (H * C + 4) + off;
+    const float4 v0 = ld4(s), v1 = ld4(s + (H * C + 4)), v2 = ld4(s + 2 * (H * C + 4)), v3 = ld4(s + 3 * (H * C + 4));
+    a0 = add4(a0, v0);
+    a1 = add4(a1, v1);
+    a2 = add4(a2, v2);
+    a3 = add4(a3, v3);
+  }
+  for (; q < p1; ++q) a0 = add4(a0, ld4(partial + (int64_t)q * (H * C + 4) + off));
+  const float4 acc = add4(add4(a0, a1), add4(a2, a3));
   if (h < H) {
     st4(acc_out + (j * H + h) * C + lane * 4, acc);
   } else if (lane < H) {
@@ -2693,9 +2781,12 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)K;
-  if (n_hubs > 0)
+  if (n_hubs > 0) {
+    hipLaunchKernelGGL(k_fwd_merge_small, dim3((unsigned)((n_hubs * H + 3) / 4)), dim3(256), 0, st, hub_row, hub_ptr,
+                       (int64_t)n_hubs, H, partial, 1e-16f, m, invl, agg);
     hipLaunchKernelGGL(k_fwd_merge_wg, dim3((unsigned)n_hubs, (unsigned)H), dim3(64 * kMW), 0, st, hub_row, hub_ptr, H, partial,
                        1e-16f, m, invl, agg);
+  }
   return hipGetLastError();
 }
 
@@ -2741,8 +2832,12 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                                    row, csc_eid, csc2csr, hs, s_src, reinterpret_cast<const float4*>(nstate), g, ldg,
                                    slope, p, inv_keep, seed, seed_in, acc, S, lds, dz, partial, pz, gmax));
   if (n_hubs > 0)
-    PPGAT_XH(H, hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs, HH + 1), dim3(64 * kMWb), 0, st, hub_row,
-                                   hub_ptr, partial, acc, S, lds));
+    PPGAT_XH(H, {
+      hipLaunchKernelGGL((k_bwd_g_merge_small<256, HH>), dim3((unsigned)((n_hubs * (HH + 1) + 3) / 4)), dim3(256), 0,
+                         st, hub_row, hub_ptr, (int64_t)n_hubs, partial, acc, S, lds);
+      hipLaunchKernelGGL((k_bwd_g_merge_wg<256, HH>), dim3((unsigned)n_hubs, HH + 1), dim3(64 * kMWb), 0, st, hub_row,
+                         hub_ptr, partial, acc, S, lds);
+    });
   (void)C;
   return hipGetLastError();
 }
