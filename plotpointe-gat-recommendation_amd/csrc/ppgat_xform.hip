@@ -2035,7 +2035,8 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t 
 // 1M edges = 3,900 pieces of 256 edges, on the rank that owns it -- merging for 4 ms per call,
 // 10 ms per step of that rank (profiles/r04/v16_probe5_r0_kernel_stats.csv).
 // ---------------------------------------------------------------------------
-constexpr int kMW = 8;    // waves per hub (forward and dz merges; 16 measured slower for the forward: 133 vs 94 us)
+constexpr int kMW = 8;    // waves per hub in the dz merge
+constexpr int kMWf = 16;  // waves per (hub, head) in the forward merge (its hubs all above kSmallP pieces)
 constexpr int kMWb = 16;  // waves per hub in the backward merge (8: 89 us per call at the config-5 share; 16: 75)
 // Hubs of at most kSmallP pieces (most of them: config 5's share has 3,740 hubs, few above a
 // dozen pieces) are merged by one wave per (hub, head) instead -- a workgroup of 8-16 waves on
@@ -2087,14 +2088,14 @@ __global__ void __launch_bounds__(256) k_fwd_merge_small(const int32_t* __restri
 }
 
 // aggregate-then-transform forward: agg[i,h] = sum_q e^(m_q - M) ax_q / sum_q e^(m_q - M) l_q
-__global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __restrict__ hub_row,
+__global__ void __launch_bounds__(64 * kMWf) k_fwd_merge_wg(const int32_t* __restrict__ hub_row,
                                                            const int32_t* __restrict__ hub_ptr, int heads,
                                                            const float* __restrict__ partial, float eps,
                                                            float* __restrict__ m_out, float* __restrict__ invl_out,
                                                            float* __restrict__ agg_out) {
   constexpr int C = 256;
-  __shared__ float4 red[kMW][64];
-  __shared__ float sr[kMW];
+  __shared__ float4 red[kMWf][64];
+  __shared__ float sr[kMWf];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t hb = blockIdx.x;
   const int64_t i = hub_row[hb];
@@ -2104,38 +2105,38 @@ __global__ void __launch_bounds__(64 * kMW) k_fwd_merge_wg(const int32_t* __rest
   {
     const int hd = blockIdx.y;  // one workgroup per (hub, head): 3,740 hubs x 4 heads at the config-5 share
     float M = -INFINITY;
-    for (int q = p0 + tid; q < p1; q += 64 * kMW) M = fmaxf(M, slot(q, hd)[C]);
+    for (int q = p0 + tid; q < p1; q += 64 * kMWf) M = fmaxf(M, slot(q, hd)[C]);
     M = wave_max(M);
     if (lane == 0) sr[w] = M;
     __syncthreads();
     M = sr[0];
-    for (int k = 1; k < kMW; ++k) M = fmaxf(M, sr[k]);
+    for (int k = 1; k < kMWf; ++k) M = fmaxf(M, sr[k]);
     __syncthreads();
     float t = 0.f;
-    for (int q = p0 + tid; q < p1; q += 64 * kMW) t += slot(q, hd)[C + 1] * expf(slot(q, hd)[C] - M);
+    for (int q = p0 + tid; q < p1; q += 64 * kMWf) t += slot(q, hd)[C + 1] * expf(slot(q, hd)[C] - M);
     t = wave_sum(t);
     if (lane == 0) sr[w] = t;
     float4 a0 = f4(0.f), a1 = f4(0.f), a2 = f4(0.f), a3 = f4(0.f);
     int q = p0 + w;
-    for (; q + 3 * kMW < p1; q += 4 * kMW) {
+    for (; q + 3 * kMWf < p1; q += 4 * kMWf) {
       const float* s0 = slot(q, hd);
-      const float* s1 = slot(q + kMW, hd);
-      const float* s2 = slot(q + 2 * kMW, hd);
-      const float* s3 = slot(q + 3 * kMW, hd);
+      const float* s1 = slot(q + kMWf, hd);
+      const float* s2 = slot(q + 2 * kMWf, hd);
+      const float* s3 = slot(q + 3 * kMWf, hd);
       const float4 v0 = ld4(s0 + lane * 4), v1 = ld4(s1 + lane * 4), v2 = ld4(s2 + lane * 4), v3 = ld4(s3 + lane * 4);
       a0 = fma4(expf(s0[C] - M), v0, a0);
       a1 = fma4(expf(s1[C] - M), v1, a1);
       a2 = fma4(expf(s2[C] - M), v2, a2);
       a3 = fma4(expf(s3[C] - M), v3, a3);
     }
-    for (; q < p1; q += kMW) a0 = fma4(expf(slot(q, hd)[C] - M), ld4(slot(q, hd) + lane * 4), a0);
+    for (; q < p1; q += kMWf) a0 = fma4(expf(slot(q, hd)[C] - M), ld4(slot(q, hd) + lane * 4), a0);
     red[w][lane] = add4(add4(a0, a1), add4(a2, a3));
     __syncthreads();
     if (w == 0) {
       float l = 0.f;
-      for (int k = 0; k < kMW; ++k) l += sr[k];
+      for (int k = 0; k < kMWf; ++k) l += sr[k];
       float4 acc = red[0][lane];
-      for (int k = 1; k < kMW; ++k) acc = add4(acc, red[k][lane]);
+      for (int k = 1; k < kMWf; ++k) acc = add4(acc, red[k][lane]);
       const float invl = 1.f / (l + eps);
       st4(agg_out + (i * heads + hd) * C + lane * 4, mul4(acc, invl));
       if (lane == 0) {
@@ -2166,7 +2167,14 @@ __global__ void __launch_bounds__(64 * kMWb) k_bwd_g_merge_wg(const int32_t* __r
   const int off = h < H ? h * C + lane * 4 : H * C;
   float4 a = f4(0.f), b = f4(0.f);
   int q = p0 + w;
-  // four pieces' loads in flight per wave (pieces q, q + kMWb into a, the other two into b)
+  // eight, then four pieces' loads in flight per wave (the first half into a, the rest into b)
+  for (; q + 7 * kMWb < p1; q += 8 * kMWb) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(partial + (int64_t)(q + u * kMWb) * (H * C + 4) + off);
+    a = add4(add4(add4(add4(a, v[0]), v[1]), v[2]), v[3]);
+    b = add4(add4(add4(add4(b, v[4]), v[5]), v[6]), v[7]);
+  }
   for (; q + 3 * kMWb < p1; q += 4 * kMWb) {
     float4 v[4];
 #pragma unroll
@@ -2784,7 +2792,7 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
   if (n_hubs > 0) {
     hipLaunchKernelGGL(k_fwd_merge_small, dim3((unsigned)((n_hubs * H + 3) / 4)), dim3(256), 0, st, hub_row, hub_ptr,
                        (int64_t)n_hubs, H, partial, 1e-16f, m, invl, agg);
-    hipLaunchKernelGGL(k_fwd_merge_wg, dim3((unsigned)n_hubs, (unsigned)H), dim3(64 * kMW), 0, st, hub_row, hub_ptr, H, partial,
+    hipLaunchKernelGGL(k_fwd_merge_wg, dim3((unsigned)n_hubs, (unsigned)H), dim3(64 * kMWf), 0, st, hub_row, hub_ptr, H, partial,
                        1e-16f, m, invl, agg);
   }
   return hipGetLastError();
