@@ -1162,7 +1162,20 @@ __global__ void __launch_bounds__(256) k_colmax_bits(const float* __restrict__ X
   const int T = C >> 2, P = 256 / T, t = threadIdx.x, cg = t % T, rl = t / T;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   float4 m = f4(0.f);
-  if (rl < P) {
+  auto mx = [](float4 a, float4 v) {
+    return make_float4(fmaxf(a.x, fabsf(v.x)), fmaxf(a.y, fabsf(v.y)), fmaxf(a.z, fabsf(v.z)), fmaxf(a.w, fabsf(v.w)));
+  };
+  if (rl < P && rp == nullptr) {  // eight rows' loads in flight per thread (a max: any order, same bits)
+    int64_t r = r0 + rl;
+    for (; r + 7 * P < r1; r += 8 * P) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld4(X + (r + u * P) * ldx + 4 * cg);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) m = mx(m, v[u]);
+    }
+    for (; r < r1; r += P) m = mx(m, ld4(X + r * ldx + 4 * cg));
+  } else if (rl < P) {
     for (int64_t r = r0 + rl; r < r1; r += P) {
       if (rp != nullptr && rp[r + 1] == rp[r]) continue;
       const float4 v = ld4(X + r * ldx + 4 * cg);
