@@ -100,7 +100,9 @@ def _graph(rng, n, e, hub_rows=0):
 @pytest.mark.parametrize("gather", ["gd", "gd-free", "g", "gt"])
 @pytest.mark.parametrize("n,e,C,heads,p,hubs", [(2000, 20_000, 256, 4, 0.0, 0), (1500, 30_000, 256, 4, 0.2, 3),
                                                 (1200, 12_000, 128, 2, 0.1, 0), (900, 25_000, 256, 2, 0.0, 2),
-                                                (1500, 60_000, 256, 4, 0.1, 1)])  # 47-piece hubs: workgroup merges
+                                                (1500, 60_000, 256, 4, 0.1, 1),  # 47-piece hubs: workgroup merges
+                                                # hubs of 16 / 17 pieces: either side of the one-wave merges' limit
+                                                (1500, 20_400, 256, 4, 0.1, 1), (1500, 20_600, 256, 4, 0.0, 1)])
 def test_gatconv_aggregate_then_transform_vs_oracle(pkg, oracle, cuda, monkeypatch, n, e, C, heads, p, hubs, gather):
     """Both backward edge passes: gathering g_i (hs = x W^T / H per source, acc, dx = acc W / H;
     ppgat_xgat_bwd_edges_g, C == 256) and gathering gt_i (ppgat_xgat_bwd_edges).  "gd-free": the
