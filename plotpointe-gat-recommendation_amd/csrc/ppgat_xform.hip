@@ -2050,7 +2050,7 @@ __global__ void __launch_bounds__(256) k_xgat_dz(XItems it, int64_t w0, int64_t 
 // ---------------------------------------------------------------------------
 constexpr int kMW = 8;    // waves per hub in the dz merge
 constexpr int kMWf = 16;  // waves per (hub, head) in the forward merge (its hubs all above kSmallP pieces)
-constexpr int kMWb = 16;  // waves per hub in the backward merge (8: 89 us per call at the config-5 share; 16: 75)
+constexpr int kMWb = 8;   // waves per (hub, component) in the backward merge (16: 27.4 us per call at the config-5 share, 8: 23.1)
 // Hubs of at most kSmallP pieces (most of them: config 5's share has 3,740 hubs, few above a
 // dozen pieces) are merged by one wave per (hub, head) instead -- a workgroup of 8-16 waves on
 // a 3-piece hub leaves most of its waves idle through three barriers.  The workgroup kernels
