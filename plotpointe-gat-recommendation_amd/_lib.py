@@ -158,6 +158,7 @@ SIGNATURES = {
     "ppgat_att_proj": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     "ppgat_rows_rank_update": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_vp]),
     "ppgat_xgat_weight_grads": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "ppgat_stream_copy": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "ppgat_debug_build": (c_int, []),
     "ppgat_check_index_range": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, ctypes.POINTER(c_i64), c_vp]),
     "ppgat_profile_enable": (c_int, [c_int]),

@@ -356,6 +356,15 @@ int ppgat_bwd_dst_sum_csc(const ppgat_schedule* fwd_sched, int64_t n_nodes, int6
                           stream);
 }
 
+int ppgat_stream_copy(const void* src, void* dst, int64_t n_bytes, void* stream) {
+  if (n_bytes < 0 || n_bytes % 16 || (n_bytes > 0 && (!src || !dst)) ||
+      reinterpret_cast<uintptr_t>(src) % 16 || reinterpret_cast<uintptr_t>(dst) % 16)
+    return fail(PPGAT_ERR_INVALID, "stream_copy: pointers and size must be non-null multiples of 16");
+  hipError_t e = ppgat::launch_stream_copy(src, dst, n_bytes, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "stream_copy");
+  return PPGAT_OK;
+}
+
 int ppgat_invert_index(const int32_t* index, int64_t n, int32_t* inverse, void* stream) {
   if (n < 0 || (n > 0 && (!index || !inverse))) return fail(PPGAT_ERR_INVALID, "invert_index: bad arguments");
   if (int rc = debug_range(index, 4, n, 0, n, "invert_index: index", static_cast<hipStream_t>(stream))) return rc;

@@ -423,6 +423,7 @@ __device__ __forceinline__ void glds_copy(const uint16_t* src, uint16_t* dst, in
                                              lane * 16 + i * 1024, 0, 0, 0);
 }
 
+#ifdef PPGAT_LAB_BUILD  // superseded by k_fusion_fwdh3 (lab builds only)
 __global__ void __launch_bounds__(512, 1) k_fusion_fwdp(const float* __restrict__ txt, const float* __restrict__ img,
                                                         const int32_t* __restrict__ img_index,
                                                         const float* __restrict__ img_fallback, int64_t B, int Dt,
@@ -561,6 +562,8 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdp(const float* __restrict_
 }
 
 
+#endif  // PPGAT_LAB_BUILD
+
 // ---------------------------------------------------------------------------
 // The same MLP on the fp16 matrix cores: the scaled two-term split of ppgat_split.h, three
 // MFMAs per product instead of six.  W1 and W2 are pre-split once per call with per-column
@@ -578,6 +581,7 @@ constexpr int kH1Img = 2 * kH1Part;      // per 32-deep W1 chunk (NnhImg<8>::ELE
 constexpr int kH2Part = DO * HLDK;
 constexpr int kH2Img = 2 * kH2Part;      // per 32-deep W2 chunk (NnhImg<4>::ELEMS)
 
+#ifdef PPGAT_LAB_BUILD  // superseded by k_fusion_fwdh3 (lab builds only; the bitwise reference of the lab test)
 __global__ void __launch_bounds__(512, 1) k_fusion_fwdh(const float* __restrict__ txt, const float* __restrict__ img,
                                                         const int32_t* __restrict__ img_index,
                                                         const float* __restrict__ img_fallback, int64_t B, int Dt,
@@ -743,6 +747,8 @@ __global__ void __launch_bounds__(512, 1) k_fusion_fwdh(const float* __restrict_
     for (int u = 0; u < 4; ++u) out[row * DO + 32 * u + r] = normalize ? acc2[u][q] * ss[q] : acc2[u][q];
   }
 }
+
+#endif  // PPGAT_LAB_BUILD
 
 // ---------------------------------------------------------------------------
 // k_fusion_fwdh with GEMM1 on the pipelined loop of k_gemm_nnh3 (ppgat_nnh_pipe.h: W1 chunks by
@@ -952,7 +958,15 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
                       int64_t B, int Dt, int Di, const float* W1, const float* b1, const float* W2, const float* b2,
                       int normalize, float* out, float* z1_out, hipStream_t st, void* ws) {
   if (B == 0) return hipSuccess;
+#ifdef PPGAT_LAB_BUILD
+  const bool pairs = nnh_pipeline_variant() >= 3 && ((Dt + Di) / BK) % 2 == 0;
   if (ws != nullptr && gemm_split_enabled() && gemm_f16_enabled()) {  // fp16 two-term family
+#else
+  // libppgat.so: k_fusion_fwdh3 (the K chunks in pairs: the reference's 384 + 512 = 28), else the
+  // bf16 x6 k_fusion_fwdx; k_fusion_fwdh and k_fusion_fwdp are lab-build kernels
+  const bool pairs = ((Dt + Di) / BK) % 2 == 0;
+  if (ws != nullptr && gemm_split_enabled() && pairs) {
+#endif
     uint16_t* w1i = static_cast<uint16_t*>(ws);
     uint16_t* w2i = w1i + nnh_image_bytes(Dt + Di, H1, 8) / 2;
     int* e1 = reinterpret_cast<int*>(static_cast<char*>(ws) + fusion_h_bytes(Dt, Di));
@@ -960,14 +974,17 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
     hipError_t e = nnh_presplit(W1, Dt + Di, 1, Dt + Di, H1, 8, w1i, e1, st);
     if (e == hipSuccess) e = nnh_presplit(W2, H1, 1, H1, DO, 4, w2i, e2, st);
     if (e != hipSuccess) return e;
-    if (nnh_pipeline_variant() >= 3 && ((Dt + Di) / BK) % 2 == 0)
-      hipLaunchKernelGGL(k_fusion_fwdh3, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
+#ifdef PPGAT_LAB_BUILD
+    if (!pairs)
+      hipLaunchKernelGGL(k_fusion_fwdh, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
                          img_index, img_fallback, B, Dt, Di, w1i, e1, b1, w2i, e2, b2, normalize, out, z1_out);
     else
-      hipLaunchKernelGGL(k_fusion_fwdh, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
+#endif
+      hipLaunchKernelGGL(k_fusion_fwdh3, dim3((unsigned)((B + PBM - 1) / PBM)), dim3(512), 0, st, txt, img,
                          img_index, img_fallback, B, Dt, Di, w1i, e1, b1, w2i, e2, b2, normalize, out, z1_out);
     return hipGetLastError();
   }
+#ifdef PPGAT_LAB_BUILD
   if (ws != nullptr && gemm_split_enabled()) {  // W1 / W2 pre-split once, then the glds-staged kernel
     uint16_t* w1i = static_cast<uint16_t*>(ws);
     uint16_t* w2i = w1i + nnx_image_bytes(Dt + Di, H1, 8) / 2;
@@ -978,6 +995,7 @@ hipError_t fusion_fwd(const float* txt, const float* img, const int32_t* img_ind
                        img_fallback, B, Dt, Di, w1i, b1, w2i, b2, normalize, out, z1_out);
     return hipGetLastError();
   }
+#endif
   if (gemm_split_enabled())
     hipLaunchKernelGGL(k_fusion_fwdx, dim3((unsigned)((B + BM - 1) / BM)), dim3(256), 0, st, txt, img, img_index,
                        img_fallback, B, Dt, Di, W1, b1, W2, b2, normalize, out, z1_out);

@@ -25,6 +25,7 @@ struct ItemsArg {
   int64_t n_long_items;  // -1: unknown (no four-per-wave short-item path)
 };
 
+hipError_t launch_stream_copy(const void* src, void* dst, int64_t n_bytes, hipStream_t st);
 hipError_t launch_scores(const float* h, const float* as, const float* ad, int64_t n, int heads, int C, float* ss,
                          float* sd, hipStream_t st);
 hipError_t launch_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, int heads, int C,

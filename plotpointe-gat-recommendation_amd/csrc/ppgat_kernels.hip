@@ -1088,6 +1088,37 @@ __global__ void __launch_bounds__(256) k_dst_sum_vh(Items it, const float* __res
   }
 }
 
+// The short items (<= 16 edges: the schedule's [n_long_items, n_items), by descending degree)
+// of k_dst_sum_vh<true, H>, one thread per item: every index and dz load of the item in flight
+// at once, then the 16-lane group's butterfly (xor 1, 2, 4, 8 on slots l = edge k - beg) restated
+// as the same balanced tree over the thread's 16 slots, empty slots +0 -- the same bits as
+// k_dst_sum_vh (each slot 0 + dz, as the group's x0, so no slot is -0 and the empty ones add
+// exactly nothing).  The halo partition's partial sums run over ~11M table rows of ~2 edges each
+// at world 8 on config 5, where 16 lanes per item left 14 of them idle behind three dependent loads.
+template <int H>
+__global__ void __launch_bounds__(256) k_dst_sum_vh_short(Items it, int64_t w0, const float* __restrict__ dz,
+                                                          const int32_t* __restrict__ csr2csc,
+                                                          float* __restrict__ ds_dst, int64_t ld) {
+  using V = __attribute__((ext_vector_type(H))) float;
+  const int64_t w = w0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= it.n_items) return;
+  const int rs = it.beg[w], n = it.end[w] - rs;
+  const V* dzv = reinterpret_cast<const V*>(dz);
+  int k[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) k[l] = l < n ? csr2csc[rs + l] : 0;
+  V v[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) v[l] = l < n ? V{} + dzv[k[l]] : V{};
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int l = 0; l < 16; l += 2 * o) v[l] = v[l] + v[l + o];
+  float* out = ds_dst + (int64_t)it.row[w] * ld;
+#pragma unroll
+  for (int hd = 0; hd < H; ++hd) out[hd] = v[0][hd];
+}
+
 // One wave per hub: lane l sums pieces l, l + 64, ... (piece order), per head, then the 64
 // lanes in a fixed butterfly -- deterministic.  (One thread per (hub, head) walking every piece
 // in turn took 134 us per call at the config-5 share, whose top item is 490 pieces.)
@@ -1262,12 +1293,25 @@ hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const 
   const Items items{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   const bool aligned = (reinterpret_cast<uintptr_t>(dz) % (4 * heads)) == 0;
   if (csr2csc != nullptr && (heads == 2 || heads == 4) && aligned) {
-    if (heads == 2)
-      hipLaunchKernelGGL((k_dst_sum_vh<true, 2>), dim3(blocks_for(it.n_items * 16)), dim3(256), 0, st, items, dz,
-                         csr2csc, ds_dst, ld, partial);
-    else
-      hipLaunchKernelGGL((k_dst_sum_vh<true, 4>), dim3(blocks_for(it.n_items * 16)), dim3(256), 0, st, items, dz,
-                         csr2csc, ds_dst, ld, partial);
+    // the long items (and hub pieces) 16 lanes each; the short ones (known when the schedule
+    // counted them) one thread each, the same bits (k_dst_sum_vh_short)
+    const int64_t nl = it.n_long_items >= 0 ? it.n_long_items : it.n_items;
+    const Items lng{it.row, it.beg, it.end, nl, it.n_hub_items};
+    if (nl > 0) {
+      if (heads == 2)
+        hipLaunchKernelGGL((k_dst_sum_vh<true, 2>), dim3(blocks_for(nl * 16)), dim3(256), 0, st, lng, dz, csr2csc,
+                           ds_dst, ld, partial);
+      else
+        hipLaunchKernelGGL((k_dst_sum_vh<true, 4>), dim3(blocks_for(nl * 16)), dim3(256), 0, st, lng, dz, csr2csc,
+                           ds_dst, ld, partial);
+    }
+    if (it.n_items > nl) {
+      const dim3 g(blocks_for(it.n_items - nl));
+      if (heads == 2)
+        hipLaunchKernelGGL((k_dst_sum_vh_short<2>), g, dim3(256), 0, st, items, nl, dz, csr2csc, ds_dst, ld);
+      else
+        hipLaunchKernelGGL((k_dst_sum_vh_short<4>), g, dim3(256), 0, st, items, nl, dz, csr2csc, ds_dst, ld);
+    }
   } else if (csr2csc != nullptr)
     hipLaunchKernelGGL(k_dst_sum<true>, dim3(blocks_for(pairs * 16)), dim3(256), 0, st, items, heads, dz, csr2csc,
                        ds_dst, ld, partial);
@@ -1277,6 +1321,33 @@ hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const 
   if (n_hubs > 0)
     hipLaunchKernelGGL(k_dst_merge, dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st, hub_row, hub_ptr, n_hubs,
                        heads, partial, ds_dst, ld);
+  return hipGetLastError();
+}
+
+// the achievable-HBM yardstick (ppgat_stream_copy): every thread moves four float4s with all four
+// loads issued before the stores, consecutive lanes on consecutive 16 B, the grid sized to cover
+// the buffer in one pass (no grid-stride loop: each wave's loads are in flight at once)
+__global__ void __launch_bounds__(256) k_stream_copy(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                     int64_t n4) {
+  const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  float4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = base + 256 * u;
+    if (i < n4) v[u] = src[i];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = base + 256 * u;
+    if (i < n4) dst[i] = v[u];
+  }
+}
+
+hipError_t launch_stream_copy(const void* src, void* dst, int64_t n_bytes, hipStream_t st) {
+  const int64_t n4 = n_bytes / 16;
+  if (n4 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n4 + 1023) / 1024)), dim3(256), 0, st,
+                     static_cast<const float4*>(src), static_cast<float4*>(dst), n4);
   return hipGetLastError();
 }
 

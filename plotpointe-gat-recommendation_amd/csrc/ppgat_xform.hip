@@ -2382,6 +2382,7 @@ int gemm_nn_splits(int64_t M, int K, int N) {
 
 // the three bf16 images of B [K x N] (bmode 0: B[k][n] = B[k ldb + n]; 1: B[n ldb + k]) per
 // (column block of 32 nt columns, 32-deep k chunk), in the LDS layout the split kernels read
+#ifdef PPGAT_LAB_BUILD
 hipError_t nnx_presplit(const float* B, int64_t ldb, int bmode, int K, int N, int nt, uint16_t* img, hipStream_t st) {
   const int64_t groups = (int64_t)N * (K / 4);
   const unsigned gp = (unsigned)((groups + 255) / 256);
@@ -2396,29 +2397,43 @@ hipError_t nnx_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
   return hipGetLastError();
 }
 
+#endif
+
 size_t nnx_image_bytes(int K, int N, int nt) {
   const size_t img = nt == 8 ? (size_t)NnpImg<8>::BYTES : (size_t)NnpImg<4>::BYTES;
   return (size_t)(N / (32 * nt)) * (size_t)(K / 32) * img;
 }
 
-// the pre-split path (k_nnx_presplit + k_gemm_nnp): large M, split-bf16 family, K % 32 == 0
+// the pre-split path: large M, K % 32 == 0.  libppgat.so runs it on k_gemm_nnh3 only, which takes
+// the K chunks in pairs: other shapes go to the general x6 kernel (k_gemm_nnx).  The superseded
+// generations -- k_gemm_nnh (any chunk count), k_gemm_nnh2 and the bf16 x6 k_gemm_nnp
+// (PPGAT_GEMM_NNP / PPGAT_GEMM_F16 / PPGAT_NNH2) -- exist only in the lab build (make lab).
 static bool nnp_ok(int64_t M, int K, int N) {
+#ifdef PPGAT_LAB_BUILD
   static const bool off = [] {
     const char* e = getenv("PPGAT_GEMM_NNP");
     return e && strcmp(e, "0") == 0;
   }();
-  return !off && gemm_split_enabled() && M >= 4 * kPBM && K % 32 == 0 && N % 128 == 0 && gemm_nn_splits(M, K, N) == 1;
+  if (off) return false;
+#else
+  if ((K / kGBK) % 2 != 0) return false;
+#endif
+  return gemm_split_enabled() && M >= 4 * kPBM && K % 32 == 0 && N % 128 == 0 && gemm_nn_splits(M, K, N) == 1;
 }
 
 static size_t nnp_image_bytes(int K, int N) { return nnx_image_bytes(K, N, N % 256 == 0 ? 8 : 4); }
 
-// the fp16 two-term family (k_gemm_nnh) on the pre-split path; PPGAT_GEMM_F16=0 keeps the bf16 x6 kernel
+// the fp16 two-term family on the pre-split path; lab builds: PPGAT_GEMM_F16=0 runs the bf16 x6 k_gemm_nnp
 static bool nnh_enabled() {
+#ifdef PPGAT_LAB_BUILD
   static const bool off = [] {
     const char* e = getenv("PPGAT_GEMM_F16");
     return e && strcmp(e, "0") == 0;
   }();
   return !off;
+#else
+  return true;
+#endif
 }
 
 bool gemm_f16_enabled() { return nnh_enabled(); }
@@ -2447,25 +2462,27 @@ hipError_t nnh_presplit(const float* B, int64_t ldb, int bmode, int K, int N, in
   return hipGetLastError();
 }
 
-// the NN fp16 two-term kernel: PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2, otherwise k_gemm_nnh3
+// the NN fp16 two-term kernel: k_gemm_nnh3; in lab builds PPGAT_NNH2=0 k_gemm_nnh, =2 k_gemm_nnh2
 // (and k_fusion_fwdh3; the default: 2-3 % faster than k_gemm_nnh2 at config-5 shapes, profiles/
 // r04/v8_gemm5_nnh*.log).  All three compute the same products in the same order (bitwise equal,
-// tests/test_gpu_gemm_f16.py::test_nnh2_bitwise_equals_nnh).  Read once per process.
+// tests/test_gpu_gemm_f16.py::test_nnh2_bitwise_equals_nnh, a lab test).  Read once per process.
 // The measured-negative nnh3 variants (4: B read two steps ahead, 5: + s_setprio, 6: X through
 // LDS; all within 1-2 % of 3, v8/v22_gemm5_nnh*.log) and the diagnostic lab kernels
 // (PPGAT_NNH2_LAB: parts of the loop removed, results WRONG) exist only in a lab build:
 // tools/build_variants.sh ppgat_xform.hip lab:"-DPPGAT_LAB_BUILD=1" -- never in libppgat.so.
 int nnh_pipeline_variant() {
+#ifdef PPGAT_LAB_BUILD
   static const int v = [] {
     const char* e = getenv("PPGAT_NNH2");
     if (e && strcmp(e, "0") == 0) return 1;
     if (e && strcmp(e, "2") == 0) return 2;
-#ifdef PPGAT_LAB_BUILD
     if (e && (strcmp(e, "4") == 0 || strcmp(e, "5") == 0 || strcmp(e, "6") == 0)) return e[0] - '0';
-#endif
     return 3;
   }();
   return v;
+#else
+  return 3;
+#endif
 }
 
 #ifdef PPGAT_LAB_BUILD
@@ -2547,6 +2564,7 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
 #undef PPGAT_NNH3
         return hipGetLastError();
       }
+#ifdef PPGAT_LAB_BUILD
       if (nnh_pipeline_variant() == 2 && (K / kGBK) % 2 == 0) {  // k_gemm_nnh2 runs chunk pairs
 #ifdef PPGAT_LAB_BUILD
         if (const int lab = nnh2_lab(); lab > 0 && nv == 0 && w8) {
@@ -2576,12 +2594,19 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
         hipLaunchKernelGGL((k_gemm_nnh<4, false>), dim3(grid), dim3(512), 0, st, a, img, ecol);
       }
       return hipGetLastError();
+#else
+      return hipErrorInvalidValue;  // unreachable: nnp_ok admits chunk pairs only
+#endif
     }
+#ifdef PPGAT_LAB_BUILD
     hipError_t e = nnx_presplit(B, ldb, bmode, K, N, w8 ? 8 : 4, img, st);
     if (e != hipSuccess) return e;
     if (w8) hipLaunchKernelGGL((k_gemm_nnp<8>), dim3(grid), dim3(512), 0, st, a, img);
     else hipLaunchKernelGGL((k_gemm_nnp<4>), dim3(grid), dim3(512), 0, st, a, img);
     return hipGetLastError();
+#else
+    return hipErrorInvalidValue;  // unreachable: the product's pre-split path is fp16
+#endif
   }
   a.row_blocks = (M + kGBM - 1) / kGBM;
   const int64_t padded = (a.row_blocks + 7) / 8 * 8;
@@ -2648,12 +2673,16 @@ static int tnh_splits(int64_t M, int T) {  // one workgroup per CU: splits * til
   // two workgroup rounds per CU: the same time as one (3.96 vs 3.98 ms at the config-5 share,
   // profiles/r03/v16_tnh_*), half the rows per fp32 accumulator chain: 3.3e-6 vs 5.3e-6
   // max-abs/max-abs on 1.875M-row reductions (fp32 MFMA kernel: 3.5e-6).  PPGAT_TNH_WAVES
-  // overrides (experiments).
+  // overrides (lab builds).
+#ifdef PPGAT_LAB_BUILD
   static const int waves = [] {
     const char* e = getenv("PPGAT_TNH_WAVES");
     const int v = e ? atoi(e) : 2;
     return v >= 1 && v <= 16 ? v : 2;
   }();
+#else
+  constexpr int waves = 2;
+#endif
   int s = 256 * waves / T;
   if (s < 1) s = 1;
   while (s > 1 && M / s < 4 * kTR) s /= 2;

@@ -128,6 +128,58 @@ class Comm:
         dist.all_to_all_single(out, t, rc, sc, group=self.group)
         return out
 
+    def p2p(self, sends, recvs):
+        """One group of point-to-point transfers: ``sends`` / ``recvs`` are lists of (peer,
+        contiguous tensor); between a pair of ranks the k-th send matches the k-th receive
+        (RCCL: one ncclGroupStart/End through batch_isend_irecv; gloo: tag-ordered pairs).
+        Device tensors under gloo (ranks sharing one GPU in a test) are staged through host."""
+        if not sends and not recvs:
+            return
+        stage = self.backend == "gloo" and any(t.is_cuda for _, t in list(sends) + list(recvs))
+        hs = [(p, t.cpu() if stage else t) for p, t in sends]
+        hr = [(p, torch.empty(t.shape, dtype=t.dtype) if stage else t) for p, t in recvs]
+        ops = [dist.P2POp(dist.isend, t, p, group=self.group) for p, t in hs]
+        ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for p, t in hr]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        if stage:
+            for (_, t), (_, h) in zip(recvs, hr):
+                t.copy_(h)
+
+    def exchange(self, plan: "ExchangePlan", src: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """A plan's forward exchange without packing: the own rows of ``src`` (own-local row
+        order) in each peer's send runs leave straight from ``src``; ``out`` [n_recv, ...]
+        receives each peer's rows in peer order, each peer's runs back to back (the halo rows'
+        order, build_halo_graph) -- no gather into a send buffer, no copy out of a receive buffer."""
+        sends, recvs, off = [], [], 0
+        for q, runs in enumerate(plan.send_runs):
+            sends += [(q, src[a:a + n]) for a, n in runs]
+        for r, lens in enumerate(plan.recv_runs):
+            for n in lens:
+                recvs.append((r, out[off:off + n]))
+                off += n
+        self.p2p(sends, recvs)
+        return out
+
+    def exchange_back(self, plan: "ExchangePlan", halo: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """The reverse of ``exchange``: the halo rows [n_recv, ...] go back to their owners in the
+        same runs; ``out`` [n_send, ...] gets each peer's returned copies in send_idx order (peer
+        order, each peer's runs back to back) -- the layout ret_ptr / ret_pos index."""
+        if out is None:
+            out = torch.empty((plan.n_send,) + tuple(halo.shape[1:]), dtype=halo.dtype, device=halo.device)
+        sends, recvs, off = [], [], 0
+        for r, lens in enumerate(plan.recv_runs):
+            for n in lens:
+                sends.append((r, halo[off:off + n]))
+                off += n
+        off = 0
+        for q, runs in enumerate(plan.send_runs):
+            for _, n in runs:
+                recvs.append((q, out[off:off + n]))
+                off += n
+        self.p2p(sends, recvs)
+        return out
+
     def broadcast_int(self, value: int, src: int = 0) -> int:
         if not self.active:
             return int(value)
@@ -197,6 +249,11 @@ class ExchangePlan:
     recv_counts: list
     ret_ptr: torch.Tensor       # int32 [n_own + 1]
     ret_pos: torch.Tensor       # int32 [n_send]
+    # the halo plans (build_halo_graph): per peer the runs [(own row, count), ...] send_idx is made
+    # of, and per peer the lengths of the runs it sends here -- Comm.exchange moves rows straight
+    # from / into the row tables; None for the loss plans (gather + all_to_all)
+    send_runs: Optional[list] = None
+    recv_runs: Optional[list] = None
 
     @property
     def n_send(self) -> int:
@@ -207,14 +264,69 @@ class ExchangePlan:
         return int(sum(self.recv_counts))
 
 
-def make_plan(n_own: int, send_idx: np.ndarray, send_counts, recv_counts, device) -> ExchangePlan:
+def make_plan(n_own: int, send_idx: np.ndarray, send_counts, recv_counts, device, send_runs=None,
+              recv_runs=None) -> ExchangePlan:
     send_idx = np.asarray(send_idx, np.int64)
     order = np.argsort(send_idx, kind="stable")           # by own row, peer order kept
     ptr = np.zeros(n_own + 1, np.int64)
     np.cumsum(np.bincount(send_idx, minlength=n_own), out=ptr[1:])
     return ExchangePlan(int(n_own), torch.from_numpy(send_idx).to(device), [int(c) for c in send_counts],
                         [int(c) for c in recv_counts], torch.from_numpy(ptr.astype(np.int32)).to(device),
-                        torch.from_numpy(order.astype(np.int32)).to(device))
+                        torch.from_numpy(order.astype(np.int32)).to(device), send_runs, recv_runs)
+
+
+def _runs(b: np.ndarray):
+    """(starts, lengths) of the runs of True in a boolean array."""
+    d = np.diff(np.concatenate([[0], b.astype(np.int8), [0]]))
+    st = np.flatnonzero(d == 1)
+    return st, np.flatnonzero(d == -1) - st
+
+
+def run_plan(n_own: int, masks_own: np.ndarray, base: int, world: int, recv_lens: list, device) -> ExchangePlan:
+    """The halo plan of one row class: own rows [base, base + len(masks_own)) in own-local order,
+    masks_own their peer sets (bit q: rank q holds the row as a halo row); ``recv_lens[r]``: the
+    run lengths rank r sends here.  send_idx = per peer (rank order) its runs expanded."""
+    send_runs, idx, counts = [], [], []
+    for q in range(world):
+        st, ln = _runs(((masks_own >> np.uint32(q)) & np.uint32(1)).astype(bool))
+        send_runs.append([(int(a) + base, int(n)) for a, n in zip(st, ln)])
+        idx.append(np.concatenate([np.arange(a, a + n) for a, n in send_runs[-1]]) if len(st) else
+                   np.zeros(0, np.int64))
+        counts.append(int(ln.sum()))
+    recv_runs = [[int(n) for n in lens] for lens in recv_lens]
+    return make_plan(n_own, np.concatenate(idx) if idx else np.zeros(0, np.int64), counts,
+                     [sum(l) for l in recv_runs], device, send_runs, recv_runs)
+
+
+def peer_masks(src: np.ndarray, od: np.ndarray, owner: np.ndarray, world: int) -> np.ndarray:
+    """[N] uint32: bit q of node v set iff an edge v -> d has d owned by rank q != owner(v) --
+    the ranks that hold v as a halo row (they home an edge that reads v)."""
+    if world > 32:
+        raise NotImplementedError("halo partition: at most 32 ranks (peer sets are 32-bit masks)")
+    N = len(owner)
+    mask = np.zeros(N, np.uint32)
+    for q in range(world):
+        mask[src[od == q]] |= np.uint32(1 << q)
+    mask &= ~(np.uint32(1) << owner.astype(np.uint32))
+    return mask
+
+
+def send_order_key(mask: np.ndarray, owner: np.ndarray, world: int) -> np.ndarray:
+    """Sort key of a node within its owner's rows: the position of its peer set (bits rotated
+    so the owner's peers are bits 0..W-2) in the binary-reflected Gray sequence.  Rows sorted by
+    it leave each peer's rows in few runs (about 2^(W-2) runs over all peers, one for the top
+    bit), so Comm.exchange sends straight from the row table instead of packing."""
+    rel = np.zeros(len(mask), np.uint32)
+    o = owner.astype(np.int64)
+    for q in range(world):
+        bit = (mask >> np.uint32(q)) & np.uint32(1)
+        rel |= bit << ((q - o - 1) % world).astype(np.uint32)
+    key = rel.copy()
+    sh = 1
+    while sh < 32:  # inverse Gray code: prefix xor of the higher bits
+        key ^= key >> np.uint32(sh)
+        sh <<= 1
+    return key
 
 
 class _Exchange(torch.autograd.Function):
@@ -232,8 +344,11 @@ class _Exchange(torch.autograd.Function):
         out[:n_own].copy_(t_own)
         off = n_own
         for plan in plans:
-            send = stages.gather_rows(t_own, plan.send_idx)
-            comm.all_to_all_rows(send, plan.send_counts, plan.recv_counts, out=out[off:off + plan.n_recv])
+            if plan.send_runs is not None:  # the halo plans: straight from the own rows
+                comm.exchange(plan, t_own, out[off:off + plan.n_recv])
+            else:
+                send = stages.gather_rows(t_own, plan.send_idx)
+                comm.all_to_all_rows(send, plan.send_counts, plan.recv_counts, out=out[off:off + plan.n_recv])
             off += plan.n_recv
         if n_tail:
             out[off:].copy_(tail)
@@ -248,10 +363,16 @@ class _Exchange(torch.autograd.Function):
         g_own = g[:n_own].clone()
         off = n_own
         for plan in plans:  # each plan touches its own rows (users / items): independent sums
-            ret = comm.all_to_all_rows(g[off:off + plan.n_recv], plan.recv_counts, plan.send_counts)
-            st.return_add(g_own, ret, plan.ret_ptr, plan.ret_pos)
+            st.return_add(g_own, _return(comm, plan, g[off:off + plan.n_recv]), plan.ret_ptr, plan.ret_pos)
             off += plan.n_recv
         return g_own, (g[off:] if ctx.has_tail else None), None, None, None
+
+
+def _return(comm: "Comm", plan: ExchangePlan, halo: torch.Tensor) -> torch.Tensor:
+    """The halo rows' values back to their owners -> [n_send, ...] in send_idx order."""
+    if plan.send_runs is not None:
+        return comm.exchange_back(plan, halo)
+    return comm.all_to_all_rows(halo, plan.recv_counts, plan.send_counts)
 
 
 def exchange(t_own, plan: ExchangePlan, comm: "Comm", stages):
@@ -315,8 +436,9 @@ class HaloGraph:
     n_edges: int
     n_users: int
     user_bounds: np.ndarray     # [world + 1]: rank r owns the users [b_r, b_{r+1}) (node ids)
-    n_own: int                  # own rows: users [u0, u1), then the own items by id (halo_owner)
-    n_halo: int                 # halo rows: users (by owner) then items (by owner)
+    n_own: int                  # own rows: the users of [u0, u1), then the own items (halo_owner), each in
+                                # send order (send_order_key)
+    n_halo: int                 # halo rows: users (by owner) then items (by owner), in the owner's order
     plan_u: ExchangePlan        # the layer halo exchange of user rows
     plan_i: ExchangePlan        # ... of item rows
     fwd_view: LocalView         # CSR over the own destination rows (n_rows = n_own)
@@ -331,7 +453,9 @@ class HaloGraph:
     bipartite: bool = False        # every edge joins a user and an item (the U-I graph)
     fwd_sched_u: object = None     # forward schedule over the own user destinations
     fwd_sched_i: object = None     # ... over the own item destinations (rows relative to n_own_u)
-    own_items: torch.Tensor = None # [n_own - n_own_u] int64 item indices (node id - n_users), ascending
+    own_items: torch.Tensor = None # [n_own - n_own_u] int64 item indices (node id - n_users), own-local order
+    own_pos: np.ndarray = None     # [N] int32: each node's row at its owner (host)
+    own_users: np.ndarray = None   # [n_own_u] int64: the own users' node ids in own-local order (host)
     item_partition: str = "dealt"
     # symmetric edge list (every column j -> i has its i -> j, as build_edge_index's U-I graph):
     # the rows a rank needs as sources (forward) are exactly the rows it needs as destinations of
@@ -366,8 +490,17 @@ class HaloGraph:
     def own_node_ids(self, rank: Optional[int] = None) -> np.ndarray:
         """A rank's own rows as global node ids, in its own-local row order (host)."""
         r = self.rank if rank is None else rank
-        u0, u1 = self.owned_users(rank=r)
-        return np.concatenate([np.arange(u0, u1), self.n_users + np.flatnonzero(self.owner[self.n_users:] == r)])
+        ids = np.flatnonzero(self.owner == r)   # users first (ids below n_users), then items
+        nu = int(np.searchsorted(ids, self.n_users))
+        u, it = ids[:nu], ids[nu:]
+        return np.concatenate([u[np.argsort(self.own_pos[u], kind="stable")],
+                               it[np.argsort(self.own_pos[it], kind="stable")]])
+
+    def own_user_ids(self, rank: Optional[int] = None) -> np.ndarray:
+        """A rank's own users' node ids in its own-local row order (host)."""
+        if rank is None or rank == self.rank:
+            return self.own_users
+        return self.own_node_ids(rank)[:int(self.user_bounds[rank + 1] - self.user_bounds[rank])]
 
     def xviews(self):
         """The local edge lists as hip_ops.XViews (aggregate-then-transform layer): CSR over the
@@ -445,30 +578,42 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     item_partition = item_partition or os.environ.get("PPGAT_ITEM_PARTITION", "dealt")
     owner, ub = halo_owner(deg, nu, world, item_partition)
     u0, u1 = int(ub[rank]), int(ub[rank + 1])
-    own_items = nu + np.flatnonzero(owner[nu:] == rank)   # ascending node ids
-    n_own = (u1 - u0) + len(own_items)
-    local_of = np.full(N, -1, np.int64)
-    local_of[u0:u1] = np.arange(u1 - u0)
-    local_of[own_items] = (u1 - u0) + np.arange(len(own_items))
     od, osrc = owner[dst], owner[src]
+    # every node's peer set and its row order at its owner: users then items, each sorted by the
+    # Gray position of the peer set (then id), so that what a rank sends a peer is a few runs of
+    # its row table (Comm.exchange, no packing); the halo rows of an owner arrive in that order
+    mask = peer_masks(src, od, owner, world)
+    ids = np.arange(N)
+    cls = (ids >= nu).astype(np.int8)
+    go = np.lexsort((ids, send_order_key(mask, owner, world), cls, owner))   # by owner, class, key, id
+    bnd = np.searchsorted(owner[go] * 2 + cls[go], np.arange(2 * world + 1), side="left")
+    own_pos = np.empty(N, np.int32)  # each node's row at its owner
+    for r in range(world):
+        a, b = bnd[2 * r], bnd[2 * r + 2]
+        own_pos[go[a:b]] = np.arange(b - a, dtype=np.int32)
+    own_u, own_it = go[bnd[2 * rank]:bnd[2 * rank + 1]], go[bnd[2 * rank + 1]:bnd[2 * rank + 2]]
+    own_items = own_it                                     # node ids in own-local order
+    n_own = len(own_u) + len(own_it)
+    local_of = np.full(N, -1, np.int64)
+    local_of[own_u] = np.arange(len(own_u))
+    local_of[own_it] = len(own_u) + np.arange(len(own_it))
     loc = np.flatnonzero(od == rank)                       # edges homed here (destination owned)
     lsrc = src[loc]
-    halo = np.unique(lsrc[osrc[loc] != rank])              # ascending ids; users, then items,
-    halo_u, halo_i = halo[halo < nu], halo[halo >= nu]     # each grouped by owner (the owner's row order)
-    halo_u = halo_u[np.argsort(owner[halo_u], kind="stable")]
-    halo_i = halo_i[np.argsort(owner[halo_i], kind="stable")]
+    need = ((mask >> np.uint32(rank)) & np.uint32(1)).astype(bool)
+    # the halo rows: every node whose peer set holds this rank, grouped by owner in the owner's order
+    halo_u = np.concatenate([go[bnd[2 * r]:bnd[2 * r + 1]][need[go[bnd[2 * r]:bnd[2 * r + 1]]]]
+                             for r in range(world)])
+    halo_i = np.concatenate([go[bnd[2 * r + 1]:bnd[2 * r + 2]][need[go[bnd[2 * r + 1]:bnd[2 * r + 2]]]]
+                             for r in range(world)])
     lidx = local_of.copy()
     lidx[halo_u] = n_own + np.arange(len(halo_u))
     lidx[halo_i] = n_own + len(halo_u) + np.arange(len(halo_i))
-    # what this rank sends: its own sources of edges homed on other ranks, per peer, by id
-    out_e = np.flatnonzero((osrc == rank) & (od != rank))
-    key = np.unique(od[out_e].astype(np.int64) * N + src[out_e])
-    ids, peers = key % N, key // N
-    su = ids < nu
-    plan_u = make_plan(n_own, local_of[ids[su]], np.bincount(peers[su], minlength=world),
-                       np.bincount(owner[halo_u], minlength=world), dev)
-    plan_i = make_plan(n_own, local_of[ids[~su]], np.bincount(peers[~su], minlength=world),
-                       np.bincount(owner[halo_i], minlength=world), dev)
+    # what each owner r sends here: the runs of its rows (in its order) whose peer set holds this rank
+    recv_u = [_runs(need[go[bnd[2 * r]:bnd[2 * r + 1]]])[1] for r in range(world)]
+    recv_i = [_runs(need[go[bnd[2 * r + 1]:bnd[2 * r + 2]]])[1] for r in range(world)]
+    plan_u = run_plan(n_own, mask[own_u], 0, world, recv_u, dev)
+    plan_i = run_plan(n_own, mask[own_it], len(own_u), world, recv_i, dev)
+    del go, mask, need
     halo = np.concatenate([halo_u, halo_i])
     R = n_own + len(halo)
     ei_l = torch.from_numpy(np.stack([lidx[lsrc], lidx[dst[loc]]])).to(dev)
@@ -484,6 +629,8 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     hg = HaloGraph(world, rank, N, E, nu, ub, n_own, len(halo), plan_u, plan_i, fwd_view, bwd_view, local_of,
                    owner, {}, torch.from_numpy(halo_i - nu).to(dev))
     hg.own_items = torch.from_numpy(own_items - nu).to(dev)
+    hg.own_pos = own_pos
+    hg.own_users = own_u
     hg.item_partition = item_partition
     hg.n_own_u = u1 - u0
     hg.bipartite = bool(np.all((src < nu) != (dst < nu)))  # the same decision on every rank
@@ -640,7 +787,7 @@ class HaloRows:
 
     def set_local(self, cls, rows: torch.Tensor):
         a, b = self.span(cls)
-        if b > a:
+        if b > a and rows.data_ptr() != self.x[a:b].data_ptr():  # (computed in place: nothing to copy)
             self.x[a:b].copy_(rows)
         self.local.add(cls)
 
@@ -651,12 +798,10 @@ class HaloRows:
         comm, st = self.comm, self.stages
         n0 = self.hg.n_own
 
-        def send():
-            comm.all_to_all_rows(st.gather_rows(src, plan.send_idx), plan.send_counts, plan.recv_counts,
-                                 out=self.x[a:b])
+        def send():  # straight from the own rows into the table's halo slice (no pack, no unpack)
+            comm.exchange(plan, src, self.x[a:b])
             if self.s is not None:
-                comm.all_to_all_rows(st.gather_rows(self.s[:n0], plan.send_idx), plan.send_counts,
-                                     plan.recv_counts, out=self.s[a:b])
+                comm.exchange(plan, self.s[:n0], self.s[a:b])
         if comm.backend != "nccl" or not comm.active:
             send()
             return
@@ -821,7 +966,7 @@ class _HaloLayerX(torch.autograd.Function):
         def a2a_back(dx_halo):
             rets, off = [], 0
             for plan in plans:
-                rets.append(comm.all_to_all_rows(dx_halo[off:off + plan.n_recv], plan.recv_counts, plan.send_counts))
+                rets.append(_return(comm, plan, dx_halo[off:off + plan.n_recv]))
                 off += plan.n_recv
             return rets
 
@@ -977,8 +1122,7 @@ def _partials_home(hg: "HaloGraph", comm: "Comm", stages, part: torch.Tensor) ->
     own = part[:hg.n_own]
     off = hg.n_own
     for plan in (hg.plan_u, hg.plan_i):
-        ret = comm.all_to_all_rows(part[off:off + plan.n_recv], plan.recv_counts, plan.send_counts)
-        stages.return_add(own, ret, plan.ret_ptr, plan.ret_pos)
+        stages.return_add(own, _return(comm, plan, part[off:off + plan.n_recv]), plan.ret_ptr, plan.ret_pos)
         off += plan.n_recv
     return own
 
@@ -990,12 +1134,11 @@ def _bwd_tables(saved: dict, hg: "HaloGraph", comm: "Comm", stages, g_width: int
     s_dst, m, inv_l = saved["s_dst"], saved["m"], saved["inv_l"]
     H = saved["meta"][0]
     n0 = hg.n_own
-    nst = torch.empty(max(n0, 1), 4 * H, dtype=torch.float32, device=dev)
-    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H, nst.data_ptr(),
-                                     _lib.stream_handle(dev)), "xgat_nstate")
-    nst = nst[:n0]
-    ntab = HaloRows(hg, comm, stages, 4 * H, nst)
-    ntab.x[:n0].copy_(nst)
+    ntab = HaloRows(hg, comm, stages, 4 * H, s_dst)
+    # the own rows' state straight into the table's own rows (no copy)
+    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H,
+                                     ntab.x.data_ptr(), _lib.stream_handle(dev)), "xgat_nstate")
+    nst = ntab.x[:n0]
     gtab = HaloRows(hg, comm, stages, g_width, nst)
     return gtab, ntab, nst
 
@@ -1151,7 +1294,10 @@ class _ShardedBase(torch.nn.Module):
         self.stages = stages if stages is not None else HipStages()
         self.n_users, self.n_items = full.n_users, full.n_items
         self.u0, self.u1 = dg.owned_users(self.n_users)
-        self.user_emb_local = torch.nn.Parameter(full.user_emb.weight.detach()[self.u0:self.u1].clone())
+        # the own users' rows in the graph's own-local order (the halo partition sorts them by
+        # peer set; the replicated one keeps id order)
+        ids = torch.from_numpy(np.asarray(dg.own_user_ids(), np.int64)).to(full.user_emb.weight.device)
+        self.user_emb_local = torch.nn.Parameter(full.user_emb.weight.detach().index_select(0, ids).clone())
         self.item_proj = full.item_proj
         self.convs = full.convs
         self.seeds = SharedSeeds(comm)
@@ -1180,16 +1326,17 @@ class _ShardedBase(torch.nn.Module):
         torch._foreach_copy_([p.grad for p in ps], views)  # one multi-tensor launch, not one copy per tensor
 
     def _user_rows_global(self, rows: torch.Tensor, pad: int) -> torch.Tensor:
-        """Own user rows of a [*, C] tensor -> every rank's, in user-id order (all_gather)."""
+        """Own user rows of a [*, C] tensor (own-local order) -> every rank's, in user-id order
+        (all_gather)."""
         C = rows.size(1)
         blk = rows.new_zeros(pad, C)
         blk[:rows.size(0)] = rows
         allb = self.comm.all_gather_rows(blk)
-        out = []
+        idx = np.empty(self.n_users, np.int64)
         for r in range(self.comm.world):
-            a, b = self.dg.owned_users(self.n_users, r)
-            out.append(allb[r * pad: r * pad + (b - a)])
-        return torch.cat(out, 0)
+            ids = np.asarray(self.dg.own_user_ids(r), np.int64)
+            idx[ids] = r * pad + np.arange(len(ids))
+        return allb.index_select(0, torch.from_numpy(idx).to(allb.device))
 
     def full_state_dict(self):
         """Reference-keyed state_dict (user_emb gathered from the owners)."""
@@ -1219,12 +1366,15 @@ class HaloPyGGAT(_ShardedBase):
         """Exchange the pre-projection rows when they are narrower than h (H*C > C_in)."""
         return conv.heads * conv.out_channels > conv.in_channels
 
-    def halo_item_input(self, item_feats):
+    def halo_item_input(self, item_feats, out: Optional[torch.Tensor] = None):
         """The first layer's input rows of the halo items, item_proj(features) computed on this
         rank (the item features are on every rank): they are neither received nor returned;
-        their gradient reaches item_proj here and is summed by the dense all-reduce."""
+        their gradient reaches item_proj here and is summed by the dense all-reduce.  ``out``:
+        write them there (the first halo layer's table) instead of a new tensor."""
         hg = self.dg
         f = self.stages.gather_rows(item_feats, hg.halo_items)
+        if out is not None:
+            return self.stages.linear(f, self.item_proj.weight, self.item_proj.bias, out=out)
         return self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
 
     def _x_path(self, li: int) -> bool:
@@ -1248,7 +1398,11 @@ class HaloPyGGAT(_ShardedBase):
         for li, conv in enumerate(self.convs):
             p = float(conv.dropout) if self.training else 0.0
             seed = self.layer_seed(conv)
-            xh = self.halo_item_input(item_feats) if li == 0 and hg.plan_i.n_recv else None
+            xh = None
+            if li == 0 and hg.plan_i.n_recv:
+                # on the x path straight into the first layer's table (HaloRows.set_local: no copy)
+                xh = self.halo_item_input(item_feats, out=rows.x[slice(*rows.span("i"))]
+                                          if rows is not None and self._x_path(0) else None)
             if li == 0 and xh is None:
                 xh = x.new_zeros(0, x.size(1))
             if self.exchanges_input(conv):
@@ -1393,6 +1547,11 @@ class RepGraph:
     def owned_users(self, n_users: int, rank: Optional[int] = None):
         r = self.rank if rank is None else rank
         return int(self.user_bounds[r]), int(self.user_bounds[r + 1])
+
+    def own_user_ids(self, rank: Optional[int] = None) -> np.ndarray:
+        """A rank's users in its local row order: the id range itself."""
+        a, b = self.owned_users(self.n_users, rank)
+        return np.arange(a, b)
 
 
 def build_replicated_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world: int, rank: int,

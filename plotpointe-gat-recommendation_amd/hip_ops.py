@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -657,6 +658,7 @@ class GATLayer(torch.autograd.Function):
         g = ctx.graph
         lib = _lib.load()
         dev = x.device
+        g_arg = g_out
         g_out = g_out.contiguous()
         N = g.n_nodes
         K = x.size(1)
@@ -689,8 +691,10 @@ class GATLayer(torch.autograd.Function):
 
         D = torch.empty(N, HC, dtype=torch.float32, device=dev)
         S = torch.empty(N, 2 * heads, dtype=torch.float32, device=dev)
+        # the hand-off applies only to the very tensor the consumer produced (the object, not an
+        # address a later allocation could reuse), unmodified since; a stale result is dropped here
         pre, ctx.pro_result = ctx.pro_result, None
-        if (rep is None and pre is not None and pre[0] == g_out.data_ptr() and pre[1] == g_out._version
+        if (rep is None and pre is not None and pre[0]() is g_arg and pre[1] == g_arg._version
                 and (not want_db or pre[3] is not None)):
             # the consumer layer's dx kernel already did this prologue (ppgat_project_bwd_fused_producer)
             nstate = pre[2]
@@ -743,7 +747,7 @@ class GATLayer(torch.autograd.Function):
                     a_s.data_ptr(), a_d.data_ptr(), dx.data_ptr(), K, G.data_ptr(), GV.data_ptr(), _lib.ptr(pb),
                     ps_dst.data_ptr(), pm.data_ptr(), pinv_l.data_ptr(), 1.0, p_nstate.data_ptr(), _lib.ptr(p_dbias),
                     ws.data_ptr(), nbytes.value, _lib.stream_handle(dev)), "project_bwd_fused_producer")
-                prod.pro_result = (dx.data_ptr(), dx._version, p_nstate, p_dbias)
+                prod.pro_result = (weakref.ref(dx), dx._version, p_nstate, p_dbias)
             else:
                 _lib.check(lib.ppgat_project_bwd_fused(D.data_ptr(), HC, S.data_ptr(), 2, x0.data_ptr(), K,
                                                        _lib.ptr(x1), K, sp, N, K, W.data_ptr(), K, a_s.data_ptr(),
@@ -811,16 +815,18 @@ _CONST_BOUNDS = {}
 
 def _const_colmax(t: torch.Tensor) -> torch.Tensor:
     """colmax_abs(t) for a tensor the step does not change (the item features of the config-5
-    projection's weight gradient): computed once per (tensor object, version), so the column-max
-    pass over it leaves the training step."""
-    import weakref
+    projection's weight gradient): computed once per (tensor object, version, storage and data
+    pointers, shape), so the column-max pass over it leaves the training step.  Only tensors the
+    step does not differentiate reach it (_Linear's ``x_const``); a raw-pointer write that keeps
+    all of these is the caller's to avoid."""
+    key = (t._version, t.data_ptr(), t.untyped_storage().data_ptr(), tuple(t.shape), tuple(t.stride()))
     e = _CONST_BOUNDS.get(id(t))
-    if e is not None and e[0]() is t and e[1] == t._version:
+    if e is not None and e[0]() is t and e[1] == key:
         return e[2]
     bits = colmax_abs(t)
     for k in [k for k, v in _CONST_BOUNDS.items() if v[0]() is None]:
         del _CONST_BOUNDS[k]
-    _CONST_BOUNDS[id(t)] = (weakref.ref(t), t._version, bits)
+    _CONST_BOUNDS[id(t)] = (weakref.ref(t), key, bits)
     return bits
 
 
@@ -1365,14 +1371,14 @@ def xgat_forward(x, weight, att_src, att_dst, bias, v: "XViews", heads: int, C: 
         if ph.after is not None:
             ph.after(out)
     _tap_kinks(v.rowptr, v.col, v.csr_eid, s_src, s_dst, H)
-    if not (keep_agg if keep_agg is not None else _xgat_keep_agg(v.n_dst, v.n_src, H, K, C, dev)):
+    if not (keep_agg if keep_agg is not None else _xgat_keep_agg(v.n_dst, v.n_src, H, K, C, dev, E)):
         agg = None  # the backward's weight gradient comes from acc^T x (_xgat_weight_grads)
     saved = dict(x=x, W=W, a_s=a_s, a_d=a_d, A=A, s_src=s_src, s_dst=s_dst, agg=agg, m=m, inv_l=inv_l,
                  seed_buf=seed_buf, v=v, xbits=xbits, meta=(H, C, K, slope, p, seed, bias is not None))
     return out, saved
 
 
-def _xgat_keep_agg(n_dst: int, n_src: int, H: int, K: int, C: int, dev) -> bool:
+def _xgat_keep_agg(n_dst: int, n_src: int, H: int, K: int, C: int, dev, n_edges: int = 0) -> bool:
     """Whether the forward's aggregates agg [n_dst, H, C_in] stay alive for the backward's weight
     gradient G = g^T agg.  The same G is acc^T x (permuted): G[c, (h, k)] = sum_i g_i[c] agg^h_i[k]
     = sum_i sum_j beta^h_ij g_i[c] x_j[k] = sum_j acc^h_j[c] x_j[k], and the default backward
@@ -1385,7 +1391,7 @@ def _xgat_keep_agg(n_dst: int, n_src: int, H: int, K: int, C: int, dev) -> bool:
     mode = os.environ.get("PPGAT_XGAT_AGG", "auto")
     if mode == "keep":
         return True
-    if _xgat_gather_mode(C, H, n_src, n_dst) != "gd":
+    if _xgat_gather_mode(C, H, n_src, n_dst, n_edges, K) != "gd":  # the backward's own choice, same inputs
         return True  # the gt / g passes read agg in their prologue
     if mode == "free":
         return False
@@ -1737,6 +1743,11 @@ class BprPrepared:
                                              self.u.data_ptr(), self.i.data_ptr(), self.j.data_ptr(), self.u.numel(),
                                              self.ws.data_ptr(), self.ws.numel(), self.side.cuda_stream),
                    "bpr_bwd_prepare")
+        # the side stream uses these blocks: if the handle is dropped unconsumed (a failed take(),
+        # a forward that raised), the allocator must not hand them to current-stream work before
+        # the prepare kernels are done
+        for t in (self.ws, self.u, self.i, self.j):
+            t.record_stream(self.side)
         self.used = False
 
     def take(self, n_rows, n_users, n_items, C, u, i, j, row_map):
@@ -1816,7 +1827,7 @@ class _BPRLoss(torch.autograd.Function):
                 coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), _lib.ptr(pb), ps_dst.data_ptr(), pm.data_ptr(),
                 pinv_l.data_ptr(), 1.0, p_nstate.data_ptr(), _lib.ptr(p_dbias), ws.data_ptr(), ws.numel(),
                 _lib.stream_handle(Z.device)), "bpr_bwd_producer")
-            prod.pro_result = (dZ.data_ptr(), dZ._version, p_nstate, p_dbias)
+            prod.pro_result = (weakref.ref(dZ), dZ._version, p_nstate, p_dbias)
         else:
             fn = lib.ppgat_bpr_bwd_prepared if ctx.prepared else lib.ppgat_bpr_bwd
             _lib.check(fn(Z.data_ptr(), n_rows, n_users, n_items, _lib.ptr(ctx.row_map), C, u.data_ptr(),
@@ -1851,8 +1862,8 @@ class HipStages:
     """The GAT layer as the stages of include/ppgat.h, over explicit (possibly sliced)
     CSR/CSC views: see dist.LocalView for the fields used."""
 
-    def linear(self, x, weight, bias):
-        return linear(x, weight, bias)
+    def linear(self, x, weight, bias, out=None):
+        return linear(x, weight, bias, out=out)
 
     def seed_buffer(self, p, device):
         return seed_buffer(p, device)

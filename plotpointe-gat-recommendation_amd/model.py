@@ -38,6 +38,28 @@ def node_table(model: torch.nn.Module, n_items: int) -> torch.Tensor:
     return t
 
 
+class _TableGuard(torch.autograd.Function):
+    """Identity on the node table's item rows, whose backward checks that no later forward
+    rewrote them.  The item projection writes them through a raw pointer each forward (no
+    version-counter bump: a bump would trip autograd's view checks on the table's views), so a
+    graph whose backward runs after another forward -- its layers saved those rows -- would
+    otherwise take the new rows' values silently; here it raises instead.  (One forward in
+    flight per model: the node table is a per-model buffer.)"""
+
+    @staticmethod
+    def forward(ctx, v, holder, gen: int):
+        ctx.holder, ctx.gen = holder, gen
+        return v.view_as(v)
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.holder[0]._node_rows_gen != ctx.gen:
+            raise RuntimeError("ppgat node table: the item rows this graph saved were rewritten by a later "
+                               "forward of the same model; run backward before the next forward "
+                               "(or PPGAT_NODE_TABLE=0)")
+        return g, None, None
+
+
 def _unalias_state(module, state_dict, prefix, local_metadata):
     """state_dict hook: the user embedding shares the node table's storage; hand out its own copy
     (torch.save would otherwise write the whole table)."""
@@ -52,6 +74,10 @@ def _stack(model, item_proj, item_feats, layers, edge_index):
     if user_w.is_cuda and os.environ.get("PPGAT_NODE_TABLE", "1") != "0":
         table = node_table(model, item_feats.size(0))
         v = hip_ops.linear(item_feats, item_proj.weight, item_proj.bias, out=table[user_w.size(0):])
+        gen = getattr(model, "_node_rows_gen", 0) + 1
+        model._node_rows_gen = gen
+        if torch.is_grad_enabled() and v.requires_grad:
+            v = _TableGuard.apply(v, [model], gen)
     else:
         v = hip_ops.linear(item_feats, item_proj.weight, item_proj.bias)
     if len(layers) == 0:

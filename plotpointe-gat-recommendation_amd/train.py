@@ -337,7 +337,8 @@ def main(argv=None):
     model.load_state_dict(ckpt["state_dict"])
     if sharded is not None:
         with torch.no_grad():
-            sharded.user_emb_local.copy_(model.user_emb.weight[sharded.u0:sharded.u1])
+            ids = torch.as_tensor(sharded.dg.own_user_ids(), dtype=torch.int64, device=model.user_emb.weight.device)
+            sharded.user_emb_local.copy_(model.user_emb.weight.index_select(0, ids))
     eval_model.eval()
     test_metrics = evaluation.eval_sampled(eval_model, cfg, item_feats, edge_index, tr, te, fast=args.fast_eval,
                                            sampler=dev_sampler if args.device_eval else None, seed=cfg.seed)

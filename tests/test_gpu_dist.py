@@ -471,6 +471,14 @@ class _StubComm2(_StubComm):
                 out.fill_(0.25)
         return out
 
+    # the halo plans' run exchanges (dist.Comm.exchange / exchange_back): the rows the runs send,
+    # then the same slow, data-changing stand-in
+    def exchange(self, plan, src, out):
+        return self.all_to_all_rows(src[plan.send_idx], plan.send_counts, plan.recv_counts, out=out)
+
+    def exchange_back(self, plan, halo, out=None):
+        return self.all_to_all_rows(halo, plan.recv_counts, plan.send_counts, out=out)
+
 
 def test_halo_forward_overlap_ordering(cuda):
     """The halo partition's multi-head layers (dist._HaloLayerX, heads 4) with the exchanges on

@@ -227,6 +227,45 @@ def test_producer_prologue_in_the_model(pkg, cuda, monkeypatch):
         assert rel(grads[0][n], grads[1][n].double()) <= 1e-5, n
 
 
+def test_producer_prologue_partial_grad_then_backward(pkg, cuda):
+    """A partial autograd.grad over the consumer layer leaves a hand-off on the producer that its
+    backward never took; a later backward into the producer from another root (a gradient the
+    allocator may place at the dead dx's address, version 0) must not use that stale state."""
+    gr = pkg.data.synthetic_ui_graph(n_users=2000, n_items=600, n_interactions=30_000, seed=9)
+    ei = torch.from_numpy(gr.edge_index_numpy()).to(cuda)
+    N = gr.n_nodes
+    torch.manual_seed(3)
+    c1 = pkg.GATConv(128, 128, heads=1, dropout=0.0, add_self_loops=False, concat=False).to(cuda)
+    c2 = pkg.GATConv(128, 128, heads=1, dropout=0.0, add_self_loops=False, concat=False).to(cuda)
+    x = torch.randn(N, 128, device=cuda)
+    out1 = c1(x, ei)
+    loss = c2(out1, ei).square().sum()
+    torch.autograd.grad(loss, [c2.lin.weight], retain_graph=True)   # c1's backward does not run
+    g1 = torch.randn_like(out1)                                      # likely the dead dx's block
+    out1.backward(g1)
+    got = {n: p.grad.detach().clone() for n, p in c1.named_parameters()}
+    for p in c1.parameters():
+        p.grad = None
+    c1(x, ei).backward(g1)                                           # no consumer: no hand-off
+    for n, p in c1.named_parameters():
+        assert rel(got[n], p.grad.double()) <= 1e-6, n
+
+
+def test_node_table_second_forward_is_caught(pkg, cuda):
+    """The node table's item rows are rewritten by every forward (a raw-pointer write): a graph
+    that saved the previous rows must fail autograd's version check, not silently use new rows."""
+    gr = pkg.data.synthetic_ui_graph(n_users=1500, n_items=400, n_interactions=20_000, seed=4)
+    ei = torch.from_numpy(gr.edge_index_numpy()).to(cuda)
+    feats = torch.from_numpy(pkg.data.synthetic_item_features(gr.n_items, 64, seed=4)).to(cuda)
+    torch.manual_seed(0)
+    model = pkg.PyGGAT(gr.n_users, gr.n_items, item_feat_dim=64, hidden=128, layers=2, heads=1,
+                       attn_dropout=0.0).to(cuda).train()
+    first = model(feats, ei).square().sum()
+    model(feats * 2, ei)                      # a second forward before the first backward
+    with pytest.raises(RuntimeError, match="rewritten by a later forward"):
+        first.backward()
+
+
 def test_gemm_tn_segments(pkg, cuda):
     ops = _ops()
     g = torch.Generator().manual_seed(11)
@@ -350,11 +389,16 @@ def test_gemm_tn_large_shape_deterministic(pkg, cuda):
 def test_both_gemm_families(cuda, family, f16):
     """Projection (x W^T + scores, + bias), dx and weight-gradient GEMMs at config-2 rows, and
     the config-5 NN shapes, in a fresh process per family (split: the large-M NN products on the
-    fp16 two-term kernel, or with PPGAT_GEMM_F16=0 on the bf16 x6 one; fp32 MFMA): all within
+    fp16 two-term kernel, or with PPGAT_GEMM_F16=0 -- a lab-build switch -- on the bf16 x6 one; fp32 MFMA): all within
     2e-6 of fp64 (tighter than the suite's 1e-5), bitwise repeatable, the two B layouts of the
     NN GEMM identical."""
     root = Path(__file__).resolve().parents[1]
     env = dict(os.environ, PPGAT_GEMM=family, PPGAT_GEMM_F16=f16)
+    if f16 == "0":  # the bf16 x6 pre-split NN kernel is a lab-build kernel now
+        lab = root / "lab_build" / "libppgat.so"
+        if not lab.exists():
+            pytest.skip("lab build absent (make -C plotpointe-gat-recommendation_amd/csrc lab)")
+        env["PPGAT_LIB"] = str(lab)
     res = {}
     for extra in ([], ["--cfg5"]):
         out = subprocess.run([sys.executable, str(root / "tools" / "gemm_split_check.py"), "--iters", "3"] + extra,

@@ -240,7 +240,7 @@ def test_linear_constant_input_bound_cached(pkg, cuda):
         (ops.linear(xd, Wd, bd) * G.float().to(cuda)).sum().backward()
         assert rel(Wd.grad, ref) <= 1e-5
         e = ops._CONST_BOUNDS.get(id(xd))
-        assert e is not None and e[0]() is xd and e[1] == xd._version
+        assert e is not None and e[0]() is xd and e[1][0] == xd._version and e[1][1] == xd.data_ptr()
         if it == 1:
             xd.mul_(2.0)                          # a new version: the bound is recomputed
             x = x * 2.0

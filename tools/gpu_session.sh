@@ -36,15 +36,15 @@ for s in $STEPS; do
     probe5) for a in ${PROBES:-0:0 7:0 7:640}; do set -- ${a%%:*} ${a#*:}
               run "probe5_r$1_a$2" 900 python -u tools/scale_probe.py --config 5 --world 8 --rank $1 --streams --a2a-gbs $2 --steps 5 --warmup 2 ${PROBE_ARGS:-}
             done ;;
-    gemm5) run gemm5_nnh 300 env PPGAT_NNH2=0 python tools/bench_gemm.py --cfg5 --iters 10 && \
-           run gemm5_nnh2 300 env PPGAT_NNH2=2 python tools/bench_gemm.py --cfg5 --iters 10 && \
+    gemm5) run gemm5_nnh 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH2=0 python tools/bench_gemm.py --cfg5 --iters 10 && \
+           run gemm5_nnh2 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH2=2 python tools/bench_gemm.py --cfg5 --iters 10 && \
            for v in ${NNHVS:-3}; do run "gemm5_nnh$v" 300 env PPGAT_NNH2=$v python tools/bench_gemm.py --cfg5 --iters 10; done ;;
     pmcdst) (cd /tmp && run pmcdst_a 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_a" -o a -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             (cd /tmp && run pmcdst_b 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_b" -o b -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
             python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
     nnhpmc) run "nnhpmc${NNHV:-3}" 500 env GEMM_ARGS=--cfg5 GEMM_TAG="_nnh${NNHV:-3}" PPGAT_NNH2="${NNHV:-3}" bash tools/gemm_pmc.sh ;;
-    nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_LIB=build_variants/lab/libppgat.so PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
+    nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
     profprobe) (cd /tmp && run rocprof_probe5 900 rocprofv3 --kernel-trace --stats -d "$OUT/profprobe" -o run --output-format csv -- python "$R/tools/scale_probe.py" --config 5 --world 8 --rank ${PROBE_RANK:-7} --streams --steps 3 --warmup 1) ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--config", type=int, default=5)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--item-partition", choices=["dealt", "contiguous"], default="dealt")
+    ap.add_argument("--runs", action="store_true",
+                    help="also the send runs per rank and peer (dist.peer_masks / send_order_key: Comm.exchange "
+                         "sends each run straight from the row table)")
     args = ap.parse_args()
     d = pkg.data
     if args.config == 5:
@@ -41,6 +44,24 @@ def main():
     deg = np.bincount(users, minlength=N) * 2 + np.bincount(items, minlength=N) * 2 + 4.0
     owner, _ = pkg.dist.halo_owner(deg.astype(np.float64), nu, W, args.item_partition)  # the partition code itself
     ou, oi = owner[users], owner[items]
+    if args.runs:
+        D = pkg.dist
+        src = np.concatenate([users, items])
+        dst = np.concatenate([items, users])
+        mask = D.peer_masks(src, owner[dst], owner, W)
+        del src, dst
+        key = D.send_order_key(mask, owner, W)
+        ids = np.arange(N)
+        for r in range(W):
+            row = {"rank": r}
+            for name, sel in (("users", ids[:nu]), ("items", ids[nu:])):
+                mine = sel[owner[sel] == r]
+                mine = mine[np.lexsort((mine, key[mine]))]
+                m = mask[mine]
+                runs = [int(D._runs(((m >> np.uint32(q)) & np.uint32(1)).astype(bool))[0].size) for q in range(W)]
+                row[name] = {"rows": int(len(mine)), "runs_per_peer": runs, "runs": int(sum(runs)),
+                             "classes": int(np.unique(m).size)}
+            print(json.dumps(row), flush=True)
     out = []
     for r in range(W):
         own = int((owner == r).sum())

@@ -75,6 +75,20 @@ class NullComm:
                 out = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return out
 
+    def exchange(self, plan, src, out):
+        """Comm.exchange stub: the plan's rows are not moved (timing only); holds the stream for
+        max(rows sent, rows received) x row bytes."""
+        row = (src[0].numel() if src.dim() and src.size(0) else int(np.prod(src.shape[1:]))) * src.element_size()
+        self._hold(max(plan.n_send, plan.n_recv) * row)
+        return out
+
+    def exchange_back(self, plan, halo, out=None):
+        row = (int(np.prod(halo.shape[1:])) if halo.dim() > 1 else 1) * halo.element_size()
+        self._hold(max(plan.n_send, plan.n_recv) * row)
+        if out is None:
+            out = torch.zeros((plan.n_send,) + tuple(halo.shape[1:]), dtype=halo.dtype, device=halo.device)
+        return out
+
     def all_to_all_counts(self, counts):
         return [int(c) for c in counts]
 
