@@ -227,6 +227,11 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    def note(msg):  # progress on stderr (the large config-5 setup takes minutes before the first step)
+        if rank == 0 and args.config == 5:
+            print(f"bench: {msg} ({time.perf_counter() - t_start:.0f} s)", file=sys.stderr, flush=True)
+    t_start = time.perf_counter()
+
     # ---- synthetic inputs; identical on every rank ----
     if args.config == 5:
         scale = args.scale if args.scale is not None else world / 8.0
@@ -242,6 +247,7 @@ def main():
         rows, cols, _ = data.synthetic_ii_edges(g, k=20, seed=42)
         ei_np = np.concatenate([ei_np, data.ii_edge_columns(g.n_users, rows, cols)], 1)
     E, N = ei_np.shape[1], g.n_nodes
+    note(f"graph generated: {N:,} nodes, {E:,} edge_index columns")
     u, i, j = data.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items, args.samples, seed=42)
     ei = torch.from_numpy(ei_np).to(dev)
     feats = torch.from_numpy(feats_np).to(dev)
@@ -265,6 +271,7 @@ def main():
     else:
         model = full
         pkg.graph_cache.get(ei, N)  # one-time CSR/CSC build (not timed)
+    note("model and graph views on the device")
     # same Adam update as train_gat_pyg.py:299 (lr 1e-3, L2 1e-4): libppgat's device Adam (optim.py)
     # hipGraph replay by default (one captured step: ~150 launches enqueued once), except the
     # gloo rehearsal whose collectives run on the host
@@ -296,6 +303,7 @@ def main():
         return loss
 
     graph = None
+    note("warming up")
     if use_graph:
         # warm up on a side stream (allocator pools, RCCL communicators, lazy inits), then
         # capture one whole step -- forward, loss, backward, collectives, Adam -- and replay it
@@ -335,6 +343,7 @@ def main():
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize()
+    note("warm; timing")
     _lib.profile_reset()
     _lib.profile_enable(graph is None)  # per-kernel events in eager mode only (not capturable)
     if dist_path:

@@ -1514,7 +1514,7 @@ struct XItems {
 // K = 256: one float4 per lane, one edge at a time across the wave, 8 rows in flight.
 // Hub pieces leave [ax^h (K) | m | l | - -] per (item, head) for k_fwd_merge_wg.
 // ---------------------------------------------------------------------------
-template <int K, int H>
+template <int K, int H, int U = 8>
 __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restrict__ col,
                                                const int32_t* __restrict__ eid, const float* __restrict__ x,
                                                int64_t ldx, const float* __restrict__ s_src,
@@ -1526,7 +1526,6 @@ __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restr
   // xmax != NULL: the column maxima of |x_j| over the gathered rows (every source of an edge)
   // merged into it -- the bound of |agg| the weight gradient's fp16 split needs, for free
   static_assert(K == 256, "k_fwd_x: K == 256 (one float4 per lane)");
-  constexpr int U = 8;
   if (p > 0.f) seed = *seed_in;
   __shared__ int recj[4][64];
   __shared__ float recw[4][H][64];
@@ -2824,10 +2823,27 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
                     const int32_t* hub_row, const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, unsigned* xmax) {
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
+#ifdef PPGAT_LAB_BUILD
+  static const int fu = [] {  // rows in flight per wave (PPGAT_FWDX_U: 4 / 6 / 8)
+    const char* e = getenv("PPGAT_FWDX_U");
+    return e ? atoi(e) : 8;
+  }();
+#define PPGAT_FWDX(U_)                                                                                               \
+  PPGAT_XH(H, hipLaunchKernelGGL((k_fwd_x<256, HH, U_>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, \
+                                 its, col, eid, x, ldx, s_src, s_dst, slope, p, inv_keep, seed, seed_in, agg, m, invl, \
+                                 partial, xmax))
+  if (it.n_items > 0) {
+    if (fu == 4) PPGAT_FWDX(4);
+    else if (fu == 6) PPGAT_FWDX(6);
+    else PPGAT_FWDX(8);
+  }
+#undef PPGAT_FWDX
+#else
   if (it.n_items > 0)
     PPGAT_XH(H, hipLaunchKernelGGL((k_fwd_x<256, HH>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, its,
                                    col, eid, x, ldx, s_src, s_dst, slope, p, inv_keep, seed, seed_in, agg, m, invl,
                                    partial, xmax));
+#endif
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)K;

@@ -38,6 +38,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 from types import SimpleNamespace
 from typing import Callable, Optional
@@ -335,13 +336,23 @@ class _Exchange(torch.autograd.Function):
     itself (the first layer's halo items, from the replicated item features)."""
 
     @staticmethod
-    def forward(ctx, t_own, tail, plans, comm: "Comm", stages):
+    def forward(ctx, t_own, tail, plans, comm: "Comm", stages, inplace_grad: bool = False,
+                handoff: Optional[dict] = None):
         t_own = t_own.contiguous()
         n_tail = tail.size(0) if tail is not None else 0
         n_own = plans[0].n_own
-        out = torch.empty((n_own + sum(p.n_recv for p in plans) + n_tail,) + tuple(t_own.shape[1:]),
-                          dtype=t_own.dtype, device=t_own.device)
-        out[:n_own].copy_(t_own)
+        n_out = n_own + sum(p.n_recv for p in plans) + n_tail
+        row = t_own[0].numel() if t_own.dim() > 1 else 1
+        st_ = t_own.untyped_storage()
+        if (inplace_grad and t_own.dim() == 2 and n_tail == 0 and t_own.size(0) == n_own and
+                st_.nbytes() >= (t_own.storage_offset() + n_out * row) * t_own.element_size()):
+            # the own rows lie at the top of a buffer with room for the received rows (the top
+            # layer's output, HaloPyGGAT._top_out): receive behind them, no copy of the own rows
+            out = t_own.new_empty(0).set_(st_, t_own.storage_offset(), (n_out, row), (row, 1))
+        else:
+            out = torch.empty((n_out,) + tuple(t_own.shape[1:]), dtype=t_own.dtype, device=t_own.device)
+            out[:n_own].copy_(t_own)
+        ctx.inplace_grad, ctx.handoff = inplace_grad, handoff
         off = n_own
         for plan in plans:
             if plan.send_runs is not None:  # the halo plans: straight from the own rows
@@ -360,12 +371,18 @@ class _Exchange(torch.autograd.Function):
         plans, comm, st = ctx.plans, ctx.comm, ctx.stages
         g = g.contiguous()
         n_own = plans[0].n_own
-        g_own = g[:n_own].clone()
+        # the own rows' sums in place in the incoming gradient (a buffer of its own: the loss's or
+        # the layer's fresh gradient) instead of a copy of them (1.9 GB at world 8 on config 5)
+        g_own = g[:n_own] if (g._base is None or ctx.inplace_grad) else g[:n_own].clone()
+        if ctx.handoff is not None:
+            # the loss's dZ buffer: hand it to the top layer's backward by object identity (a later
+            # tensor at the same address is never taken for it)
+            ctx.handoff["g"] = weakref.ref(g_own)
         off = n_own
         for plan in plans:  # each plan touches its own rows (users / items): independent sums
             st.return_add(g_own, _return(comm, plan, g[off:off + plan.n_recv]), plan.ret_ptr, plan.ret_pos)
             off += plan.n_recv
-        return g_own, (g[off:] if ctx.has_tail else None), None, None, None
+        return g_own, (g[off:] if ctx.has_tail else None), None, None, None, None, None
 
 
 def _return(comm: "Comm", plan: ExchangePlan, halo: torch.Tensor) -> torch.Tensor:
@@ -375,8 +392,12 @@ def _return(comm: "Comm", plan: ExchangePlan, halo: torch.Tensor) -> torch.Tenso
     return comm.all_to_all_rows(halo, plan.recv_counts, plan.send_counts)
 
 
-def exchange(t_own, plan: ExchangePlan, comm: "Comm", stages):
-    return _Exchange.apply(t_own, None, [plan], comm, stages)
+def exchange(t_own, plan: ExchangePlan, comm: "Comm", stages, inplace_grad: bool = False,
+             handoff: Optional[dict] = None):
+    """``inplace_grad``: the incoming gradient is a buffer of the caller's own (the loss's dZ):
+    the own rows' sums are formed in place in it; ``handoff``: a dict that receives a weak
+    reference to the own rows' gradient (key "g") for the layer below."""
+    return _Exchange.apply(t_own, None, [plan], comm, stages, inplace_grad, handoff)
 
 
 def halo_exchange(t_own, hg: "HaloGraph", comm: "Comm", stages, halo_items: Optional[torch.Tensor] = None):
@@ -753,9 +774,11 @@ class HaloRows:
     the phase of layer l that produced them) -- or computed locally (``set_local``: the first
     layer's halo items).  ``wait(cls)`` orders the current stream after that class's rows."""
 
-    def __init__(self, hg: "HaloGraph", comm: "Comm", stages, width: int, like: torch.Tensor):
+    def __init__(self, hg: "HaloGraph", comm: "Comm", stages, width: int, like: torch.Tensor,
+                 x: Optional[torch.Tensor] = None):
         self.hg, self.comm, self.stages = hg, comm, stages
-        self.x = torch.empty((hg.R, width), dtype=like.dtype, device=like.device)
+        # x: a caller's [R, width] table (the first layer's persistent one, HaloPyGGAT._first_table)
+        self.x = x if x is not None else torch.empty((hg.R, width), dtype=like.dtype, device=like.device)
         self.events = {}
         self.local = set()
         self.started = []   # exchanged classes, in start order
@@ -842,8 +865,9 @@ class _CatInto(torch.autograd.Function):
     def forward(ctx, holder, a, b):
         dest = holder[0]
         na = a.size(0)
-        dest[:na].copy_(a)
-        dest[na:].copy_(b)
+        for part, src in ((dest[:na], a), (dest[na:], b)):
+            if src.numel() and part.data_ptr() != src.data_ptr():  # (a block already in place: no copy)
+                part.copy_(src)
         ctx.na = na
         return dest
 
@@ -902,7 +926,7 @@ class _HaloLayerX(torch.autograd.Function):
     def forward(ctx, x_own, x_halo_items, weight, att_src, att_dst, bias, hg: "HaloGraph", comm: "Comm", stages,
                 heads: int, C: int, slope: float, p: float, seed: int, rows_in: Optional[HaloRows] = None,
                 rows_out: Optional[HaloRows] = None, link_in: Optional[dict] = None,
-                link_out: Optional[dict] = None):
+                link_out: Optional[dict] = None, out_buf: Optional[list] = None):
         from .hip_ops import xgat_forward
         x_own = x_own.contiguous()
         if rows_in is None:
@@ -927,6 +951,8 @@ class _HaloLayerX(torch.autograd.Function):
             xgat_scores_rows(x_halo_items, rows_in.A, rows_in.s[a:b])
         # the output rows go straight into the next layer's table (its own rows)
         dest = rows_out.x[:hg.n_own] if rows_out is not None and rows_out.x.size(1) == C else None
+        if dest is None and out_buf is not None:  # the top layer: rows reserved after its own (the loss's)
+            dest = out_buf[0][:hg.n_own]
         scores = (rows_in.s, rows_in.s_dst) if rows_in.s is not None else None
         out, ctx.saved = xgat_forward(x_loc, weight, att_src, att_dst, bias, hg.xviews(), heads, C, slope, p, seed,
                                       phases=_halo_phases(hg, rows_in, rows_out), out=dest, scores=scores,
@@ -960,7 +986,7 @@ class _HaloLayerX(torch.autograd.Function):
             # rank); the halo rows' -- incl. the first layer's locally computed halo items -- are
             # their owners' business
             return (dx, None, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                    None, None, None, None, None, None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None, None, None, None, None, None)
         pending = {}
 
         def a2a_back(dx_halo):
@@ -993,7 +1019,7 @@ class _HaloLayerX(torch.autograd.Function):
             st.return_add(dx_own, ret, plan.ret_ptr, plan.ret_pos)
         d_items = dx[hg.n_own + hg.n_halo_u:] if ctx.local_items else None
         return (dx_own, d_items, dW, datt_src.view(ctx.att_shapes[0]), datt_dst.view(ctx.att_shapes[1]), dbias,
-                None, None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def source_homed_backward(hg: "HaloGraph") -> bool:
@@ -1127,9 +1153,11 @@ def _partials_home(hg: "HaloGraph", comm: "Comm", stages, part: torch.Tensor) ->
     return own
 
 
-def _bwd_tables(saved: dict, hg: "HaloGraph", comm: "Comm", stages, g_width: int, dev):
-    """The backward's row tables of one multi-head halo layer: g [R, C] (own rows to be filled)
-    and the softmax state nstate {s_dst, m, inv_l, .} [R, 4H] (own rows filled here)."""
+def _bwd_tables(saved: dict, hg: "HaloGraph", comm: "Comm", stages, g_width: int, dev,
+                g_table: Optional[torch.Tensor] = None):
+    """The backward's row tables of one multi-head halo layer: g [R, C] (own rows to be filled;
+    ``g_table``: a caller's buffer) and the softmax state nstate {s_dst, m, inv_l, .} [R, 4H]
+    (own rows filled here)."""
     lib = _lib.load()
     s_dst, m, inv_l = saved["s_dst"], saved["m"], saved["inv_l"]
     H = saved["meta"][0]
@@ -1139,7 +1167,7 @@ def _bwd_tables(saved: dict, hg: "HaloGraph", comm: "Comm", stages, g_width: int
     _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H,
                                      ntab.x.data_ptr(), _lib.stream_handle(dev)), "xgat_nstate")
     nst = ntab.x[:n0]
-    gtab = HaloRows(hg, comm, stages, g_width, nst)
+    gtab = HaloRows(hg, comm, stages, g_width, nst, x=g_table)
     return gtab, ntab, nst
 
 
@@ -1175,7 +1203,16 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     E = sv.n_edges
     seed_buf = saved["seed_buf"]
     order = _small_class_first(hg)
-    if pre is not None:
+    handed = getattr(hg, "grad_handoff", {}).pop("g", None)
+    if pre is None and handed is not None and handed() is g and g.is_contiguous() and n0 and \
+            g.data_ptr() == g.untyped_storage().data_ptr() and g.untyped_storage().nbytes() >= R * C * 4:
+        # g is the top of an [R, C] buffer (the loss backward's dZ, halo_bpr_loss grad_rows): it is
+        # the g table, its own rows already in place (its rows past n0 held the loss's received
+        # rows' gradients, already returned to their owners in stream order before this point)
+        gtab, ntab, nst = _bwd_tables(saved, hg, comm, stages, C, dev,
+                                      g_table=g.new_empty(0).set_(g.untyped_storage(), 0, (R, C), (C, 1)))
+        _bwd_start(hg, gtab, ntab, nst, g)
+    elif pre is not None:
         # started by the layer above from its dx, which is g when nothing sits between the two
         # layers (HaloPyGGAT links a layer only to the one consumer of its output).  If autograd
         # hands over another tensor (a hook, a residual, an activation in between), the halo rows
@@ -1348,17 +1385,74 @@ class _ShardedBase(torch.nn.Module):
         return sd
 
 
+def _unalias_local(module, state_dict, prefix, local_metadata):
+    """state_dict hook: user_emb_local may share the first-layer table's storage
+    (HaloPyGGAT._first_table); hand out its own copy (torch.save would write the whole table)."""
+    k = prefix + "user_emb_local"
+    v = state_dict.get(k)
+    if v is not None and v.untyped_storage().nbytes() > v.numel() * v.element_size():
+        state_dict[k] = v.clone()
+
+
 class HaloPyGGAT(_ShardedBase):
     """PyGGAT with row-sharded users and items and halo all_to_all exchange (module doc).
     ``forward`` returns the own rows [n_own, C]: own users, then own items."""
 
+    def __init__(self, full, dg, comm: "Comm", stages=None):
+        super().__init__(full, dg, comm, stages)
+        self._register_state_dict_hook(_unalias_local)
+
+    def _item_feats(self, item_feats, which: str) -> torch.Tensor:
+        """The item feature rows of the own ("own") or halo ("halo") items, gathered once per
+        feature tensor: the features are a constant input and the partition is static, so the
+        gathers (0.6 + 2.9 GB at world 8 on config 5) leave the step, and the item projection's
+        weight-gradient operand is the same tensor every step (its column bound is cached,
+        hip_ops._const_colmax)."""
+        key = (item_feats.data_ptr(), item_feats._version, tuple(item_feats.shape), str(item_feats.device))
+        cache = getattr(self, "_feat_cache", None)
+        if cache is None or cache[0] != key:
+            cache = (key, {})
+            self._feat_cache = cache
+        hit = cache[1].get(which)
+        if hit is None:
+            idx = self.dg.own_items if which == "own" else self.dg.halo_items
+            hit = self.stages.gather_rows(item_feats, idx)
+            cache[1][which] = hit
+        return hit
+
+    def _first_table(self, width: int, like: torch.Tensor) -> torch.Tensor:
+        """The first layer's input table [R, width], kept across steps, whose first rows ARE the
+        user embedding's storage (re-pointed once, as model.node_table): the own users' rows need
+        no copy into it, the item projections write their rows in place."""
+        hg = self.dg
+        t = getattr(self, "_tab0", None)
+        if t is None or tuple(t.shape) != (hg.R, width) or t.device != like.device or t.dtype != like.dtype:
+            t = torch.empty((hg.R, width), dtype=like.dtype, device=like.device)
+            self._tab0 = t
+        w = self.user_emb_local
+        if w.size(0) and w.data_ptr() != t.data_ptr():
+            t[:w.size(0)].copy_(w.detach())
+            w.data = t[:w.size(0)]
+        return t
+
+    def _top_out(self, C: int, like: torch.Tensor):
+        """The top layer's output rows, with room after them for the rows the loss receives
+        (halo_bpr_loss sets hg.loss_tail_rows once its plan exists): the loss's exchange then
+        receives straight behind the own rows instead of copying them (_Exchange)."""
+        tail = int(getattr(self.dg, "loss_tail_rows", 0))
+        if not tail:
+            return None
+        return [torch.empty((self.dg.n_own + tail, C), dtype=like.dtype, device=like.device)]
+
     def node_features(self, item_feats, into: Optional[torch.Tensor] = None):
         """[own users | own items] input rows; ``into``: write them there (the first halo layer's
         table) instead of a new tensor."""
-        f = self.stages.gather_rows(item_feats, self.dg.own_items)
-        x_items = self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
+        f = self._item_feats(item_feats, "own")
         if into is not None:
+            nu = self.user_emb_local.size(0)
+            x_items = self.stages.linear(f, self.item_proj.weight, self.item_proj.bias, out=into[nu:])
             return _CatInto.apply([into], self.user_emb_local, x_items)
+        x_items = self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
         return torch.cat([self.user_emb_local, x_items], 0)
 
     @staticmethod
@@ -1371,8 +1465,7 @@ class HaloPyGGAT(_ShardedBase):
         rank (the item features are on every rank): they are neither received nor returned;
         their gradient reaches item_proj here and is summed by the dense all-reduce.  ``out``:
         write them there (the first halo layer's table) instead of a new tensor."""
-        hg = self.dg
-        f = self.stages.gather_rows(item_feats, hg.halo_items)
+        f = self._item_feats(item_feats, "halo")
         if out is not None:
             return self.stages.linear(f, self.item_proj.weight, self.item_proj.bias, out=out)
         return self.stages.linear(f, self.item_proj.weight, self.item_proj.bias)
@@ -1388,7 +1481,8 @@ class HaloPyGGAT(_ShardedBase):
         if self._x_path(0):
             # the first layer's halo user rows are parameters: their exchange starts before
             # the item projections (the own and the halo items' rows) are computed
-            rows = HaloRows(hg, self.comm, self.stages, self.user_emb_local.size(1), self.user_emb_local)
+            rows = HaloRows(hg, self.comm, self.stages, self.user_emb_local.size(1), self.user_emb_local,
+                            x=self._first_table(self.user_emb_local.size(1), self.user_emb_local))
             c0 = self.convs[0]
             rows.enable_scores(xgat_att_proj(c0.lin.weight, c0.att_src, c0.att_dst, c0.heads, c0.out_channels))
             rows.score_rows(self.user_emb_local.detach(), 0, hg.n_own_u)  # sent beside the user rows
@@ -1410,7 +1504,11 @@ class HaloPyGGAT(_ShardedBase):
                     # aggregate-then-transform on the local rows: no halo projection; the next
                     # layer's halo rows start moving as this layer's phases finish, and the
                     # return of the halo gradients overlaps the own rows' backward
-                    nxt = link_out = None
+                    nxt = link_out = out_buf = None
+                    if li + 1 == len(self.convs):
+                        out_buf = self._top_out(conv.out_channels, x)
+                        # the loss's dZ in an [R, C] buffer: this layer's backward takes it as its g table
+                        hg.loss_grad_rows = hg.R if source_homed_backward(hg) else 0
                     if li + 1 < len(self.convs) and self._x_path(li + 1):
                         nxt = HaloRows(hg, self.comm, self.stages, conv.out_channels, x)
                         cn = self.convs[li + 1]
@@ -1419,7 +1517,8 @@ class HaloPyGGAT(_ShardedBase):
                         link_out = {}
                     x = _HaloLayerX.apply(x, xh, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, hg,
                                           self.comm, self.stages, conv.heads, conv.out_channels,
-                                          float(conv.negative_slope), p, seed, rows, nxt, link_in, link_out)
+                                          float(conv.negative_slope), p, seed, rows, nxt, link_in, link_out,
+                                          out_buf)
                     rows, link_in = nxt, link_out
                     continue
                 h = self.stages.linear(halo_exchange(x, hg, self.comm, self.stages, xh), conv.lin.weight, None)
@@ -1480,7 +1579,13 @@ def halo_bpr_loss(Z_own, hg: HaloGraph, comm: "Comm", u, i, j, n_users: int, n_i
         from .hip_ops import HipStages
         stages = HipStages()
     plan, rmap = _loss_plan(hg, comm, u, i, j, plan_key)
-    Zl = exchange(Z_own, plan, comm, stages)
+    hg.loss_tail_rows = plan.n_recv  # the next forward's top layer leaves room for these rows
+    grad_rows = int(getattr(hg, "loss_grad_rows", 0))
+    hg.grad_handoff = {}
+    Zl = exchange(Z_own, plan, comm, stages, inplace_grad=True, handoff=hg.grad_handoff if grad_rows else None)
+    if grad_rows and getattr(stages, "bpr_grad_rows", False):
+        # dZ inside an [R, C] buffer: the top layer's backward uses it as its g table (no copy)
+        return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss, grad_rows=grad_rows)
     return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss)
 
 

@@ -906,6 +906,11 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, out_holder=None):
+        # no gradient reached the output (the halo partition's locally computed halo item rows,
+        # whose gradients are their owners' business): skip the backward instead of running it on
+        # a materialised zero gradient (a zero fill, two column-max passes and a TN GEMM over the
+        # 2.8M halo rows per step at world 8 on config 5)
+        ctx.set_materialize_grads(False)
         x_const = not x.requires_grad  # (an input the step does not differentiate: the item features)
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
@@ -924,6 +929,8 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g is None:
+            return None, None, None, None
         x, weight = ctx.saved_tensors
         g = g.contiguous()
         dx = None
@@ -1769,8 +1776,9 @@ def bpr_prepare(n_rows: int, n_users: int, n_items: int, C: int, u, i, j, row_ma
 
 class _BPRLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map, prep=None):
+    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map, prep=None, grad_rows: int = 0):
         lib = _lib.load()
+        ctx.grad_rows = int(grad_rows)
         # Z straight from a heads = 1 GATLayer: the loss backward also does that layer's prologue
         ctx.producer = (_producer_of(Z, N=Z.size(0), C=Z.size(1))
                         if (row_map is None and prep is None and _producer_fusion_enabled()) else None)
@@ -1814,7 +1822,10 @@ class _BPRLoss(torch.autograd.Function):
         Z, u, i, j, coef = ctx.saved_tensors
         n_rows, n_users, n_items, C, S = ctx.meta
         gl = gl.reshape(1).to(torch.float32).contiguous()
-        dZ = torch.empty_like(Z)
+        # grad_rows > n_rows: dZ is the top of a [grad_rows, C] buffer (the halo partition's top
+        # layer takes the buffer as its gradient table, dist._halo_xgat_backward_deferred_d)
+        dZ = (torch.empty(ctx.grad_rows, C, dtype=Z.dtype, device=Z.device)[:n_rows] if ctx.grad_rows > n_rows
+              else torch.empty_like(Z))
         ws = ctx.ws
         prod, ctx.producer = ctx.producer, None
         if prod is not None and prod.pro_state is not None:
@@ -1834,7 +1845,7 @@ class _BPRLoss(torch.autograd.Function):
                           i.data_ptr(), j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(),
                           ws.numel(), _lib.stream_handle(Z.device)), "bpr_bwd")
         ctx.ws = None
-        return dZ, None, None, None, None, None, None, None, None
+        return dZ, None, None, None, None, None, None, None, None, None
 
 
 def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr", prepared: BprPrepared = None) -> torch.Tensor:
@@ -1847,11 +1858,12 @@ def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr", prepared
 
 
 def bpr_loss_mapped(Z: torch.Tensor, n_users: int, n_items: int, row_map: torch.Tensor, u, i, j,
-                    loss: str = "bpr", prepared: BprPrepared = None) -> torch.Tensor:
-    """bpr_loss over a Z whose rows are laid out by row_map (node id -> row)."""
+                    loss: str = "bpr", prepared: BprPrepared = None, grad_rows: int = 0) -> torch.Tensor:
+    """bpr_loss over a Z whose rows are laid out by row_map (node id -> row).  ``grad_rows``: the
+    gradient of Z is the top of a buffer of that many rows (the rest is the caller's)."""
     if Z.size(1) not in (32, 64, 128, 256):
         raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
-    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map, prepared)
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map, prepared, grad_rows)
 
 
 # ---------------------------------------------------------------------------
@@ -1893,8 +1905,10 @@ class HipStages:
                                              cols, _lib.stream_handle(dst.device)), "rows_return_add")
         return dst
 
-    def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss):
-        return bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, loss)
+    bpr_grad_rows = True  # bpr() takes grad_rows (dist.halo_bpr_loss)
+
+    def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss, grad_rows: int = 0):
+        return bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, loss, grad_rows=grad_rows)
 
     def scores(self, h, att_src, att_dst, heads, channels):
         return node_scores(h, att_src, att_dst, heads, channels)

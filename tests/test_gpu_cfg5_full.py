@@ -1,0 +1,128 @@
+"""The whole 200M-edge config-5 graph on one GPU (GPU only, -m gpu).
+
+One GATConv(256, 256, heads=4) layer (train_gat_pyg.py:77, lin 256 -> 1024) in train mode
+(attention dropout 0.1) over all 15M nodes and 200M edge_index columns of
+``data.synthetic_scaling_graph(1.0)`` -- the scale at which the layer drops its aggregates
+and takes the weight gradient from acc^T x (hip_ops._xgat_keep_agg), and at which the most
+popular item has ~1M in-edges (~3,900 hub pieces).  Checked at that size:
+
+* finiteness of out, dx, dW, datt and dbias;
+* a bitwise repeat of the whole forward and backward (same mask seed);
+* the exact fp64 oracle on sampled destination blocks: the upstream gradient G is zero outside
+  three blocks (the top hub item, a run of users, a run of tail items), so L = sum(G * out)
+  involves only those destinations' in-edges and every gradient of the full-graph layer --
+  dx of every row, dW, datt_src, datt_dst, dbias -- equals the oracle's on that subgraph
+  (``oracle.pyg_gat_conv_rows``: the same global edge ids, so the same dropout mask), and
+  out on the blocks' rows equals the oracle's.
+Tolerances as tests/test_gpu_fullsize.py (max-abs / max-abs; dx per row on the scale of its
+terms is not repeated here -- the sampled blocks hold no in-degree-1 cancellations the share
+test does not already cover).
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_kink_ties, check_att_dst, kink_report, row_rel, write_report
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1100)]
+
+SEED = 515151
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def test_cfg5_full_graph_layer(pkg, oracle, cuda):
+    ops = importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
+    cm = importlib.import_module("plotpointe-gat-recommendation_amd.conv")
+    H, C = 4, 256
+    g = pkg.data.synthetic_scaling_graph(1.0, seed=42)
+    ei_np = g.edge_index_numpy()
+    N, E = g.n_nodes, ei_np.shape[1]
+    assert E == 200_000_000 and N == 15_000_000
+    indeg = np.bincount(ei_np[1], minlength=N)
+    hub = int(np.argmax(indeg))
+    assert indeg[hub] > 256 * 1000  # a hub of more than a thousand pieces
+    nu = g.n_users
+    tail = nu + int(np.flatnonzero(indeg[nu:] > 0)[-1])
+    blocks = [(hub, hub + 1), (4_000_000, 4_002_000), (max(nu, tail - 3000), tail + 1)]
+    rows = np.concatenate([np.arange(a, b) for a, b in blocks])
+    rng = np.random.default_rng(1)
+    x = torch.from_numpy(rng.standard_normal((N, C), dtype=np.float32))
+    Gb = torch.from_numpy(rng.standard_normal((len(rows), C), dtype=np.float32))
+    rows_t = torch.from_numpy(rows).to(cuda)
+    torch.manual_seed(11)
+    conv = pkg.GATConv(C, C, heads=H, dropout=0.1, add_self_loops=False, concat=False)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.1, 0.1)
+    conv = conv.to(cuda).train()
+    orig = cm._dropout_seed
+    cm._dropout_seed = lambda: SEED
+    names = ("out_rows", "dx", "lin.weight", "att_src", "att_dst", "bias")
+    try:
+        ei = torch.from_numpy(ei_np).to(cuda)
+        del ei_np
+        xd = x.to(cuda).requires_grad_(True)
+        Gd = torch.zeros(N, C, device=cuda)
+        Gd[rows_t] = Gb.to(cuda)
+        res = []
+        for rep in range(2):
+            ops.KINK_TAP = [] if rep == 0 else None
+            try:
+                out = conv(xd, ei)
+                if rep == 0:
+                    tap = [(e, p[..., None] if p.dim() == 1 else p) for e, p in ops.KINK_TAP]
+            finally:
+                ops.KINK_TAP = None
+            (out * Gd).sum().backward()
+            torch.cuda.synchronize()
+            res.append((out.detach()[rows_t].clone(), xd.grad.clone(), conv.lin.weight.grad.clone(),
+                        conv.att_src.grad.clone(), conv.att_dst.grad.clone(), conv.bias.grad.clone()))
+            finite = bool(torch.isfinite(out).all()) and all(bool(torch.isfinite(t).all()) for t in res[-1])
+            assert finite, f"non-finite values in pass {rep}"
+            del out
+            xd.grad = None
+            conv.zero_grad(set_to_none=True)
+        for n, a, b in zip(names, res[0], res[1]):
+            assert torch.equal(a, b), n
+    finally:
+        cm._dropout_seed = orig
+    del xd, Gd, res[1]
+    torch.cuda.empty_cache()
+    # the kernels' LeakyReLU side of the sampled blocks' edges (the oracle takes the same side)
+    sel = torch.nonzero(torch.isin(ei[1], rows_t)).squeeze(1)
+    pos = torch.zeros(E, H, dtype=torch.bool, device=cuda)
+    for e_, p_ in tap:
+        pos[e_.to(cuda)] = p_.to(cuda).view(-1, H)
+    del tap
+    P = {k: v.detach() for k, v in conv.named_parameters()}
+    kst = []
+    out_r, nodes, dx_r, grads = oracle.pyg_gat_conv_rows(P, x.to(cuda), ei, sel, rows_t, Gb.to(cuda), H, 0.1, SEED,
+                                                         kink_pos=pos, kink_stats=kst)
+    dx = res[0][1]
+    dx_nodes = dx[nodes].double()
+    dx[nodes] = 0
+    off_nodes = float(dx.abs().max())      # rows no sampled destination reads: exactly zero
+    errs = {"out_rows": rel(res[0][0], out_r), "dx": float((dx_nodes - dx_r).abs().max() / dx_r.abs().max())}
+    errs.update({n: rel(a, grads[n]) for n, a in zip(names[2:], res[0][2:])})
+    write_report("cfg5_full_graph_layer", {
+        "edges": E, "nodes": N, "heads": H, "channels": C, "hub_in_degree": int(indeg[hub]),
+        "blocks": [list(map(int, b)) for b in blocks], "block_edges": int(sel.numel()), "rel": errs,
+        "out_row_rel_max": row_rel(res[0][0], out_r)[0], "dx_outside_blocks_max_abs": off_nodes,
+        "kink_ties": kink_report(kst),
+        "bitwise_repeat": True, "finite": True,
+        "oracle": "fp64 pyg_gat_conv on the sampled destination blocks' in-edges (global edge ids), "
+                  "LeakyReLU sides as the kernels took them"})
+    assert_kink_ties(kst)
+    tol = {"out_rows": 1e-5, "dx": 1e-5, "lin.weight": 1e-5, "att_src": 1e-4, "att_dst": 1e-4, "bias": 1e-5}
+    assert off_nodes == 0.0
+    for n in names:
+        if n == "att_dst":  # (sums that cancel at in-degree-1 users: judged on the pair's scale there)
+            err = float((res[0][4].double() - grads["att_dst"]).abs().max())
+            check_att_dst(err, grads["att_dst"].cpu(), grads["att_src"].cpu(), tol[n])
+            continue
+        assert errs[n] <= tol[n], (n, errs[n])

@@ -49,6 +49,9 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
+    fwdxu) for u in ${FWDXU:-8 6 4}; do run "bench5_fwdx_u$u" 600 env PPGAT_LIB=lab_build/libppgat.so PPGAT_FWDX_U=$u python -u bench.py --config 5 --steps 5 --warmup 2 --graph off; done ;;
+    bench5full) run bench_cfg5_full 1000 python -u bench.py --config 5 --scale 1 --steps ${FULL_STEPS:-3} --warmup 1 --graph ${FULL_GRAPH:-on} ;;
+    prof5full) (cd /tmp && run rocprof_cfg5_full 1000 rocprofv3 --kernel-trace --stats -d "$OUT/prof5full" -o run --output-format csv -- python -u "$R/bench.py" --config 5 --scale 1 --steps 2 --warmup 1 --graph off) ;;
     bench5) run bench_cfg5 900 python -u bench.py --config 5 --steps 10 --warmup 3 ;;
     prof5)  (cd /tmp && run rocprof_cfg5 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof5" -o run --output-format csv -- python "$R/bench.py" --config 5 --steps 5 --warmup 2) ;;
     pmc5)  (cd /tmp && run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc5_fetch" -o fetch -- python "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
@@ -57,6 +60,10 @@ for s in $STEPS; do
     fusion) run bench_fusion 300 python tools/bench_fusion.py && \
             run bench_fusion3 300 env PPGAT_NNH2=3 python tools/bench_fusion.py ;;
     fusionpmc) run "fusionpmc${NNHV:-3}" 500 env PPGAT_NNH2="${NNHV:-3}" FUSION_TAG="_nnh${NNHV:-3}" bash tools/fusion_pmc.sh ;;
+    pmc6)  for pass in fetch:FETCH_SIZE write:WRITE_SIZE dram:"TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum"; do
+             (cd /tmp && run "pmc6_${pass%%:*}" 300 timeout -s KILL 240 rocprofv3 --pmc ${pass#*:} --kernel-trace --output-format csv -d "$OUT/pmc6_${pass%%:*}" -o p -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) || exit 1
+           done
+           python "$R/tools/pmc_summary.py" "$OUT/pmc6_fetch" "$OUT/pmc6_write" "$OUT/cfg2_pmc_traffic.json" 2 dram_dir="$OUT/pmc6_dram" > "$OUT/pmc6_summary.log" 2>&1 ;;
     prof)  (cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$R/bench.py" --steps 10 --warmup 3 --cpu-baseline-seconds 0) ;;
     pmc)   (cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o fetch -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \
            (cd /tmp && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o write -- python "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline-seconds 0) && \

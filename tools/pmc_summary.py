@@ -45,6 +45,14 @@ def load(d, counter):
 def main():
     fd, wd, out = sys.argv[1:4]
     config = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    dram_dir = None
+    extra = []
+    for kv in sys.argv[5:]:
+        if kv.startswith("dram_dir="):
+            dram_dir = kv.split("=", 1)[1]
+        else:
+            extra.append(kv)
+    sys.argv[5:] = extra
     fetch = load(fd, "FETCH_SIZE")
     write = load(wd, "WRITE_SIZE")
     res = {"note": "per-launch HBM-side bytes (L2 fabric requests, Infinity-Cache hits included); "
@@ -64,6 +72,27 @@ def main():
     for k, parts in PASSES.items():
         if any(q in res["per_launch_bytes"] for q in parts):
             res["per_launch_bytes"][k] = sum(res["per_launch_bytes"].get(q, 0.0) for q in parts)
+    if dram_dir:
+        # a third pass: the L2's fabric requests split by destination (TCC_EA0_{RD,WR}REQ vs their
+        # _DRAM parts, "destined for DRAM (MC)").  The memory-side Infinity Cache sits behind the
+        # MC, so _DRAM requests still include MALL hits: this splits off GMI/IO traffic, not the
+        # on-die cache (rocprofv3 exposes no MALL hit counter on gfx950)
+        cnt = {c: load(dram_dir, c) for c in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_WRREQ_sum",
+                                              "TCC_EA0_WRREQ_DRAM_sum")}
+        mean = lambda c, k: sum(cnt[c].get(k, [0])) / max(len(cnt[c].get(k, [])), 1)  # noqa: E731
+        res["dram_destined"] = {}
+        res["per_launch_dram_bytes"] = {}
+        for k in res["raw_kib"]:
+            rd, rdd, wr, wrd = (mean(c, k) for c in cnt)
+            frd = rdd / rd if rd else 0.0
+            fwr = wrd / wr if wr else 0.0
+            f, w = res["raw_kib"][k]["fetch"], res["raw_kib"][k]["write"]
+            res["dram_destined"][k] = {"rdreq": rd, "rdreq_dram": rdd, "wrreq": wr, "wrreq_dram": wrd,
+                                       "read_frac": frd, "write_frac": fwr}
+            res["per_launch_dram_bytes"][k] = (2 * f * frd + w * fwr) * 1024
+        for k, parts in PASSES.items():
+            if any(q in res["per_launch_dram_bytes"] for q in parts):
+                res["per_launch_dram_bytes"][k] = sum(res["per_launch_dram_bytes"].get(q, 0.0) for q in parts)
     json.dump(res, open(out, "w"), indent=2)
     print(json.dumps(res, indent=2))
 
