@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
                     help="approximate CPU time budget of the oracle baseline leg (0 disables)")
     ap.add_argument("--traffic-json", default=None,
-                    help="committed PMC summary (default: profiles/r02/cfg2_pmc_traffic.json for config 2, "
+                    help="committed PMC summary (default: profiles/r06/cfg2_pmc_traffic.json for config 2, "
                          "profiles/r03/cfg5_pmc_traffic.json for config 5 at its default scale)")
     ap.add_argument("--partition", choices=["auto", "replicated", "halo"], default="auto",
                     help="N>1: 'replicated' = users sharded, item rows on every rank (dist.build_replicated_graph); "
@@ -421,18 +421,20 @@ def main():
     else:
         ab = algo_bytes(dom, N, E, H, C, args.attn_dropout > 0, xform_k, gather_g=gather_mode if gather_g else False)
     achieved = ab / avg_s / 1e9
-    traffic = None
+    traffic = traffic_src = traffic_dram = None
     try:
         if dist_path:
             raise LookupError("the committed PMC summary is for the unsharded graph")
         tj_path = args.traffic_json or str(ROOT / "profiles" / ("r03/cfg5_pmc_traffic.json" if args.config == 5
-                                                                 else "r02/cfg2_pmc_traffic.json"))
+                                                                 else "r06/cfg2_pmc_traffic.json"))
         tj_ = json.loads(Path(tj_path).read_text())
         # PMC summaries are per workload (config, scale) and per multi-head backward formulation
         if tj_.get("config", 2) == args.config and tj_.get("scale", scale if args.config == 5 else None) == (
                 scale if args.config == 5 else None) and (
                 not xform_k or tj_.get("bwd_gather", "gt") == (gather_mode if gather_g else "gt")):
             traffic = tj_.get("per_launch_bytes", {}).get(dom)
+            traffic_src = os.path.relpath(tj_path, ROOT)
+            traffic_dram = tj_.get("per_launch_dram_bytes", {}).get(dom)
     except Exception:
         pass
     copies = measured_copy_gbs(dev) if rank == 0 else None
@@ -489,6 +491,10 @@ def main():
         "kernel_ms_per_step": {k: ms / K for k, (ms, n) in kern.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     # the L2's fabric requests destined for DRAM (TCC_EA0_*REQ_DRAM / *REQ): the
+                     # memory-side Infinity Cache sits behind them, so its hits are not split off
+                     "traffic_dram_destined": traffic_dram,
                      "algo_bytes_per_launch": ab, "avg_launch_ms": avg_s * 1e3, "launches": dom_n,
                      "launches_per_layer_pass": dom_n / max(passes, 1),
                      "measured_copy_gbs": copy_gbs,

@@ -696,9 +696,9 @@ int ppgat_check_index_range(const void* idx, int elem_bytes, int64_t n, int64_t 
 
 /* ---- measurement ------------------------------------------------------------------------
  * ppgat_stream_copy: dst[0 .. n_bytes) = src[...], a float4 streaming copy (16 B per lane,
- *   four loads in flight per thread, one pass over a grid of 8 workgroups per CU): the
- *   achievable-HBM yardstick bench.py reports beside the 8 TB/s spec peak (the guide's measured
- *   float4 copy: 6.29 TB/s).  n_bytes and both pointers must be multiples of 16. */
+ *   non-temporal loads and stores, one pass): the achievable-HBM yardstick bench.py reports
+ *   beside the 8 TB/s spec peak (the guide's measured float4 copy: 6.29 TB/s; this one 6.58 on
+ *   1 GiB, profiles/r06/x3_copy_lab.log).  n_bytes and both pointers must be multiples of 16. */
 int ppgat_stream_copy(const void* src, void* dst, int64_t n_bytes, void* stream);
 
 /* ---- in-process kernel timing (HIP events on the launch stream) --------- */

@@ -1324,30 +1324,22 @@ hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const 
   return hipGetLastError();
 }
 
-// the achievable-HBM yardstick (ppgat_stream_copy): every thread moves four float4s with all four
-// loads issued before the stores, consecutive lanes on consecutive 16 B, the grid sized to cover
-// the buffer in one pass (no grid-stride loop: each wave's loads are in flight at once)
-__global__ void __launch_bounds__(256) k_stream_copy(const float4* __restrict__ src, float4* __restrict__ dst,
+// the achievable-HBM yardstick (ppgat_stream_copy): one float4 per thread, non-temporal load and
+// store, the grid covering the buffer in one pass -- the fastest of the variants measured
+// (tools/copy_lab.hip, profiles/r06/x3_copy_lab.log: 6.58 TB/s on a 1 GiB copy; 2-8 float4 per
+// thread, default-policy accesses or a grid-stride loop 4.3-6.2 TB/s)
+typedef float stream_f4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_stream_copy(const stream_f4* __restrict__ src, stream_f4* __restrict__ dst,
                                                      int64_t n4) {
-  const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x;
-  float4 v[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int64_t i = base + 256 * u;
-    if (i < n4) v[u] = src[i];
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int64_t i = base + 256 * u;
-    if (i < n4) dst[i] = v[u];
-  }
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 hipError_t launch_stream_copy(const void* src, void* dst, int64_t n_bytes, hipStream_t st) {
   const int64_t n4 = n_bytes / 16;
   if (n4 <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n4 + 1023) / 1024)), dim3(256), 0, st,
-                     static_cast<const float4*>(src), static_cast<float4*>(dst), n4);
+  hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const stream_f4*>(src), static_cast<stream_f4*>(dst), n4);
   return hipGetLastError();
 }
 

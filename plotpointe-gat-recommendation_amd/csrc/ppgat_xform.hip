@@ -1417,6 +1417,186 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tnh(TnhArg a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_gemm_tnh256: k_gemm_tnh with a 256 x 256 output tile (A's 256 columns x B's 256) when Ma is a
+// multiple of 256 (config 5's weight gradient G = g^T agg: Ma = 256, Nb = 1024).  The 128 x 256
+// tile split every staged A row once per B tile (four times) and every B row once per A tile
+// (twice): 3,072 fp16 splits per row of the product against 2,048 here (A four times, B once).
+// 16 waves (1,024 threads, four per SIMD, <= 128 registers): wave w owns A block w & 7 (32
+// columns) x B half w >> 3 (128 columns), acc[4] as in k_gemm_tnh; threads 0-511 stage the two
+// A halves, 512-1023 the two B halves, two rows x four columns of each per thread, one register
+// stage (chunk c + 1 loads while chunk c computes).  LDS: two buffers of eight [32][128] fp16
+// images (A half 0/1 and B half 0/1, hi/lo each) = 128 KB, + scales + colsum slots.  The row
+// splits are tnh_splits(M, tiles of the 128 x 256 kernel) and every output element takes
+// k_gemm_tnh's products in k_gemm_tnh's order: the same bits (tests/test_gpu_gemm_f16.py).
+// ---------------------------------------------------------------------------
+constexpr int kTh2Buf = 8 * kThImg;  // 64 KB
+constexpr size_t kTh2Lds = 2 * kTh2Buf + (2 * 256 + 2 * 256 + 16 * 256) * sizeof(float);
+
+__global__ void __launch_bounds__(1024, 1) k_gemm_tnh256(TnhArg a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char th_lds[];
+  float* const sFa = reinterpret_cast<float*>(th_lds + 2 * kTh2Buf);  // [0,256): 2^e, [256,512): 2^-e
+  float* const sFb = sFa + 2 * 256;                                   // [0,256): 2^e, [256,512): 2^-e
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int wa = w & 7, wb = w >> 3;
+  const int T = a.tiles_a * a.tiles_b;
+  const int64_t b = blockIdx.x;
+  const int64_t idx = b >> 3;
+  const int tile = (int)(idx % T);
+  const int64_t split = (b & 7) + 8 * (idx / T);  // one split's tiles share an XCD (and its L2)
+  if (split >= a.splits) return;
+  const int ta = tile % a.tiles_a, tb = tile / a.tiles_a;
+  const int64_t r0 = split * a.rows_per_split;
+  const int64_t r1 = min(a.M, r0 + a.rows_per_split);
+  const int steps = r1 > r0 ? (int)((r1 - r0 + kTR - 1) / kTR) : 0;
+  if (tid < 256) {
+    const float m = __uint_as_float(a.amax[ta * 256 + tid]);
+    const int e = (m > 0.f && m <= 3.4e38f) ? split::scale_exp16(m) : 0;
+    sFa[tid] = ldexpf(1.f, e);
+    sFa[256 + tid] = ldexpf(1.f, -e);
+  } else if (tid < 512) {
+    const int c = tid - 256;
+    const float m = __uint_as_float(a.bmax[(tb * 256 + c) % a.bperiod]) * a.bscale;
+    const int e = (m > 0.f && m <= 3.4e38f) ? split::scale_exp16(m) : 0;
+    sFb[c] = ldexpf(1.f, e);
+    sFb[256 + c] = ldexpf(1.f, -e);
+  }
+  __syncthreads();
+
+  // ---- staging: thread t -> operand t >> 9 (A / B), rows (t >> 5) & 15 and + 16 of the chunk,
+  // columns 4 (t % 32) .. +3 of both 128-column halves of that operand ----
+  const int sc = (tid & 31) * 4, slr = (tid >> 5) & 15, isb = tid >> 9;
+  const float* const src = isb ? a.B + tb * 256 + sc : a.A + ta * 256 + sc;
+  const int64_t ld = isb ? a.ldb : a.lda;
+  const float* const scl = (isb ? sFb : sFa) + sc;
+  const bool clamp = !isb && a.aclamp != 0;
+  float4 S[2][2];  // [row p][half]
+  auto load = [&](int64_t row0) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int64_t row = min(row0 + slr + 16 * p, r1 - 1);
+      S[p][0] = ld4(src + row * ld);
+      S[p][1] = ld4(src + row * ld + 128);
+    }
+  };
+  // column sums of A (cpart; the B tile 0 workgroups): the A staging thread's 4 columns of each
+  // half over its rows in chunk order, raw values, in its own LDS slots sC[slr][256]
+  const bool csum = a.cpart != nullptr && tb == 0 && !isb;
+  float4* const sCs = reinterpret_cast<float4*>(sFb + 2 * 256) + slr * 64 + (sc >> 2);  // sC: [16][256]
+  if (csum) {
+    sCs[0] = f4(0.f);
+    sCs[32] = f4(0.f);
+  }
+  auto put = [&](int buf, int64_t row0) {
+    unsigned char* img = th_lds + buf * kTh2Buf + 4 * isb * kThImg;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lr = slr + 16 * p;
+      const bool ok = row0 + lr < r1;
+      const int off = th_off(lr, sc >> 3) + 8 * ((sc >> 2) & 1);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        if (csum && ok) {
+          const float4 c = sCs[32 * hh];
+          sCs[32 * hh] = make_float4(c.x + S[p][hh].x, c.y + S[p][hh].y, c.z + S[p][hh].z, c.w + S[p][hh].w);
+        }
+        uint2 h, l;
+        split2h_4(ok ? S[p][hh] : f4(0.f), *reinterpret_cast<const float4*>(scl + 128 * hh), h, l, clamp);
+        *reinterpret_cast<uint2*>(img + 2 * hh * kThImg + off) = h;
+        *reinterpret_cast<uint2*>(img + (2 * hh + 1) * kThImg + off) = l;
+      }
+    }
+  };
+
+  // transposed-read lane address (as k_gemm_tnh): lane 4 q + p of 16-lane group g reads row q of
+  // a 4-row block, columns 4 p .. +3 of the group's 16 (16 (g & 1) within a 32-column block)
+  // th_off(row, (32 blk + c0) >> 3) + 8 ((c0 >> 2) & 1) with c0 = 16 (tg & 1) + 4 tp splits into a
+  // row part and a block part: the row's swizzle is (tq << 2) | (2 (tg >> 1) + (u & 1)) for every
+  // row this lane reads, so block blk sits at 64 (blk ^ tq) -- 9 registers instead of 20
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int c0 = 16 * (tg & 1) + 4 * tp;
+  int obase[4], oq[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = 16 * (u >> 1) + 8 * (tg >> 1) + 4 * (u & 1) + tq;
+    obase[u] = 256 * row + 16 * ((c0 >> 3) ^ (2 * (tg >> 1) + (u & 1))) + 8 * ((c0 >> 2) & 1);
+    oq[u] = 64 * (u ^ tq);
+  }
+  const int oqa = 64 * ((wa & 3) ^ tq);
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x16{};
+
+  auto compute = [&](const int buf) {
+    const unsigned char* img = th_lds + buf * kTh2Buf;
+    const unsigned char* aimg = img + 2 * (wa >> 2) * kThImg;
+    const unsigned char* bimg = img + (4 + 2 * wb) * kThImg;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      split::u32x4 fa[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint2 v = th_tr16(aimg + e * kThImg + obase[2 * ks + t] + oqa);
+          fa[e][2 * t] = v.x;
+          fa[e][2 * t + 1] = v.y;
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        split::u32x4 fb[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint2 v = th_tr16(bimg + e * kThImg + obase[2 * ks + t] + oq[q]);
+            fb[e][2 * t] = v.x;
+            fb[e][2 * t + 1] = v.y;
+          }
+        acc[q] = split::mfma32_h3(fa, fb, acc[q]);
+      }
+    }
+  };
+
+  if (steps > 0) {
+    load(r0);
+    put(0, r0);
+    __syncthreads();
+  }
+  for (int st = 0; st < steps; ++st) {
+    const bool more = st + 1 < steps;
+    if (more) load(r0 + (int64_t)(st + 1) * kTR);
+    compute(st & 1);
+    if (more) put((st + 1) & 1, r0 + (int64_t)(st + 1) * kTR);
+    __syncthreads();
+  }
+  // ---- unscale (exact powers of two) and store this split's partial ----
+  float* P = a.part + (size_t)split * a.Ma * a.Nb;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int nl = 128 * wb + 32 * t + r;
+    const float fb = sFb[256 + nl];
+    const int col = tb * 256 + nl;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ml = 32 * wa + (q & 3) + 8 * (q >> 2) + 4 * hf;
+      P[(size_t)(ta * 256 + ml) * a.Nb + col] = acc[t][q] * sFa[256 + ml] * fb;
+    }
+  }
+  if (a.cpart != nullptr && tb == 0) {  // (workgroup-uniform) the 16 row threads of each column in order
+    const float* sC = sFb + 2 * 256;
+    __syncthreads();
+    if (tid < 256) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += sC[q * 256 + tid];
+      a.cpart[(size_t)split * a.Ma + ta * 256 + tid] = s;
+    }
+  }
+}
+
 // ===========================================================================
 // aggregate-then-transform layer pieces
 // ===========================================================================
@@ -1511,10 +1691,13 @@ struct XItems {
 // ---------------------------------------------------------------------------
 // forward edge pass: one wave per destination item (CSR), the neighbour row x_j (K floats)
 // gathered ONCE per edge for all H heads: ax^h += p^h x_j with the online softmax per head.
-// K = 256: one float4 per lane, one edge at a time across the wave, 8 rows in flight.
+// K = 256: one float4 per lane, one edge at a time across the wave, U rows in flight.
 // Hub pieces leave [ax^h (K) | m | l | - -] per (item, head) for k_fwd_merge_wg.
 // ---------------------------------------------------------------------------
-template <int K, int H, int U = 8>
+// U rows in flight per wave: 4 (96 VGPRs, five waves per SIMD) -- 8 rows (144 VGPRs, three waves)
+// left the pass at 7.1 ms per call on the config-5 share, 4 gives 6.0-6.3 (profiles/r06/x2/x3_bench5_fwdx_u*.log;
+// 2, 3 and 6 within noise of 4); the FMA order per lane is the same for every U (same bits)
+template <int K, int H, int U = 4>
 __global__ void __launch_bounds__(256) k_fwd_x(XItems it, const int32_t* __restrict__ col,
                                                const int32_t* __restrict__ eid, const float* __restrict__ x,
                                                int64_t ldx, const float* __restrict__ s_src,
@@ -2755,8 +2938,27 @@ hipError_t gemm_tn_big(const float* A, int64_t lda, const float* B, int64_t ldb,
     if (e == hipSuccess && !a_bound) e = colmax_bits(A, lda, M, Ma, mx, st);
     if (e == hipSuccess && !b_bound) e = colmax_bits(B, ldb, M, Nb, mx + Ma, st);
     if (e != hipSuccess) return e;
-    const unsigned grid = (unsigned)(8 * T * ((a.splits + 7) / 8));
-    hipLaunchKernelGGL(k_gemm_tnh, dim3(grid), dim3(512), kThLds, st, a);
+#ifdef PPGAT_LAB_BUILD
+    static const bool t256 = [] {  // PPGAT_TNH256=0: the 128 x 256 tile everywhere (A/B runs)
+      const char* e = getenv("PPGAT_TNH256");
+      return !(e && strcmp(e, "0") == 0);
+    }();
+#else
+    constexpr bool t256 = true;
+#endif
+    if (t256 && Ma % 256 == 0) {  // the 256 x 256 tile, the same row splits (the same bits)
+      static const bool attr2 = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tnh256),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTh2Lds) == hipSuccess;
+      }();
+      (void)attr2;
+      a.tiles_a = Ma / 256;
+      const int T2 = a.tiles_a * a.tiles_b;
+      hipLaunchKernelGGL(k_gemm_tnh256, dim3((unsigned)(8 * T2 * ((a.splits + 7) / 8))), dim3(1024), kTh2Lds, st, a);
+    } else {
+      const unsigned grid = (unsigned)(8 * T * ((a.splits + 7) / 8));
+      hipLaunchKernelGGL(k_gemm_tnh, dim3(grid), dim3(512), kThLds, st, a);
+    }
     const int64_t n4 = (int64_t)Ma * Nb / 4;
     hipLaunchKernelGGL(k_split_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a.part, n4, a.splits, out);
     if (colsum_out)
@@ -2824,18 +3026,21 @@ hipError_t xgat_fwd(const ItemsArg& it, const int32_t* col, const int32_t* eid, 
   const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const XItems its{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
 #ifdef PPGAT_LAB_BUILD
-  static const int fu = [] {  // rows in flight per wave (PPGAT_FWDX_U: 4 / 6 / 8)
+  static const int fu = [] {  // rows in flight per wave (PPGAT_FWDX_U: 2 / 3 / 4 / 5 / 6 / 8)
     const char* e = getenv("PPGAT_FWDX_U");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 4;
   }();
 #define PPGAT_FWDX(U_)                                                                                               \
   PPGAT_XH(H, hipLaunchKernelGGL((k_fwd_x<256, HH, U_>), dim3((unsigned)((it.n_items + 3) / 4)), dim3(256), 0, st, \
                                  its, col, eid, x, ldx, s_src, s_dst, slope, p, inv_keep, seed, seed_in, agg, m, invl, \
                                  partial, xmax))
   if (it.n_items > 0) {
-    if (fu == 4) PPGAT_FWDX(4);
+    if (fu == 2) PPGAT_FWDX(2);
+    else if (fu == 3) PPGAT_FWDX(3);
+    else if (fu == 5) PPGAT_FWDX(5);
     else if (fu == 6) PPGAT_FWDX(6);
-    else PPGAT_FWDX(8);
+    else if (fu == 8) PPGAT_FWDX(8);
+    else PPGAT_FWDX(4);
   }
 #undef PPGAT_FWDX
 #else

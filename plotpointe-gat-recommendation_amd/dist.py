@@ -958,6 +958,9 @@ class _HaloLayerX(torch.autograd.Function):
                                       phases=_halo_phases(hg, rows_in, rows_out), out=dest, scores=scores,
                                       keep_agg=True)  # the halo backward's weight gradient reads agg
         rows_in.wait_all()
+        if (source_homed_backward(hg) and os.environ.get("PPGAT_XGAT_GATHER") != "g"
+                and any(ctx.needs_input_grad[:6])):
+            _ntab_forward(ctx.saved, hg, comm, stages, x_own.device)
         # links between consecutive halo layers (_halo_xgat_backward_deferred_d): this layer's
         # state for the layer above, whose backward starts this layer's exchanges early
         if link_out is not None:
@@ -1158,17 +1161,35 @@ def _bwd_tables(saved: dict, hg: "HaloGraph", comm: "Comm", stages, g_width: int
     """The backward's row tables of one multi-head halo layer: g [R, C] (own rows to be filled;
     ``g_table``: a caller's buffer) and the softmax state nstate {s_dst, m, inv_l, .} [R, 4H]
     (own rows filled here)."""
-    lib = _lib.load()
-    s_dst, m, inv_l = saved["s_dst"], saved["m"], saved["inv_l"]
-    H = saved["meta"][0]
     n0 = hg.n_own
-    ntab = HaloRows(hg, comm, stages, 4 * H, s_dst)
-    # the own rows' state straight into the table's own rows (no copy)
-    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, n0, H,
-                                     ntab.x.data_ptr(), _lib.stream_handle(dev)), "xgat_nstate")
+    ntab = saved.pop("ntab", None)  # started at the end of the forward (_ntab_forward)
+    if ntab is None:
+        ntab = _ntab_make(saved, hg, comm, stages, dev)
     nst = ntab.x[:n0]
     gtab = HaloRows(hg, comm, stages, g_width, nst, x=g_table)
     return gtab, ntab, nst
+
+
+def _ntab_make(saved: dict, hg: "HaloGraph", comm: "Comm", stages, dev) -> "HaloRows":
+    """The softmax-state table {s_dst, m, inv_l, .} [R, 4H] of a multi-head halo layer, the own
+    rows filled (straight into the table, no copy)."""
+    lib = _lib.load()
+    s_dst, m, inv_l = saved["s_dst"], saved["m"], saved["inv_l"]
+    H = saved["meta"][0]
+    ntab = HaloRows(hg, comm, stages, 4 * H, s_dst)
+    _lib.check(lib.ppgat_xgat_nstate(s_dst.data_ptr(), m.data_ptr(), inv_l.data_ptr(), None, hg.n_own, H,
+                                     ntab.x.data_ptr(), _lib.stream_handle(dev)), "xgat_nstate")
+    return ntab
+
+
+def _ntab_forward(saved: dict, hg: "HaloGraph", comm: "Comm", stages, dev):
+    """The backward's softmax state depends on the forward only: build the table and start its
+    exchange as the forward ends (the communication stream is idle then, after the next layer's
+    rows), so the backward waits only for g (saved["ntab"], taken by _bwd_tables)."""
+    ntab = _ntab_make(saved, hg, comm, stages, dev)
+    for cls in _small_class_first(hg):
+        ntab.start(cls, ntab.x[:hg.n_own])
+    saved["ntab"] = ntab
 
 
 def _bwd_start(hg: "HaloGraph", gtab: "HaloRows", ntab: "HaloRows", nst, g):
@@ -1176,7 +1197,8 @@ def _bwd_start(hg: "HaloGraph", gtab: "HaloRows", ntab: "HaloRows", nst, g):
     from the global segment sizes), so the phase that reads it starts while the other class is
     still on the wire."""
     for cls in _small_class_first(hg):
-        ntab.start(cls, nst)
+        if cls not in ntab.started:  # (not already started by the forward)
+            ntab.start(cls, nst)
         gtab.start(cls, g)
 
 

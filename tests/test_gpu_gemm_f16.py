@@ -181,6 +181,50 @@ def test_skinny_tn_vs_fp64(pkg, cuda, N, M, K):
     assert torch.equal(out, out2)
 
 
+_TNH256_CHECK = r"""
+import hashlib, importlib, json, sys, torch
+sys.path.insert(0, sys.argv[1])
+ops = importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(23)
+out = {}
+for M, Ma, Nb in ((200_000, 256, 1024), (70_001, 512, 256), (65_536, 256, 256), (130_001, 768, 512)):
+    A = torch.randn(M, Ma, device=dev, generator=g) * 1e-3
+    B = torch.randn(M, Nb, device=dev, generator=g)
+    A[5, :7] *= 1e4                                   # a row far above its columns' others
+    B[M - 1] *= 3e3                                   # the column maxima in the last row
+    G, cs = ops.gemm_tn_big(A, B, want_colsum=True)
+    Gb = ops.gemm_tn_big(A, B, b_bound=(ops.colmax_abs(B), Nb, 1.0), a_bits=ops.colmax_abs(A))
+    torch.cuda.synchronize()
+    out[f"{M}x{Ma}x{Nb}"] = [hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest() for t in (G, cs, Gb)]
+print(json.dumps(out))
+"""
+
+
+def test_tnh256_bitwise_equals_tnh(cuda):
+    """k_gemm_tnh256 (the 256 x 256 output tile, libppgat.so's TN kernel when Ma % 256 == 0) gives
+    k_gemm_tnh's bits -- the same row splits, the same products per element in the same order --
+    with the column sums and with caller bounds, on several Ma / Nb / ragged M.  The reference is
+    the lab build with PPGAT_TNH256=0 (the 128 x 256 tile everywhere).  Lab test: skips without
+    lab_build/libppgat.so (make -C plotpointe-gat-recommendation_amd/csrc lab)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    lab = root / "lab_build" / "libppgat.so"
+    if not lab.exists():
+        pytest.skip("lab build absent")
+
+    def run(env):
+        r = subprocess.run([sys.executable, "-c", _TNH256_CHECK, str(root)], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    assert run({}) == run({"PPGAT_LIB": str(lab), "PPGAT_TNH256": "0"})
+
+
 def test_tnh_bounded_equals_exact_bound(pkg, cuda):
     """ppgat_gemm_tn_big_bounded: with the exact column maxima as the bound the result is the
     unbounded call's bit for bit; with a looser bound (x-derived, as the multi-head layer passes

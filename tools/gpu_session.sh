@@ -49,6 +49,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --cpu-baseline-seconds 0 ;;
+    copylab) run copy_lab 120 tools/copy_lab ;;
     fwdxu) for u in ${FWDXU:-8 6 4}; do run "bench5_fwdx_u$u" 600 env PPGAT_LIB=lab_build/libppgat.so PPGAT_FWDX_U=$u python -u bench.py --config 5 --steps 5 --warmup 2 --graph off; done ;;
     bench5full) run bench_cfg5_full 1000 python -u bench.py --config 5 --scale 1 --steps ${FULL_STEPS:-3} --warmup 1 --graph ${FULL_GRAPH:-on} ;;
     prof5full) (cd /tmp && run rocprof_cfg5_full 1000 rocprofv3 --kernel-trace --stats -d "$OUT/prof5full" -o run --output-format csv -- python -u "$R/bench.py" --config 5 --scale 1 --steps 2 --warmup 1 --graph off) ;;
