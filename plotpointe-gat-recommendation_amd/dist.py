@@ -147,12 +147,21 @@ class Comm:
             for (_, t), (_, h) in zip(recvs, hr):
                 t.copy_(h)
 
-    def exchange(self, plan: "ExchangePlan", src: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    def exchange(self, plan: "ExchangePlan", src: torch.Tensor, out: torch.Tensor, part: Optional[int] = None
+                 ) -> torch.Tensor:
         """A plan's forward exchange without packing: the own rows of ``src`` (own-local row
         order) in each peer's send runs leave straight from ``src``; ``out`` [n_recv, ...]
         receives each peer's rows in peer order, each peer's runs back to back (the halo rows'
         order, build_halo_graph) -- no gather into a send buffer, no copy out of a receive buffer."""
         sends, recvs, off = [], [], 0
+        if part is not None:  # one of the two halves (run_plan): the other half's rows untouched
+            sp, rp = plan.parts[part]
+            for q, runs in enumerate(sp):
+                sends += [(q, src[a:a + n]) for a, n in runs if n]
+            for r, runs in enumerate(rp):
+                recvs += [(r, out[o:o + n]) for o, n in runs if n]
+            self.p2p(sends, recvs)
+            return out
         for q, runs in enumerate(plan.send_runs):
             sends += [(q, src[a:a + n]) for a, n in runs]
         for r, lens in enumerate(plan.recv_runs):
@@ -255,6 +264,7 @@ class ExchangePlan:
     # from / into the row tables; None for the loss plans (gather + all_to_all)
     send_runs: Optional[list] = None
     recv_runs: Optional[list] = None
+    parts: Optional[list] = None    # [(send runs, recv (offset, count) runs) per peer] of the two halves
 
     @property
     def n_send(self) -> int:
@@ -283,10 +293,13 @@ def _runs(b: np.ndarray):
     return st, np.flatnonzero(d == -1) - st
 
 
-def run_plan(n_own: int, masks_own: np.ndarray, base: int, world: int, recv_lens: list, device) -> ExchangePlan:
+def run_plan(n_own: int, masks_own: np.ndarray, base: int, world: int, recv: list, device) -> ExchangePlan:
     """The halo plan of one row class: own rows [base, base + len(masks_own)) in own-local order,
-    masks_own their peer sets (bit q: rank q holds the row as a halo row); ``recv_lens[r]``: the
-    run lengths rank r sends here.  send_idx = per peer (rank order) its runs expanded."""
+    masks_own their peer sets (bit q: rank q holds the row as a halo row); ``recv[r]`` = (starts,
+    lengths, class rows): the runs rank r sends here, as positions in r's own rows of the class,
+    and r's row count of the class.  send_idx = per peer (rank order) its runs expanded.
+    The plan can also move in two parts split at half of each owner's class rows (exchange
+    ``part``): a producer that finishes the first half of its rows sends them at once."""
     send_runs, idx, counts = [], [], []
     for q in range(world):
         st, ln = _runs(((masks_own >> np.uint32(q)) & np.uint32(1)).astype(bool))
@@ -294,9 +307,43 @@ def run_plan(n_own: int, masks_own: np.ndarray, base: int, world: int, recv_lens
         idx.append(np.concatenate([np.arange(a, a + n) for a, n in send_runs[-1]]) if len(st) else
                    np.zeros(0, np.int64))
         counts.append(int(ln.sum()))
-    recv_runs = [[int(n) for n in lens] for lens in recv_lens]
-    return make_plan(n_own, np.concatenate(idx) if idx else np.zeros(0, np.int64), counts,
+    recv_runs = [[int(n) for n in ln] for _, ln, _ in recv]
+    plan = make_plan(n_own, np.concatenate(idx) if idx else np.zeros(0, np.int64), counts,
                      [sum(l) for l in recv_runs], device, send_runs, recv_runs)
+    # the two parts: sends clipped at base + len // 2; each owner's runs clipped at its class // 2,
+    # landing at their places inside that owner's block of the halo slice
+    cut = base + len(masks_own) // 2
+    sp = [[], []]
+    for runs in send_runs:
+        lo, hi = [], []
+        for a, n in runs:
+            if a + n <= cut:
+                lo.append((a, n))
+            elif a >= cut:
+                hi.append((a, n))
+            else:
+                lo.append((a, cut - a))
+                hi.append((cut, a + n - cut))
+        sp[0].append(lo)
+        sp[1].append(hi)
+    rp, off = [[], []], 0
+    for st, ln, cnt in recv:
+        ocut = int(cnt) // 2
+        lo, hi = [], []
+        for a, n in zip(st, ln):
+            a, n = int(a), int(n)
+            if a + n <= ocut:
+                lo.append((off, n))
+            elif a >= ocut:
+                hi.append((off, n))
+            else:
+                lo.append((off, ocut - a))
+                hi.append((off + ocut - a, a + n - ocut))
+            off += n
+        rp[0].append(lo)
+        rp[1].append(hi)
+    plan.parts = [(sp[0], rp[0]), (sp[1], rp[1])]
+    return plan
 
 
 def peer_masks(src: np.ndarray, od: np.ndarray, owner: np.ndarray, world: int) -> np.ndarray:
@@ -630,8 +677,9 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
     lidx[halo_u] = n_own + np.arange(len(halo_u))
     lidx[halo_i] = n_own + len(halo_u) + np.arange(len(halo_i))
     # what each owner r sends here: the runs of its rows (in its order) whose peer set holds this rank
-    recv_u = [_runs(need[go[bnd[2 * r]:bnd[2 * r + 1]]])[1] for r in range(world)]
-    recv_i = [_runs(need[go[bnd[2 * r + 1]:bnd[2 * r + 2]]])[1] for r in range(world)]
+    recv_u = [_runs(need[go[bnd[2 * r]:bnd[2 * r + 1]]]) + (bnd[2 * r + 1] - bnd[2 * r],) for r in range(world)]
+    recv_i = [_runs(need[go[bnd[2 * r + 1]:bnd[2 * r + 2]]]) + (bnd[2 * r + 2] - bnd[2 * r + 1],)
+              for r in range(world)]
     plan_u = run_plan(n_own, mask[own_u], 0, world, recv_u, dev)
     plan_i = run_plan(n_own, mask[own_it], len(own_u), world, recv_i, dev)
     del go, mask, need
@@ -687,6 +735,14 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
         # other class, so a phase needs only that class's halo rows; _HaloLayerX)
         hg.fwd_sched_u = sched_builder(rowptr_own[:hg.n_own_u + 1].contiguous(), El)
         hg.fwd_sched_i = sched_builder(rowptr_own[hg.n_own_u:].contiguous(), El)
+        if int(os.environ.get("PPGAT_HALO_PARTS", "2")) == 2:
+            # each class's destinations in two halves (_halo_phases), split where the plans split
+            nu_, n0_ = hg.n_own_u, n_own
+            mu, mi = nu_ // 2, nu_ + (n0_ - nu_) // 2
+            hg.fwd_sched_halves = {"u": (sched_builder(rowptr_own[:mu + 1].contiguous(), El),
+                                         sched_builder(rowptr_own[mu:nu_ + 1].contiguous(), El)),
+                                   "i": (sched_builder(rowptr_own[nu_:mi + 1].contiguous(), El),
+                                         sched_builder(rowptr_own[mi:].contiguous(), El))}
         if hg.src_views is not None:
             sv = hg.src_views
             sv.fwd_sched = sched_builder(sv.rowptr, sv.n_edges)   # destination sums over the R table rows
@@ -814,17 +870,21 @@ class HaloRows:
             self.x[a:b].copy_(rows)
         self.local.add(cls)
 
-    def start(self, cls, src: torch.Tensor):
-        """Send the own rows of ``src`` (own-local row order) of class ``cls`` to the peers."""
+    def start(self, cls, src: torch.Tensor, part: Optional[int] = None):
+        """Send the own rows of ``src`` (own-local row order) of class ``cls`` to the peers;
+        ``part`` (0 / 1): only that half of the class (run_plan), the other half sent by a later
+        call -- wait(cls) then waits for both (one stream: the last event covers the first)."""
         plan, (a, b) = self.plan(cls), self.span(cls)
-        self.started.append(cls)
+        if cls not in self.started:
+            self.started.append(cls)
         comm, st = self.comm, self.stages
         n0 = self.hg.n_own
+        kw = {} if part is None else {"part": part}
 
         def send():  # straight from the own rows into the table's halo slice (no pack, no unpack)
-            comm.exchange(plan, src, self.x[a:b])
+            comm.exchange(plan, src, self.x[a:b], **kw)
             if self.s is not None:
-                comm.exchange(plan, self.s[:n0], self.s[a:b])
+                comm.exchange(plan, self.s[:n0], self.s[a:b], **kw)
         if comm.backend != "nccl" or not comm.active:
             send()
             return
@@ -884,14 +944,14 @@ def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows
     rows of that destination class).  Otherwise one phase after both classes."""
     from .hip_ops import XPhase
 
-    def send(cls, d0=0, d1=0):
+    def send(cls, d0=0, d1=0, part=None):
         if rows_out is None:
             return lambda out: None
 
         def go(out):
             if rows_out.s is not None:  # the next layer's scores of the rows this phase produced
                 rows_out.score_rows(out, d0, d1)
-            rows_out.start(cls, out)
+            rows_out.start(cls, out, part)
         return go
     if not (hg.bipartite and hg.fwd_sched_u is not None and hg.fwd_sched_i is not None):
         def after_all(out):
@@ -906,8 +966,22 @@ def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows
     ph = {"u": (0, hg.n_own_u, hg.fwd_sched_u, "i"), "i": (hg.n_own_u, hg.n_own, hg.fwd_sched_i, "u")}
     order = sorted(ph, key=lambda d: (ph[d][3] not in rows_in.local,
                                       rows_in.started.index(ph[d][3]) if ph[d][3] in rows_in.started else 0))
-    return [XPhase(ph[d][0], ph[d][1], ph[d][2], (rows_in.span(ph[d][3]),),
-                   (lambda c: (lambda: rows_in.wait(c)))(ph[d][3]), send(d, ph[d][0], ph[d][1])) for d in order]
+    halves = getattr(hg, "fwd_sched_halves", None) if rows_out is not None else None
+    if not halves:
+        return [XPhase(ph[d][0], ph[d][1], ph[d][2], (rows_in.span(ph[d][3]),),
+                       (lambda c: (lambda: rows_in.wait(c)))(ph[d][3]), send(d, ph[d][0], ph[d][1])) for d in order]
+    # each destination class in two halves (the plans' parts): the first half's output rows start
+    # towards the peers while the second half is computed, so the next layer's rows arrive half a
+    # phase earlier.  Per destination the same kernels and order as one phase: the same results.
+    out = []
+    for d in order:
+        d0, d1, _, need = ph[d]
+        dm = d0 + (d1 - d0) // 2
+        (s0, s1) = halves[d]
+        out.append(XPhase(d0, dm, s0, (rows_in.span(need),), (lambda c: (lambda: rows_in.wait(c)))(need),
+                          send(d, d0, dm, 0)))
+        out.append(XPhase(dm, d1, s1, (), None, send(d, dm, d1, 1)))
+    return out
 
 
 class _HaloLayerX(torch.autograd.Function):
@@ -1331,8 +1405,25 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     if below is not None and n0:
         # the layer below's g = this dx: straight into its table, its exchanges started now
         gtab1, ntab1, nst1 = _bwd_tables(below, hg, comm, stages, K, dev)
-        dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K)), out=gtab1.x[:n0])
-        _bwd_start(hg, gtab1, ntab1, nst1, dx)
+        dx = gtab1.x[:n0]
+        A2 = A.view(2 * H, K)
+        if getattr(hg, "fwd_sched_halves", None) and hg.bipartite:
+            # the GEMM by class in exchange order, the larger class in the plans' two halves, each
+            # piece's rows sent as soon as they exist (per row the same kernel: the same bits)
+            nu = hg.n_own_u
+            span = {"u": (0, nu), "i": (nu, n0)}
+            for k, cls in enumerate(_small_class_first(hg)):
+                c0, c1 = span[cls]
+                cuts = [(c0, c1, None)] if k == 0 else [(c0, c0 + (c1 - c0) // 2, 0), (c0 + (c1 - c0) // 2, c1, 1)]
+                if cls not in ntab1.started:
+                    ntab1.start(cls, nst1)
+                for p0, p1, part in cuts:
+                    if p1 > p0:
+                        O.gemm_nn(acc[p0:p1], W, 0, K, alpha=1.0 / H, rank=(S[p0:p1], A2), out=dx[p0:p1])
+                    gtab1.start(cls, dx, part)
+        else:
+            O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A2), out=dx)
+            _bwd_start(hg, gtab1, ntab1, nst1, dx)
         link_in["pre"] = (gtab1, ntab1, nst1)
     else:
         dx = O.gemm_nn(acc[:n0], W, 0, K, alpha=1.0 / H, rank=(S, A.view(2 * H, K))) if n0 else \

@@ -251,3 +251,60 @@ def test_small_class_first_is_global():
     D = importlib.import_module("plotpointe-gat-recommendation_amd.dist")
     assert D._small_class_first(SimpleNamespace(n_nodes=15, n_users=10)) == ("i", "u")
     assert D._small_class_first(SimpleNamespace(n_nodes=15, n_users=5)) == ("u", "i")
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_halo_runs_deliver_every_row(world):
+    """The halo plans' runs (dist.run_plan: own rows in peer-set Gray order, Comm.exchange sending
+    runs of the row table): emulating every rank's point-to-point calls in one process, each rank's
+    halo slice receives exactly its halo rows' node ids -- whole plans and the two halves alike, the
+    k-th send of r to q matching the k-th receive of q from r in size; each row in exactly one half."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _cpu_stages import csr_builder
+    pkg, g, ei, feats, full, _ = _setup(n_users=400, n_items=150, n_int=4000)
+    D = pkg.dist
+    hgs = [D.build_halo_graph(ei, g.n_nodes, g.n_users, world, r, csr_builder=csr_builder, sched_builder=None)
+           for r in range(world)]
+    ids = [torch.from_numpy(h.own_node_ids().astype(np.float64))[:, None] for h in hgs]
+
+    def emulate(plan_of, part):
+        got = []
+        for q, hq in enumerate(hgs):
+            pq = plan_of(hq)
+            out = torch.full((pq.n_recv, 1), -1.0, dtype=torch.float64)
+            for r, hr in enumerate(hgs):
+                pr = plan_of(hr)
+                if part is None:
+                    sends = [ids[r][a:a + n] for a, n in pr.send_runs[q]]
+                    offs, lens, o = [], [], int(sum(sum(l) for l in pq.recv_runs[:r]))
+                    for n in pq.recv_runs[r]:
+                        offs.append(o)
+                        lens.append(n)
+                        o += n
+                else:
+                    sends = [ids[r][a:a + n] for a, n in pr.parts[part][0][q] if n]
+                    rr = [(o, n) for o, n in pq.parts[part][1][r] if n]
+                    offs, lens = [o for o, _ in rr], [n for _, n in rr]
+                assert [len(t) for t in sends] == lens, (r, q, part)
+                for t, o in zip(sends, offs):
+                    out[o:o + len(t)] = t
+            got.append(out)
+        return got
+    for cls, plan_of, span in (("u", lambda h: h.plan_u, lambda h: (h.n_own, h.n_own + h.n_halo_u)),
+                               ("i", lambda h: h.plan_i, lambda h: (h.n_own + h.n_halo_u, h.R))):
+        whole = emulate(plan_of, None)
+        halves = [emulate(plan_of, k) for k in (0, 1)]
+        for q, hq in enumerate(hgs):
+            a, b = span(hq)
+            # the halo rows of the table: recovered through the CSR columns' node ids (every halo
+            # row is some local edge's source), compared with what the runs delivered
+            src_ids = ei[0].numpy()[hq.fwd_view.csr_eid.long().numpy()]
+            cols = hq.fwd_view.col.long().numpy()
+            table = np.full(hq.R, -1, np.int64)
+            table[cols] = src_ids
+            exp = table[a:b]
+            assert (exp >= 0).all()
+            assert np.array_equal(whole[q][:, 0].numpy().astype(np.int64), exp), (cls, q)
+            merged = torch.where(halves[0][q] >= 0, halves[0][q], halves[1][q])
+            assert np.array_equal(merged[:, 0].numpy().astype(np.int64), exp), (cls, q)
+            assert ((halves[0][q] >= 0) != (halves[1][q] >= 0)).all()  # each row in exactly one half

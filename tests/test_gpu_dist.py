@@ -473,7 +473,7 @@ class _StubComm2(_StubComm):
 
     # the halo plans' run exchanges (dist.Comm.exchange / exchange_back): the rows the runs send,
     # then the same slow, data-changing stand-in
-    def exchange(self, plan, src, out):
+    def exchange(self, plan, src, out, part=None):  # (a part rewrites the whole slice the same way)
         return self.all_to_all_rows(src[plan.send_idx], plan.send_counts, plan.recv_counts, out=out)
 
     def exchange_back(self, plan, halo, out=None):

@@ -33,8 +33,8 @@ for s in $STEPS; do
     traj) for v in default:PPGAT_NONE=1 fuseddxw0:PPGAT_FUSED_DXW=0 gemmfp32:PPGAT_GEMM=fp32; do
             run "traj_${v%%:*}" 900 env PPGAT_REPORT_TAG="${v%%:*}" "${v#*:}" python -u -m pytest tests/test_gpu_trajectory.py -m gpu -v -s -rf --timeout 800 --timeout-method thread
           done ;;
-    probe5) for a in ${PROBES:-0:0 7:0 7:640}; do set -- ${a%%:*} ${a#*:}
-              run "probe5_r$1_a$2" 900 python -u tools/scale_probe.py --config 5 --world 8 --rank $1 --streams --a2a-gbs $2 --steps 5 --warmup 2 ${PROBE_ARGS:-}
+    probe5) for a in ${PROBES:-0:0 7:0 7:640}; do IFS=: read -r pr pg pe <<< "$a"
+              run "probe5_r${pr}_a${pg}${pe:+_${pe//=/}}" 900 env ${pe:-PPGAT_NONE=1} python -u tools/scale_probe.py --config 5 --world 8 --rank $pr --streams --a2a-gbs $pg --steps 5 --warmup 2 ${PROBE_ARGS:-}
             done ;;
     gemm5) run gemm5_nnh 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH2=0 python tools/bench_gemm.py --cfg5 --iters 10 && \
            run gemm5_nnh2 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH2=2 python tools/bench_gemm.py --cfg5 --iters 10 && \
@@ -43,8 +43,16 @@ for s in $STEPS; do
             (cd /tmp && run pmcdst_b 300 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum --kernel-trace --output-format csv -d "$OUT/pmcdst_b" -o b -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) && \
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
             python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
+    tnpmc) run tn5_256 120 python tools/bench_gemm.py --tn5 --iters 10 && \
+           run tn5_128 120 env PPGAT_LIB=lab_build/libppgat.so PPGAT_TNH256=0 python tools/bench_gemm.py --tn5 --iters 10 && \
+           run tnpmc256 400 env GEMM_ARGS=--tn5 GEMM_TAG=_tn256 bash tools/gemm_pmc.sh && \
+           python tools/pmc_kernel.py "k_gemm_tnh256" "$OUT/gemm_pmc_tn256/p1" "$OUT/gemm_pmc_tn256/p2" "$OUT/gemm_pmc_tn256/p3" > "$OUT/tn256_pmc.json" ;;
     nnhpmc) run "nnhpmc${NNHV:-3}" 500 env GEMM_ARGS=--cfg5 GEMM_TAG="_nnh${NNHV:-3}" PPGAT_NNH2="${NNHV:-3}" bash tools/gemm_pmc.sh ;;
     nnhlab) for l in ${LABS:-0 1 2 3}; do run "nnhlab$l" 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH2_LAB=$l python tools/bench_gemm.py --cfg5 --iters 10; done ;;
+    probec2) for a in ${C2PROBES:-2:300 4:300 8:300 8:0}; do set -- ${a%%:*} ${a#*:}
+              run "probec2_w$1_a$2" 300 python -u tools/scale_probe.py --world $1 --rank 0 --graph --streams --a2a-gbs $2 --steps 20 --warmup 5
+            done ;;
+    profprobe640) (cd /tmp && run rocprof_probe5_640 900 rocprofv3 --kernel-trace --stats -d "$OUT/profprobe640" -o run --output-format csv -- python "$R/tools/scale_probe.py" --config 5 --world 8 --rank ${PROBE_RANK:-0} --streams --a2a-gbs 640 --steps 3 --warmup 1) ;;
     profprobe) (cd /tmp && run rocprof_probe5 900 rocprofv3 --kernel-trace --stats -d "$OUT/profprobe" -o run --output-format csv -- python "$R/tools/scale_probe.py" --config 5 --world 8 --rank ${PROBE_RANK:-7} --streams --steps 3 --warmup 1) ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;

@@ -75,11 +75,17 @@ class NullComm:
                 out = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         return out
 
-    def exchange(self, plan, src, out):
+    def exchange(self, plan, src, out, part=None):
         """Comm.exchange stub: the plan's rows are not moved (timing only); holds the stream for
-        max(rows sent, rows received) x row bytes."""
+        max(rows sent, rows received) x row bytes (of the part's runs when ``part`` is given)."""
         row = (src[0].numel() if src.dim() and src.size(0) else int(np.prod(src.shape[1:]))) * src.element_size()
-        self._hold(max(plan.n_send, plan.n_recv) * row)
+        if part is None:
+            ns, nr = plan.n_send, plan.n_recv
+        else:
+            sp, rp = plan.parts[part]
+            ns = sum(n for runs in sp for _, n in runs)
+            nr = sum(n for runs in rp for _, n in runs)
+        self._hold(max(ns, nr) * row)
         return out
 
     def exchange_back(self, plan, halo, out=None):
