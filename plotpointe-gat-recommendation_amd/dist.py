@@ -524,6 +524,7 @@ class HaloGraph:
     own_items: torch.Tensor = None # [n_own - n_own_u] int64 item indices (node id - n_users), own-local order
     own_pos: np.ndarray = None     # [N] int32: each node's row at its owner (host)
     own_users: np.ndarray = None   # [n_own_u] int64: the own users' node ids in own-local order (host)
+    halo_ids: np.ndarray = None    # [n_halo] int64: the halo rows' node ids in table order (host)
     item_partition: str = "dealt"
     # symmetric edge list (every column j -> i has its i -> j, as build_edge_index's U-I graph):
     # the rows a rank needs as sources (forward) are exactly the rows it needs as destinations of
@@ -699,6 +700,7 @@ def build_halo_graph(edge_index: torch.Tensor, n_nodes: int, n_users: int, world
                    owner, {}, torch.from_numpy(halo_i - nu).to(dev))
     hg.own_items = torch.from_numpy(own_items - nu).to(dev)
     hg.own_pos = own_pos
+    hg.halo_ids = halo
     hg.own_users = own_u
     hg.item_partition = item_partition
     hg.n_own_u = u1 - u0
@@ -885,6 +887,29 @@ class HaloRows:
             comm.exchange(plan, src, self.x[a:b], **kw)
             if self.s is not None:
                 comm.exchange(plan, self.s[:n0], self.s[a:b], **kw)
+        self._launch(cls, send, src)
+
+    def start_touched(self, cls, src: torch.Tensor, tp: "TouchPlan"):
+        """start() for a table whose halo rows are zero except the rows ``tp`` lists (the loss's
+        gradient: nonzero only on the rows the triples touch, _touch_plans): only those rows
+        travel -- gathered at the owner, one all_to_all, scattered into their places in the
+        halo slice; every other halo row keeps the zero the table holds (the caller's part)."""
+        a, b = self.span(cls)
+        if cls not in self.started:
+            self.started.append(cls)
+        comm, st = self.comm, self.stages
+
+        def send():
+            buf = st.gather_rows(src, tp.send_idx) if tp.n_send else src.new_empty((0, src.size(1)))
+            got = comm.all_to_all_rows(buf, tp.send_counts, tp.recv_counts)
+            if tp.n_recv:
+                self.x[a:b].index_copy_(0, tp.recv_pos, got)
+        self._launch(cls, send, src)
+
+    def _launch(self, cls, send, src):
+        """Run ``send`` on the communication stream (RCCL) after the current stream's work so
+        far, recording the class's event; inline under gloo or an inactive communicator."""
+        comm = self.comm
         if comm.backend != "nccl" or not comm.active:
             send()
             return
@@ -1307,7 +1332,19 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
         # rows' gradients, already returned to their owners in stream order before this point)
         gtab, ntab, nst = _bwd_tables(saved, hg, comm, stages, C, dev,
                                       g_table=g.new_empty(0).set_(g.untyped_storage(), 0, (R, C), (C, 1)))
-        _bwd_start(hg, gtab, ntab, nst, g)
+        touch = getattr(hg, "top_touch", None)
+        if touch is not None and touch["buf"] is not None and touch["buf"].data_ptr() == g.data_ptr():
+            # the persistent table of halo_bpr_loss: only the touched rows travel; the rows the
+            # loss's own exchange received (now returned to their owners) go back to zero first
+            tail = int(getattr(hg, "loss_tail_rows", 0))
+            if tail:
+                gtab.x[n0:n0 + tail].zero_()
+            for cls in order:
+                if cls not in ntab.started:
+                    ntab.start(cls, nst)
+                gtab.start_touched(cls, g, touch[cls])
+        else:
+            _bwd_start(hg, gtab, ntab, nst, g)
     elif pre is not None:
         # started by the layer above from its dx, which is g when nothing sits between the two
         # layers (HaloPyGGAT links a layer only to the one consumer of its output).  If autograd
@@ -1643,6 +1680,79 @@ class HaloPyGGAT(_ShardedBase):
         return x
 
 
+@dataclass
+class TouchPlan:
+    """One halo class of the top layer's g exchange restricted to the rows the loss touches
+    (_touch_plans): this rank's own rows ``send_idx`` (per peer in rank order, ``send_counts``),
+    and the positions ``recv_pos`` in the class's halo slice of the rows each owner sends here
+    (owners in rank order, ``recv_counts``)."""
+    send_idx: torch.Tensor      # int64 [n_send] own-local rows
+    send_counts: list
+    recv_pos: torch.Tensor      # int64 [n_recv] rows of the class's halo slice
+    recv_counts: list
+
+    @property
+    def n_send(self) -> int:
+        return int(sum(self.send_counts))
+
+    @property
+    def n_recv(self) -> int:
+        return int(sum(self.recv_counts))
+
+
+def _touch_plans(hg: HaloGraph, comm: "Comm", un: np.ndarray, inn: np.ndarray, jn: np.ndarray, dev):
+    """The loss reads the rows of the triples only (users u, items i and j,
+    train_gat_pyg.py:313-322), so the top layer's incoming gradient is exactly zero on every
+    other row (the loss backward writes those zeros).  The top layer's source-homed backward
+    needs g of its halo rows: only the touched ones carry anything, a few percent of the 9M
+    halo rows at config 5 -- so they alone travel (HaloRows.start_touched) and the rest of the
+    table stays zero, the same table the dense exchange would deliver, bit for bit.
+
+    Every rank derives the touched set from the full triple arrays it was given (each rank
+    passes the same draw and keeps its own users' triples, _loss_plan), so the plans need no
+    exchange; one all_reduce of a hash of the arrays confirms the ranks agree, else (or with
+    PPGAT_SPARSE_TOP_G=0, or the destination-homed backward) the dense exchange stays: None.
+    -> {"u": TouchPlan, "i": TouchPlan, "buf": None (the persistent zeroed g table, made by
+    halo_bpr_loss)}."""
+    if hg.src_views is None or hg.halo_ids is None or os.environ.get("PPGAT_SPARSE_TOP_G", "1") == "0":
+        return None
+    nu, N, n0 = hg.n_users, hg.n_nodes, hg.n_own
+    rows = np.concatenate([un, inn + nu, jn + nu]).astype(np.int64)
+    with np.errstate(over="ignore"):
+        h = int(_mix64(rows.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15) +
+                       np.arange(len(rows), dtype=np.uint64)).sum(dtype=np.uint64) >> np.uint64(2))
+    chk = torch.tensor([h, -h], dtype=torch.int64, device=dev if comm.backend == "nccl" else "cpu")
+    chk = comm.all_reduce_(chk, op=dist.ReduceOp.MAX).cpu()
+    if int(chk[0]) != -int(chk[1]):
+        return None  # different triple sets on different ranks: keep the dense exchange
+    T = np.zeros(N, bool)
+    T[rows[(rows >= 0) & (rows < N)]] = True
+    own = np.flatnonzero(hg.local_of >= 0)
+    own_ids = np.empty(n0, np.int64)
+    own_ids[hg.local_of[own]] = own
+    t_own = T[own_ids]
+    out = {"buf": None}
+    halo_t = T[hg.halo_ids]
+    for cls, plan, h0 in (("u", hg.plan_u, 0), ("i", hg.plan_i, hg.n_halo_u)):
+        sidx, scnt = [], []
+        for runs in plan.send_runs:
+            idx = (np.concatenate([np.arange(a, a + n, dtype=np.int64) for a, n in runs]) if runs
+                   else np.zeros(0, np.int64))
+            idx = idx[t_own[idx]]
+            sidx.append(idx)
+            scnt.append(len(idx))
+        tm = halo_t[h0:h0 + plan.n_recv]
+        rpos, rcnt, off = [], [], 0
+        for c in plan.recv_counts:
+            p_ = np.flatnonzero(tm[off:off + c]) + off
+            rpos.append(p_)
+            rcnt.append(len(p_))
+            off += c
+        out[cls] = TouchPlan(torch.from_numpy(np.concatenate(sidx)).to(dev), scnt,
+                             torch.from_numpy(np.concatenate(rpos).astype(np.int64)).to(dev), rcnt)
+    return out
+
+
 def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j, plan_key=None):
     """Exchange plan + row map for the triples of this rank's own users: the item rows they
     read that other ranks own come by one all_to_all.
@@ -1676,7 +1786,7 @@ def _loss_plan(hg: HaloGraph, comm: "Comm", u, i, j, plan_key=None):
     own_items = items[hg.owner[items] == hg.rank]
     rmap[own_items] = hg.local_of[own_items]
     rmap[req] = hg.n_own + np.arange(len(req))
-    res = (plan, torch.from_numpy(rmap.astype(np.int32)).to(dev))
+    res = (plan, torch.from_numpy(rmap.astype(np.int32)).to(dev), _touch_plans(hg, comm, un, inn, jn, dev))
     hg.loss_plans.clear()  # one live triple set at a time (an epoch's draw)
     if plan_key is not None:
         hg.loss_plans[plan_key] = res
@@ -1691,13 +1801,23 @@ def halo_bpr_loss(Z_own, hg: HaloGraph, comm: "Comm", u, i, j, n_users: int, n_i
     if stages is None:
         from .hip_ops import HipStages
         stages = HipStages()
-    plan, rmap = _loss_plan(hg, comm, u, i, j, plan_key)
+    plan, rmap, touch = _loss_plan(hg, comm, u, i, j, plan_key)
     hg.loss_tail_rows = plan.n_recv  # the next forward's top layer leaves room for these rows
     grad_rows = int(getattr(hg, "loss_grad_rows", 0))
     hg.grad_handoff = {}
+    hg.top_touch = None
     Zl = exchange(Z_own, plan, comm, stages, inplace_grad=True, handoff=hg.grad_handoff if grad_rows else None)
     if grad_rows and getattr(stages, "bpr_grad_rows", False):
         # dZ inside an [R, C] buffer: the top layer's backward uses it as its g table (no copy)
+        if touch is not None and grad_rows == hg.R:
+            # ... a persistent one, zeroed once per triple set: the touched rows' exchange
+            # (_touch_plans) leaves every other halo row of it at that zero
+            C = Z_own.size(1)
+            buf = touch["buf"]
+            if buf is None or buf.shape != (hg.R, C) or buf.dtype != Z_own.dtype or buf.device != Z_own.device:
+                buf = touch["buf"] = torch.zeros(hg.R, C, dtype=Z_own.dtype, device=Z_own.device)
+            hg.top_touch = touch
+            return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss, grad_rows=grad_rows, grad_buf=buf)
         return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss, grad_rows=grad_rows)
     return stages.bpr(Zl, n_users, n_items, rmap, u, i, j, loss)
 

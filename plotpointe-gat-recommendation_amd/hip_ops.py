@@ -1776,9 +1776,11 @@ def bpr_prepare(n_rows: int, n_users: int, n_items: int, C: int, u, i, j, row_ma
 
 class _BPRLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map, prep=None, grad_rows: int = 0):
+    def forward(ctx, Z, u, i, j, n_users: int, n_items: int, kind: int, row_map, prep=None, grad_rows: int = 0,
+                grad_buf=None):
         lib = _lib.load()
         ctx.grad_rows = int(grad_rows)
+        ctx.grad_buf = grad_buf
         # Z straight from a heads = 1 GATLayer: the loss backward also does that layer's prologue
         ctx.producer = (_producer_of(Z, N=Z.size(0), C=Z.size(1))
                         if (row_map is None and prep is None and _producer_fusion_enabled()) else None)
@@ -1824,8 +1826,16 @@ class _BPRLoss(torch.autograd.Function):
         gl = gl.reshape(1).to(torch.float32).contiguous()
         # grad_rows > n_rows: dZ is the top of a [grad_rows, C] buffer (the halo partition's top
         # layer takes the buffer as its gradient table, dist._halo_xgat_backward_deferred_d)
-        dZ = (torch.empty(ctx.grad_rows, C, dtype=Z.dtype, device=Z.device)[:n_rows] if ctx.grad_rows > n_rows
-              else torch.empty_like(Z))
+        # (``grad_buf``: that buffer, the caller's persistent one -- its rows past n_rows are the caller's)
+        buf, ctx.grad_buf = ctx.grad_buf, None
+        if buf is not None:
+            _require(buf.dim() == 2 and buf.size(0) >= n_rows and buf.size(1) == C and buf.dtype == Z.dtype and
+                     buf.device == Z.device and buf.is_contiguous(), "bpr: grad_buf must be a contiguous "
+                     "[>= n_rows, C] buffer of Z's dtype and device")
+            dZ = buf[:n_rows]
+        else:
+            dZ = (torch.empty(ctx.grad_rows, C, dtype=Z.dtype, device=Z.device)[:n_rows] if ctx.grad_rows > n_rows
+                  else torch.empty_like(Z))
         ws = ctx.ws
         prod, ctx.producer = ctx.producer, None
         if prod is not None and prod.pro_state is not None:
@@ -1845,7 +1855,7 @@ class _BPRLoss(torch.autograd.Function):
                           i.data_ptr(), j.data_ptr(), S, coef.data_ptr(), gl.data_ptr(), dZ.data_ptr(), ws.data_ptr(),
                           ws.numel(), _lib.stream_handle(Z.device)), "bpr_bwd")
         ctx.ws = None
-        return dZ, None, None, None, None, None, None, None, None, None
+        return dZ, None, None, None, None, None, None, None, None, None, None
 
 
 def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr", prepared: BprPrepared = None) -> torch.Tensor:
@@ -1858,12 +1868,15 @@ def bpr_loss(Z: torch.Tensor, n_users: int, u, i, j, loss: str = "bpr", prepared
 
 
 def bpr_loss_mapped(Z: torch.Tensor, n_users: int, n_items: int, row_map: torch.Tensor, u, i, j,
-                    loss: str = "bpr", prepared: BprPrepared = None, grad_rows: int = 0) -> torch.Tensor:
+                    loss: str = "bpr", prepared: BprPrepared = None, grad_rows: int = 0,
+                    grad_buf: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bpr_loss over a Z whose rows are laid out by row_map (node id -> row).  ``grad_rows``: the
-    gradient of Z is the top of a buffer of that many rows (the rest is the caller's)."""
+    gradient of Z is the top of a buffer of that many rows (the rest is the caller's);
+    ``grad_buf``: that buffer, supplied by the caller (kept across steps)."""
     if Z.size(1) not in (32, 64, 128, 256):
         raise NotImplementedError("bpr_loss: hidden size must be 32/64/128/256")
-    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map, prepared, grad_rows)
+    return _BPRLoss.apply(Z, u, i, j, int(n_users), int(n_items), LOSS_KINDS[loss], row_map, prepared, grad_rows,
+                          grad_buf)
 
 
 # ---------------------------------------------------------------------------
@@ -1907,8 +1920,8 @@ class HipStages:
 
     bpr_grad_rows = True  # bpr() takes grad_rows (dist.halo_bpr_loss)
 
-    def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss, grad_rows: int = 0):
-        return bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, loss, grad_rows=grad_rows)
+    def bpr(self, Z, n_users, n_items, row_map, u, i, j, loss, grad_rows: int = 0, grad_buf=None):
+        return bpr_loss_mapped(Z, n_users, n_items, row_map, u, i, j, loss, grad_rows=grad_rows, grad_buf=grad_buf)
 
     def scores(self, h, att_src, att_dst, heads, channels):
         return node_scores(h, att_src, att_dst, heads, channels)

@@ -308,3 +308,48 @@ def test_halo_runs_deliver_every_row(world):
             merged = torch.where(halves[0][q] >= 0, halves[0][q], halves[1][q])
             assert np.array_equal(merged[:, 0].numpy().astype(np.int64), exp), (cls, q)
             assert ((halves[0][q] >= 0) != (halves[1][q] >= 0)).all()  # each row in exactly one half
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_touch_plans_deliver_touched_rows(world):
+    """dist._touch_plans (the top layer's g exchange, touched rows only): emulating every rank's
+    gather + all_to_all + scatter in one process, each rank's halo slice holds exactly the rows
+    the dense exchange delivers wherever the triples touch a row, and the zero of the table
+    elsewhere -- where the dense exchange delivers the owner's zero rows.  hg.halo_ids names the
+    halo rows as the CSR columns do."""
+    from types import SimpleNamespace
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _cpu_stages import csr_builder
+    pkg, g, ei, feats, full, (u, i, j) = _setup(n_users=400, n_items=150, n_int=4000)
+    D = pkg.dist
+    hgs = [D.build_halo_graph(ei, g.n_nodes, g.n_users, world, r, csr_builder=csr_builder, sched_builder=None)
+           for r in range(world)]
+    comm = SimpleNamespace(backend="gloo", all_reduce_=lambda t, op=None: t)
+    un, inn, jn = (t.numpy().astype(np.int64) for t in (u, i, j))
+    tps = [D._touch_plans(h, comm, un, inn, jn, "cpu") for h in hgs]
+    touched = np.zeros(g.n_nodes, bool)
+    touched[np.concatenate([un, inn + g.n_users, jn + g.n_users])] = True
+    assert 0 < touched.sum() < g.n_nodes
+    for cls in ("u", "i"):
+        for q, hq in enumerate(hgs):
+            a, b = (hq.n_own, hq.n_own + hq.n_halo_u) if cls == "u" else (hq.n_own + hq.n_halo_u, hq.R)
+            src_ids = ei[0].numpy()[hq.fwd_view.csr_eid.long().numpy()]
+            table = np.full(hq.R, -1, np.int64)
+            table[hq.fwd_view.col.long().numpy()] = src_ids
+            assert np.array_equal(hq.halo_ids, table[hq.n_own:])
+            tq = tps[q][cls]
+            got = np.full(b - a, -1, np.int64)
+            chunks = []
+            for r, hr in enumerate(hgs):
+                tr = tps[r][cls]
+                own_ids = hr.own_node_ids()
+                s0 = int(sum(tr.send_counts[:q]))
+                sent = own_ids[tr.send_idx.numpy()[s0:s0 + tr.send_counts[q]]]
+                assert len(sent) == tq.recv_counts[r], (cls, r, q)
+                chunks.append(sent)
+            got[tq.recv_pos.numpy()] = np.concatenate(chunks)
+            exp = np.where(touched[table[a:b]], table[a:b], -1)
+            assert np.array_equal(got, exp), (cls, q)
+    # different triple sets on the ranks: no plans (the dense exchange stays)
+    comm_x = SimpleNamespace(backend="gloo", all_reduce_=lambda t, op=None: t.abs())
+    assert D._touch_plans(hgs[0], comm_x, un, inn, jn, "cpu") is None

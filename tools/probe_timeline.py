@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where a scale_probe step waits on the modelled exchange: reads a rocprofv3 kernel trace of
-`tools/scale_probe.py --streams --a2a-gbs G` (the exchange stand-in is a sleep kernel on the
-communication stream) and prints, for the last full step (between the last two Adam kernels),
+`tools/scale_probe.py --streams --a2a-gbs G` (the exchange stand-in is torch's spin kernel on
+the communication stream) and prints, for the last full step (between the last two Adam kernels),
 the compute-stream idle gaps longer than a threshold with the kernels around them and the sleeps
 in flight -- i.e. the exposed exchange and what it blocks.
 
@@ -24,8 +24,9 @@ def main():
     adam = [i for i, r in enumerate(rows) if "k_adam" in r["Kernel_Name"]]
     a, b = adam[-2] + 1, adam[-1] + 1
     step = rows[a:b]
-    sleeps = [r for r in step if "sleep" in r["Kernel_Name"].lower()]
-    comp = [r for r in step if "sleep" not in r["Kernel_Name"].lower()]
+    is_sleep = lambda r: "sleep" in r["Kernel_Name"].lower() or "spin_kernel" in r["Kernel_Name"]
+    sleeps = [r for r in step if is_sleep(r)]
+    comp = [r for r in step if not is_sleep(r)]
     per_q = defaultdict(float)
     for r in comp:
         per_q[r["Queue_Id"]] += (r["t1"] - r["t0"]) / 1e3
