@@ -1016,7 +1016,30 @@ __global__ void __launch_bounds__(1024) k_col_reduce(const float* __restrict__ p
 // hub pieces leave a partial that k_dst_merge adds up in piece order (deterministic).
 // Written with row stride ld.
 // ---------------------------------------------------------------------------
-template <bool PERM>
+// The dz gathers of the destination sums.  AUX != 0 (lab builds only, PPGAT_DST_AUX): the same
+// gather as a buffer load carrying that cache policy (sc0 = 1, nt = 2, sc1 = 16), to measure
+// whether the L2 then fetches less than a whole 128-B line per 4- / 16-B gather.
+template <int AUX>
+__device__ __forceinline__ float dz_ld(const float* dz, int64_t i) {
+  if constexpr (AUX == 0) {
+    return dz[i];
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)dz, (short)0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4), 0, AUX));
+  }
+}
+
+template <int AUX, class V>
+__device__ __forceinline__ V dz_ldv(const V* dzv, int64_t i) {
+  if constexpr (AUX == 0 || sizeof(V) != 16) {
+    return dzv[i];
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)dzv, (short)0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, AUX));
+  }
+}
+
+template <bool PERM, int AUX = 0>
 __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const float* __restrict__ dz,
                                                  const int32_t* __restrict__ csr2csc,
                                                  float* __restrict__ ds_dst, int64_t ld,
@@ -1037,12 +1060,12 @@ __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const floa
     const int rs = it.beg[w], re = it.end[w];
     int k = rs + l;
     for (; k + 48 < re; k += 64) {
-      x0 += dz[at(k) * heads + hd];
-      x1 += dz[at(k + 16) * heads + hd];
-      x2 += dz[at(k + 32) * heads + hd];
-      x3 += dz[at(k + 48) * heads + hd];
+      x0 += dz_ld<AUX>(dz, at(k) * heads + hd);
+      x1 += dz_ld<AUX>(dz, at(k + 16) * heads + hd);
+      x2 += dz_ld<AUX>(dz, at(k + 32) * heads + hd);
+      x3 += dz_ld<AUX>(dz, at(k + 48) * heads + hd);
     }
-    for (; k < re; k += 16) x0 += dz[at(k) * heads + hd];
+    for (; k < re; k += 16) x0 += dz_ld<AUX>(dz, at(k) * heads + hd);
   }
   float x = (x0 + x1) + (x2 + x3);
   x = group_reduce<Op::Sum, 1, 8>(x);  // the 16 lanes of a DPP row
@@ -1054,7 +1077,7 @@ __global__ void __launch_bounds__(256) k_dst_sum(Items it, int heads, const floa
 
 // heads in {2, 4}: one 16-lane group per item for all heads, each edge's H logit gradients
 // loaded as one vector (dz rows of H floats), the same per-head summation order as k_dst_sum
-template <bool PERM, int H>
+template <bool PERM, int H, int AUX = 0>
 __global__ void __launch_bounds__(256) k_dst_sum_vh(Items it, const float* __restrict__ dz,
                                                     const int32_t* __restrict__ csr2csc, float* __restrict__ ds_dst,
                                                     int64_t ld, float* __restrict__ partial) {
@@ -1070,12 +1093,12 @@ __global__ void __launch_bounds__(256) k_dst_sum_vh(Items it, const float* __res
     const int rs = it.beg[w], re = it.end[w];
     int k = rs + l;
     for (; k + 48 < re; k += 64) {
-      x0 += dzv[at(k)];
-      x1 += dzv[at(k + 16)];
-      x2 += dzv[at(k + 32)];
-      x3 += dzv[at(k + 48)];
+      x0 += dz_ldv<AUX>(dzv, at(k));
+      x1 += dz_ldv<AUX>(dzv, at(k + 16));
+      x2 += dz_ldv<AUX>(dzv, at(k + 32));
+      x3 += dz_ldv<AUX>(dzv, at(k + 48));
     }
-    for (; k < re; k += 16) x0 += dzv[at(k)];
+    for (; k < re; k += 16) x0 += dz_ldv<AUX>(dzv, at(k));
   }
   const V xs = (x0 + x1) + (x2 + x3);
 #pragma unroll
@@ -1095,7 +1118,7 @@ __global__ void __launch_bounds__(256) k_dst_sum_vh(Items it, const float* __res
 // k_dst_sum_vh (each slot 0 + dz, as the group's x0, so no slot is -0 and the empty ones add
 // exactly nothing).  The halo partition's partial sums run over ~11M table rows of ~2 edges each
 // at world 8 on config 5, where 16 lanes per item left 14 of them idle behind three dependent loads.
-template <int H>
+template <int H, int AUX = 0>
 __global__ void __launch_bounds__(256) k_dst_sum_vh_short(Items it, int64_t w0, const float* __restrict__ dz,
                                                           const int32_t* __restrict__ csr2csc,
                                                           float* __restrict__ ds_dst, int64_t ld) {
@@ -1109,7 +1132,7 @@ __global__ void __launch_bounds__(256) k_dst_sum_vh_short(Items it, int64_t w0, 
   for (int l = 0; l < 16; ++l) k[l] = l < n ? csr2csc[rs + l] : 0;
   V v[16];
 #pragma unroll
-  for (int l = 0; l < 16; ++l) v[l] = l < n ? V{} + dzv[k[l]] : V{};
+  for (int l = 0; l < 16; ++l) v[l] = l < n ? V{} + dz_ldv<AUX>(dzv, k[l]) : V{};
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1)
 #pragma unroll
@@ -1292,6 +1315,43 @@ hipError_t launch_dst_sum(const ItemsArg& it, int heads, const float* dz, const 
   if (pairs == 0) return hipSuccess;
   const Items items{it.row, it.beg, it.end, it.n_items, it.n_hub_items};
   const bool aligned = (reinterpret_cast<uintptr_t>(dz) % (4 * heads)) == 0;
+#ifdef PPGAT_LAB_BUILD
+  static const int aux = [] {
+    const char* e = getenv("PPGAT_DST_AUX");
+    return e ? atoi(e) : 0;
+  }();
+  if (aux != 0 && csr2csc != nullptr && (heads == 1 || (heads == 4 && aligned))) {
+    if (heads == 1) {
+#define PPGAT_DST_LAB(A) hipLaunchKernelGGL((k_dst_sum<true, A>), dim3(blocks_for(pairs * 16)), dim3(256), 0, st, \
+                                            items, heads, dz, csr2csc, ds_dst, ld, partial)
+      if (aux == 2) PPGAT_DST_LAB(2);
+      else if (aux == 17) PPGAT_DST_LAB(17);
+      else if (aux == 19) PPGAT_DST_LAB(19);
+      else PPGAT_DST_LAB(1);
+#undef PPGAT_DST_LAB
+    } else {
+      const int64_t nl = it.n_long_items >= 0 ? it.n_long_items : it.n_items;
+      const Items lng{it.row, it.beg, it.end, nl, it.n_hub_items};
+      const dim3 gl(blocks_for(nl * 16)), gs(blocks_for(it.n_items - nl));
+#define PPGAT_DST_LAB(A)                                                                                        \
+  do {                                                                                                          \
+    if (nl > 0)                                                                                                 \
+      hipLaunchKernelGGL((k_dst_sum_vh<true, 4, A>), gl, dim3(256), 0, st, lng, dz, csr2csc, ds_dst, ld, partial); \
+    if (it.n_items > nl)                                                                                        \
+      hipLaunchKernelGGL((k_dst_sum_vh_short<4, A>), gs, dim3(256), 0, st, items, nl, dz, csr2csc, ds_dst, ld);    \
+  } while (0)
+      if (aux == 2) PPGAT_DST_LAB(2);
+      else if (aux == 17) PPGAT_DST_LAB(17);
+      else if (aux == 19) PPGAT_DST_LAB(19);
+      else PPGAT_DST_LAB(1);
+#undef PPGAT_DST_LAB
+    }
+    if (n_hubs > 0)
+      hipLaunchKernelGGL(k_dst_merge, dim3((unsigned)((n_hubs + 3) / 4)), dim3(256), 0, st, hub_row, hub_ptr, n_hubs,
+                         heads, partial, ds_dst, ld);
+    return hipGetLastError();
+  }
+#endif
   if (csr2csc != nullptr && (heads == 2 || heads == 4) && aligned) {
     // the long items (and hub pieces) 16 lanes each; the short ones (known when the schedule
     // counted them) one thread each, the same bits (k_dst_sum_vh_short)

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--runs", action="store_true",
                     help="also the send runs per rank and peer (dist.peer_masks / send_order_key: Comm.exchange "
                          "sends each run straight from the row table)")
+    ap.add_argument("--touched", action="store_true",
+                    help="also the halo rows the loss's 200k triples touch (bench / scale_probe draw): the rows "
+                         "the top layer's g exchange carries (dist._touch_plans)")
     args = ap.parse_args()
     d = pkg.data
     if args.config == 5:
@@ -62,6 +65,27 @@ def main():
                 row[name] = {"rows": int(len(mine)), "runs_per_peer": runs, "runs": int(sum(runs)),
                              "classes": int(np.unique(m).size)}
             print(json.dumps(row), flush=True)
+    if args.touched:
+        D = pkg.dist
+        src = np.concatenate([users, items])
+        dst = np.concatenate([items, users])
+        mask = D.peer_masks(src, owner[dst], owner, W)
+        del src, dst
+        tu, ti, tj = d.sample_bpr_numpy(g.user_ptr, g.user_items, g.n_items, 200_000, seed=42)
+        T = np.zeros(N, bool)
+        T[np.concatenate([tu, ti + nu, tj + nu])] = True
+        pc = np.zeros(N, np.int64)  # peers holding each row
+        for q in range(W):
+            pc += ((mask >> np.uint32(q)) & np.uint32(1)).astype(np.int64)
+        print(json.dumps({"touched_rows": int(T.sum()), "touched_users": int(T[:nu].sum()),
+                          "touched_items": int(T[nu:].sum())}), flush=True)
+        for r in range(W):
+            held = ((mask >> np.uint32(r)) & np.uint32(1)).astype(bool)
+            own = owner == r
+            print(json.dumps({"rank": r, "halo_rows": int(held.sum()), "halo_rows_touched": int((held & T).sum()),
+                              "sent_rows": int(pc[own].sum()), "sent_rows_touched": int(pc[own & T].sum()),
+                              "recv_GB_dense": held.sum() * row_bytes / 1e9,
+                              "recv_GB_touched": (held & T).sum() * row_bytes / 1e9}), flush=True)
     out = []
     for r in range(W):
         own = int((owner == r).sum())
