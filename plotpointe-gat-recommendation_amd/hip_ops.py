@@ -256,13 +256,22 @@ KINK_TAP: Optional[list] = None
 def _tap_kinks(rowptr, col, csr_eid, s_src, s_dst, heads: int):
     if KINK_TAP is None or col is None or rowptr is None:
         return
-    n = rowptr.numel() - 1
     E = int(col.numel())
     if E == 0:
         return
-    dst = torch.repeat_interleave(torch.arange(n, device=col.device), (rowptr[1:] - rowptr[:-1]).long())[:E]
-    z = s_src.reshape(-1, heads)[col[:E].long()] + s_dst.reshape(-1, heads)[dst]
-    KINK_TAP.append((csr_eid[:E].long().clone(), z > 0))
+    # in slices of 2^23 edges, each edge's destination found in the row pointers: one
+    # repeat_interleave over all 200M edges of config 5's whole graph gave wrong destinations for
+    # part of them on this torch build (the full-graph test's kink sides; the kernels were right)
+    rp = rowptr.long()
+    ss, sd = s_src.reshape(-1, heads), s_dst.reshape(-1, heads)
+    sides = torch.empty(E, heads, dtype=torch.bool, device=col.device)
+    step = 1 << 23
+    for a in range(0, E, step):
+        b = min(E, a + step)
+        k = torch.arange(a, b, device=col.device)
+        dst = torch.searchsorted(rp, k, right=True) - 1
+        sides[a:b] = (ss[col[a:b].long()] + sd[dst]) > 0
+    KINK_TAP.append((csr_eid[:E].long().clone(), sides))
 
 
 def seed_buffer(dropout_p: float, device) -> Optional[torch.Tensor]:

@@ -167,6 +167,49 @@ def test_chunked_oracle_equals_whole_graph(oracle):
     assert float(U[one]) > 0
 
 
+def test_rows_oracle_equals_whole_graph(oracle):
+    """pyg_gat_conv_rows (the full-graph test's checker: the layer restricted to sampled
+    destination rows, the upstream gradient zero elsewhere) gives the chunked whole-graph
+    oracle's rows, dx and parameter gradients -- with the heaviest row on the scatter-free
+    single-destination path (``heavy`` below its in-degree) and on the general one, with kink
+    sides given."""
+    g = _load("skewed_c128")
+    rng = np.random.default_rng(5)
+    H, C, Cin = 2, 16, 24
+    n = g["x"].shape[0]
+    ei = torch.from_numpy(g["edge_index"])
+    x = torch.from_numpy(rng.standard_normal((n, Cin))).double()
+    P = {"lin.weight": torch.from_numpy(rng.standard_normal((H * C, Cin)) * 0.2),
+         "att_src": torch.from_numpy(rng.standard_normal((1, H, C)) * 0.2),
+         "att_dst": torch.from_numpy(rng.standard_normal((1, H, C)) * 0.2),
+         "bias": torch.from_numpy(rng.standard_normal(C) * 0.1)}
+    indeg = torch.bincount(ei[1], minlength=n)
+    hub = int(torch.argmax(indeg))
+    rows = torch.tensor([hub] + [r for r in range(5, n, max(1, n // 7)) if r != hub][:6])
+    Gr = torch.from_numpy(rng.standard_normal((rows.numel(), C)))
+    G = torch.zeros(n, C, dtype=torch.float64)
+    G[rows] = Gr
+    out_c, dx_c, gr_c = oracle.pyg_gat_conv_chunked(P, x, ei, G, H, 0.1, 77, max_edges=700)
+    cols = torch.nonzero(torch.isin(ei[1], rows)).squeeze(1)
+    for heavy in (int(indeg[hub]) + 1, int(indeg[hub]) - 1):
+        o, nodes, dxn, gr = oracle.pyg_gat_conv_rows(P, x, ei, cols, rows, Gr, H, 0.1, 77, heavy=heavy)
+        assert _rel(o, out_c[rows]) <= 1e-12, heavy
+        assert _rel(dxn, dx_c[nodes]) <= 1e-12, heavy
+        dx_c_off = dx_c.clone()
+        dx_c_off[nodes] = 0
+        assert float(dx_c_off.abs().max()) == 0.0    # no other row carries a gradient
+        for k in P:
+            assert _rel(gr[k], gr_c[k]) <= 1e-11, (heavy, k)
+    kp = torch.from_numpy(rng.random((ei.shape[1], H)) > 0.5)
+    a, b = [], []
+    ra = oracle.pyg_gat_conv_rows(P, x, ei, cols, rows, Gr, H, 0.1, 77, kink_pos=kp, kink_stats=a,
+                                  heavy=int(indeg[hub]) + 1)
+    rb = oracle.pyg_gat_conv_rows(P, x, ei, cols, rows, Gr, H, 0.1, 77, kink_pos=kp, kink_stats=b,
+                                  heavy=int(indeg[hub]) - 1)
+    assert _rel(ra[0], rb[0]) <= 1e-12 and _rel(ra[2], rb[2]) <= 1e-12
+    assert sum(s[0] for s in a) == sum(s[0] for s in b) > 0
+
+
 def test_kink_sides_option(oracle):
     """kink_pos = the fp64 signs leaves the layer unchanged (bitwise) and reports no tie; all
     sides forced to slope 1 gives the layer without the LeakyReLU; flipped sides are reported."""

@@ -44,10 +44,10 @@ for s in $STEPS; do
             python "$R/tools/pmc_kernel.py" "k_dst_sum<true>" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_dst_sum.json" && \
             python "$R/tools/pmc_kernel.py" "k_bwd_src<" "$OUT/pmcdst_a" "$OUT/pmcdst_b" > "$OUT/pmc_bwd_src_tcc.json" ;;
     dstlab) for a in ${DSTAUX:-0 2 17 19}; do
-              (cd /tmp && run "dstlab2_aux$a" 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_DST_AUX=$a timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RD_UNCACHED_32B_sum --kernel-trace --output-format csv -d "$OUT/dstlab2_$a" -o p -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) || exit 1
+              (cd /tmp && run "dstlab2_aux$a" 300 env PPGAT_LIB=$R/lab_build/libppgat.so PPGAT_DST_AUX=$a timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RD_UNCACHED_32B_sum --kernel-trace --output-format csv -d "$OUT/dstlab2_$a" -o p -- python "$R/bench.py" --steps 3 --warmup 1 --graph off --cpu-baseline-seconds 0) || exit 1
               python "$R/tools/pmc_kernel.py" "k_dst_sum<true" "$OUT/dstlab2_$a" > "$OUT/dstlab2_aux$a.json"
               if [ -n "${DST5:-}" ]; then
-                (cd /tmp && run "dstlab5_aux$a" 400 env PPGAT_LIB=lab_build/libppgat.so PPGAT_DST_AUX=$a timeout -s KILL 360 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RD_UNCACHED_32B_sum --kernel-trace --output-format csv -d "$OUT/dstlab5_$a" -o p -- python -u "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) || exit 1
+                (cd /tmp && run "dstlab5_aux$a" 400 env PPGAT_LIB=$R/lab_build/libppgat.so PPGAT_DST_AUX=$a timeout -s KILL 360 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RD_UNCACHED_32B_sum --kernel-trace --output-format csv -d "$OUT/dstlab5_$a" -o p -- python -u "$R/bench.py" --config 5 --steps 2 --warmup 1 --graph off --cpu-baseline-seconds 0) || exit 1
                 python "$R/tools/pmc_kernel.py" "k_dst_sum_vh<" "$OUT/dstlab5_$a" > "$OUT/dstlab5_long_aux$a.json"
                 python "$R/tools/pmc_kernel.py" "k_dst_sum_vh_short" "$OUT/dstlab5_$a" > "$OUT/dstlab5_short_aux$a.json"
               fi
