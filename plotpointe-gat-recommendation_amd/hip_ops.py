@@ -259,9 +259,10 @@ def _tap_kinks(rowptr, col, csr_eid, s_src, s_dst, heads: int):
     E = int(col.numel())
     if E == 0:
         return
-    # in slices of 2^23 edges, each edge's destination found in the row pointers: one
-    # repeat_interleave over all 200M edges of config 5's whole graph gave wrong destinations for
-    # part of them on this torch build (the full-graph test's kink sides; the kernels were right)
+    # in slices of 2^23 edges: formed in one piece over the 200M edges of config 5's whole graph
+    # ([E, H] gathers and compare) the sides came out wrong for part of the edges on this torch
+    # build -- the destinations themselves and the kernels' results were right
+    # (tests/test_gpu_cfg5_diag.py); sliced, the full-graph test's oracle agrees with them
     rp = rowptr.long()
     ss, sd = s_src.reshape(-1, heads), s_dst.reshape(-1, heads)
     sides = torch.empty(E, heads, dtype=torch.bool, device=col.device)
