@@ -15,6 +15,7 @@ N>1: launched by torch.distributed.run, one rank per GPU.
 from __future__ import annotations
 
 import argparse
+import gc
 import importlib
 import json
 import os
@@ -314,6 +315,11 @@ def main():
                 step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize()
+        # the warm-up's cached blocks back to the device: the capture allocates the step's
+        # buffers in a private pool of its own, and at the whole 200M-edge graph (229 GB peak)
+        # two copies of the working set do not fit in 288 GB
+        gc.collect()
+        torch.cuda.empty_cache()
         ok = 1
         try:
             graph = torch.cuda.CUDAGraph()
@@ -324,6 +330,8 @@ def main():
         except Exception as exc:  # capture refused (driver / RCCL): time the same step eagerly instead
             print(f"bench: hipGraph capture failed ({type(exc).__name__}: {exc})", file=sys.stderr, flush=True)
             graph, ok = None, 0
+            gc.collect()
+            torch.cuda.empty_cache()  # the failed capture's private pool, before the eager steps
         torch.cuda.synchronize()
         if dist_path:
             # one shared decision: replay only if every rank captured (a rank running eagerly
