@@ -277,6 +277,11 @@ def main():
     # hipGraph replay by default (one captured step: ~150 launches enqueued once), except the
     # gloo rehearsal whose collectives run on the host
     use_graph = args.graph == "on" or (args.graph == "auto" and not (dist_path and args.dist_backend == "gloo"))
+    if args.config == 5 and scale > 0.5 and args.graph == "auto":
+        # the whole 200M-edge graph on one GPU: a capture holds the step's buffers in a private
+        # pool beside the persistent ~150 GB and does not fit 288 GB (profiles/r06/
+        # x11_bench_cfg5_full_graph_oom.log); the eager step enqueues in 9 ms of a 558-ms step
+        use_graph = False
     opt = pkg.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=use_graph)
     # the loss backward's sort on a side stream beside the forward: off by default, measured no
     # faster inside the captured step (1.890 vs 1.881 ms, profiles/r05/w1_bench.log)
@@ -330,6 +335,8 @@ def main():
         except Exception as exc:  # capture refused (driver / RCCL): time the same step eagerly instead
             print(f"bench: hipGraph capture failed ({type(exc).__name__}: {exc})", file=sys.stderr, flush=True)
             graph, ok = None, 0
+        if graph is None:
+            # (outside the handler: the exception's frames hold the failed capture's tensors)
             gc.collect()
             torch.cuda.empty_cache()  # the failed capture's private pool, before the eager steps
         torch.cuda.synchronize()
