@@ -1598,6 +1598,12 @@ def _xgat_dst_sum(lib, v: "XViews", dz, S, H: int, E: int, st, col0: Optional[in
     col0 = H if col0 is None else col0
     ld = 2 * H if ld is None else ld
     fs = v.fwd_sched.cstruct()
+    if E > 6 * max(v.n_dst, 1):
+        # a thread per short destination (k_dst_sum_vh_short) pays off on the halo tables' rows of
+        # ~2 edges (4 x 1.48 -> 4 x 0.71 ms per step at the world-8 probe); at the share's ~13 it
+        # measured slower than 16 lanes per item (0.70 vs 0.54 ms per call, profiles/r06/
+        # x13_cfg5_kernel_stats.csv against r05/w43): all items on the 16-lane kernel (same bits)
+        fs.n_long_items = -1
     dws = torch.empty(max(v.fwd_sched.n_hub_items * H, 1), dtype=torch.float32, device=dev)
     if v.dz_slot is None:
         _lib.check(lib.ppgat_bwd_dst_sum_csc(ctypes.byref(fs), v.n_dst, E, H, dz.data_ptr(),
