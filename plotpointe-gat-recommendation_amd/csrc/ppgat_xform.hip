@@ -900,7 +900,11 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
 // k_gemm_nnh3: k_gemm_nnh2's pipeline with the next chunk prepared inside the current chunk's
 // MFMA sequence (ppgat_nnh_pipe.h: nnh3_loop), same products in the same order as k_gemm_nnh.
 // ---------------------------------------------------------------------------
-template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false>
+// E4 (lab builds, PPGAT_NNH_E4=1): the epilogue without rank terms through a per-wave LDS
+// transpose -- each lane's column of 16 rows is written to the (now idle) B buffers and read back
+// as float4 pieces of rows, so a wave stores its 32 x 32 block per column tile in 4 float4
+// instructions (8 rows x 128 B each) instead of 16 scalar ones; the same values (same bits).
+template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false, bool E4 = false>
 __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
@@ -974,6 +978,30 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* _
           if (v < nv) y = fmaf(sv[v], ra[t][v], y);
         if (row < M) a.Y[row * a.ldy + n0 + 32 * t + r] = y;
       }
+    }
+  } else if constexpr (E4) {
+    // the B buffers are idle: every wave passed the last chunk's barrier after its last B reads
+    float* T = reinterpret_cast<float*>(sB) + wv * (32 * 40);  // this wave's [32 rows][40] tile
+    const int rl = lane >> 3, c4 = 4 * (lane & 7);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 32 * t + r;
+      const float bv = a.bias != nullptr ? a.bias[col] : 0.f;
+      const float ic = ldexpf(a.alpha, -ecol[col]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) T[((q & 3) + 8 * (q >> 2) + 4 * hf) * 40 + r] = fmaf(acc[t][q] * fr[q], ic, bv);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t row = row0 + rl + 8 * j;
+        const float4 v = *reinterpret_cast<const float4*>(T + (rl + 8 * j) * 40 + c4);
+        if (row < M) *reinterpret_cast<float4*>(a.Y + row * a.ldy + n0 + 32 * t + c4) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   } else {
 #pragma unroll
@@ -2736,6 +2764,15 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
     }                                                                                                            \
   } while (0)
 #ifdef PPGAT_LAB_BUILD
+        static const bool e4 = [] {
+          const char* e = getenv("PPGAT_NNH_E4");
+          return e != nullptr && atoi(e) == 1;
+        }();
+        if (e4 && nv == 0 && a.ldy % 4 == 0 && reinterpret_cast<uintptr_t>(Y) % 16 == 0) {
+          if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, false, 1, false, 0, false, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          else hipLaunchKernelGGL((k_gemm_nnh3<4, false, 1, false, 0, false, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
+          return hipGetLastError();
+        }
         if (v == 4) PPGAT_NNH3(2, false, false);
         else if (v == 5) PPGAT_NNH3(2, true, false);
         else if (v == 6) PPGAT_NNH3(1, false, true);

@@ -225,6 +225,48 @@ def test_tnh256_bitwise_equals_tnh(cuda):
     assert run({}) == run({"PPGAT_LIB": str(lab), "PPGAT_TNH256": "0"})
 
 
+_E4_CHECK = r"""
+import hashlib, importlib, json, sys, torch
+sys.path.insert(0, sys.argv[1])
+ops = importlib.import_module("plotpointe-gat-recommendation_amd.hip_ops")
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(29)
+out = {}
+for M, K, N, mode, bias in ((200_001, 256, 1024, 1, False), (70_001, 1024, 256, 0, True), (65_536, 512, 128, 0, True),
+                            (100_003, 256, 256, 1, False)):
+    X = torch.randn(M, K, device=dev, generator=g)
+    X[7, :5] *= 1e4
+    B = torch.randn(*((K, N) if mode == 0 else (N, K)), device=dev, generator=g)
+    b = torch.randn(N, device=dev, generator=g) if bias else None
+    Y = ops.gemm_nn(X, B, mode, N, alpha=0.25, bias=b)
+    torch.cuda.synchronize()
+    out[f"{M}x{K}x{N}"] = hashlib.sha1(Y.cpu().numpy().tobytes()).hexdigest()
+print(json.dumps(out))
+"""
+
+
+def test_nnh3_e4_epilogue_bitwise(cuda):
+    """The lab NN epilogue through a per-wave LDS transpose (k_gemm_nnh3<..., E4>: float4 row
+    stores) writes the same bits as the scalar-store epilogue, on both tile widths, ragged M,
+    with and without bias.  Lab test: skips without lab_build/libppgat.so."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    lab = root / "lab_build" / "libppgat.so"
+    if not lab.exists():
+        pytest.skip("lab build absent")
+
+    def run(env):
+        r = subprocess.run([sys.executable, "-c", _E4_CHECK, str(root)], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    assert run({}) == run({"PPGAT_LIB": str(lab), "PPGAT_NNH_E4": "1"})
+
+
 def test_tnh_bounded_equals_exact_bound(pkg, cuda):
     """ppgat_gemm_tn_big_bounded: with the exact column maxima as the bound the result is the
     unbounded call's bit for bit; with a looser bound (x-derived, as the multi-head layer passes
