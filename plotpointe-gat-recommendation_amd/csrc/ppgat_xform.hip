@@ -904,8 +904,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nnh2(NnArg a, const uint16_t* _
 // transpose -- each lane's column of 16 rows is written to the (now idle) B buffers and read back
 // as float4 pieces of rows, so a wave stores its 32 x 32 block per column tile in 4 float4
 // instructions (8 rows x 128 B each) instead of 16 scalar ones; the same values (same bits).
-template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false, bool E4 = false>
-__global__ void __launch_bounds__(512, 1) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
+// OCC (lab, PPGAT_NNH_OCC2=1 with NT = 4): at least OCC waves per SIMD (HIP's launch_bounds), i.e. two
+// workgroups per CU at OCC = 4, so one's epilogue stores can run beside the other's products.
+template <int NT, bool RK, int BD = 1, bool PRIO = false, int LAB = 0, bool XT = false, bool E4 = false, int OCC = 1>
+__global__ void __launch_bounds__(512, OCC) k_gemm_nnh3(NnArg a, const uint16_t* __restrict__ img,
                                                       const int* __restrict__ ecol) {
   using I = NnhImg<NT>;
   constexpr int KC = I::KC;
@@ -2768,6 +2770,23 @@ hipError_t gemm_nn(const float* X, int64_t ldx, int64_t M, int K, const float* B
           const char* e = getenv("PPGAT_NNH_E4");
           return e != nullptr && atoi(e) == 1;
         }();
+        static const bool occ2 = [] {  // two workgroups per CU on the 128-column tile (<= 128 VGPRs)
+          const char* e = getenv("PPGAT_NNH_OCC2");
+          return e != nullptr && atoi(e) == 1;
+        }();
+        if (occ2 && nv == 0) {
+          NnArg b2 = a;
+          b2.n_blocks = N / 128;
+          const unsigned g2 = (unsigned)((b2.row_blocks + 7) / 8 * 8 * b2.n_blocks);
+          int* ecol4 = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align_up(nnh_image_bytes(K, N, 4)));
+          if (w8) {  // re-split B for the 128-column tile
+            hipError_t e2 = nnh_presplit(B, ldb, bmode, K, N, 4, img, ecol4, st);
+            if (e2 != hipSuccess) return e2;
+          }
+          hipLaunchKernelGGL((k_gemm_nnh3<4, false, 1, false, 0, false, false, 4>), dim3(g2), dim3(512), 0, st, b2, img,
+                             w8 ? ecol4 : ecol);
+          return hipGetLastError();
+        }
         if (e4 && nv == 0 && a.ldy % 4 == 0 && reinterpret_cast<uintptr_t>(Y) % 16 == 0) {
           if (w8) hipLaunchKernelGGL((k_gemm_nnh3<8, false, 1, false, 0, false, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);
           else hipLaunchKernelGGL((k_gemm_nnh3<4, false, 1, false, 0, false, true>), dim3(grid), dim3(512), 0, st, a, img, ecol);

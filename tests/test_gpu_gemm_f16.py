@@ -264,7 +264,9 @@ def test_nnh3_e4_epilogue_bitwise(cuda):
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         return json.loads(r.stdout.strip().splitlines()[-1])
-    assert run({}) == run({"PPGAT_LIB": str(lab), "PPGAT_NNH_E4": "1"})
+    base = run({})
+    assert base == run({"PPGAT_LIB": str(lab), "PPGAT_NNH_E4": "1"})
+    assert base == run({"PPGAT_LIB": str(lab), "PPGAT_NNH_OCC2": "1"})  # 128-column tile, 2 workgroups per CU
 
 
 def test_tnh_bounded_equals_exact_bound(pkg, cuda):

@@ -55,6 +55,8 @@ for s in $STEPS; do
     e4lab) run gemm5_base 300 python tools/bench_gemm.py --cfg5 --iters 10 && \
            run gemm5_e4 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH_E4=1 python tools/bench_gemm.py --cfg5 --iters 10 && \
            run bench5_e4 600 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH_E4=1 python -u bench.py --config 5 --steps 10 --warmup 3 ;;
+    occ2lab) run gemm5_base 300 python tools/bench_gemm.py --cfg5 --iters 10 && \
+           run gemm5_occ2 300 env PPGAT_LIB=lab_build/libppgat.so PPGAT_NNH_OCC2=1 python tools/bench_gemm.py --cfg5 --iters 10 ;;
     tnpmc) run tn5_256 120 python tools/bench_gemm.py --tn5 --iters 10 && \
            run tn5_128 120 env PPGAT_LIB=lab_build/libppgat.so PPGAT_TNH256=0 python tools/bench_gemm.py --tn5 --iters 10 && \
            run tnpmc256 400 env GEMM_ARGS=--tn5 GEMM_TAG=_tn256 bash tools/gemm_pmc.sh && \
