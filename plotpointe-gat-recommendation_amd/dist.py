@@ -840,6 +840,7 @@ class HaloRows:
         self.events = {}
         self.local = set()
         self.started = []   # exchanged classes, in start order
+        self.last = []      # exchanged classes, in the order of their latest start (complete last = last)
         self.keep = {}      # class -> the source tensors of its exchange in flight
         self.s = self.s_dst = self.A = None  # the consuming layer's node scores (enable_scores)
 
@@ -879,6 +880,9 @@ class HaloRows:
         plan, (a, b) = self.plan(cls), self.span(cls)
         if cls not in self.started:
             self.started.append(cls)
+        if cls in self.last:
+            self.last.remove(cls)
+        self.last.append(cls)
         comm, st = self.comm, self.stages
         n0 = self.hg.n_own
         kw = {} if part is None else {"part": part}
@@ -989,8 +993,9 @@ def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows
                        after_all)]
     # destination class -> (rows, schedule, the source class it reads)
     ph = {"u": (0, hg.n_own_u, hg.fwd_sched_u, "i"), "i": (hg.n_own_u, hg.n_own, hg.fwd_sched_i, "u")}
+    # the class whose rows complete first (its latest start earliest) first
     order = sorted(ph, key=lambda d: (ph[d][3] not in rows_in.local,
-                                      rows_in.started.index(ph[d][3]) if ph[d][3] in rows_in.started else 0))
+                                      rows_in.last.index(ph[d][3]) if ph[d][3] in rows_in.last else 0))
     halves = getattr(hg, "fwd_sched_halves", None) if rows_out is not None else None
     if not halves:
         return [XPhase(ph[d][0], ph[d][1], ph[d][2], (rows_in.span(ph[d][3]),),
@@ -998,14 +1003,28 @@ def _halo_phases(hg: "HaloGraph", rows_in: HaloRows, rows_out: Optional[HaloRows
     # each destination class in two halves (the plans' parts): the first half's output rows start
     # towards the peers while the second half is computed, so the next layer's rows arrive half a
     # phase earlier.  Per destination the same kernels and order as one phase: the same results.
+    # Link order (PPGAT_HALO_DEFER=1, the default): the first class's second half leaves after the
+    # second class's two halves, so the class the next layer's second phase needs is the one
+    # still on the wire while its first phase runs -- with the exchange at 640 GB/s the forward
+    # is link-bound and ends with the next layer's second phase.
     out = []
-    for d in order:
+    defer = os.environ.get("PPGAT_HALO_DEFER", "1") == "1" and len(order) == 2
+    held = []
+    for k, d in enumerate(order):
         d0, d1, _, need = ph[d]
         dm = d0 + (d1 - d0) // 2
         (s0, s1) = halves[d]
         out.append(XPhase(d0, dm, s0, (rows_in.span(need),), (lambda c: (lambda: rows_in.wait(c)))(need),
                           send(d, d0, dm, 0)))
-        out.append(XPhase(dm, d1, s1, (), None, send(d, dm, d1, 1)))
+        if defer and k == 0:
+            go = send(d, dm, d1, 1)
+            held.append(go)
+            out.append(XPhase(dm, d1, s1, (), None, (lambda o: None)))
+        elif defer:
+            last = send(d, dm, d1, 1)
+            out.append(XPhase(dm, d1, s1, (), None, (lambda o, a=last, b=held: (a(o), [f(o) for f in b]))))
+        else:
+            out.append(XPhase(dm, d1, s1, (), None, send(d, dm, d1, 1)))
     return out
 
 
