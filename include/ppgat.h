@@ -658,6 +658,11 @@ int ppgat_xgat_bwd_edges_gd_colmax(const ppgat_schedule* src_sched, const int32_
                                    void* workspace, size_t workspace_bytes, void* stream);
 int ppgat_xgat_nstate(const float* s_dst, const float* m, const float* inv_l, const float* D, int64_t n_dst, int heads,
                       float* nstate, void* stream);
+/* Halo partition (dist.py): set the D component of every row of an nstate table whose other three
+ * came by exchange -- nstate[i][h].w = D[i * heads + h] for i < n_rows.  Replaces dist.py:
+ * `ntab.x.view(R, H, 4)[:, :, 3].copy_(Dtab.x)` (no reference counterpart: the reference has no
+ * sharded backward). */
+int ppgat_xgat_nstate_set_d(float* nstate, const float* D, int64_t n_rows, int heads, void* stream);
 int ppgat_xgat_bwd_dz_workspace_bytes(int64_t n_hub_items, int heads, size_t* bytes);
 int ppgat_xgat_bwd_dz(const ppgat_schedule* src_sched, const int32_t* row, const int32_t* csc_eid,
                       const int32_t* dz_slot, int64_t n_edges, int heads, const float* s_src, const float* nstate,

@@ -151,6 +151,7 @@ SIGNATURES = {
     "ppgat_xgat_bwd_edges_gd_colmax": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                                c_i64, c_f, c_f, c_u64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ppgat_xgat_nstate": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
+    "ppgat_xgat_nstate_set_d": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp]),
     "ppgat_xgat_bwd_dz_workspace_bytes": (c_int, [c_i64, c_int, ctypes.POINTER(c_sz)]),
     "ppgat_xgat_bwd_dz": (c_int, [SP, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_f, c_f, c_u64, c_vp, c_vp, c_vp,
                                   c_i64, c_vp, c_sz, c_vp]),

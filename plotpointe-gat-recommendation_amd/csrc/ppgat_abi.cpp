@@ -1436,6 +1436,16 @@ int ppgat_xgat_nstate(const float* s_dst, const float* m, const float* inv_l, co
   return PPGAT_OK;
 }
 
+int ppgat_xgat_nstate_set_d(float* nstate, const float* D, int64_t n_rows, int heads, void* stream) {
+  if (n_rows < 0 || heads < 1) return fail(PPGAT_ERR_INVALID, "xgat_nstate_set_d: bad sizes");
+  if (n_rows > 0 && (!nstate || !D)) return fail(PPGAT_ERR_INVALID, "xgat_nstate_set_d: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Timed t(PPGAT_K_BWD_PRO, st);
+  hipError_t e = ppgat::xgat_nstate_set_d(nstate, D, n_rows, heads, st);
+  if (e != hipSuccess) return hip_fail(e, "xgat_nstate_set_d");
+  return PPGAT_OK;
+}
+
 int ppgat_xgat_bwd_dz_workspace_bytes(int64_t n_hub_items, int heads, size_t* bytes) {
   if (!bytes || n_hub_items < 0 || heads < 1) return fail(PPGAT_ERR_INVALID, "xgat_bwd_dz_workspace_bytes: bad sizes");
   *bytes = (size_t)n_hub_items * heads * sizeof(float);

@@ -240,6 +240,7 @@ hipError_t xgat_bwd_edges_g(const ItemsArg& it, const int32_t* row, const int32_
                             const int32_t* hub_ptr, int64_t n_hubs, hipStream_t st, float* pz = nullptr,
                             unsigned* gmax = nullptr);
 int nnh_pipeline_variant();  // the fp16 NN main loop: 1 k_gemm_nnh, 2 k_gemm_nnh2, 3 k_gemm_nnh3 (PPGAT_NNH2)
+hipError_t xgat_nstate_set_d(float* nstate, const float* D, int64_t n, int H, hipStream_t st);
 hipError_t xgat_nstate(const float* s_dst, const float* m, const float* invl, const float* D, int64_t n, int H,
                        float* nstate, hipStream_t st);
 hipError_t xgat_bwd_dz(const ItemsArg& it, const int32_t* row, const int32_t* csc_eid, const int32_t* csc2csr, int H,

@@ -1422,7 +1422,8 @@ def _halo_xgat_backward_deferred_d(saved: dict, g, hg: "HaloGraph", comm: "Comm"
     for cls in ("u", "i"):
         Dtab.start(cls, Dtab.x[:n0])
     Dtab.wait_all()
-    ntab.x.view(R, H, 4)[:, :, 3].copy_(Dtab.x)  # nstate {s_dst, m, inv_l, D} of every table row
+    Dx = Dtab.x.contiguous()  # nstate {s_dst, m, inv_l, D} of every table row
+    _lib.check(lib.ppgat_xgat_nstate_set_d(ntab.x.data_ptr(), Dx.data_ptr(), R, H, st), "xgat_nstate_set_d")
     del Dtab
     # dz in place over dalpha, ds_src per own source
     S = torch.zeros(max(n0, 1), 2 * H, dtype=torch.float32, device=dev)
