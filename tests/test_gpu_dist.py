@@ -209,6 +209,18 @@ def test_sharded_world2_shared_gpu(cuda, tmp_path, heads, part):
     _check(torch.load(tmp_path / "sharded_2.pt", weights_only=False), (Z, loss, grads))
 
 
+@pytest.mark.parametrize("world,heads,part", [(3, 4, "halo"), (4, 4, "halo"), (4, 1, "halo"), (4, 1, "replicated")])
+def test_sharded_world34_shared_gpu(cuda, tmp_path, world, heads, part):
+    """Three and four ranks on this GPU over gloo: the halo plans' runs and halves, the
+    touched-rows gradient exchange and the link order with more than one peer per rank (the
+    8-GPU node's paths at a size that fits here), against the unsharded fp64 oracle."""
+    store = _master_store()
+    mp.start_processes(_worker, args=(world, store.port, str(tmp_path), heads, part), nprocs=world, join=True,
+                       start_method="spawn")
+    del store
+    _check(torch.load(tmp_path / f"sharded_{world}.pt", weights_only=False), _oracle(heads))
+
+
 @pytest.mark.parametrize("heads,part", [(4, "halo"), (4, "halo-g2"), (1, "halo"), (1, "replicated"),
                                         (2, "replicated-fsplit")])
 def test_sharded_world2_rccl(cuda, tmp_path, heads, part):
